@@ -1,0 +1,340 @@
+// capi.cpp — extern "C" boundary of libgeos_gtfv3_interface.so.
+// See include/geos_gtfv3_interface.h (reference symbols) and include/gtfv3_device.h.
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <mutex>
+#include <sstream>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/geos_gtfv3_interface.h"
+#include "../../include/gtfv3_device.h"
+#include "bridge.hpp"
+#include "dycore.hpp"
+#include "hip_util.hpp"
+#include "stencils_registry.hpp"
+
+namespace gtfv3 {
+namespace {
+std::mutex g_err_mu;
+std::string g_err;
+}  // namespace
+std::string last_error() {
+  std::lock_guard<std::mutex> l(g_err_mu);
+  return g_err;
+}
+void set_error(const std::string& m) {
+  std::lock_guard<std::mutex> l(g_err_mu);
+  g_err = m;
+}
+
+Namelist parse_config(const char* cfg) {
+  Namelist nl;
+  std::string s = cfg ? cfg : "";
+  std::stringstream ss(s);
+  std::string item;
+  while (std::getline(ss, item, ';')) {
+    if (item.empty()) continue;
+    auto eq = item.find('=');
+    if (eq == std::string::npos) throw std::runtime_error("config item without '=': " + item);
+    std::string k = item.substr(0, eq), v = item.substr(eq + 1);
+    double x = std::stod(v);
+    int ix = (int)x;
+    if (k == "npx") nl.npx = nl.npy = ix;
+    else if (k == "npz") nl.npz = ix;
+    else if (k == "nq") nl.nq = ix;
+    else if (k == "layout_x") nl.layout_x = ix;
+    else if (k == "layout_y") nl.layout_y = ix;
+    else if (k == "dt") nl.dt_atmos = x;
+    else if (k == "k_split") nl.k_split = ix;
+    else if (k == "n_split") nl.n_split = ix;
+    else if (k == "hord_mt") nl.hord_mt = ix;
+    else if (k == "hord_vt") nl.hord_vt = ix;
+    else if (k == "hord_tm") nl.hord_tm = ix;
+    else if (k == "hord_dp") nl.hord_dp = ix;
+    else if (k == "hord_tr") nl.hord_tr = ix;
+    else if (k == "kord_mt") nl.kord_mt = ix;
+    else if (k == "kord_wz") nl.kord_wz = ix;
+    else if (k == "kord_tr") nl.kord_tr = ix;
+    else if (k == "kord_tm") nl.kord_tm = ix;
+    else if (k == "dddmp") nl.dddmp = x;
+    else if (k == "d2_bg") nl.d2_bg = x;
+    else if (k == "p_fac") nl.p_fac = x;
+    else if (k == "dz_min") nl.dz_min = x;
+    else if (k == "fill") nl.fill = ix != 0;
+    else if (k == "adiabatic") nl.adiabatic = ix != 0;
+    else if (k == "ptop") nl.ptop = x;
+    else if (k == "host_only") nl.host_only = ix != 0;
+    else throw std::runtime_error("unknown config key: " + k);
+  }
+  for (int h : {nl.hord_mt, nl.hord_vt, nl.hord_tm, nl.hord_dp, nl.hord_tr})
+    if (h != 5 && h != 6) throw std::runtime_error("hord must be 5 or 6");
+  return nl;
+}
+
+}  // namespace gtfv3
+
+using namespace gtfv3;
+
+#define API_TRY try {
+#define API_CATCH                      \
+  }                                    \
+  catch (const std::exception& e) {    \
+    set_error(e.what());               \
+    return -1;                         \
+  }                                    \
+  return 0;
+
+static Dycore* D(void* h) {
+  if (!h) throw std::runtime_error("null dycore handle");
+  return static_cast<Dycore*>(h);
+}
+
+extern "C" {
+
+int geos_gtfv3_last_error(char* buf, int len) {
+  std::string e = last_error();
+  if (buf && len > 0) {
+    std::strncpy(buf, e.c_str(), (size_t)len - 1);
+    buf[len - 1] = 0;
+  }
+  return (int)e.size();
+}
+
+void* gtfv3_create(const char* config, int rank, int nranks, const void* nccl_id) {
+  try {
+    Namelist nl = parse_config(config);
+    return new Dycore(nl, rank, nranks, nccl_id);
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return nullptr;
+  }
+}
+
+void gtfv3_destroy(void* h) { delete static_cast<Dycore*>(h); }
+
+int gtfv3_get_unique_id(void* out) {
+  API_TRY
+  ncclUniqueId id;
+  if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
+  std::memcpy(out, &id, sizeof(id));
+  API_CATCH
+}
+
+int gtfv3_dims(void* h, int* out) {
+  API_TRY
+  Dycore* d = D(h);
+  int v[10] = {d->d.nx, d->d.ny, d->d.pitch, d->d.nj, d->d.nsub, d->d.npz, d->dc.N, d->dc.lx, d->dc.ly, d->nl.nq};
+  std::memcpy(out, v, sizeof(v));
+  API_CATCH
+}
+
+int gtfv3_sub_info(void* h, int s, int* out) {
+  API_TRY
+  Dycore* d = D(h);
+  if (s < 0 || s >= d->d.nsub) throw std::runtime_error("sub index out of range");
+  const SubInfo& si = d->hsubs[s];
+  int v[8] = {si.tile, si.ioff, si.joff, si.N, si.flags, si.gid, 0, 0};
+  std::memcpy(out, v, sizeof(v));
+  API_CATCH
+}
+
+int gtfv3_field_create(void* h, const char* name, int nk) {
+  API_TRY
+  D(h)->field(name, nk);
+  API_CATCH
+}
+
+int gtfv3_field_nk(void* h, const char* name) {
+  try {
+    Field* f = D(h)->find(name);
+    return f ? f->nk : 0;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return -1;
+  }
+}
+
+int gtfv3_field_upload(void* h, const char* name, int nk, const double* host) {
+  API_TRY
+  D(h)->upload(name, host, nk);
+  API_CATCH
+}
+
+int gtfv3_field_download(void* h, const char* name, double* host) {
+  API_TRY
+  D(h)->download(name, host);
+  API_CATCH
+}
+
+void* gtfv3_field_ptr(void* h, const char* name) {
+  try {
+    Field* f = D(h)->find(name);
+    return f ? f->p : nullptr;
+  } catch (...) {
+    return nullptr;
+  }
+}
+
+int gtfv3_get_metric(void* h, const char* name, double* out) {
+  API_TRY
+  Dycore* d = D(h);
+  for (int m = 0; m < NMETRIC; ++m)
+    if (std::strcmp(kMetricNames[m], name) == 0) {
+      std::memcpy(out, d->hm.at(m, 0), sizeof(double) * d->d.nsub * d->d.plane);
+      return 0;
+    }
+  throw std::runtime_error(std::string("unknown metric ") + name);
+  API_CATCH
+}
+
+int gtfv3_get_xyz(void* h, double* out) {
+  API_TRY
+  Dycore* d = D(h);
+  std::memcpy(out, d->hm.xyz.data(), sizeof(double) * d->hm.xyz.size());
+  API_CATCH
+}
+
+int gtfv3_get_scalars(void* h, double* out) {
+  API_TRY
+  Dycore* d = D(h);
+  out[0] = d->hm.da_min;
+  out[1] = d->hm.da_min_c;
+  for (size_t i = 0; i < d->hm.corner_w.size(); ++i) out[2 + i] = d->hm.corner_w[i];
+  API_CATCH
+}
+
+int gtfv3_halo_table(void* h, int kind, int* out, int cap) {
+  try {
+    const auto& t = D(h)->halo.local_table(kind);
+    int n = (int)t.size();
+    if (out && cap >= n) std::memcpy(out, t.data(), sizeof(HaloEntry) * n);
+    return n;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return -1;
+  }
+}
+
+int gtfv3_halo_update(void* h, const char* spec) {
+  API_TRY
+  std::vector<std::pair<std::string, char>> items;
+  std::stringstream ss(spec);
+  std::string it;
+  while (std::getline(ss, it, ',')) {
+    auto c = it.find(':');
+    if (c == std::string::npos || c + 1 >= it.size()) throw std::runtime_error("halo spec item: " + it);
+    items.push_back({it.substr(0, c), it[c + 1]});
+  }
+  D(h)->halo_update(items);
+  API_CATCH
+}
+
+int gtfv3_stencil(void* h, const char* name, const char* fields_csv, const double* params, int np) {
+  API_TRY
+  std::vector<std::string> names;
+  std::stringstream ss(fields_csv ? fields_csv : "");
+  std::string it;
+  while (std::getline(ss, it, ',')) names.push_back(it);
+  std::vector<double> p(params, params + (np > 0 ? np : 0));
+  run_registered_stencil(*D(h), name, names, p);
+  API_CATCH
+}
+
+int gtfv3_set_vertical(void* h, const double* ak, const double* bk, int ks) {
+  API_TRY
+  D(h)->set_vertical(ak, bk, ks);
+  API_CATCH
+}
+
+int gtfv3_step(void* h, int nsteps) {
+  API_TRY
+  for (int n = 0; n < nsteps; ++n) D(h)->step();
+  API_CATCH
+}
+
+int gtfv3_sync(void* h) {
+  API_TRY
+  HIP_CHECK(hipStreamSynchronize(D(h)->st));
+  API_CATCH
+}
+
+void* gtfv3_stream(void* h) {
+  try {
+    return (void*)D(h)->st;
+  } catch (...) {
+    return nullptr;
+  }
+}
+
+int gtfv3_timers(void* h, char* buf, int len) {
+  API_TRY
+  std::string s;
+  for (auto& kv : D(h)->timers) s += kv.first + "=" + std::to_string(kv.second) + ";";
+  if (buf && len > 0) {
+    std::strncpy(buf, s.c_str(), (size_t)len - 1);
+    buf[len - 1] = 0;
+  }
+  API_CATCH
+}
+
+// ---------------- reference bridge symbols ----------------
+
+void geos_gtfv3_init_c(void* comm, int npx, int npy, int npz, int ntiles, int is, int ie, int js, int je, int isd,
+                       int ied, int jsd, int jed, float bdt, int nq_tot) {
+  try {
+    bridge_init(comm, npx, npy, npz, ntiles, is, ie, js, je, isd, ied, jsd, jed, bdt, nq_tot);
+  } catch (const std::exception& e) {
+    bridge_fatal(e.what());
+  }
+}
+
+void geos_gtfv3_run_c(void* comm, int npx, int npy, int npz, int ntiles, int is, int ie, int js, int je, int isd,
+                      int ied, int jsd, int jed, float bdt, int nq_tot, int ng, float ptop, int ks, int layout_1,
+                      int layout_2, int adiabatic, float* ak, float* bk, float* u, float* v, float* w, float* delz,
+                      float* pt, float* delp, float* q, float* ps, float* pe, float* pk, float* peln, float* pkz,
+                      float* phis, float* q_con, float* omga, float* ua, float* va, float* uc, float* vc,
+                      float* mfx, float* mfy, float* cx, float* cy, float* diss_est) {
+  try {
+    BridgeArgs<float> a{comm, npx, npy, npz, ntiles, is, ie, js, je, isd, ied, jsd, jed, bdt, nq_tot, ng, ptop, ks,
+                        layout_1, layout_2, adiabatic, ak, bk, u, v, w, delz, pt, delp, q, ps, pe, pk, peln, pkz,
+                        phis, q_con, omga, ua, va, uc, vc, mfx, mfy, cx, cy, diss_est};
+    bridge_run(a);
+  } catch (const std::exception& e) {
+    bridge_fatal(e.what());
+  }
+}
+
+void geos_gtfv3_run_f64_c(void* comm, int npx, int npy, int npz, int ntiles, int is, int ie, int js, int je, int isd,
+                          int ied, int jsd, int jed, float bdt, int nq_tot, int ng, float ptop, int ks, int layout_1,
+                          int layout_2, int adiabatic, double* ak, double* bk, double* u, double* v, double* w,
+                          double* delz, double* pt, double* delp, double* q, double* ps, double* pe, double* pk,
+                          double* peln, double* pkz, double* phis, double* q_con, double* omga, double* ua,
+                          double* va, double* uc, double* vc, double* mfx, double* mfy, double* cx, double* cy,
+                          double* diss_est) {
+  try {
+    BridgeArgs<double> a{comm, npx, npy, npz, ntiles, is, ie, js, je, isd, ied, jsd, jed, bdt, nq_tot, ng, ptop, ks,
+                         layout_1, layout_2, adiabatic, ak, bk, u, v, w, delz, pt, delp, q, ps, pe, pk, peln, pkz,
+                         phis, q_con, omga, ua, va, uc, vc, mfx, mfy, cx, cy, diss_est};
+    bridge_run(a);
+  } catch (const std::exception& e) {
+    bridge_fatal(e.what());
+  }
+}
+
+void geos_gtfv3_finalize_c(void) {
+  try {
+    bridge_finalize();
+  } catch (const std::exception& e) {
+    bridge_fatal(e.what());
+  }
+}
+
+}  // extern "C"

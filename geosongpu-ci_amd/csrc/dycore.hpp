@@ -1,0 +1,69 @@
+// dycore.hpp — process-global dycore context behind geos_gtfv3_{init,run,finalize}
+// (reference hook surface: templates/hook.py.jinja2:11-34; lifecycle of
+// init once, run once per dycore step, finalize).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "grid.hpp"
+#include "halo.hpp"
+#include "kernels.hpp"
+
+namespace gtfv3 {
+
+struct Field {
+  double* p = nullptr;
+  int nk = 0;
+  long elems() const;
+};
+
+class Dycore {
+ public:
+  Dycore(const Namelist& nl, int rank, int nranks, const void* nccl_id);
+  ~Dycore();
+  Dycore(const Dycore&) = delete;
+  Dycore& operator=(const Dycore&) = delete;
+
+  Namelist nl;
+  Decomp dc;
+  Dims d{};
+  std::unique_ptr<CubedSphere> cs;
+  HostMetrics hm;
+  std::vector<SubInfo> hsubs;
+  SubInfo* dsubs = nullptr;
+  double* dmet = nullptr;
+  double* dcornerw = nullptr;
+  HaloExchanger halo;
+  hipStream_t st = nullptr;
+  ncclComm_t comm = nullptr;
+  std::map<std::string, Field> fields;
+  std::vector<double> ak, bk;  // npz+1
+  int ks = 0;
+  std::map<std::string, double> timers;  // accumulated ms per phase (events)
+
+  Field& field(const std::string& name, int nk);  // get or create (zeroed)
+  Field* find(const std::string& name);
+  Ctx ctx() const;
+  long field_elems(int nk) const { return (long)d.nsub * nk * d.plane; }
+
+  // host <-> device copies of a whole named field in the padded device layout
+  void upload(const std::string& name, const double* host, int nk);
+  void download(const std::string& name, double* host);
+
+  // halo update of named fields; kinds: 'c' cell, 'b' corner, 'd' D-grid pair, 'C' C-grid pair, 'a' A-grid pair
+  void halo_update(const std::vector<std::pair<std::string, char>>& items);
+  // max-reduce across ranks (in place, device, n doubles)
+  void allreduce_max(double* dev, int n);
+
+  // algorithm blocks
+  void tracer_2d(int nq, double dt);
+  void set_vertical(const double* ak_, const double* bk_, int ks_);
+  void step();  // one fv_dynamics call on device-resident state
+};
+
+}  // namespace gtfv3

@@ -1,0 +1,263 @@
+// halo.hip — table construction (host) and halo gather / pack / unpack kernels.
+#include <algorithm>
+#include <stdexcept>
+
+#include "halo.hpp"
+#include "hip_util.hpp"
+
+namespace gtfv3 {
+
+namespace {
+
+inline void rot_dir(int rot, int dx, int dy, int& ox, int& oy) {
+  switch (rot & 3) {
+    case 0: ox = dx; oy = dy; break;
+    case 1: ox = -dy; oy = dx; break;
+    case 2: ox = -dx; oy = -dy; break;
+    default: ox = dy; oy = -dx; break;
+  }
+}
+
+// staggering of component c of halo kind k
+inline int comp_stagger(int kind, int c) {
+  switch (kind) {
+    case H_CELL: return CELL;
+    case H_CORNER: return CORNER;
+    case H_DGRID: return c == 0 ? XEDGE : YEDGE;   // u along x-edges, v along y-edges
+    case H_CGRID: return c == 0 ? YEDGE : XEDGE;   // uc normal to y-edges, vc to x-edges
+    default: return CELL;                           // A-grid pair
+  }
+}
+inline int ncomp(int kind) { return (kind == H_CELL || kind == H_CORNER) ? 1 : 2; }
+
+struct Src {
+  int rank, lsub, off, comp, sign;
+  bool zero;
+};
+
+}  // namespace
+
+HaloExchanger::~HaloExchanger() {
+  for (int k = 0; k < H_NKIND; ++k) {
+    if (d_local_[k]) (void)hipFree(d_local_[k]);
+    if (d_send_[k]) (void)hipFree(d_send_[k]);
+    if (d_recv_[k]) (void)hipFree(d_recv_[k]);
+  }
+  if (sendbuf_) (void)hipFree(sendbuf_);
+  if (recvbuf_) (void)hipFree(recvbuf_);
+}
+
+void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d, int max_nk,
+                          int max_fields, bool device) {
+  d_ = d;
+  rank_ = dc.rank;
+  nranks_ = dc.nranks;
+  const int nper = dc.nsub_per_rank();
+  const int nx = d.nx, ny = d.ny;
+
+  // resolve the source of one halo point of (global sub g, component c, staggering st)
+  auto resolve = [&](int g, int kind, int c, int i, int j) -> Src {
+    SubInfo si = dc.sub(g);
+    int st = comp_stagger(kind, c);
+    int x2 = 2 * (i + si.ioff) + ((st == CELL || st == XEDGE) ? 1 : 0);
+    int y2 = 2 * (j + si.joff) + ((st == CELL || st == YEDGE) ? 1 : 0);
+    Mapped m = cs.map(si.tile, x2, y2, false);
+    Src s{};
+    if (!m.valid) { s.zero = true; return s; }
+    // owning sub-domain in tile m.t
+    int found = -1, li = 0, lj = 0;
+    for (int py = 0; py < dc.ly && found < 0; ++py)
+      for (int px = 0; px < dc.lx && found < 0; ++px) {
+        int ioff = px * nx, joff = py * ny;
+        int ii = (m.x2 - (m.x2 & 1)) / 2 - ioff;
+        int jj = (m.y2 - (m.y2 & 1)) / 2 - joff;
+        int imax = (m.x2 & 1) ? nx - 1 : nx;
+        int jmax = (m.y2 & 1) ? ny - 1 : ny;
+        if (ii >= 0 && ii <= imax && jj >= 0 && jj <= jmax) {
+          found = m.t * dc.lx * dc.ly + py * dc.lx + px;
+          li = ii; lj = jj;
+        }
+      }
+    if (found < 0) throw std::runtime_error("halo: no owner sub-domain");
+    s.rank = dc.owner_rank(found);
+    s.lsub = found % nper;
+    s.off = (int)pidx(d, li, lj);
+    if (ncomp(kind) == 1) { s.comp = 0; s.sign = 1; }
+    else {
+      int dx = c == 0 ? 1 : 0, dy = c == 0 ? 0 : 1, ox, oy;
+      rot_dir(m.rot, dx, dy, ox, oy);
+      s.comp = ox != 0 ? 0 : 1;
+      s.sign = ox + oy;
+    }
+    s.zero = false;
+    return s;
+  };
+
+  for (int kind = 0; kind < H_NKIND; ++kind) {
+    h_local_[kind].clear();
+    std::vector<std::vector<PackEntry>> send(nranks_), recv(nranks_);
+    for (int q = 0; q < nranks_; ++q) {
+      for (int ls = 0; ls < nper; ++ls) {
+        int g = q * nper + ls;
+        for (int c = 0; c < ncomp(kind); ++c) {
+          int st = comp_stagger(kind, c);
+          int sx = (st == YEDGE || st == CORNER) ? 1 : 0;
+          int sy = (st == XEDGE || st == CORNER) ? 1 : 0;
+          for (int j = -NG; j <= ny - 1 + NG + sy; ++j)
+            for (int i = -NG; i <= nx - 1 + NG + sx; ++i) {
+              bool inside = i >= 0 && i <= nx - 1 + sx && j >= 0 && j <= ny - 1 + sy;
+              if (inside) continue;
+              if (q != rank_) {
+                // only needed when this rank is the owner of the source
+                Src s = resolve(g, kind, c, i, j);
+                if (!s.zero && s.rank == rank_) send[q].push_back({s.lsub, s.off, s.comp, s.sign, 0, 0});
+                continue;
+              }
+              Src s = resolve(g, kind, c, i, j);
+              int doff = (int)pidx(d, i, j);
+              if (s.zero) h_local_[kind].push_back({ls, doff, -1, 0, c, 0});
+              else if (s.rank == rank_)
+                h_local_[kind].push_back({ls, doff, s.lsub, s.off, c | (s.comp << 1), s.sign});
+              else recv[s.rank].push_back({ls, doff, c, 0, 0, 0});
+            }
+        }
+      }
+    }
+    // concatenate per peer
+    std::vector<PackEntry> hs, hr;
+    send_peer_start_[kind].assign(nranks_, 0); send_peer_count_[kind].assign(nranks_, 0);
+    recv_peer_start_[kind].assign(nranks_, 0); recv_peer_count_[kind].assign(nranks_, 0);
+    for (int p = 0; p < nranks_; ++p) {
+      send_peer_start_[kind][p] = (int)hs.size();
+      send_peer_count_[kind][p] = (int)send[p].size();
+      for (auto e : send[p]) { e.pstart = send_peer_start_[kind][p]; e.pcount = (int)send[p].size(); hs.push_back(e); }
+      recv_peer_start_[kind][p] = (int)hr.size();
+      recv_peer_count_[kind][p] = (int)recv[p].size();
+      for (auto e : recv[p]) { e.pstart = recv_peer_start_[kind][p]; e.pcount = (int)recv[p].size(); hr.push_back(e); }
+    }
+    n_local_[kind] = (int)h_local_[kind].size();
+    n_send_[kind] = (int)hs.size();
+    n_recv_[kind] = (int)hr.size();
+    if (!device) continue;
+    if (n_local_[kind]) {
+      HIP_CHECK(hipMalloc(&d_local_[kind], sizeof(HaloEntry) * n_local_[kind]));
+      HIP_CHECK(hipMemcpy(d_local_[kind], h_local_[kind].data(), sizeof(HaloEntry) * n_local_[kind], hipMemcpyHostToDevice));
+    }
+    if (n_send_[kind]) {
+      HIP_CHECK(hipMalloc(&d_send_[kind], sizeof(PackEntry) * n_send_[kind]));
+      HIP_CHECK(hipMemcpy(d_send_[kind], hs.data(), sizeof(PackEntry) * n_send_[kind], hipMemcpyHostToDevice));
+    }
+    if (n_recv_[kind]) {
+      HIP_CHECK(hipMalloc(&d_recv_[kind], sizeof(PackEntry) * n_recv_[kind]));
+      HIP_CHECK(hipMemcpy(d_recv_[kind], hr.data(), sizeof(PackEntry) * n_recv_[kind], hipMemcpyHostToDevice));
+    }
+  }
+  if (!device) return;
+  size_t maxe = 0;
+  for (int k = 0; k < H_NKIND; ++k) maxe = std::max<size_t>(maxe, std::max(n_send_[k], n_recv_[k]));
+  buf_elems_ = maxe * (size_t)max_nk * max_fields;
+  if (buf_elems_) {
+    HIP_CHECK(hipMalloc(&sendbuf_, sizeof(double) * buf_elems_));
+    HIP_CHECK(hipMalloc(&recvbuf_, sizeof(double) * buf_elems_));
+  }
+}
+
+namespace {
+
+__global__ void halo_local_kernel(const HaloEntry* __restrict__ tab, int n, int nk, long plane,
+                                  double* __restrict__ p0, double* __restrict__ p1) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  int k = blockIdx.y;
+  if (e >= n) return;
+  HaloEntry h = tab[e];
+  double v = 0.0;
+  if (h.src_sub >= 0) {
+    const double* src = (h.comp & 2) ? p1 : p0;
+    v = h.sign * src[((long)h.src_sub * nk + k) * plane + h.src_off];
+  }
+  double* dst = (h.comp & 1) ? p1 : p0;
+  dst[((long)h.dst_sub * nk + k) * plane + h.dst_off] = v;
+}
+
+__global__ void halo_pack_kernel(const PackEntry* __restrict__ tab, int n, int nk, long plane,
+                                 const double* __restrict__ p0, const double* __restrict__ p1,
+                                 double* __restrict__ buf) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  int k = blockIdx.y;
+  if (e >= n) return;
+  PackEntry h = tab[e];
+  const double* src = h.comp ? p1 : p0;
+  buf[(long)h.pstart * nk + (long)k * h.pcount + (e - h.pstart)] =
+      h.sign * src[((long)h.sub * nk + k) * plane + h.off];
+}
+
+__global__ void halo_unpack_kernel(const PackEntry* __restrict__ tab, int n, int nk, long plane,
+                                   double* __restrict__ p0, double* __restrict__ p1,
+                                   const double* __restrict__ buf) {
+  int e = blockIdx.x * blockDim.x + threadIdx.x;
+  int k = blockIdx.y;
+  if (e >= n) return;
+  PackEntry h = tab[e];
+  double* dst = h.comp ? p1 : p0;
+  dst[((long)h.sub * nk + k) * plane + h.off] = buf[(long)h.pstart * nk + (long)k * h.pcount + (e - h.pstart)];
+}
+
+}  // namespace
+
+void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream) {
+  // remote part first (pack + post), then local gather while messages fly
+  bool remote = nranks_ > 1;
+  size_t off = 0;
+  std::vector<size_t> foff(nf);
+  if (remote) {
+    for (int f = 0; f < nf; ++f) {
+      const HaloField& F = fields[f];
+      foff[f] = off;
+      int n = n_send_[F.kind];
+      if (n) {
+        hipLaunchKernelGGL(halo_pack_kernel, dim3(cdiv(n, 256), F.nk), dim3(256), 0, stream,
+                           d_send_[F.kind], n, F.nk, d_.plane, F.p[0], F.p[1] ? F.p[1] : F.p[0],
+                           sendbuf_ + off);
+        HIP_LAUNCH_CHECK();
+      }
+      off += (size_t)std::max(n_send_[F.kind], n_recv_[F.kind]) * F.nk;
+    }
+    if (off > buf_elems_) throw std::runtime_error("halo: exchange buffer too small");
+    if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
+    for (int f = 0; f < nf; ++f) {
+      const HaloField& F = fields[f];
+      for (int p = 0; p < nranks_; ++p) {
+        int ns = send_peer_count_[F.kind][p], nr = recv_peer_count_[F.kind][p];
+        if (ns)
+          if (ncclSend(sendbuf_ + foff[f] + (size_t)send_peer_start_[F.kind][p] * F.nk, (size_t)ns * F.nk,
+                       ncclDouble, p, comm_, stream) != ncclSuccess)
+            throw std::runtime_error("ncclSend failed");
+        if (nr)
+          if (ncclRecv(recvbuf_ + foff[f] + (size_t)recv_peer_start_[F.kind][p] * F.nk, (size_t)nr * F.nk,
+                       ncclDouble, p, comm_, stream) != ncclSuccess)
+            throw std::runtime_error("ncclRecv failed");
+      }
+    }
+    if (ncclGroupEnd() != ncclSuccess) throw std::runtime_error("ncclGroupEnd failed");
+  }
+  for (int f = 0; f < nf; ++f) {
+    const HaloField& F = fields[f];
+    int n = n_local_[F.kind];
+    if (!n) continue;
+    hipLaunchKernelGGL(halo_local_kernel, dim3(cdiv(n, 256), F.nk), dim3(256), 0, stream, d_local_[F.kind], n,
+                       F.nk, d_.plane, F.p[0], F.p[1] ? F.p[1] : F.p[0]);
+    HIP_LAUNCH_CHECK();
+  }
+  if (remote) {
+    for (int f = 0; f < nf; ++f) {
+      const HaloField& F = fields[f];
+      int n = n_recv_[F.kind];
+      if (!n) continue;
+      hipLaunchKernelGGL(halo_unpack_kernel, dim3(cdiv(n, 256), F.nk), dim3(256), 0, stream, d_recv_[F.kind], n,
+                         F.nk, d_.plane, F.p[0], F.p[1] ? F.p[1] : F.p[0], recvbuf_ + foff[f]);
+      HIP_LAUNCH_CHECK();
+    }
+  }
+}
+
+}  // namespace gtfv3

@@ -1,0 +1,69 @@
+// halo.hpp — cubed-sphere halo update (replaces the NDSL/mpp halo updater the
+// reference's external dycore uses over CUDA-aware MPI; the only comm touchpoint
+// in the reference is the communicator hand-off, py_ftn_interface/base.py:72-96).
+//
+// Every halo point of every local sub-domain is resolved ONCE on the host to
+// (owner rank, owner sub-domain, plane offset, component, sign): vector fields
+// across rotated cube edges swap u<->v and flip sign by the lattice rotation
+// between the two tiles.  Cube-corner regions (three tiles meet) are zero-filled;
+// the stencils fill them on the fly (copy_corners / fill_4corners).
+//  * same-rank sources: one gather kernel (tile edges on one GPU are device copies)
+//  * other ranks: pack -> ncclSend/ncclRecv grouped per neighbour -> unpack,
+//    point-to-point over xGMI (never a ring collective).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <vector>
+
+#include "grid.hpp"
+
+namespace gtfv3 {
+
+struct HaloEntry {
+  int dst_sub, dst_off, src_sub, src_off;  // src_sub < 0: zero-fill
+  int comp;                                 // bit0: dst component, bit1: src component
+  int sign;
+};
+struct PackEntry {
+  int sub, off, comp, sign;  // sign 0 unused for unpack
+  int pstart, pcount;        // peer segment start/length (entries)
+};
+
+struct HaloField {
+  double* p[2];  // component pointers (p[1] == nullptr for scalars)
+  int nk;
+  int kind;      // HaloKind
+};
+
+class HaloExchanger {
+ public:
+  HaloExchanger() = default;
+  ~HaloExchanger();
+  void build(const CubedSphere& cs, const Decomp& dc, const Dims& d, int max_nk, int max_fields, bool device = true);
+  void set_comm(ncclComm_t comm) { comm_ = comm; }
+  // fill halos of all listed fields (enqueued on `stream`)
+  void exchange(const HaloField* fields, int nf, hipStream_t stream);
+  // host copies of tables for tests
+  const std::vector<HaloEntry>& local_table(int kind) const { return h_local_[kind]; }
+  int nranks() const { return nranks_; }
+
+ private:
+  Dims d_{};
+  int rank_ = 0, nranks_ = 1;
+  ncclComm_t comm_ = nullptr;
+  std::vector<HaloEntry> h_local_[H_NKIND];
+  HaloEntry* d_local_[H_NKIND] = {};
+  int n_local_[H_NKIND] = {};
+  // remote: per kind, concatenated over peers
+  std::vector<int> send_peer_start_[H_NKIND], send_peer_count_[H_NKIND];
+  std::vector<int> recv_peer_start_[H_NKIND], recv_peer_count_[H_NKIND];
+  PackEntry* d_send_[H_NKIND] = {};
+  PackEntry* d_recv_[H_NKIND] = {};
+  int n_send_[H_NKIND] = {}, n_recv_[H_NKIND] = {};
+  double* sendbuf_ = nullptr;
+  double* recvbuf_ = nullptr;
+  size_t buf_elems_ = 0;
+};
+
+}  // namespace gtfv3

@@ -1,0 +1,112 @@
+// stencil_common.hpp — device helpers shared by the FV3 stencil kernels.
+//
+// Index conventions (0-based, local to a sub-domain; global = local + ioff/joff):
+//   cell (i,j)      i in [0,nx)         centre of cell i
+//   x-edge (i,j)    edge from corner (i,j) to (i+1,j)   (D-grid u, C-grid vc, fy, yfx, cry)
+//   y-edge (i,j)    edge from corner (i,j) to (i,j+1)   (D-grid v, C-grid uc, fx, xfx, crx)
+//   corner (i,j)    grid point (i,j)
+// FV3 Fortran index f (is=1) maps to global 0-based g = f-1; "npx" as an index is g = N.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "grid.hpp"
+#include "hip_util.hpp"
+
+namespace gtfv3 {
+
+// metric plane of sub-domain s
+__device__ __forceinline__ const double* met(const double* __restrict__ M, const Dims& d, int metric, int s) {
+  return M + ((long)metric * d.nsub + s) * d.plane;
+}
+
+// Block shape for plane-parallel stencils: one wavefront row of 64 columns x 4 rows.
+constexpr int BX = 64, BY = 4;
+
+struct Launch2D {
+  int i0, j0;  // first point covered
+  int ni, nj;  // extent
+};
+
+__device__ __forceinline__ bool thread_point(const Launch2D& L, int& i, int& j) {
+  i = L.i0 + (int)(blockIdx.x * BX + threadIdx.x);
+  j = L.j0 + (int)(blockIdx.y * BY + threadIdx.y);
+  return i < L.i0 + L.ni && j < L.j0 + L.nj;
+}
+
+// FV3 copy_corners source cell (global indices) for a cube-corner halo cell,
+// dir = 1 (x sweep) or 2 (y sweep).  Restated from fv_grid_utils copy_corners;
+// fill_4corners / fill2_4corners are the same map restricted to the first ring.
+__device__ __forceinline__ void corner_src(int I, int J, int N, int dir, int& Is, int& Js) {
+  if (dir == 1) {
+    if (I < 0 && J < 0) { Is = J; Js = -I - 1; }
+    else if (I >= N && J < 0) { Is = N - J - 1; Js = I - N; }
+    else if (I >= N && J >= N) { Is = J; Js = 2 * N - I - 1; }
+    else { Is = N - J - 1; Js = N + I; }
+  } else {
+    if (I < 0 && J < 0) { Is = -J - 1; Js = I; }
+    else if (I >= N && J < 0) { Is = N + J; Js = N - I - 1; }
+    else if (I >= N && J >= N) { Is = 2 * N - J - 1; Js = I; }
+    else { Is = J - N; Js = N - I - 1; }
+  }
+}
+
+// plane offset of cell (i,j) after the copy_corners remap for sweep `dir`
+__device__ __forceinline__ long cc_off(const Dims& d, const SubInfo& s, int i, int j, int dir) {
+  int I = i + s.ioff, J = j + s.joff, N = s.N;
+  if ((I < 0 || I >= N) && (J < 0 || J >= N)) {
+    int Is, Js;
+    corner_src(I, J, N, dir, Is, Js);
+    i = Is - s.ioff;
+    j = Js - s.joff;
+  }
+  return pidx(d, i, j);
+}
+
+// PPM constants (FV3 tp_core)
+constexpr double P1 = 7.0 / 12.0, P2 = -1.0 / 12.0;
+constexpr double C1 = -2.0 / 14.0, C2 = 11.0 / 14.0, C3 = 5.0 / 14.0;
+
+// 4th-order interface value al at global interface g (between cells g-1, g),
+// with the cubed-sphere tile-edge treatment (grid_type < 3):
+//   q[0..3] = q(g-2), q(g-1), q(g), q(g+1);  dx[0..3] = dxa at the same cells.
+__device__ __forceinline__ double ppm_al(int g, int N, const double* q, const double* dx) {
+  if (g == -1 || g == N - 1) return C1 * q[0] + C2 * q[1] + C3 * q[2];
+  if (g == 1 || g == N + 1) return C3 * q[1] + C2 * q[2] + C1 * q[3];
+  if (g == 0 || g == N)
+    return 0.5 * (((2.0 * dx[1] + dx[0]) * q[1] - dx[1] * q[0]) / (dx[0] + dx[1]) +
+                  ((2.0 * dx[2] + dx[3]) * q[2] - dx[2] * q[3]) / (dx[2] + dx[3]));
+  return P1 * (q[1] + q[2]) + P2 * (q[0] + q[3]);
+}
+
+// PPM flux through interface g for hord 5 / 6 (FV3 xppm/yppm, iord < 8 branch).
+//   q[0..5] = q(g-3) .. q(g+2); dx[0..5] = dxa at those cells; c = Courant number.
+template <int ORD>
+__device__ __forceinline__ double ppm_flux(int g, int N, const double* q, const double* dx, double c) {
+  double alm = ppm_al(g - 1, N, q + 0, dx + 0);
+  double al0 = ppm_al(g, N, q + 1, dx + 1);
+  double alp = ppm_al(g + 1, N, q + 2, dx + 2);
+  double blm = alm - q[2], brm = al0 - q[2], b0m = blm + brm;
+  double bl0 = al0 - q[3], br0 = alp - q[3], b00 = bl0 + br0;
+  bool sm, s0;
+  if (ORD == 5) {
+    sm = blm * brm < 0.0;
+    s0 = bl0 * br0 < 0.0;
+  } else {
+    sm = 3.0 * fabs(b0m) < fabs(blm - brm);
+    s0 = 3.0 * fabs(b00) < fabs(bl0 - br0);
+  }
+  bool smooth = sm || s0;
+  if (c > 0.0) {
+    double fx1 = (1.0 - c) * (brm - c * b0m);
+    return q[2] + (smooth ? fx1 : 0.0);
+  } else {
+    double fx1 = (1.0 + c) * (bl0 + c * b00);
+    return q[3] + (smooth ? fx1 : 0.0);
+  }
+}
+
+__device__ __forceinline__ double ppm_flux_ord(int ord, int g, int N, const double* q, const double* dx, double c) {
+  return ord == 5 ? ppm_flux<5>(g, N, q, dx, c) : ppm_flux<6>(g, N, q, dx, c);
+}
+
+}  // namespace gtfv3

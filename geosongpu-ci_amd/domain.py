@@ -1,0 +1,148 @@
+"""Python handle on a device-resident dycore domain (libgeos_gtfv3_interface.so).
+
+Arrays crossing this boundary use the HBM layout of DESIGN.md, fp64:
+    field[s, k, j + NG, i + NG]      shape (nsub, nk, nj, pitch)
+with s the local sub-domain, i,j local indices (compute cells 0..nx-1 / 0..ny-1,
+halo down to -NG), staggered fields sharing the same padded plane.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import GTFV3Error, check, dptr, lib
+
+NG = 3
+
+DEFAULT_CONFIG = dict(
+    npx=49, npz=72, nq=4, layout_x=1, layout_y=1, dt=900.0, k_split=1, n_split=6,
+    hord_mt=6, hord_vt=6, hord_tm=6, hord_dp=6, hord_tr=6,
+    kord_mt=9, kord_wz=9, kord_tr=9, kord_tm=-9,
+    dddmp=0.2, d2_bg=0.0, p_fac=0.05, fill=1, adiabatic=0, ptop=1.0,
+)
+
+
+def config_string(cfg: dict) -> bytes:
+    return ";".join(f"{k}={v}" for k, v in cfg.items()).encode()
+
+
+class Domain:
+    def __init__(self, rank=0, nranks=1, nccl_id: bytes = None, **cfg):
+        self.cfg = dict(DEFAULT_CONFIG)
+        self.cfg.update(cfg)
+        L = lib()
+        idp = None
+        if nccl_id is not None:
+            self._id = ctypes.create_string_buffer(bytes(nccl_id), 128)
+            idp = ctypes.cast(self._id, ctypes.c_void_p)
+        self.h = L.gtfv3_create(config_string(self.cfg), rank, nranks, idp)
+        if not self.h:
+            from ._lib import last_error
+            raise GTFV3Error(last_error())
+        out = (ctypes.c_int * 10)()
+        check(L.gtfv3_dims(self.h, out))
+        (self.nx, self.ny, self.pitch, self.nj, self.nsub, self.npz, self.N,
+         self.layout_x, self.layout_y, self.nq) = list(out)
+        self.rank, self.nranks = rank, nranks
+        self.subs = []
+        for s in range(self.nsub):
+            o = (ctypes.c_int * 8)()
+            check(L.gtfv3_sub_info(self.h, s, o))
+            self.subs.append(dict(tile=o[0], ioff=o[1], joff=o[2], N=o[3], flags=o[4], gid=o[5]))
+
+    # ---- lifecycle ----
+    def close(self):
+        if getattr(self, "h", None):
+            lib().gtfv3_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # ---- shapes ----
+    def shape(self, nk):
+        return (self.nsub, nk, self.nj, self.pitch)
+
+    def zeros(self, nk):
+        return np.zeros(self.shape(nk))
+
+    # ---- grid ----
+    def metric(self, name):
+        out = np.zeros((self.nsub, self.nj, self.pitch))
+        check(lib().gtfv3_get_metric(self.h, name.encode(), dptr(out)))
+        return out
+
+    def corner_xyz(self):
+        H = NG + 1
+        out = np.zeros((self.nsub, self.ny + 2 * H + 1, self.nx + 2 * H + 1, 3))
+        check(lib().gtfv3_get_xyz(self.h, dptr(out)))
+        return out
+
+    def scalars(self):
+        out = np.zeros(2 + 12 * self.nsub)
+        check(lib().gtfv3_get_scalars(self.h, dptr(out)))
+        return dict(da_min=out[0], da_min_c=out[1], corner_w=out[2:].reshape(self.nsub, 4, 3))
+
+    # ---- fields ----
+    def create(self, name, nk):
+        check(lib().gtfv3_field_create(self.h, name.encode(), nk))
+
+    def nk_of(self, name):
+        return lib().gtfv3_field_nk(self.h, name.encode())
+
+    def upload(self, name, arr):
+        arr = np.ascontiguousarray(arr, dtype=np.float64)
+        if arr.ndim != 4 or arr.shape[0] != self.nsub or arr.shape[2:] != (self.nj, self.pitch):
+            raise ValueError(f"{name}: array shape {arr.shape} is not (nsub, nk, nj, pitch)")
+        check(lib().gtfv3_field_upload(self.h, name.encode(), arr.shape[1], dptr(arr)))
+
+    def download(self, name):
+        nk = self.nk_of(name)
+        if nk <= 0:
+            raise GTFV3Error(f"no field {name}")
+        out = np.zeros(self.shape(nk))
+        check(lib().gtfv3_field_download(self.h, name.encode(), dptr(out)))
+        return out
+
+    def device_ptr(self, name):
+        return lib().gtfv3_field_ptr(self.h, name.encode())
+
+    # ---- operations ----
+    def halo_update(self, spec: str):
+        check(lib().gtfv3_halo_update(self.h, spec.encode()))
+
+    def stencil(self, name, fields, params=()):
+        p = np.ascontiguousarray(params, dtype=np.float64) if len(params) else np.zeros(1)
+        check(lib().gtfv3_stencil(self.h, name.encode(), ",".join(fields).encode(), dptr(p), len(params)))
+
+    def set_vertical(self, ak, bk, ks):
+        ak = np.ascontiguousarray(ak, dtype=np.float64)
+        bk = np.ascontiguousarray(bk, dtype=np.float64)
+        check(lib().gtfv3_set_vertical(self.h, dptr(ak), dptr(bk), int(ks)))
+
+    def step(self, n=1):
+        check(lib().gtfv3_step(self.h, n))
+
+    def sync(self):
+        check(lib().gtfv3_sync(self.h))
+
+    def stream(self):
+        return lib().gtfv3_stream(self.h)
+
+    def timers(self):
+        buf = ctypes.create_string_buffer(8192)
+        check(lib().gtfv3_timers(self.h, buf, 8192))
+        out = {}
+        for item in buf.value.decode().split(";"):
+            if "=" in item:
+                k, v = item.split("=")
+                out[k] = float(v)
+        return out
+
+
+def unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(128)
+    check(lib().gtfv3_get_unique_id(ctypes.cast(buf, ctypes.c_void_p)))
+    return buf.raw

@@ -1,0 +1,67 @@
+/* gtfv3_device.h — device-resident API of libgeos_gtfv3_interface.so.
+ *
+ * Used by the Python hook (geosongpu-ci_amd/hook.py, mirror of
+ * templates/hook.py.jinja2:11-34), the NDSL-style stencil surface
+ * (geosongpu-ci_amd/stencils.py, call shape of dsl_patterns/Do__get_top_of_the_column.py:28-55)
+ * and bench.py.  All functions return 0 on success and -1 on error
+ * (message: geos_gtfv3_last_error).  Fields live in HBM in the padded
+ * layout [sub][level][j][i] described in DESIGN.md; host buffers passed to
+ * upload/download use that same layout, fp64.
+ */
+#ifndef GTFV3_DEVICE_H
+#define GTFV3_DEVICE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* config: "key=value;..." (npx, npz, nq, layout_x, layout_y, dt, n_split, k_split,
+ * hord_*, kord_*, dddmp, d2_bg, p_fac, fill, adiabatic, ptop).  nccl_id: 128-byte
+ * ncclUniqueId shared by all ranks (NULL when nranks == 1). */
+void* gtfv3_create(const char* config, int rank, int nranks, const void* nccl_id);
+void gtfv3_destroy(void* h);
+int gtfv3_get_unique_id(void* out128);
+
+/* out[0..9] = nx, ny, pitch, nj, nsub, npz, N, layout_x, layout_y, nq */
+int gtfv3_dims(void* h, int* out);
+/* out[0..7] per local sub-domain s: tile, ioff, joff, N, flags, gid */
+int gtfv3_sub_info(void* h, int s, int* out);
+
+int gtfv3_field_create(void* h, const char* name, int nk);
+int gtfv3_field_nk(void* h, const char* name);
+int gtfv3_field_upload(void* h, const char* name, int nk, const double* host);
+int gtfv3_field_download(void* h, const char* name, double* host);
+/* raw device pointer of a field (for zero-copy interop), NULL if missing */
+void* gtfv3_field_ptr(void* h, const char* name);
+
+/* metric plane(s) [nsub][plane] by name (see grid.cpp kMetricNames) */
+int gtfv3_get_metric(void* h, const char* name, double* out);
+/* corner points xyz [nsub][ny+2*NG+3][nx+2*NG+3][3] and scalars da_min, da_min_c */
+int gtfv3_get_xyz(void* h, double* out);
+int gtfv3_get_scalars(void* h, double* out);
+
+/* host copy of the same-rank halo table of a kind (0 cell, 1 corner, 2 D-grid, 3 C-grid,
+ * 4 A-grid): 6 ints per entry {dst_sub, dst_off, src_sub, src_off, comp, sign}; returns the
+ * entry count (writes only when cap >= count). */
+int gtfv3_halo_table(void* h, int kind, int* out, int cap);
+
+/* halo update, spec "name:kind,..." kind c=cell b=corner d=D-grid pair C=C-grid pair a=A-grid pair
+ * (a pair lists x then y component, e.g. "u:d,v:d") */
+int gtfv3_halo_update(void* h, const char* spec);
+
+/* run one named stencil on named fields: NDSL-style `stencil(*fields, params)` */
+int gtfv3_stencil(void* h, const char* name, const char* fields_csv, const double* params, int nparams);
+
+int gtfv3_set_vertical(void* h, const double* ak, const double* bk, int ks);
+/* nsteps fv_dynamics calls on the device-resident state */
+int gtfv3_step(void* h, int nsteps);
+int gtfv3_sync(void* h);
+/* hipStream_t of the dycore */
+void* gtfv3_stream(void* h);
+/* accumulated per-phase timers (ms), "name=value;..." into buf */
+int gtfv3_timers(void* h, char* buf, int len);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,51 @@
+"""The C-ABI library loads and exports every symbol include/*.h declares (CPU)."""
+import ctypes
+import os
+import re
+
+from conftest import ROOT
+
+
+def _declared():
+    names = set()
+    for h in ("geos_gtfv3_interface.h", "gtfv3_device.h"):
+        txt = open(os.path.join(ROOT, "include", h)).read()
+        txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+        for m in re.finditer(r"^\s*(?:void\s*\*?|int)\s+(\w+)\s*\(", txt, flags=re.M):
+            names.add(m.group(1))
+    return names
+
+
+def test_library_exports_all_declared_symbols(pkg):
+    lib = ctypes.CDLL(pkg.LIB_PATH)
+    declared = _declared()
+    assert {"geos_gtfv3_init_c", "geos_gtfv3_run_c", "geos_gtfv3_finalize_c"} <= declared
+    for name in declared:
+        assert hasattr(lib, name), name
+    assert declared == set(pkg.BRIDGE_SYMBOLS) | set(pkg.DEVICE_SYMBOLS)
+
+
+def test_reference_signature_order():
+    """Argument order of geos_gtfv3_run_c == example_def_dycore.yaml:21-70 (inputs, then inouts)."""
+    yaml_order = ["comm", "npx", "npy", "npz", "ntiles", "is", "ie", "js", "je", "isd", "ied", "jsd", "jed", "bdt",
+                  "nq_tot", "ng", "ptop", "ks", "layout_1", "layout_2", "adiabatic", "ak", "bk", "u", "v", "w",
+                  "delz", "pt", "delp", "q", "ps", "pe", "pk", "peln", "pkz", "phis", "q_con", "omga", "ua", "va",
+                  "uc", "vc", "mfx", "mfy", "cx", "cy", "diss_est"]
+    txt = open(os.path.join(ROOT, "include", "geos_gtfv3_interface.h")).read()
+    m = re.search(r"void geos_gtfv3_run_c\((.*?)\);", txt, flags=re.S)
+    args = [a.strip().split()[-1].lstrip("*") for a in m.group(1).split(",")]
+    assert args == yaml_order
+    types = [a.strip().rsplit(" ", 1)[0].replace(" ", "") for a in m.group(1).split(",")]
+    # argument.py:54-86 type map: MPI->void*, int->int, float->float, array_float->float*
+    assert types[0] == "void*"
+    assert types[13] == "float" and types[16] == "float"
+    assert all(t == "float*" for t in types[21:])
+
+
+def test_last_error_channel(pkg):
+    lib = pkg.lib()
+    h = lib.gtfv3_create(b"npx=13;bogus_key=1", 0, 1, None)
+    assert not h
+    buf = ctypes.create_string_buffer(256)
+    n = lib.geos_gtfv3_last_error(buf, 256)
+    assert n > 0 and b"bogus_key" in buf.value

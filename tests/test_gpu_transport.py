@@ -1,0 +1,117 @@
+"""GPU parity: halo exchange, fv_tp_2d and tracer_2d_1l HIP kernels vs the oracle.
+
+Bar: fp64, max relative difference <= 1e-12 (SURVEY.md §8c adopted tolerance;
+kernels are built with -ffp-contract=off and keep the Fortran operation order,
+so most points are bit-identical)."""
+import numpy as np
+import pytest
+
+from conftest import metrics_of, rng
+from oracle import NG
+from oracle import halo as ohalo
+from oracle import tp_core
+
+pytestmark = pytest.mark.gpu
+RTOL = 1e-12
+
+
+def relerr(a, b):
+    scale = max(np.abs(b).max(), 1e-300)
+    return np.abs(a - b).max() / scale
+
+
+def make_dom(pkg, npx=13, npz=5, nq=1, lx=1, ly=1):
+    return pkg.Domain(npx=npx, npz=npz, nq=nq, layout_x=lx, layout_y=ly)
+
+
+@pytest.mark.parametrize("layout", [(1, 1), (2, 2)])
+def test_halo_exchange_gpu(pkg, require_gpu, layout):
+    d = make_dom(pkg, 13, 4, 1, *layout)
+    lay = ohalo.Layout(d.N, *layout)
+    r = rng(3)
+    for kind, spec in (("cell", "c"), ("corner", "b")):
+        a = r.standard_normal(d.shape(4))
+        d.upload("h_a", a)
+        d.halo_update(f"h_a:{spec}")
+        got = d.download("h_a")
+        ohalo.fill_scalar(a, lay, kind)
+        np.testing.assert_array_equal(got, a)
+    for vk, spec in (("dgrid", "d"), ("cgrid", "C"), ("agrid", "a")):
+        u = r.standard_normal(d.shape(4))
+        v = r.standard_normal(d.shape(4))
+        d.upload("h_u", u)
+        d.upload("h_v", v)
+        d.halo_update(f"h_u:{spec},h_v:{spec}")
+        gu, gv = d.download("h_u"), d.download("h_v")
+        ohalo.fill_vector(u, v, lay, vk)
+        np.testing.assert_array_equal(gu, u)
+        np.testing.assert_array_equal(gv, v)
+
+
+def tp_inputs(d, npz, r):
+    area = d.metric("area")[:, None]
+    sh = d.shape(npz)
+    q = 1.0 + 0.3 * r.standard_normal(sh)
+    crx = r.uniform(-0.45, 0.45, sh)
+    cry = r.uniform(-0.45, 0.45, sh)
+    xfx = 0.3 * r.uniform(-1, 1, sh) * area
+    yfx = 0.3 * r.uniform(-1, 1, sh) * area
+    ra_x = area + xfx - np.roll(xfx, -1, axis=-1)
+    ra_y = area + yfx - np.roll(yfx, -1, axis=-2)
+    mfx = 800.0 * xfx
+    mfy = 800.0 * yfx
+    return dict(q=q, crx=crx, cry=cry, xfx=xfx, yfx=yfx, ra_x=ra_x, ra_y=ra_y, mfx=mfx, mfy=mfy)
+
+
+@pytest.mark.parametrize("ord_", [5, 6])
+@pytest.mark.parametrize("layout", [(1, 1), (2, 2)])
+def test_fv_tp_2d_parity(pkg, require_gpu, ord_, layout):
+    npz = 3
+    d = make_dom(pkg, 13, npz, 1, *layout)
+    r = rng(11)
+    inp = tp_inputs(d, npz, r)
+    for k, v in inp.items():
+        d.upload("t_" + k, v)
+    d.stencil("fv_tp_2d", ["t_q", "t_crx", "t_cry", "t_xfx", "t_yfx", "t_ra_x", "t_ra_y", "t_mfx", "t_mfy",
+                           "t_fx", "t_fy"], [ord_, 1])
+    gfx, gfy = d.download("t_fx"), d.download("t_fy")
+    ms = metrics_of(d)
+    nx, ny = d.nx, d.ny
+    for s in range(d.nsub):
+        fx, fy = tp_core.fv_tp_2d(inp["q"][s], inp["crx"][s], inp["cry"][s], inp["xfx"][s], inp["yfx"][s],
+                                  inp["ra_x"][s], inp["ra_y"][s], d.subs[s], ms[s], nx, ny, ord_,
+                                  inp["mfx"][s], inp["mfy"][s])
+        ax = gfx[s][:, NG:NG + ny, NG:NG + nx + 1]
+        bx = fx[:, NG:NG + ny, NG:NG + nx + 1]
+        ay = gfy[s][:, NG:NG + ny + 1, NG:NG + nx]
+        by = fy[:, NG:NG + ny + 1, NG:NG + nx]
+        assert relerr(ax, bx) <= RTOL, (s, relerr(ax, bx))
+        assert relerr(ay, by) <= RTOL, (s, relerr(ay, by))
+
+
+@pytest.mark.parametrize("cmax_amp", [0.35, 1.2])
+def test_tracer_2d_1l_parity(pkg, require_gpu, cmax_amp):
+    npz, nq = 6, 3
+    d = make_dom(pkg, 13, npz, nq)
+    lay = ohalo.Layout(d.N)
+    r = rng(5)
+    area = d.metric("area")[:, None]
+    sh = d.shape(npz)
+    q = np.abs(1e-3 * (1.0 + 0.5 * r.standard_normal(d.shape(nq * npz))))
+    dp1 = 500.0 + 100.0 * r.random(sh)
+    cx = r.uniform(-cmax_amp, cmax_amp, sh)
+    cy = r.uniform(-cmax_amp, cmax_amp, sh)
+    mfx = 0.02 * r.uniform(-1, 1, sh) * area * 500.0
+    mfy = 0.02 * r.uniform(-1, 1, sh) * area * 500.0
+    for name, v in (("q", q), ("dp1", dp1), ("cx", cx), ("cy", cy), ("mfx", mfx), ("mfy", mfy)):
+        d.upload(name, v)
+    d.stencil("tracer_2d_1l", [], [nq])
+    got = d.download("q")
+    ms = metrics_of(d)
+    ref, nsplt = tp_core.tracer_2d_1l(q, dp1, mfx, mfy, cx, cy, d.subs, ms, d.nx, d.ny, npz, nq, 6,
+                                      lambda a: ohalo.fill_scalar(a, lay, "cell"))
+    if cmax_amp > 1:
+        assert nsplt.max() >= 2
+    a = got[:, :, NG:NG + d.ny, NG:NG + d.nx]
+    b = ref[:, :, NG:NG + d.ny, NG:NG + d.nx]
+    assert relerr(a, b) <= RTOL, relerr(a, b)
