@@ -1,0 +1,31 @@
+// kernels_sw.hpp — launchers of the shallow-water core (sw.hip) and the
+// non-hydrostatic / vertical pieces (nh.hip, remap.hip).
+#pragma once
+#include "kernels.hpp"
+
+namespace gtfv3 {
+
+struct CswArgs {
+  int npz;
+  double dt2;
+  const double *delp, *pt, *w, *u, *v;
+  double *uc, *vc, *ua, *va, *ut, *vt;  // outputs (ut, vt: dt2 * area fluxes)
+  double *delpc, *ptc, *wc;
+  double *utmp, *vtmp, *ke, *vort;  // scratch
+};
+void c_sw(const Ctx& c, const CswArgs& a);
+
+struct DswArgs {
+  int npz;
+  double dt, dddmp, d2_bg;
+  int hord_mt, hord_vt, hord_tm, hord_dp;
+  double *delp, *pt, *w, *u, *v;      // updated in place (u, v left multiplied by dx, dy)
+  const double *uc, *vc, *ua, *va;
+  double *crx, *cry, *xfx, *yfx;      // per level, saved for update_dz_d
+  double *cx, *cy, *mfx, *mfy;        // accumulated
+  double *ut, *vt, *ra_x, *ra_y, *fx, *fy, *gwx, *gwy, *gtx, *gty, *ke, *vort;  // scratch
+  double *tp_fx2, *tp_fy2, *tp_qi, *tp_qj;
+};
+void d_sw(const Ctx& c, const DswArgs& a);
+
+}  // namespace gtfv3

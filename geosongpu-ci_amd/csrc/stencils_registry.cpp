@@ -7,6 +7,7 @@
 
 #include "dycore.hpp"
 #include "kernels.hpp"
+#include "kernels_sw.hpp"
 
 namespace gtfv3 {
 
@@ -45,6 +46,44 @@ std::map<std::string, Fn>& reg() {
          a.qi = dy.field("_tp_qi", q.nk).p; a.qj = dy.field("_tp_qj", q.nk).p;
          a.ord = ord;
          fv_tp_2d(dy.ctx(), a);
+       }},
+      // c_sw(delp, pt, w, u, v | uc, vc, ua, va, ut, vt, delpc, ptc, wc) params: dt2
+      {"c_sw",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 14, "c_sw");
+         const int npz = F(dy, f[0]).nk;
+         auto out = [&](int n) { return dy.field(f[n], npz).p; };
+         CswArgs a{};
+         a.npz = npz;
+         a.dt2 = p.at(0);
+         a.delp = F(dy, f[0]).p; a.pt = F(dy, f[1]).p; a.w = F(dy, f[2]).p; a.u = F(dy, f[3]).p; a.v = F(dy, f[4]).p;
+         a.uc = out(5); a.vc = out(6); a.ua = out(7); a.va = out(8); a.ut = out(9); a.vt = out(10);
+         a.delpc = out(11); a.ptc = out(12); a.wc = out(13);
+         a.utmp = dy.field("_cs_utmp", npz).p; a.vtmp = dy.field("_cs_vtmp", npz).p;
+         a.ke = dy.field("_cs_ke", npz).p; a.vort = dy.field("_cs_vort", npz).p;
+         c_sw(dy.ctx(), a);
+       }},
+      // d_sw(delp, pt, w, u, v, uc, vc, ua, va | crx, cry, xfx, yfx, cx, cy, mfx, mfy, ke)
+      // params: dt, dddmp, d2_bg, hord_mt, hord_vt, hord_tm, hord_dp
+      {"d_sw",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 18, "d_sw");
+         const int npz = F(dy, f[0]).nk;
+         auto out = [&](int n) { return dy.field(f[n], npz).p; };
+         auto scr = [&](const char* n) { return dy.field(n, npz).p; };
+         DswArgs a{};
+         a.npz = npz;
+         a.dt = p.at(0); a.dddmp = p.at(1); a.d2_bg = p.at(2);
+         a.hord_mt = (int)p.at(3); a.hord_vt = (int)p.at(4); a.hord_tm = (int)p.at(5); a.hord_dp = (int)p.at(6);
+         a.delp = F(dy, f[0]).p; a.pt = F(dy, f[1]).p; a.w = F(dy, f[2]).p; a.u = F(dy, f[3]).p; a.v = F(dy, f[4]).p;
+         a.uc = F(dy, f[5]).p; a.vc = F(dy, f[6]).p; a.ua = F(dy, f[7]).p; a.va = F(dy, f[8]).p;
+         a.crx = out(9); a.cry = out(10); a.xfx = out(11); a.yfx = out(12);
+         a.cx = out(13); a.cy = out(14); a.mfx = out(15); a.mfy = out(16); a.ke = out(17);
+         a.ut = scr("_ds_ut"); a.vt = scr("_ds_vt"); a.ra_x = scr("_ds_ra_x"); a.ra_y = scr("_ds_ra_y");
+         a.fx = scr("_ds_fx"); a.fy = scr("_ds_fy"); a.gwx = scr("_ds_gwx"); a.gwy = scr("_ds_gwy");
+         a.gtx = scr("_ds_gtx"); a.gty = scr("_ds_gty"); a.vort = scr("_ds_vort");
+         a.tp_fx2 = scr("_tp1_fx2"); a.tp_fy2 = scr("_tp1_fy2"); a.tp_qi = scr("_tp1_qi"); a.tp_qj = scr("_tp1_qj");
+         d_sw(dy.ctx(), a);
        }},
       // tracer_2d_1l: uses state fields q, dp1, cx, cy, mfx, mfy. params: nq
       {"tracer_2d_1l",

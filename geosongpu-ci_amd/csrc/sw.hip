@@ -1,0 +1,657 @@
+// sw.hip — FV3 C-D grid shallow-water core on gfx950: c_sw (with d2a2c_vect)
+// and d_sw (nord = 0, no vorticity / w damping, d_con = 0).  Each routine is a
+// short chain of plane-parallel kernels over (i, j) x (sub, level); fv_tp_2d is
+// the shared transport operator (tp.hip).  Index conventions: stencil_common.hpp.
+// Fortran index f (1-based, npx = N+1) appears here as tile-global g = f-1.
+#include "kernels_sw.hpp"
+#include "stencil_common.hpp"
+
+namespace gtfv3 {
+namespace {
+
+constexpr double A1 = 0.5625, A2 = -0.0625;
+constexpr double BIG = 1.0e8;
+
+#define KSETUP(nk_)                                                  \
+  int i, j;                                                          \
+  if (!thread_point(L, i, j)) return;                                \
+  const int z = blockIdx.z, s = z / (nk_);                           \
+  const SubInfo sub = subs[s];                                       \
+  const int N = sub.N;                                               \
+  const int I = i + sub.ioff, J = j + sub.joff;                      \
+  const long zo = (long)z * d.plane;                                 \
+  const long o = pidx(d, i, j);                                      \
+  (void)I; (void)J; (void)N; (void)zo;
+#define MT(name) met(M, d, name, s)
+#define AT(arr, di, dj) arr[zo + o + (long)(dj) * d.pitch + (di)]
+#define MA(arr, di, dj) arr[o + (long)(dj) * d.pitch + (di)]
+
+__device__ __forceinline__ double ei4(double u0, double u1, double u2, double u3, double d0, double d1, double d2,
+                                      double d3) {
+  double t1 = d0 + d1;
+  double t2 = d2 + d3;
+  return 0.5 * (((t1 + d1) * u1 - d1 * u0) / t1 + ((t2 + d2) * u2 - d2 * u3) / t2);
+}
+
+// ---------------- c_sw ----------------
+
+// d2a2c_vect part 1: utmp, vtmp (4th order interior / 2nd order near tile edges) and generic ua, va
+__global__ void __launch_bounds__(256) cs_tmp(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                              int npz, const double* __restrict__ u, const double* __restrict__ v,
+                                              double* __restrict__ utmp, double* __restrict__ vtmp,
+                                              double* __restrict__ ua, double* __restrict__ va) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  KSETUP(npz)
+  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+  double ut = BIG, vt = BIG;
+  if (i <= nx + NG - 1 && j <= ny + NG - 1) {
+    const bool rows = J >= max(2, jo - 1) && J <= min(N - 3, jo + ny);
+    const bool cols = I >= max(2, io - 1) && I <= min(N - 3, io + nx);
+    if (rows) ut = A2 * (AT(u, 0, -1) + AT(u, 0, 2)) + A1 * (AT(u, 0, 0) + AT(u, 0, 1));
+    if (cols) vt = A2 * (AT(v, -1, 0) + AT(v, 2, 0)) + A1 * (AT(v, 0, 0) + AT(v, 1, 0));
+    bool two = false;
+    if (jo == 0 && J >= jo - 3 && J <= 1) two = true;
+    if (jo + ny == N && J >= N - 2 && J <= jo + ny + 2) two = true;
+    if (rows && io == 0 && I >= io - 3 && I <= 1) two = true;
+    if (rows && io + nx == N && I >= N - 2 && I <= io + nx + 2) two = true;
+    if (two) {
+      ut = 0.5 * (AT(u, 0, 0) + AT(u, 0, 1));
+      vt = 0.5 * (AT(v, 0, 0) + AT(v, 1, 0));
+    }
+  }
+  AT(utmp, 0, 0) = ut;
+  AT(vtmp, 0, 0) = vt;
+  double a = 0.0, b = 0.0;
+  if (i >= -2 && i <= nx + 1 && j >= -2 && j <= ny + 1) {
+    const double cs = MA(MT(M_COSA_S), 0, 0), r2 = MA(MT(M_RSIN2), 0, 0);
+    a = (ut - vt * cs) * r2;
+    b = (vt - ut * cs) * r2;
+  }
+  AT(ua, 0, 0) = a;
+  AT(va, 0, 0) = b;
+}
+
+// d2a2c_vect cube-corner fixes of utmp/vtmp/ua/va (reads generic values at non-corner points only)
+__global__ void cs_corner_fix(Dims d, const SubInfo* __restrict__ subs, int npz, double* __restrict__ utmp,
+                              double* __restrict__ vtmp, double* __restrict__ ua, double* __restrict__ va) {
+  const int z = blockIdx.x, s = z / npz;
+  const SubInfo sub = subs[s];
+  const int N = sub.N, io = sub.ioff, jo = sub.joff;
+  const long zo = (long)z * d.plane;
+  auto P = [&](double* a, int I, int J) -> double& { return a[zo + pidx(d, I - io, J - jo)]; };
+  auto own = [&](int I, int J) { return I >= io && I <= io + d.nx && J >= jo && J <= jo + d.ny; };
+  const int t = threadIdx.x;
+  // gather everything first (threads act on disjoint targets; sources are never targets)
+  double val = 0.0;
+  double* tgt = nullptr;
+  if (own(0, 0)) {
+    if (t < 3) { int Ig = -3 + t; val = -P(vtmp, -1, -Ig - 1); tgt = &P(utmp, Ig, -1); }
+    else if (t < 6) { int Jg = -3 + (t - 3); val = -P(utmp, -Jg - 1, -1); tgt = &P(vtmp, -1, Jg); }
+    else if (t == 6) { val = -P(va, -1, 1); tgt = &P(ua, -2, -1); }
+    else if (t == 7) { val = -P(va, -1, 0); tgt = &P(ua, -1, -1); }
+    else if (t == 8) { val = -P(ua, 1, -1); tgt = &P(va, -1, -2); }
+    else if (t == 9) { val = -P(ua, 0, -1); tgt = &P(va, -1, -1); }
+  }
+  if (own(N, 0) && t >= 16 && t < 32) {
+    int q = t - 16;
+    if (q < 3) { val = P(vtmp, N, q); tgt = &P(utmp, N + q, -1); }
+    else if (q < 6) { int Jg = -3 + (q - 3); val = P(utmp, N + Jg, -1); tgt = &P(vtmp, N, Jg); }
+    else if (q == 6) { val = P(va, N, 0); tgt = &P(ua, N, -1); }
+    else if (q == 7) { val = P(va, N, 1); tgt = &P(ua, N + 1, -1); }
+    else if (q == 8) { val = P(ua, N - 1, -1); tgt = &P(va, N, -1); }
+    else if (q == 9) { val = P(ua, N - 2, -1); tgt = &P(va, N, -2); }
+  }
+  if (own(N, N) && t >= 32 && t < 48) {
+    int q = t - 32;
+    if (q < 3) { val = -P(vtmp, N, N - 1 - q); tgt = &P(utmp, N + q, N); }
+    else if (q < 6) { int jj = q - 3; val = -P(utmp, N - jj - 1, N); tgt = &P(vtmp, N, N + jj); }
+    else if (q == 6) { val = -P(va, N, N - 1); tgt = &P(ua, N, N); }
+    else if (q == 7) { val = -P(va, N, N - 2); tgt = &P(ua, N + 1, N); }
+    else if (q == 8) { val = -P(ua, N - 1, N); tgt = &P(va, N, N); }
+    else if (q == 9) { val = -P(ua, N - 2, N); tgt = &P(va, N, N + 1); }
+  }
+  if (own(0, N) && t >= 48 && t < 64) {
+    int q = t - 48;
+    if (q < 3) { int Ig = -3 + q; val = P(vtmp, -1, N + Ig); tgt = &P(utmp, Ig, N); }
+    else if (q < 6) { int jj = q - 3; val = P(utmp, jj, N); tgt = &P(vtmp, -1, N + jj); }
+    else if (q == 6) { val = P(va, -1, N - 2); tgt = &P(ua, -2, N); }
+    else if (q == 7) { val = P(va, -1, N - 1); tgt = &P(ua, -1, N); }
+    else if (q == 8) { val = P(ua, 0, N); tgt = &P(va, -1, N); }
+    else if (q == 9) { val = P(ua, 1, N); tgt = &P(va, -1, N + 1); }
+  }
+  __syncthreads();
+  if (tgt) *tgt = val;
+}
+
+// d2a2c_vect part 2 (uc, ut | vc, vt) + the dt2*area scaling of ut, vt done by c_sw
+__global__ void __launch_bounds__(256) cs_cgrid(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                                int npz, double dt2, const double* __restrict__ u,
+                                                const double* __restrict__ v, const double* __restrict__ utmp,
+                                                const double* __restrict__ vtmp, const double* __restrict__ ua,
+                                                const double* __restrict__ va, double* __restrict__ uc,
+                                                double* __restrict__ vc, double* __restrict__ ut,
+                                                double* __restrict__ vt) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  KSETUP(npz)
+  const int nx = d.nx, ny = d.ny;
+  // x: y-edges, local i in [-1, nx+1], j in [-1, ny]
+  double ucv = 0.0, utv = 0.0;
+  if (i >= -1 && i <= nx + 1 && j >= -1 && j <= ny) {
+    if (I == 0 || I == N) {
+      const double* dxa = MT(M_DXA);
+      double e = ei4(AT(ua, -2, 0), AT(ua, -1, 0), AT(ua, 0, 0), AT(ua, 1, 0), MA(dxa, -2, 0), MA(dxa, -1, 0),
+                     MA(dxa, 0, 0), MA(dxa, 1, 0));
+      ucv = e * (e > 0.0 ? MA(MT(M_SIN3), -1, 0) : MA(MT(M_SIN1), 0, 0));
+      utv = e;
+    } else {
+      if (I == -1 || I == N - 1) ucv = C1 * AT(utmp, -2, 0) + C2 * AT(utmp, -1, 0) + C3 * AT(utmp, 0, 0);
+      else if (I == 1) ucv = C1 * AT(utmp, 1, 0) + C2 * AT(utmp, 0, 0) + C3 * AT(utmp, -1, 0);
+      else if (I == N + 1) ucv = C3 * AT(utmp, -1, 0) + C2 * AT(utmp, 0, 0) + C1 * AT(utmp, 1, 0);
+      else ucv = A2 * (AT(utmp, -2, 0) + AT(utmp, 1, 0)) + A1 * (AT(utmp, -1, 0) + AT(utmp, 0, 0));
+      utv = (ucv - AT(v, 0, 0) * MA(MT(M_COSA_U), 0, 0)) * MA(MT(M_RSIN_U), 0, 0);
+    }
+    // c_sw: ut -> dt2 * ut * dy * sin_sg (upwind side)
+    const double dy = MA(MT(M_DY), 0, 0);
+    utv = utv > 0.0 ? dt2 * utv * dy * MA(MT(M_SIN3), -1, 0) : dt2 * utv * dy * MA(MT(M_SIN1), 0, 0);
+  }
+  AT(uc, 0, 0) = ucv;
+  AT(ut, 0, 0) = utv;
+  double vcv = 0.0, vtv = 0.0;
+  if (i >= -1 && i <= nx && j >= -1 && j <= ny + 1) {
+    if (J == 0 || J == N) {
+      const double* dya = MT(M_DYA);
+      double e = ei4(AT(va, 0, -2), AT(va, 0, -1), AT(va, 0, 0), AT(va, 0, 1), MA(dya, 0, -2), MA(dya, 0, -1),
+                     MA(dya, 0, 0), MA(dya, 0, 1));
+      vcv = e * (e > 0.0 ? MA(MT(M_SIN4), 0, -1) : MA(MT(M_SIN2), 0, 0));
+      vtv = e;
+    } else {
+      if (J == -1 || J == N - 1) vcv = C1 * AT(vtmp, 0, -2) + C2 * AT(vtmp, 0, -1) + C3 * AT(vtmp, 0, 0);
+      else if (J == 1 || J == N + 1) vcv = C1 * AT(vtmp, 0, 1) + C2 * AT(vtmp, 0, 0) + C3 * AT(vtmp, 0, -1);
+      else vcv = A2 * (AT(vtmp, 0, -2) + AT(vtmp, 0, 1)) + A1 * (AT(vtmp, 0, -1) + AT(vtmp, 0, 0));
+      vtv = (vcv - AT(u, 0, 0) * MA(MT(M_COSA_V), 0, 0)) * MA(MT(M_RSIN_V), 0, 0);
+    }
+    const double dx = MA(MT(M_DX), 0, 0);
+    vtv = vtv > 0.0 ? dt2 * vtv * dx * MA(MT(M_SIN4), 0, -1) : dt2 * vtv * dx * MA(MT(M_SIN2), 0, 0);
+  }
+  AT(vc, 0, 0) = vcv;
+  AT(vt, 0, 0) = vtv;
+}
+
+// c_sw: upwind transport of delp/pt/w -> delpc/ptc/wc and the cell kinetic energy ke
+__global__ void __launch_bounds__(256) cs_transport_ke(
+    Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M, int npz, double dt2,
+    const double* __restrict__ delp, const double* __restrict__ pt, const double* __restrict__ w,
+    const double* __restrict__ u, const double* __restrict__ v, const double* __restrict__ uc,
+    const double* __restrict__ vc, const double* __restrict__ ua, const double* __restrict__ va,
+    const double* __restrict__ ut, const double* __restrict__ vt, double* __restrict__ delpc,
+    double* __restrict__ ptc, double* __restrict__ wc, double* __restrict__ ke) {
+  Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
+  KSETUP(npz)
+  const double* dp = delp + zo;
+  const double* pp = pt + zo;
+  const double* ww = w + zo;
+  // x fluxes at faces i and i+1 (x-corner-filled scalars), y fluxes at j and j+1 (y-filled)
+  double fx1[2], fx[2], fx2[2], fy1[2], fy[2], fy2[2];
+#pragma unroll
+  for (int f = 0; f < 2; ++f) {
+    const long oi = o + f;  // face (i+f, j)
+    double c = ut[zo + oi];
+    long src = c > 0.0 ? cc_off(d, sub, i + f - 1, j, 1) : cc_off(d, sub, i + f, j, 1);
+    fx1[f] = c * dp[src];
+    fx[f] = fx1[f] * pp[src];
+    fx2[f] = fx1[f] * ww[src];
+    const long oj = o + (long)f * d.pitch;
+    double cy = vt[zo + oj];
+    long sy = cy > 0.0 ? cc_off(d, sub, i, j + f - 1, 2) : cc_off(d, sub, i, j + f, 2);
+    fy1[f] = cy * dp[sy];
+    fy[f] = fy1[f] * pp[sy];
+    fy2[f] = fy1[f] * ww[sy];
+  }
+  const long oc = cc_off(d, sub, i, j, 2);
+  const double ra = MA(MT(M_RAREA), 0, 0);
+  const double dpc = dp[oc] + (fx1[0] - fx1[1] + fy1[0] - fy1[1]) * ra;
+  AT(delpc, 0, 0) = dpc;
+  AT(ptc, 0, 0) = (pp[oc] * dp[oc] + (fx[0] - fx[1] + fy[0] - fy[1]) * ra) / dpc;
+  AT(wc, 0, 0) = (ww[oc] * dp[oc] + (fx2[0] - fx2[1] + fy2[0] - fy2[1]) * ra) / dpc;
+  // kinetic energy
+  double kk, vv;
+  if (AT(ua, 0, 0) > 0.0) {
+    if (I == 0 || I == N) kk = AT(uc, 0, 0) * MA(MT(M_SIN1), 0, 0) + AT(v, 0, 0) * MA(MT(M_COS1), 0, 0);
+    else kk = AT(uc, 0, 0);
+  } else {
+    if (I == -1 || I == N - 1) kk = AT(uc, 1, 0) * MA(MT(M_SIN3), 0, 0) + AT(v, 1, 0) * MA(MT(M_COS3), 0, 0);
+    else kk = AT(uc, 1, 0);
+  }
+  if (AT(va, 0, 0) > 0.0) {
+    if (J == 0 || J == N) vv = AT(vc, 0, 0) * MA(MT(M_SIN2), 0, 0) + AT(u, 0, 0) * MA(MT(M_COS2), 0, 0);
+    else vv = AT(vc, 0, 0);
+  } else {
+    if (J == -1 || J == N - 1) vv = AT(vc, 0, 1) * MA(MT(M_SIN4), 0, 0) + AT(u, 0, 1) * MA(MT(M_COS4), 0, 0);
+    else vv = AT(vc, 0, 1);
+  }
+  const double dt4 = 0.5 * dt2;
+  AT(ke, 0, 0) = dt4 * (AT(ua, 0, 0) * kk + AT(va, 0, 0) * vv);
+}
+
+// c_sw: absolute vorticity at cell corners from the C-grid circulation
+__global__ void __launch_bounds__(256) cs_vort(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                               int npz, const double* __restrict__ uc, const double* __restrict__ vc,
+                                               double* __restrict__ vort) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KSETUP(npz)
+  const double* dxc = MT(M_DXC);
+  const double* dyc = MT(M_DYC);
+  double fxs = AT(uc, 0, -1) * MA(dxc, 0, -1);
+  double fx0 = AT(uc, 0, 0) * MA(dxc, 0, 0);
+  double fyw = AT(vc, -1, 0) * MA(dyc, -1, 0);
+  double fy0 = AT(vc, 0, 0) * MA(dyc, 0, 0);
+  double vt = fxs - fx0 - fyw + fy0;
+  if ((I == 0 && J == 0) || (I == 0 && J == N)) vt = vt + fyw;
+  if ((I == N && J == 0) || (I == N && J == N)) vt = vt - fy0;
+  AT(vort, 0, 0) = MA(MT(M_FC), 0, 0) + MA(MT(M_RAREA_C), 0, 0) * vt;
+}
+
+// c_sw: time-centred C-grid winds (vorticity flux + KE gradient)
+__global__ void __launch_bounds__(256) cs_update(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                                 int npz, double dt2, const double* __restrict__ u,
+                                                 const double* __restrict__ v, const double* __restrict__ vort,
+                                                 const double* __restrict__ ke, double* __restrict__ uc,
+                                                 double* __restrict__ vc) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KSETUP(npz)
+  if (j < d.ny) {
+    double fy1 = (I == 0 || I == N) ? dt2 * AT(v, 0, 0)
+                                    : dt2 * (AT(v, 0, 0) - AT(uc, 0, 0) * MA(MT(M_COSA_U), 0, 0)) / MA(MT(M_SINA_U), 0, 0);
+    double fy = fy1 > 0.0 ? AT(vort, 0, 0) : AT(vort, 0, 1);
+    AT(uc, 0, 0) = AT(uc, 0, 0) + fy1 * fy + MA(MT(M_RDXC), 0, 0) * (AT(ke, -1, 0) - AT(ke, 0, 0));
+  }
+  if (i < d.nx) {
+    double fx1 = (J == 0 || J == N) ? dt2 * AT(u, 0, 0)
+                                    : dt2 * (AT(u, 0, 0) - AT(vc, 0, 0) * MA(MT(M_COSA_V), 0, 0)) / MA(MT(M_SINA_V), 0, 0);
+    double fx = fx1 > 0.0 ? AT(vort, 0, 0) : AT(vort, 1, 0);
+    AT(vc, 0, 0) = AT(vc, 0, 0) - fx1 * fx + MA(MT(M_RDYC), 0, 0) * (AT(ke, 0, -1) - AT(ke, 0, 0));
+  }
+}
+
+// ---------------- d_sw ----------------
+
+// contravariant ut, vt: generic + direct tile-edge values
+__global__ void __launch_bounds__(256) ds_utvt1(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                                int npz, double dt, const double* __restrict__ uc,
+                                                const double* __restrict__ vc, double* __restrict__ ut,
+                                                double* __restrict__ vt) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  KSETUP(npz)
+  const int nx = d.nx, ny = d.ny;
+  double a = 0.0, b = 0.0;
+  if (j <= ny + NG - 1) {
+    if ((I == 0 || I == N) && i >= -1 && i <= nx + 1) {
+      double c = AT(uc, 0, 0);
+      a = c * dt > 0.0 ? c / MA(MT(M_SIN3), -1, 0) : c / MA(MT(M_SIN1), 0, 0);
+    } else if (i >= -1 && i <= nx + 1 && J != -1 && J != 0 && J != N - 1 && J != N) {
+      a = (AT(uc, 0, 0) - 0.25 * MA(MT(M_COSA_U), 0, 0) * (AT(vc, -1, 0) + AT(vc, 0, 0) + AT(vc, -1, 1) + AT(vc, 0, 1))) *
+          MA(MT(M_RSIN_U), 0, 0);
+    }
+  }
+  if (i <= nx + NG - 1) {
+    if ((J == 0 || J == N)) {
+      double c = AT(vc, 0, 0);
+      b = c * dt > 0.0 ? c / MA(MT(M_SIN4), 0, -1) : c / MA(MT(M_SIN2), 0, 0);
+    } else if (j >= -1 && j <= ny + 1) {
+      b = (AT(vc, 0, 0) - 0.25 * MA(MT(M_COSA_V), 0, 0) * (AT(uc, 0, -1) + AT(uc, 1, -1) + AT(uc, 0, 0) + AT(uc, 1, 0))) *
+          MA(MT(M_RSIN_V), 0, 0);
+    }
+  }
+  AT(ut, 0, 0) = a;
+  AT(vt, 0, 0) = b;
+}
+
+struct CornerMap {
+  int N, fx, fy;
+  __device__ int L0(int l) const { return fx == 1 ? l : N - l; }
+  __device__ int L1(int l) const { return fy == 1 ? l : N - l; }
+  __device__ int C0(int c) const { return fx == 1 ? c : N - 1 - c; }
+  __device__ int C1(int c) const { return fy == 1 ? c : N - 1 - c; }
+};
+
+// ut, vt edge-adjacent cross terms and the cube-corner 2x2 solves (in place; sources never targets)
+__global__ void __launch_bounds__(256) ds_utvt2(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                                int npz, const double* __restrict__ uc, const double* __restrict__ vc,
+                                                double* __restrict__ ut, double* __restrict__ vt) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  KSETUP(npz)
+  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+  // cross terms
+  bool has_vt = false, has_ut = false;
+  double nvt = 0.0, nut = 0.0;
+  if ((I == -1 || I == 0 || I == N - 1 || I == N) && J >= max(2, jo) && J <= min(N - 2, jo + ny)) {
+    nvt = AT(vc, 0, 0) - 0.25 * MA(MT(M_COSA_V), 0, 0) * (AT(ut, 0, -1) + AT(ut, 1, -1) + AT(ut, 0, 0) + AT(ut, 1, 0));
+    has_vt = true;
+  }
+  if ((J == -1 || J == 0 || J == N - 1 || J == N) && I >= max(2, io) && I <= min(N - 2, io + nx)) {
+    nut = AT(uc, 0, 0) - 0.25 * MA(MT(M_COSA_U), 0, 0) * (AT(vt, -1, 0) + AT(vt, 0, 0) + AT(vt, -1, 1) + AT(vt, 0, 1));
+    has_ut = true;
+  }
+  // cube-corner solves: each target point of each owned corner
+  const int cc[4][2] = {{0, 0}, {N, 0}, {N, N}, {0, N}};
+  for (int q = 0; q < 4; ++q) {
+    const int cxg = cc[q][0], cyg = cc[q][1];
+    if (!(cxg >= io && cxg <= io + nx && cyg >= jo && cyg <= jo + ny)) continue;
+    CornerMap cm{N, cxg == N ? -1 : 1, cyg == N ? -1 : 1};
+    auto g = [&](const double* a, int Ig, int Jg) { return a[zo + pidx(d, Ig - io, Jg - jo)]; };
+    auto gm = [&](int metric, int Ig, int Jg) { return met(M, d, metric, s)[pidx(d, Ig - io, Jg - jo)]; };
+    auto UT = [&](int a, int b) { return g(ut, cm.L0(a), cm.C1(b)); };
+    auto VT = [&](int a, int b) { return g(vt, cm.C0(a), cm.L1(b)); };
+    auto UC = [&](int a, int b) { return g(uc, cm.L0(a), cm.C1(b)); };
+    auto VC = [&](int a, int b) { return g(vc, cm.C0(a), cm.L1(b)); };
+    auto CU = [&](int a, int b) { return gm(M_COSA_U, cm.L0(a), cm.C1(b)); };
+    auto CV = [&](int a, int b) { return gm(M_COSA_V, cm.C0(a), cm.L1(b)); };
+    if (I == cm.L0(1) && J == cm.C1(-1)) {
+      double d1 = 1.0 / (1.0 - 0.0625 * CU(1, -1) * CV(0, -1));
+      nut = (UC(1, -1) - 0.25 * CU(1, -1) *
+                             (VT(0, 0) + VT(1, 0) + VT(1, -1) + VC(0, -1) -
+                              0.25 * CV(0, -1) * (UT(0, -1) + UT(0, -2) + UT(1, -2)))) * d1;
+      has_ut = true;
+    }
+    if (I == cm.L0(1) && J == cm.C1(0)) {
+      double d3 = 1.0 / (1.0 - 0.0625 * CU(1, 0) * CV(0, 1));
+      nut = (UC(1, 0) - 0.25 * CU(1, 0) *
+                            (VT(0, 0) + VT(1, 0) + VT(1, 1) + VC(0, 1) -
+                             0.25 * CV(0, 1) * (UT(0, 0) + UT(0, 1) + UT(1, 1)))) * d3;
+      has_ut = true;
+    }
+    if (I == cm.C0(-1) && J == cm.L1(1)) {
+      double d2 = 1.0 / (1.0 - 0.0625 * CU(-1, 0) * CV(-1, 1));
+      nvt = (VC(-1, 1) - 0.25 * CV(-1, 1) *
+                             (UT(0, 0) + UT(0, 1) + UT(-1, 1) + UC(-1, 0) -
+                              0.25 * CU(-1, 0) * (VT(-1, 0) + VT(-2, 0) + VT(-2, 1)))) * d2;
+      has_vt = true;
+    }
+    if (I == cm.C0(0) && J == cm.L1(1)) {
+      double d3 = 1.0 / (1.0 - 0.0625 * CU(1, 0) * CV(0, 1));
+      nvt = (VC(0, 1) - 0.25 * CV(0, 1) *
+                            (UT(0, 0) + UT(0, 1) + UT(1, 1) + UC(1, 0) -
+                             0.25 * CU(1, 0) * (VT(0, 0) + VT(1, 0) + VT(1, 1)))) * d3;
+      has_vt = true;
+    }
+  }
+  // targets and sources are disjoint point sets, so no barrier is needed
+  if (has_ut) AT(ut, 0, 0) = nut;
+  if (has_vt) AT(vt, 0, 0) = nvt;
+}
+
+// advective Courant numbers and area fluxes (saved per level for update_dz_d) + ra_x, ra_y
+__global__ void __launch_bounds__(256) ds_courant(Dims d, const SubInfo* __restrict__ subs,
+                                                  const double* __restrict__ M, int npz, double dt,
+                                                  const double* __restrict__ ut, const double* __restrict__ vt,
+                                                  double* __restrict__ crx, double* __restrict__ cry,
+                                                  double* __restrict__ xfx, double* __restrict__ yfx) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  KSETUP(npz)
+  const int nx = d.nx, ny = d.ny;
+  double a = 0.0, b = 0.0, c = 0.0, e = 0.0;
+  if (i >= 0 && i <= nx && j <= ny + NG - 1) {
+    double xf = dt * AT(ut, 0, 0);
+    if (xf > 0.0) {
+      a = xf * MA(MT(M_RDXA), -1, 0);
+      b = MA(MT(M_DY), 0, 0) * xf * MA(MT(M_SIN3), -1, 0);
+    } else {
+      a = xf * MA(MT(M_RDXA), 0, 0);
+      b = MA(MT(M_DY), 0, 0) * xf * MA(MT(M_SIN1), 0, 0);
+    }
+  }
+  if (j >= 0 && j <= ny && i <= nx + NG - 1) {
+    double yf = dt * AT(vt, 0, 0);
+    if (yf > 0.0) {
+      c = yf * MA(MT(M_RDYA), 0, -1);
+      e = MA(MT(M_DX), 0, 0) * yf * MA(MT(M_SIN4), 0, -1);
+    } else {
+      c = yf * MA(MT(M_RDYA), 0, 0);
+      e = MA(MT(M_DX), 0, 0) * yf * MA(MT(M_SIN2), 0, 0);
+    }
+  }
+  AT(crx, 0, 0) = a;
+  AT(xfx, 0, 0) = b;
+  AT(cry, 0, 0) = c;
+  AT(yfx, 0, 0) = e;
+}
+
+__global__ void __launch_bounds__(256) ds_ra(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                             int npz, const double* __restrict__ xfx, const double* __restrict__ yfx,
+                                             double* __restrict__ ra_x, double* __restrict__ ra_y) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
+  KSETUP(npz)
+  const double area = MA(MT(M_AREA), 0, 0);
+  AT(ra_y, 0, 0) = (j >= 0 && j < d.ny) ? area + AT(yfx, 0, 0) - AT(yfx, 0, 1) : 0.0;
+  AT(ra_x, 0, 0) = (i >= 0 && i < d.nx) ? area + AT(xfx, 0, 0) - AT(xfx, 1, 0) : 0.0;
+}
+
+// Courant / mass-flux accumulation for tracer transport ("flux capacitor")
+__global__ void __launch_bounds__(256) ds_accum(Dims d, const SubInfo* __restrict__ subs, int npz,
+                                                const double* __restrict__ crx, const double* __restrict__ cry,
+                                                const double* __restrict__ fx, const double* __restrict__ fy,
+                                                double* __restrict__ cx, double* __restrict__ cy,
+                                                double* __restrict__ mfx, double* __restrict__ mfy) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  KSETUP(npz)
+  const int nx = d.nx, ny = d.ny;
+  if (i >= 0 && i <= nx && j <= ny + NG - 1) AT(cx, 0, 0) += AT(crx, 0, 0);
+  if (i >= 0 && i <= nx && j >= 0 && j < ny) AT(mfx, 0, 0) += AT(fx, 0, 0);
+  if (j >= 0 && j <= ny && i <= nx + NG - 1) AT(cy, 0, 0) += AT(cry, 0, 0);
+  if (j >= 0 && j <= ny && i >= 0 && i < nx) AT(mfy, 0, 0) += AT(fy, 0, 0);
+}
+
+// delp, pt, w update from the transported fluxes (compute cells)
+__global__ void __launch_bounds__(256) ds_thermo(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                                 int npz, const double* __restrict__ fx, const double* __restrict__ fy,
+                                                 const double* __restrict__ gwx, const double* __restrict__ gwy,
+                                                 const double* __restrict__ gtx, const double* __restrict__ gty,
+                                                 double* __restrict__ delp, double* __restrict__ pt,
+                                                 double* __restrict__ w) {
+  Launch2D L{0, 0, d.nx, d.ny};
+  KSETUP(npz)
+  const double ra = MA(MT(M_RAREA), 0, 0);
+  const double dp = AT(delp, 0, 0);
+  double wn = dp * AT(w, 0, 0) + (AT(gwx, 0, 0) - AT(gwx, 1, 0) + AT(gwy, 0, 0) - AT(gwy, 0, 1)) * ra;
+  double ptn = AT(pt, 0, 0) * dp + (AT(gtx, 0, 0) - AT(gtx, 1, 0) + AT(gty, 0, 0) - AT(gty, 0, 1)) * ra;
+  double dpn = dp + (AT(fx, 0, 0) - AT(fx, 1, 0) + AT(fy, 0, 0) - AT(fy, 0, 1)) * ra;
+  AT(pt, 0, 0) = ptn / dpn;
+  AT(delp, 0, 0) = dpn;
+  AT(w, 0, 0) = wn / dpn;
+}
+
+// kinetic energy at cell corners: B-grid contravariant winds, upwind PPM of v (ytp_v)
+// and u (xtp_u), cube-corner values, plus nord=0 divergence damping added to ke
+__global__ void __launch_bounds__(256) ds_ke(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                             int npz, double dt, int hord_mt, double dddmp, double d2_bg,
+                                             double da_min_c, const double* __restrict__ u,
+                                             const double* __restrict__ v, const double* __restrict__ uc,
+                                             const double* __restrict__ vc, const double* __restrict__ ua,
+                                             const double* __restrict__ va, const double* __restrict__ ut,
+                                             const double* __restrict__ vt, double* __restrict__ ke) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KSETUP(npz)
+  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+  const double dt5 = 0.5 * dt, dt4 = 0.25 * dt;
+  const int Ilo = max(1, io), Ihi = min(N - 1, io + nx), Jlo = max(1, jo), Jhi = min(N - 1, jo + ny);
+  const bool inner = I >= Ilo && I <= Ihi && J >= Jlo && J <= Jhi;
+  const double cosa = MA(MT(M_COSA), 0, 0), rsina = MA(MT(M_RSINA), 0, 0);
+  double vb = 0.0, ub = 0.0;
+  if (inner) vb = dt5 * (AT(vc, -1, 0) + AT(vc, 0, 0) - (AT(uc, 0, -1) + AT(uc, 0, 0)) * cosa) * rsina;
+  if (I == 0 || I == N) vb = dt4 * (-AT(vt, -2, 0) + 3.0 * (AT(vt, -1, 0) + AT(vt, 0, 0)) - AT(vt, 1, 0));
+  else if ((J == 0 || J == N) && I >= Ilo && I <= Ihi) vb = dt5 * (AT(vt, -1, 0) + AT(vt, 0, 0));
+  if (inner) ub = dt5 * (AT(uc, 0, -1) + AT(uc, 0, 0) - (AT(vc, -1, 0) + AT(vc, 0, 0)) * cosa) * rsina;
+  if (J == 0 || J == N) ub = dt4 * (-AT(ut, 0, -2) + 3.0 * (AT(ut, 0, -1) + AT(ut, 0, 0)) - AT(ut, 0, 1));
+  else if ((I == 0 || I == N) && J >= Jlo && J <= Jhi) ub = dt5 * (AT(ut, 0, -1) + AT(ut, 0, 0));
+  // ytp_v: flux of v through corner (i,j) along j
+  double qv[6], sp[6];
+  const double* dy = MT(M_DY);
+  const double* dxm = MT(M_DX);
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    qv[m] = AT(v, 0, m - 3);
+    sp[m] = MA(dy, 0, m - 3);
+  }
+  double cfl = vb > 0.0 ? vb * MA(MT(M_RDY), 0, -1) : vb * MA(MT(M_RDY), 0, 0);
+  double ubf = ppm_flux_ord(hord_mt, J, N, qv, sp, cfl);
+  double kk = vb * ubf;
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    qv[m] = AT(u, m - 3, 0);
+    sp[m] = MA(dxm, m - 3, 0);
+  }
+  cfl = ub > 0.0 ? ub * MA(MT(M_RDX), -1, 0) : ub * MA(MT(M_RDX), 0, 0);
+  double vbf = ppm_flux_ord(hord_mt, I, N, qv, sp, cfl);
+  kk = 0.5 * (kk + ub * vbf);
+  const double dt6 = dt / 6.0;
+  if (I == 0 && J == 0)
+    kk = dt6 * ((AT(ut, 0, 0) + AT(ut, 0, -1)) * AT(u, 0, 0) + (AT(vt, 0, 0) + AT(vt, -1, 0)) * AT(v, 0, 0) +
+                (AT(ut, 0, 0) + AT(vt, 0, 0)) * AT(u, -1, 0));
+  else if (I == N && J == 0)
+    kk = dt6 * ((AT(ut, 0, 0) + AT(ut, 0, -1)) * AT(u, -1, 0) + (AT(vt, 0, 0) + AT(vt, -1, 0)) * AT(v, 0, 0) +
+                (AT(ut, 0, 0) - AT(vt, -1, 0)) * AT(u, 0, 0));
+  else if (I == N && J == N)
+    kk = dt6 * ((AT(ut, 0, 0) + AT(ut, 0, -1)) * AT(u, -1, 0) + (AT(vt, 0, 0) + AT(vt, -1, 0)) * AT(v, 0, -1) +
+                (AT(ut, 0, -1) + AT(vt, -1, 0)) * AT(u, 0, 0));
+  else if (I == 0 && J == N)
+    kk = dt6 * ((AT(ut, 0, 0) + AT(ut, 0, -1)) * AT(u, 0, 0) + (AT(vt, 0, 0) + AT(vt, -1, 0)) * AT(v, 0, -1) +
+                (AT(ut, 0, -1) - AT(vt, 0, 0)) * AT(u, -1, 0));
+  // divergence damping (nord = 0): delpc at the corner from the edge divergence terms
+  auto ptc_at = [&](int di) {  // x-edge (i+di, j): u * dyc with the non-orthogonal correction
+    const int Jj = J;
+    const long oo = o + di;
+    const double dyc = MT(M_DYC)[oo];
+    const double uu = u[zo + oo];
+    if (Jj == 0 || Jj == N)
+      return vc[zo + oo] > 0.0 ? uu * dyc * MT(M_SIN4)[oo - d.pitch] : uu * dyc * MT(M_SIN2)[oo];
+    return (uu - 0.5 * (va[zo + oo - d.pitch] + va[zo + oo]) * MT(M_COSA_V)[oo]) * dyc * MT(M_SINA_V)[oo];
+  };
+  auto vrt_at = [&](int dj) {  // y-edge (i, j+dj)
+    const int Jj = J + dj;
+    (void)Jj;
+    const long oo = o + (long)dj * d.pitch;
+    const double dxc = MT(M_DXC)[oo];
+    const double vv = v[zo + oo];
+    if (I == 0 || I == N)
+      return uc[zo + oo] > 0.0 ? vv * dxc * MT(M_SIN3)[oo - 1] : vv * dxc * MT(M_SIN1)[oo];
+    if (I >= Ilo && I <= Ihi)
+      return (vv - 0.5 * (ua[zo + oo - 1] + ua[zo + oo]) * MT(M_COSA_U)[oo]) * dxc * MT(M_SINA_U)[oo];
+    return 0.0;
+  };
+  double vS = vrt_at(-1), v0 = vrt_at(0);
+  double dpc = vS - v0 + ptc_at(-1) - ptc_at(0);
+  if ((I == 0 && J == 0) || (I == N && J == 0)) dpc = dpc - vS;
+  if ((I == N && J == N) || (I == 0 && J == N)) dpc = dpc + v0;
+  dpc = MA(MT(M_RAREA_C), 0, 0) * dpc;
+  double damp = da_min_c * fmax(d2_bg, fmin(0.20, dddmp * fabs(dpc * dt)));
+  AT(ke, 0, 0) = kk + damp * dpc;
+}
+
+// relative vorticity (cell mean) + Coriolis -> the field transported by fv_tp_2d
+__global__ void __launch_bounds__(256) ds_vort(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                               int npz, const double* __restrict__ u, const double* __restrict__ v,
+                                               double* __restrict__ vort) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
+  KSETUP(npz)
+  const double* dx = MT(M_DX);
+  const double* dy = MT(M_DY);
+  double udx0 = AT(u, 0, 0) * MA(dx, 0, 0), udx1 = AT(u, 0, 1) * MA(dx, 0, 1);
+  double vdy0 = AT(v, 0, 0) * MA(dy, 0, 0), vdy1 = AT(v, 1, 0) * MA(dy, 1, 0);
+  double wk = MA(MT(M_RAREA), 0, 0) * (udx0 - udx1 + vdy1 - vdy0);
+  AT(vort, 0, 0) = wk + MA(MT(M_F0), 0, 0);
+}
+
+// final D-grid momentum (left multiplied by dx / dy; the pressure gradient divides)
+__global__ void __launch_bounds__(256) ds_uv(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                             int npz, const double* __restrict__ ke, const double* __restrict__ fxv,
+                                             const double* __restrict__ fyv, double* __restrict__ u,
+                                             double* __restrict__ v) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KSETUP(npz)
+  if (i < d.nx) AT(u, 0, 0) = AT(u, 0, 0) * MA(MT(M_DX), 0, 0) + AT(ke, 0, 0) - AT(ke, 1, 0) + AT(fyv, 0, 0);
+  if (j < d.ny) AT(v, 0, 0) = AT(v, 0, 0) * MA(MT(M_DY), 0, 0) + AT(ke, 0, 0) - AT(ke, 0, 1) - AT(fxv, 0, 0);
+}
+
+inline dim3 g2(const Dims& d, const Launch2D& L, int nz) { return dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), nz); }
+
+}  // namespace
+
+void c_sw(const Ctx& c, const CswArgs& a) {
+  const Dims& d = c.d;
+  const int nz = d.nsub * a.npz;
+  Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  hipLaunchKernelGGL(cs_tmp, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.utmp,
+                     a.vtmp, a.ua, a.va);
+  HIP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(cs_corner_fix, dim3(nz), dim3(64), 0, c.st, d, c.subs, a.npz, a.utmp, a.vtmp, a.ua, a.va);
+  HIP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(cs_cgrid, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
+                     a.utmp, a.vtmp, a.ua, a.va, a.uc, a.vc, a.ut, a.vt);
+  HIP_LAUNCH_CHECK();
+  Launch2D Lt{-1, -1, d.nx + 2, d.ny + 2};
+  hipLaunchKernelGGL(cs_transport_ke, g2(d, Lt, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.delp,
+                     a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke);
+  HIP_LAUNCH_CHECK();
+  Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
+  hipLaunchKernelGGL(cs_vort, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.vort);
+  HIP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(cs_update, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
+                     a.vort, a.ke, a.uc, a.vc);
+  HIP_LAUNCH_CHECK();
+}
+
+void d_sw(const Ctx& c, const DswArgs& a) {
+  const Dims& d = c.d;
+  const int nz = d.nsub * a.npz;
+  Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  hipLaunchKernelGGL(ds_utvt1, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.uc, a.vc,
+                     a.ut, a.vt);
+  HIP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ds_utvt2, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.ut,
+                     a.vt);
+  HIP_LAUNCH_CHECK();
+  hipLaunchKernelGGL(ds_courant, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.ut, a.vt,
+                     a.crx, a.cry, a.xfx, a.yfx);
+  HIP_LAUNCH_CHECK();
+  Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
+  hipLaunchKernelGGL(ds_ra, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.xfx, a.yfx, a.ra_x,
+                     a.ra_y);
+  HIP_LAUNCH_CHECK();
+  TpArgs t{};
+  t.nt = 1;
+  t.nk = a.npz;
+  t.crx = a.crx; t.cry = a.cry; t.xfx = a.xfx; t.yfx = a.yfx; t.ra_x = a.ra_x; t.ra_y = a.ra_y;
+  t.fx2 = a.tp_fx2; t.fy2 = a.tp_fy2; t.qi = a.tp_qi; t.qj = a.tp_qj;
+  // mass fluxes
+  t.q = a.delp; t.mfx = nullptr; t.mfy = nullptr; t.fx = a.fx; t.fy = a.fy; t.ord = a.hord_dp;
+  fv_tp_2d(c, t);
+  hipLaunchKernelGGL(ds_accum, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, a.npz, a.crx, a.cry, a.fx, a.fy,
+                     a.cx, a.cy, a.mfx, a.mfy);
+  HIP_LAUNCH_CHECK();
+  // w and pt with the mass fluxes
+  t.mfx = a.fx; t.mfy = a.fy;
+  t.q = a.w; t.fx = a.gwx; t.fy = a.gwy; t.ord = a.hord_vt;
+  fv_tp_2d(c, t);
+  t.q = a.pt; t.fx = a.gtx; t.fy = a.gty; t.ord = a.hord_tm;
+  fv_tp_2d(c, t);
+  Launch2D Li{0, 0, d.nx, d.ny};
+  hipLaunchKernelGGL(ds_thermo, g2(d, Li, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.fx, a.fy, a.gwx,
+                     a.gwy, a.gtx, a.gty, a.delp, a.pt, a.w);
+  HIP_LAUNCH_CHECK();
+  // kinetic energy (+ divergence damping) at corners
+  Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
+  hipLaunchKernelGGL(ds_ke, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.hord_mt, a.dddmp,
+                     a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke);
+  HIP_LAUNCH_CHECK();
+  // vorticity transport
+  hipLaunchKernelGGL(ds_vort, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.vort);
+  HIP_LAUNCH_CHECK();
+  t.mfx = nullptr; t.mfy = nullptr;
+  t.q = a.vort; t.fx = a.gwx; t.fy = a.gwy; t.ord = a.hord_vt;
+  fv_tp_2d(c, t);
+  hipLaunchKernelGGL(ds_uv, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.ke, a.gwx, a.gwy, a.u,
+                     a.v);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // namespace gtfv3

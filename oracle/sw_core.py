@@ -1,0 +1,434 @@
+"""Oracle: FV3 sw_core — c_sw (with d2a2c_vect) and d_sw (nord = 0, no vorticity
+or w damping, d_con = 0) in fp64 numpy.  TEST INFRASTRUCTURE ONLY.
+
+Restated from the FV3 C-D grid shallow-water solver (Lin & Rood 1997; Harris &
+Lin 2013; FV3 sw_core.F90 structure).  Fortran 1-based indices f are written
+here as 0-based tile-global g = f - 1 (npx -> N).  Arrays per sub-domain are
+(nk, nj, pitch) planes, a[k, j+NG, i+NG].
+"""
+import numpy as np
+
+from . import NG
+from .tp_core import copy_corners, fv_tp_2d
+
+np.seterr(all="ignore")  # NaN/inf only arise outside the compared regions
+from .util import Plane, sh
+
+A1, A2 = 0.5625, -0.0625
+C1, C2, C3 = -2.0 / 14.0, 11.0 / 14.0, 5.0 / 14.0
+BIG = 1.0e8
+
+
+def _ei4(u0, u1, u2, u3, d0, d1, d2, d3):
+    """edge_interpolate4"""
+    t1 = d0 + d1
+    t2 = d2 + d3
+    return 0.5 * (((t1 + d1) * u1 - d1 * u0) / t1 + ((t2 + d2) * u2 - d2 * u3) / t2)
+
+
+def d2a2c_vect(u, v, P, m):
+    """D-grid (u,v) -> A-grid (ua,va) and C-grid (uc,vc), contravariant ut, vt."""
+    N, nx, ny, io, jo = P.N, P.nx, P.ny, P.io, P.jo
+    I, J = P.I, P.J
+    cosa_s, rsin2 = m["cosa_s"], m["rsin2"]
+    utmp = np.full_like(u, BIG)
+    vtmp = np.full_like(v, BIG)
+    # interior
+    rows = (J >= max(2, jo - 1)) & (J <= min(N - 3, jo + ny)) & (P.li >= -NG) & (P.li <= nx + NG - 1)
+    utmp = np.where(rows, A2 * (sh(u, 0, -1) + sh(u, 0, 2)) + A1 * (u + sh(u, 0, 1)), utmp)
+    cols = (I >= max(2, io - 1)) & (I <= min(N - 3, io + nx)) & (P.lj >= -NG) & (P.lj <= ny + NG - 1)
+    vtmp = np.where(cols, A2 * (sh(v, -1, 0) + sh(v, 2, 0)) + A1 * (v + sh(v, 1, 0)), vtmp)
+    u2 = 0.5 * (u + sh(u, 0, 1))
+    v2 = 0.5 * (v + sh(v, 1, 0))
+    allc = (P.li >= -NG) & (P.li <= nx + NG - 1)
+    allr = (P.lj >= -NG) & (P.lj <= ny + NG - 1)
+    if jo == 0:  # south edge rows g in [jo-3, 1]
+        msk = allc & (J >= jo - 3) & (J <= 1)
+        utmp = np.where(msk, u2, utmp)
+        vtmp = np.where(msk, v2, vtmp)
+    if jo + ny == N:  # north edge rows g in [N-2, jo+ny+2]
+        msk = allc & (J >= N - 2) & (J <= jo + ny + 2)
+        utmp = np.where(msk, u2, utmp)
+        vtmp = np.where(msk, v2, vtmp)
+    midrows = (J >= max(2, jo - 1)) & (J <= min(N - 3, jo + ny))
+    if io == 0:
+        msk = midrows & (I >= io - 3) & (I <= 1)
+        utmp = np.where(msk, u2, utmp)
+        vtmp = np.where(msk, v2, vtmp)
+    if io + nx == N:
+        msk = midrows & (I >= N - 2) & (I <= io + nx + 2)
+        utmp = np.where(msk, u2, utmp)
+        vtmp = np.where(msk, v2, vtmp)
+    del allr
+    ua = np.zeros_like(u)
+    va = np.zeros_like(v)
+    reg = P.reg(-2, nx + 1, -2, ny + 1)
+    ua = np.where(reg, (utmp - vtmp * cosa_s) * rsin2, ua)
+    va = np.where(reg, (vtmp - utmp * cosa_s) * rsin2, va)
+
+    def setp(arr, Ig, Jg, val):
+        if 0 <= Jg - jo + NG < P.nj and 0 <= Ig - io + NG < P.pitch:
+            arr[:, Jg - jo + NG, Ig - io + NG] = val
+
+    def getp(arr, Ig, Jg):
+        return arr[:, Jg - jo + NG, Ig - io + NG]
+
+    sw, se = P.owns(0, 0), P.owns(N, 0)
+    ne, nw = P.owns(N, N), P.owns(0, N)
+    # corner fixes (reads of generic values only)
+    ut0, vt0, ua0, va0 = utmp.copy(), vtmp.copy(), ua.copy(), va.copy()
+    if sw:
+        for Ig in (-3, -2, -1):
+            setp(utmp, Ig, -1, -getp(vt0, -1, -Ig - 1))
+        for Jg in (-3, -2, -1):
+            setp(vtmp, -1, Jg, -getp(ut0, -Jg - 1, -1))
+        setp(ua, -2, -1, -getp(va0, -1, 1))
+        setp(ua, -1, -1, -getp(va0, -1, 0))
+        setp(va, -1, -2, -getp(ua0, 1, -1))
+        setp(va, -1, -1, -getp(ua0, 0, -1))
+    if se:
+        for i in (0, 1, 2):
+            setp(utmp, N + i, -1, getp(vt0, N, i))
+        for Jg in (-3, -2, -1):
+            setp(vtmp, N, Jg, getp(ut0, N + Jg, -1))
+        setp(ua, N, -1, getp(va0, N, 0))
+        setp(ua, N + 1, -1, getp(va0, N, 1))
+        setp(va, N, -1, getp(ua0, N - 1, -1))
+        setp(va, N, -2, getp(ua0, N - 2, -1))
+    if ne:
+        for i in (0, 1, 2):
+            setp(utmp, N + i, N, -getp(vt0, N, N - 1 - i))
+        for j in (0, 1, 2):
+            setp(vtmp, N, N + j, -getp(ut0, N - j - 1, N))
+        setp(ua, N, N, -getp(va0, N, N - 1))
+        setp(ua, N + 1, N, -getp(va0, N, N - 2))
+        setp(va, N, N, -getp(ua0, N - 1, N))
+        setp(va, N, N + 1, -getp(ua0, N - 2, N))
+    if nw:
+        for Ig in (-3, -2, -1):
+            setp(utmp, Ig, N, getp(vt0, -1, N + Ig))
+        for j in (0, 1, 2):
+            setp(vtmp, -1, N + j, getp(ut0, j, N))
+        setp(ua, -2, N, getp(va0, -1, N - 2))
+        setp(ua, -1, N, getp(va0, -1, N - 1))
+        setp(va, -1, N, getp(ua0, 0, N))
+        setp(va, -1, N + 1, getp(ua0, 1, N))
+
+    cosa_u, rsin_u, cosa_v, rsin_v = m["cosa_u"], m["rsin_u"], m["cosa_v"], m["rsin_v"]
+    dxa, dya, s1, s2, s3, s4 = m["dxa"], m["dya"], m["sin_sg1"], m["sin_sg2"], m["sin_sg3"], m["sin_sg4"]
+    # x: uc, ut at y-edges, local i in [-1, nx+1], j in [-1, ny]
+    reg = P.reg(-1, nx + 1, -1, ny)
+    gen = A2 * (sh(utmp, -2, 0) + sh(utmp, 1, 0)) + A1 * (sh(utmp, -1, 0) + utmp)
+    e_m1 = C1 * sh(utmp, -2, 0) + C2 * sh(utmp, -1, 0) + C3 * utmp  # g = -1 and g = N-1
+    e_p1 = C1 * sh(utmp, 1, 0) + C2 * utmp + C3 * sh(utmp, -1, 0)  # g = 1
+    e_np1 = C3 * sh(utmp, -1, 0) + C2 * utmp + C1 * sh(utmp, 1, 0)  # g = N+1
+    with np.errstate(all="ignore"):
+        e0 = _ei4(sh(ua, -2, 0), sh(ua, -1, 0), ua, sh(ua, 1, 0), sh(dxa, -2, 0), sh(dxa, -1, 0), dxa, sh(dxa, 1, 0))
+    uc = np.zeros_like(u)
+    uc = np.where(reg, gen, uc)
+    uc = np.where(reg & ((I == -1) | (I == N - 1)), e_m1, uc)
+    uc = np.where(reg & (I == 1), e_p1, uc)
+    uc = np.where(reg & (I == N + 1), e_np1, uc)
+    edge = reg & ((I == 0) | (I == N))
+    uc = np.where(edge, e0 * np.where(e0 > 0.0, sh(s3, -1, 0), s1), uc)
+    ut = np.zeros_like(u)
+    ut = np.where(reg, (uc - v * cosa_u) * rsin_u, ut)
+    ut = np.where(edge, e0, ut)
+    # y: vc, vt at x-edges, local i in [-1, nx], j in [-1, ny+1]
+    reg = P.reg(-1, nx, -1, ny + 1)
+    gen = A2 * (sh(vtmp, 0, -2) + sh(vtmp, 0, 1)) + A1 * (sh(vtmp, 0, -1) + vtmp)
+    e_m1 = C1 * sh(vtmp, 0, -2) + C2 * sh(vtmp, 0, -1) + C3 * vtmp
+    e_p1 = C1 * sh(vtmp, 0, 1) + C2 * vtmp + C3 * sh(vtmp, 0, -1)
+    with np.errstate(all="ignore"):
+        e0 = _ei4(sh(va, 0, -2), sh(va, 0, -1), va, sh(va, 0, 1), sh(dya, 0, -2), sh(dya, 0, -1), dya, sh(dya, 0, 1))
+    vc = np.zeros_like(v)
+    vc = np.where(reg, gen, vc)
+    vc = np.where(reg & ((J == -1) | (J == N - 1)), e_m1, vc)
+    vc = np.where(reg & ((J == 1) | (J == N + 1)), e_p1, vc)
+    edge = reg & ((J == 0) | (J == N))
+    vc = np.where(edge, e0 * np.where(e0 > 0.0, sh(s4, 0, -1), s2), vc)
+    vt = np.zeros_like(v)
+    vt = np.where(reg, (vc - u * cosa_v) * rsin_v, vt)
+    vt = np.where(edge, e0, vt)
+    return ua, va, uc, vc, ut, vt
+
+
+def c_sw(delp, pt, u, v, w, sub, m, nx, ny, dt2):
+    """FV3 c_sw (non-hydrostatic, nord = 0): returns delpc, ptc, wc, uc, vc, ua, va, ut, vt
+    (ut, vt scaled to dt2 * area fluxes)."""
+    P = Plane(sub, nx, ny, u.shape[-2], u.shape[-1])
+    N, I, J = P.N, P.I, P.J
+    ua, va, uc, vc, ut, vt = d2a2c_vect(u, v, P, m)
+    s1, s2, s3, s4 = m["sin_sg1"], m["sin_sg2"], m["sin_sg3"], m["sin_sg4"]
+    c1_, c2_, c3_, c4_ = m["cos_sg1"], m["cos_sg2"], m["cos_sg3"], m["cos_sg4"]
+    dx, dy = m["dx"], m["dy"]
+    reg = P.reg(-1, nx + 1, -1, ny)
+    ut = np.where(reg, np.where(ut > 0.0, dt2 * ut * dy * sh(s3, -1, 0), dt2 * ut * dy * s1), ut)
+    reg = P.reg(-1, nx, -1, ny + 1)
+    vt = np.where(reg, np.where(vt > 0.0, dt2 * vt * dx * sh(s4, 0, -1), dt2 * vt * dx * s2), vt)
+    # first-order upwind transport of delp, pt, w (fill_4corners via copy_corners)
+    dpx, ptx, wx = (copy_corners(a, sub, 1) for a in (delp, pt, w))
+    dpy, pty, wy = (copy_corners(a, sub, 2) for a in (delp, pt, w))
+    fx1 = np.where(ut > 0.0, sh(dpx, -1, 0), dpx)
+    fx = np.where(ut > 0.0, sh(ptx, -1, 0), ptx)
+    fx2 = np.where(ut > 0.0, sh(wx, -1, 0), wx)
+    fx1 = ut * fx1
+    fx = fx1 * fx
+    fx2 = fx1 * fx2
+    fy1 = np.where(vt > 0.0, sh(dpy, 0, -1), dpy)
+    fy = np.where(vt > 0.0, sh(pty, 0, -1), pty)
+    fy2 = np.where(vt > 0.0, sh(wy, 0, -1), wy)
+    fy1 = vt * fy1
+    fy = fy1 * fy
+    fy2 = fy1 * fy2
+    rarea = m["rarea"]
+    reg = P.reg(-1, nx, -1, ny)
+    delpc = np.zeros_like(delp)
+    ptc = np.zeros_like(pt)
+    wc = np.zeros_like(w)
+    dpc_ = dpy + (fx1 - sh(fx1, 1, 0) + fy1 - sh(fy1, 0, 1)) * rarea
+    delpc = np.where(reg, dpc_, delpc)
+    ptc = np.where(reg, (pty * dpy + (fx - sh(fx, 1, 0) + fy - sh(fy, 0, 1)) * rarea) / dpc_, ptc)
+    wc = np.where(reg, (wy * dpy + (fx2 - sh(fx2, 1, 0) + fy2 - sh(fy2, 0, 1)) * rarea) / dpc_, wc)
+    # kinetic energy at cell centres from upwind C-grid winds
+    kpos = np.where(I == 0, uc * s1 + v * c1_, np.where(I == N, uc * s1 + v * c1_, uc))
+    ucE, vE = sh(uc, 1, 0), sh(v, 1, 0)
+    kneg = np.where(I == -1, ucE * s3 + vE * c3_, np.where(I == N - 1, ucE * s3 + vE * c3_, ucE))
+    ke = np.where(ua > 0.0, kpos, kneg)
+    vpos = np.where(J == 0, vc * s2 + u * c2_, np.where(J == N, vc * s2 + u * c2_, vc))
+    vcN, uN = sh(vc, 0, 1), sh(u, 0, 1)
+    vneg = np.where(J == -1, vcN * s4 + uN * c4_, np.where(J == N - 1, vcN * s4 + uN * c4_, vcN))
+    vort = np.where(va > 0.0, vpos, vneg)
+    dt4 = 0.5 * dt2
+    ke = np.where(reg, dt4 * (ua * ke + va * vort), 0.0)
+    # circulation -> absolute vorticity at cell corners
+    fxc = uc * m["dxc"]
+    fyc = vc * m["dyc"]
+    vortc = sh(fxc, 0, -1) - fxc - sh(fyc, -1, 0) + fyc
+    fy_w = sh(fyc, -1, 0)
+    vortc = np.where(P.at(0, 0), vortc + fy_w, vortc)
+    vortc = np.where(P.at(N, 0), vortc - fyc, vortc)
+    vortc = np.where(P.at(N, N), vortc - fyc, vortc)
+    vortc = np.where(P.at(0, N), vortc + fy_w, vortc)
+    vortc = m["fC"] + m["rarea_c"] * vortc
+    # vorticity flux + KE gradient update of uc, vc
+    cosa_u, sina_u, cosa_v, sina_v = m["cosa_u"], m["sina_u"], m["cosa_v"], m["sina_v"]
+    fy1v = np.where((I == 0) | (I == N), dt2 * v, dt2 * (v - uc * cosa_u) / sina_u)
+    fyv = np.where(fy1v > 0.0, vortc, sh(vortc, 0, 1))
+    fx1v = np.where((J == 0) | (J == N), dt2 * u, dt2 * (u - vc * cosa_v) / sina_v)
+    fxv = np.where(fx1v > 0.0, vortc, sh(vortc, 1, 0))
+    ucn = uc + fy1v * fyv + m["rdxc"] * (sh(ke, -1, 0) - ke)
+    vcn = vc - fx1v * fxv + m["rdyc"] * (sh(ke, 0, -1) - ke)
+    uc = np.where(P.reg(0, nx, 0, ny - 1), ucn, uc)
+    vc = np.where(P.reg(0, nx - 1, 0, ny), vcn, vc)
+    return dict(delpc=delpc, ptc=ptc, wc=wc, uc=uc, vc=vc, ua=ua, va=va, ut=ut, vt=vt)
+
+
+# ----------------------------------------------------------------------------------
+# d_sw
+
+def _ppm_stag_x(q, c_cfl, spacing, P, ord_, i0, i1, j0, j1):
+    """xtp_u: PPM flux of a field stored at x-edge columns (cells) along i, interface = corner i."""
+    from .tp_core import xppm
+    return xppm(q, c_cfl, spacing, P.io, P.N, ord_, i0, i1, j0, j1)
+
+
+def d_sw_ut_vt(uc, vc, P, m, dt):
+    """contravariant C-grid winds ut, vt with tile-edge and cube-corner treatment"""
+    N, I, J, io, jo, nx, ny = P.N, P.I, P.J, P.io, P.jo, P.nx, P.ny
+    cosa_u, rsin_u, cosa_v, rsin_v = m["cosa_u"], m["rsin_u"], m["cosa_v"], m["rsin_v"]
+    s1, s2, s3, s4 = m["sin_sg1"], m["sin_sg2"], m["sin_sg3"], m["sin_sg4"]
+    ut = np.zeros_like(uc)
+    vt = np.zeros_like(vc)
+    reg = P.reg(-1, nx + 1, -NG, ny + NG - 1) & (J != -1) & (J != 0) & (J != N - 1) & (J != N)
+    ut = np.where(reg, (uc - 0.25 * cosa_u * (sh(vc, -1, 0) + vc + sh(vc, -1, 1) + sh(vc, 0, 1))) * rsin_u, ut)
+    reg = P.reg(-NG, nx + NG - 1, -1, ny + 1) & (J != 0) & (J != N)
+    vt = np.where(reg, (vc - 0.25 * cosa_v * (sh(uc, 0, -1) + sh(uc, 1, -1) + uc + sh(uc, 1, 0))) * rsin_v, vt)
+    # direct edge values
+    colr = (P.lj >= -NG) & (P.lj <= ny + NG - 1)
+    ut = np.where(colr & ((I == 0) | (I == N)), np.where(uc * dt > 0.0, uc / sh(s3, -1, 0), uc / s1), ut)
+    rowr = (P.li >= -NG) & (P.li <= nx + NG - 1)
+    vt = np.where(rowr & ((J == 0) | (J == N)), np.where(vc * dt > 0.0, vc / sh(s4, 0, -1), vc / s2), vt)
+    ut1, vt1 = ut.copy(), vt.copy()
+    # edge-adjacent cross terms
+    rows = (J >= max(2, jo)) & (J <= min(N - 2, jo + ny))
+    vt_edge = vc - 0.25 * cosa_v * (sh(ut1, 0, -1) + sh(ut1, 1, -1) + ut1 + sh(ut1, 1, 0))
+    vt = np.where(rows & ((I == -1) | (I == 0) | (I == N - 1) | (I == N)), vt_edge, vt)
+    cols = (I >= max(2, io)) & (I <= min(N - 2, io + nx))
+    ut_edge = uc - 0.25 * cosa_u * (sh(vt1, -1, 0) + vt1 + sh(vt1, -1, 1) + sh(vt1, 0, 1))
+    ut = np.where(cols & ((J == -1) | (J == 0) | (J == N - 1) | (J == N)), ut_edge, ut)
+    # cube corners: 2x2 solves (reflections of the south-west formulas)
+    for (cx, cy) in ((0, 0), (N, 0), (N, N), (0, N)):
+        if not P.owns(cx, cy):
+            continue
+        fx = -1 if cx == N else 1
+        fy = -1 if cy == N else 1
+
+        def L(l, axis):  # edge-line index
+            return l if (fx if axis == 0 else fy) == 1 else N - l
+
+        def C(c, axis):  # cell index
+            return c if (fx if axis == 0 else fy) == 1 else N - 1 - c
+
+        def g(arr, i, j):
+            jj, ii = P.slot(i, j)
+            return arr[..., jj, ii]
+
+        def UT(a, b):
+            return g(ut1, L(a, 0), C(b, 1))
+
+        def VT(a, b):
+            return g(vt1, C(a, 0), L(b, 1))
+
+        def UC(a, b):
+            return g(uc, L(a, 0), C(b, 1))
+
+        def VC(a, b):
+            return g(vc, C(a, 0), L(b, 1))
+
+        def CU(a, b):
+            return g(cosa_u, L(a, 0), C(b, 1))
+
+        def CV(a, b):
+            return g(cosa_v, C(a, 0), L(b, 1))
+
+        d1 = 1.0 / (1.0 - 0.0625 * CU(1, -1) * CV(0, -1))
+        n_ut_a = (UC(1, -1) - 0.25 * CU(1, -1) * (VT(0, 0) + VT(1, 0) + VT(1, -1) + VC(0, -1)
+                                                  - 0.25 * CV(0, -1) * (UT(0, -1) + UT(0, -2) + UT(1, -2)))) * d1
+        d2 = 1.0 / (1.0 - 0.0625 * CU(-1, 0) * CV(-1, 1))
+        n_vt_a = (VC(-1, 1) - 0.25 * CV(-1, 1) * (UT(0, 0) + UT(0, 1) + UT(-1, 1) + UC(-1, 0)
+                                                  - 0.25 * CU(-1, 0) * (VT(-1, 0) + VT(-2, 0) + VT(-2, 1)))) * d2
+        d3 = 1.0 / (1.0 - 0.0625 * CU(1, 0) * CV(0, 1))
+        n_ut_b = (UC(1, 0) - 0.25 * CU(1, 0) * (VT(0, 0) + VT(1, 0) + VT(1, 1) + VC(0, 1)
+                                                - 0.25 * CV(0, 1) * (UT(0, 0) + UT(0, 1) + UT(1, 1)))) * d3
+        n_vt_b = (VC(0, 1) - 0.25 * CV(0, 1) * (UT(0, 0) + UT(0, 1) + UT(1, 1) + UC(1, 0)
+                                                - 0.25 * CU(1, 0) * (VT(0, 0) + VT(1, 0) + VT(1, 1)))) * d3
+        jj, ii = P.slot(L(1, 0), C(-1, 1)); ut[:, jj, ii] = n_ut_a
+        jj, ii = P.slot(C(-1, 0), L(1, 1)); vt[:, jj, ii] = n_vt_a
+        jj, ii = P.slot(L(1, 0), C(0, 1)); ut[:, jj, ii] = n_ut_b
+        jj, ii = P.slot(C(0, 0), L(1, 1)); vt[:, jj, ii] = n_vt_b
+    return ut, vt
+
+
+def d_sw(delp, pt, u, v, w, uc, vc, ua, va, sub, m, nx, ny, dt, ords, dddmp, d2_bg, da_min_c):
+    """FV3 d_sw for all levels at once.  ords = (hord_mt, hord_vt, hord_tm, hord_dp).
+    Returns dict: delp, pt, w (updated), u, v (times dx / dy: finished by the pressure
+    gradient), crx, cry, xfx, yfx (advective), fx, fy (mass fluxes)."""
+    hord_mt, hord_vt, hord_tm, hord_dp = ords
+    P = Plane(sub, nx, ny, u.shape[-2], u.shape[-1])
+    N, I, J, io, jo = P.N, P.I, P.J, P.io, P.jo
+    ut, vt = d_sw_ut_vt(uc, vc, P, m, dt)
+    s1, s2, s3, s4 = m["sin_sg1"], m["sin_sg2"], m["sin_sg3"], m["sin_sg4"]
+    dx, dy, rdxa, rdya, area, rarea = m["dx"], m["dy"], m["rdxa"], m["rdya"], m["area"], m["rarea"]
+    z = np.zeros_like(u)
+    # advective Courant numbers / area fluxes
+    reg = P.reg(0, nx, -NG, ny + NG - 1)
+    xf = dt * ut
+    crx = np.where(reg, np.where(xf > 0.0, xf * sh(rdxa, -1, 0), xf * rdxa), z)
+    xfx = np.where(reg, np.where(xf > 0.0, dy * xf * sh(s3, -1, 0), dy * xf * s1), z)
+    reg = P.reg(-NG, nx + NG - 1, 0, ny)
+    yf = dt * vt
+    cry = np.where(reg, np.where(yf > 0.0, yf * sh(rdya, 0, -1), yf * rdya), z)
+    yfx = np.where(reg, np.where(yf > 0.0, dx * yf * sh(s4, 0, -1), dx * yf * s2), z)
+    ra_y = np.where(P.reg(-NG, nx + NG - 1, 0, ny - 1), area + yfx - sh(yfx, 0, 1), z)
+    ra_x = np.where(P.reg(0, nx - 1, -NG, ny + NG - 1), area + xfx - sh(xfx, 1, 0), z)
+    # mass fluxes
+    fx, fy = fv_tp_2d(delp, crx, cry, xfx, yfx, ra_x, ra_y, sub, m, nx, ny, hord_dp)
+    comp = P.reg(0, nx - 1, 0, ny - 1)
+    # w
+    gx, gy = fv_tp_2d(w, crx, cry, xfx, yfx, ra_x, ra_y, sub, m, nx, ny, hord_vt, fx, fy)
+    w_new = np.where(comp, delp * w + (gx - sh(gx, 1, 0) + gy - sh(gy, 0, 1)) * rarea, w)
+    # pt, delp
+    gx, gy = fv_tp_2d(pt, crx, cry, xfx, yfx, ra_x, ra_y, sub, m, nx, ny, hord_tm, fx, fy)
+    pt_new = pt * delp + (gx - sh(gx, 1, 0) + gy - sh(gy, 0, 1)) * rarea
+    dp_new = delp + (fx - sh(fx, 1, 0) + fy - sh(fy, 0, 1)) * rarea
+    pt_new = np.where(comp, pt_new / dp_new, pt)
+    dp_new = np.where(comp, dp_new, delp)
+    w_new = np.where(comp, w_new / dp_new, w_new)
+
+    # kinetic energy at corners (B-grid contravariant winds, upwind PPM of u and v)
+    dt5, dt4 = 0.5 * dt, 0.25 * dt
+    cosa, rsina = m["cosa"], m["rsina"]
+    Ilo, Ihi = max(1, io), min(N - 1, io + nx)
+    Jlo, Jhi = max(1, jo), min(N - 1, jo + ny)
+    inner = (I >= Ilo) & (I <= Ihi) & (J >= Jlo) & (J <= Jhi)
+    allx = P.reg(0, nx, 0, ny)
+    vb = np.where(inner, dt5 * (sh(vc, -1, 0) + vc - (sh(uc, 0, -1) + uc) * cosa) * rsina, z)
+    vb_we = dt4 * (-sh(vt, -2, 0) + 3.0 * (sh(vt, -1, 0) + vt) - sh(vt, 1, 0))
+    vb = np.where(allx & ((I == 0) | (I == N)), vb_we, vb)
+    vb_sn = dt5 * (sh(vt, -1, 0) + vt)
+    vb = np.where((I >= Ilo) & (I <= Ihi) & allx & ((J == 0) | (J == N)), vb_sn, vb)
+    # ytp_v: PPM of v along j with Courant vb*rdy(upwind)
+    rdy = m["rdy"]
+    cfl = np.where(vb > 0.0, vb * sh(rdy, 0, -1), vb * rdy)
+    from .tp_core import yppm
+    ub_flux = z.copy()
+    ub_flux[:, NG:NG + ny + 1, NG:NG + nx + 1] = yppm(v, cfl, dy, jo, N, hord_mt, 0, nx, 0, ny)
+    ke = np.where(allx, vb * ub_flux, z)
+    ub = np.where(inner, dt5 * (sh(uc, 0, -1) + uc - (sh(vc, -1, 0) + vc) * cosa) * rsina, z)
+    ub_we = dt5 * (sh(ut, 0, -1) + ut)
+    ub = np.where((J >= Jlo) & (J <= Jhi) & allx & ((I == 0) | (I == N)), ub_we, ub)
+    ub_sn = dt4 * (-sh(ut, 0, -2) + 3.0 * (sh(ut, 0, -1) + ut) - sh(ut, 0, 1))
+    ub = np.where(allx & ((J == 0) | (J == N)), ub_sn, ub)
+    rdx = m["rdx"]
+    cfl = np.where(ub > 0.0, ub * sh(rdx, -1, 0), ub * rdx)
+    from .tp_core import xppm
+    vb_flux = z.copy()
+    vb_flux[:, NG:NG + ny + 1, NG:NG + nx + 1] = xppm(u, cfl, dx, io, N, hord_mt, 0, nx, 0, ny)
+    ke = np.where(allx, 0.5 * (ke + ub * vb_flux), z)
+    dt6 = dt / 6.0
+
+    def g(arr, i, j):
+        jj, ii = P.slot(i, j)
+        return arr[:, jj, ii]
+
+    def put(arr, i, j, val):
+        jj, ii = P.slot(i, j)
+        arr[:, jj, ii] = val
+    if P.owns(0, 0):
+        put(ke, 0, 0, dt6 * ((g(ut, 0, 0) + g(ut, 0, -1)) * g(u, 0, 0) + (g(vt, 0, 0) + g(vt, -1, 0)) * g(v, 0, 0)
+                             + (g(ut, 0, 0) + g(vt, 0, 0)) * g(u, -1, 0)))
+    if P.owns(N, 0):
+        put(ke, N, 0, dt6 * ((g(ut, N, 0) + g(ut, N, -1)) * g(u, N - 1, 0) + (g(vt, N, 0) + g(vt, N - 1, 0)) * g(v, N, 0)
+                             + (g(ut, N, 0) - g(vt, N - 1, 0)) * g(u, N, 0)))
+    if P.owns(N, N):
+        put(ke, N, N, dt6 * ((g(ut, N, N) + g(ut, N, N - 1)) * g(u, N - 1, N)
+                             + (g(vt, N, N) + g(vt, N - 1, N)) * g(v, N, N - 1)
+                             + (g(ut, N, N - 1) + g(vt, N - 1, N)) * g(u, N, N)))
+    if P.owns(0, N):
+        put(ke, 0, N, dt6 * ((g(ut, 0, N) + g(ut, 0, N - 1)) * g(u, 0, N) + (g(vt, 0, N) + g(vt, -1, N)) * g(v, 0, N - 1)
+                             + (g(ut, 0, N - 1) - g(vt, 0, N)) * g(u, -1, N)))
+
+    # relative vorticity (cell mean)
+    udx = u * dx
+    vdy = v * dy
+    wk = np.where(P.reg(-NG, nx + NG - 1, -NG, ny + NG - 1), rarea * (udx - sh(udx, 0, 1) + sh(vdy, 1, 0) - vdy), z)
+
+    # divergence damping (nord = 0)
+    ptc = z.copy()
+    regp = P.reg(-1, nx, 0, ny)
+    ptc_edge = np.where(vc > 0.0, u * m["dyc"] * sh(s4, 0, -1), u * m["dyc"] * s2)
+    ptc_gen = (u - 0.5 * (sh(va, 0, -1) + va) * m["cosa_v"]) * m["dyc"] * m["sina_v"]
+    ptc = np.where(regp, np.where((J == 0) | (J == N), ptc_edge, ptc_gen), ptc)
+    vrt = z.copy()
+    regv = (I >= Ilo) & (I <= Ihi) & P.reg(-1, nx, -1, ny)
+    vrt = np.where(regv, (v - 0.5 * (sh(ua, -1, 0) + ua) * m["cosa_u"]) * m["dxc"] * m["sina_u"], vrt)
+    vrt_edge = np.where(uc > 0.0, v * m["dxc"] * sh(s3, -1, 0), v * m["dxc"] * s1)
+    vrt = np.where(P.reg(-1, nx, -1, ny) & ((I == 0) | (I == N)), vrt_edge, vrt)
+    delpc = np.where(allx, sh(vrt, 0, -1) - vrt + sh(ptc, -1, 0) - ptc, z)
+    vS = sh(vrt, 0, -1)
+    delpc = np.where(P.at(0, 0), delpc - vS, delpc)
+    delpc = np.where(P.at(N, 0), delpc - vS, delpc)
+    delpc = np.where(P.at(N, N), delpc + vrt, delpc)
+    delpc = np.where(P.at(0, N), delpc + vrt, delpc)
+    delpc = m["rarea_c"] * delpc
+    damp = da_min_c * np.maximum(d2_bg, np.minimum(0.20, dddmp * np.abs(delpc * dt)))
+    ke = np.where(allx, ke + damp * delpc, ke)
+
+    # vorticity transport and the final momentum update
+    vort = np.where(P.reg(-NG, nx + NG - 1, -NG, ny + NG - 1), wk + m["f0"], z)
+    fxv, fyv = fv_tp_2d(vort, crx, cry, xfx, yfx, ra_x, ra_y, sub, m, nx, ny, hord_vt)
+    u_new = np.where(P.reg(0, nx - 1, 0, ny), udx + ke - sh(ke, 1, 0) + fyv, u)
+    v_new = np.where(P.reg(0, nx, 0, ny - 1), vdy + ke - sh(ke, 0, 1) - fxv, v)
+    return dict(delp=dp_new, pt=pt_new, w=w_new, u=u_new, v=v_new, crx=crx, cry=cry, xfx=xfx, yfx=yfx,
+                fx=fx, fy=fy, ke=ke, ut=ut, vt=vt)
