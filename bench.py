@@ -1,0 +1,200 @@
+#!/usr/bin/env python3
+"""Benchmark: grid-cell-updates/sec per dycore step, Held-Suarez C180 L72 (BASELINE.json).
+
+One "step" is one fv_dynamics call (= one geos_gtfv3 run: n_split=6 acoustic
+sub-steps, tracer_2d_1l, vertical remap) on device-resident fp64 state.  At N=1
+the whole C180 L72 cubed sphere (6 tiles) lives on one MI355X; for N>1 one
+process per GPU (torch.distributed / RCCL over xGMI), the 6*layout^2 sub-domains
+split evenly across ranks, halos exchanged with RCCL send/recv (strong scaling:
+the global grid is fixed).
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    torchrun --nproc-per-node N bench.py --gpus N ...   (the driver's N>1 launch)
+
+Prints ONE JSON line on rank 0 (contract in DESIGN.md §Measurement):
+  value            whole-job cells*levels advanced per second (max-over-ranks time)
+  roofline         dominant kernel: algorithmic bytes per launch / its mean HIP-event
+                   duration over the timed steps, against 8 TB/s HBM
+  cpu_baseline     the numpy oracle (oracle/fv_dynamics.py) timed for one step on a
+                   bounded sample (C24 L72, 6 tiles) on the host, rank 0 only
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
+
+# Algorithmic HBM bytes per launch of the kernels that can dominate a step:
+# distinct fp64 fields read + written once over the kernel's domain (see DESIGN.md
+# "Kernels").  c = cells per level over the launch's sub-domains, L = levels.
+KERNEL_BYTES = {}
+
+
+def layout_for(n):
+    """(layout_x, layout_y) for n ranks: 6*lx*ly sub-domains divisible by n"""
+    return {1: (1, 1), 2: (1, 1), 3: (1, 1), 6: (1, 1), 4: (1, 2), 8: (2, 2), 12: (1, 2), 24: (2, 2)}.get(n, (2, 2))
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--npx", type=int, default=181)
+    p.add_argument("--npz", type=int, default=72)
+    p.add_argument("--nq", type=int, default=4)
+    p.add_argument("--dt", type=float, default=450.0)
+    p.add_argument("--cpu-npx", type=int, default=25, help="cpu_baseline sample grid (C24)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--no-kernel-timing", action="store_true")
+    p.add_argument("--kernel-report", default="", help="write per-kernel stats JSON here")
+    return p.parse_args()
+
+
+def cpu_baseline(pkg, npx, npz, nq, dt):
+    """One oracle fv_dynamics step of a bounded sample, single host core."""
+    import importlib
+
+    from oracle import fv_dynamics as fvd
+    state = importlib.import_module(pkg.__name__ + ".state")
+    d = pkg.Domain(npx=npx, npz=npz, nq=nq, host_only=1, dt=dt)
+    ak, bk, ks = state.hybrid_levels(npz)
+    st = state.jablonowski_williamson(d, ak, bk)
+    names = ["area", "rarea", "area_c", "rarea_c", "dx", "dy", "dxa", "dya", "dxc", "dyc", "rdx", "rdy",
+             "rdxa", "rdya", "rdxc", "rdyc"] + [f"sin_sg{i}" for i in range(1, 10)] + \
+        [f"cos_sg{i}" for i in range(1, 10)] + ["cosa_u", "sina_u", "rsin_u", "cosa_v", "sina_v", "rsin_v",
+                                                "cosa_s", "rsin2", "cosa", "rsina", "fC", "f0",
+                                                "a11", "a12", "a21", "a22", "lat", "lon"]
+    allm = {n: d.metric(n) for n in names}
+    ms = [{n: v[s] for n, v in allm.items()} for s in range(d.nsub)]
+    sc = d.scalars()
+    g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
+    nl = dict(n_split=6, dt_atmos=dt, hord_mt=6, hord_vt=6, hord_tm=6, hord_dp=6, hord_tr=6, dddmp=0.2, d2_bg=0.0,
+              p_fac=0.05, dz_min=2.0, fill=1, nq=nq)
+    t0 = time.perf_counter()
+    fvd.fv_dynamics(st, ak, bk, g, nl)
+    el = time.perf_counter() - t0
+    cells = 6 * d.N * d.N * npz
+    d.close()
+    return dict(value=cells / el, unit="grid-cell-updates/s", cores=1, kind="port",
+                sample=f"one fv_dynamics step, C{d.N} L{npz} nq={nq}, 6 tiles, numpy fp64 oracle "
+                       f"(oracle/fv_dynamics.py), {el:.1f} s on 1 host core")
+
+
+def main():
+    a = parse()
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    import torch
+    import torch.distributed as dist
+
+    import gtfv3_pkg
+    pkg = gtfv3_pkg.load()
+    import importlib
+    state = importlib.import_module(pkg.__name__ + ".state")
+
+    if not torch.cuda.is_available():
+        raise SystemExit("bench.py needs an MI355X (no GPU visible)")
+    torch.cuda.set_device(local)
+    nccl_id = None
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        obj = [pkg.unique_id() if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0)
+        nccl_id = obj[0]
+    lx, ly = layout_for(world)
+    d = pkg.Domain(rank, world, nccl_id, npx=a.npx, npz=a.npz, nq=a.nq, layout_x=lx, layout_y=ly, dt=a.dt)
+    ak, bk, ks = state.hybrid_levels(a.npz)
+    st = state.jablonowski_williamson(d, ak, bk)
+    d.set_vertical(ak, bk, ks)
+    for k, v in st.items():
+        d.upload(k, v)
+    del st
+
+    def barrier():
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+
+    for _ in range(a.warmup):
+        d.step(1)
+    if not a.no_kernel_timing:
+        d.kernel_timing(True)
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        d.step(1)
+    d.sync()
+    barrier()
+    el = time.perf_counter() - t0
+    kstats = d.kernel_stats() if not a.no_kernel_timing else {}
+    if world > 1:
+        t = torch.tensor([el], dtype=torch.float64, device="cuda")
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        el = float(t.item())
+
+    N, npz = d.N, d.npz
+    cells = 6 * N * N * npz
+    value = cells * a.steps / el
+    ms_step = 1000.0 * el / a.steps
+
+    roof = None
+    if kstats:
+        name, (tot, n) = max(kstats.items(), key=lambda kv: kv[1][0])
+        avg_ms = tot / n
+        fn = KERNEL_BYTES.get(name)
+        if fn is not None:
+            b = fn(d)
+            ach = b / (avg_ms * 1e-3) / 1e9
+            roof = dict(bound="hbm", kernel=name, achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
+                        frac=ach / HBM_PEAK_GBS, traffic=None, bytes_per_launch=b, avg_ms=avg_ms,
+                        share_of_step=tot / (ms_step * a.steps))
+        else:
+            roof = dict(bound="hbm", kernel=name, achieved=None, peak=HBM_PEAK_GBS, unit="GB/s", frac=None,
+                        traffic=None, avg_ms=avg_ms, share_of_step=tot / (ms_step * a.steps))
+        if a.kernel_report and rank == 0:
+            with open(a.kernel_report, "w") as f:
+                json.dump({k: dict(ms_total=v[0], launches=v[1], ms_per_step=v[0] / a.steps)
+                           for k, v in sorted(kstats.items(), key=lambda kv: -kv[1][0])}, f, indent=1)
+
+    cpu = None
+    if rank == 0 and world == 1 and not a.no_cpu_baseline:
+        cpu = cpu_baseline(pkg, a.cpu_npx, a.npz, a.nq, a.dt)
+
+    if rank == 0:
+        out = {
+            "metric": "grid-cell-updates/sec per dycore step, Held-Suarez C180 L72",
+            "value": value,
+            "unit": "grid-cell-updates/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": ms_step,
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f64",
+            "data": "synthetic (Jablonowski-Williamson baroclinic state on an analytic hybrid L%d grid)" % npz,
+            "config": {"workload": f"Held-Suarez C{N} L{npz} dycore step (fv_dynamics), 6 tiles on "
+                                   f"{world} MI355X", "npx": N + 1, "npz": npz, "nq": a.nq, "layout": f"{lx}x{ly}",
+                       "dt_atmos": a.dt, "n_split": 6, "k_split": 1, "cells_per_step": cells},
+            "roofline": roof,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(out))
+    d.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

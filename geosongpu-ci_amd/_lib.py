@@ -41,6 +41,8 @@ DEVICE_SYMBOLS = [
     "gtfv3_sync",
     "gtfv3_stream",
     "gtfv3_timers",
+    "gtfv3_kernel_timing",
+    "gtfv3_kernel_stats",
 ]
 
 _lib = None
@@ -87,6 +89,8 @@ def lib():
         "gtfv3_sync": (I, [P]),
         "gtfv3_stream": (P, [P]),
         "gtfv3_timers": (I, [P, ctypes.c_char_p, I]),
+        "gtfv3_kernel_timing": (I, [P, I]),
+        "gtfv3_kernel_stats": (I, [P, ctypes.c_char_p, I]),
     }
     for name, (res, args) in sig.items():
         f = getattr(L, name)

@@ -87,7 +87,7 @@ void copy_in(Dycore& dy, const char* name, int nk_dev, const T* host, const FDes
   for (int s = 0; s < g_tiles_per_rank; ++s) {
     T* st = (T*)stage(sizeof(T) * n);
     HIP_CHECK(hipMemcpyAsync(st, host + (size_t)s * n, sizeof(T) * n, hipMemcpyHostToDevice, dy.st));
-    hipLaunchKernelGGL(fort_to_dev<T>, dim3(cdiv(n, 256)), dim3(256), 0, dy.st, st, f.p, dy.d, s, nk_dev, fd, n);
+    GT_LAUNCH(fort_to_dev<T>, dim3(cdiv(n, 256)), dim3(256), 0, dy.st, st, f.p, dy.d, s, nk_dev, fd, n);
     HIP_LAUNCH_CHECK();
   }
 }
@@ -99,7 +99,7 @@ void copy_out(Dycore& dy, const char* name, T* host, const FDesc& fd) {
   long n = (long)fd.ni * fd.nj * fd.nk;
   for (int s = 0; s < g_tiles_per_rank; ++s) {
     T* st = (T*)stage(sizeof(T) * n);
-    hipLaunchKernelGGL(dev_to_fort<T>, dim3(cdiv(n, 256)), dim3(256), 0, dy.st, st, f->p, dy.d, s, f->nk, fd, n);
+    GT_LAUNCH(dev_to_fort<T>, dim3(cdiv(n, 256)), dim3(256), 0, dy.st, st, f->p, dy.d, s, f->nk, fd, n);
     HIP_LAUNCH_CHECK();
     HIP_CHECK(hipMemcpyAsync(host + (size_t)s * n, st, sizeof(T) * n, hipMemcpyDeviceToHost, dy.st));
     HIP_CHECK(hipStreamSynchronize(dy.st));

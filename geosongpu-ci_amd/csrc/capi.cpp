@@ -285,6 +285,28 @@ int gtfv3_timers(void* h, char* buf, int len) {
   API_CATCH
 }
 
+int gtfv3_kernel_timing(void* h, int on) {
+  API_TRY
+  (void)D(h);
+  gtfv3::ktimer_reset();
+  gtfv3::ktimer_enable(on != 0);
+  API_CATCH
+}
+
+int gtfv3_kernel_stats(void* h, char* buf, int len) {
+  API_TRY
+  HIP_CHECK(hipStreamSynchronize(D(h)->st));
+  gtfv3::ktimer_flush();
+  std::string s;
+  for (auto& kv : gtfv3::ktimer_stats())
+    s += kv.first + "=" + std::to_string(kv.second.ms) + "," + std::to_string(kv.second.launches) + ";";
+  if (buf && len > 0) {
+    std::strncpy(buf, s.c_str(), (size_t)len - 1);
+    buf[len - 1] = 0;
+  }
+  API_CATCH
+}
+
 // ---------------- reference bridge symbols ----------------
 
 void geos_gtfv3_init_c(void* comm, int npx, int npy, int npz, int ntiles, int is, int ie, int js, int je, int isd,

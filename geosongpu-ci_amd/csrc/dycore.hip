@@ -7,6 +7,9 @@
 #include <stdexcept>
 
 #include "hip_util.hpp"
+#include "kernels_misc.hpp"
+#include "kernels_nh.hpp"
+#include "kernels_sw.hpp"
 
 namespace gtfv3 {
 
@@ -208,6 +211,194 @@ void Dycore::tracer_2d(int nq, double /*dt*/) {
   }
 }
 
-void Dycore::step() { throw std::runtime_error("step: not built yet"); }
+Field& Dycore::need(const std::string& name, int nk) {
+  Field* f = find(name);
+  if (!f) throw std::runtime_error("step: state field '" + name + "' was never uploaded");
+  if (f->nk != nk) throw std::runtime_error("step: field '" + name + "' has the wrong level count");
+  return *f;
+}
+
+// Device copies of ak, bk and the reference layer thickness dp_ref = dak + dbk*1e5.
+const double* Dycore::vertical_dev() {
+  const int k1 = nl.npz + 1;
+  if ((int)ak.size() != k1) throw std::runtime_error("step: set_vertical() was not called");
+  if (3L * k1 > d.plane) throw std::runtime_error("vertical table larger than one plane");
+  Field& v = field("_vert", 1);
+  std::vector<double> h(3 * k1, 0.0);
+  for (int k = 0; k < k1; ++k) {
+    h[k] = ak[k];
+    h[k1 + k] = bk[k];
+  }
+  for (int k = 0; k < nl.npz; ++k) h[2 * k1 + k] = (ak[k + 1] - ak[k]) + (bk[k + 1] - bk[k]) * 1.0e5;
+  HIP_CHECK(hipMemcpyAsync(v.p, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  return v.p;
+}
+
+// One fv_dynamics call (FV3 fv_dynamics.F90 / dyn_core.F90 sequence, non-hydrostatic,
+// k_split remap cycles of n_split acoustic sub-steps, tracer_2d_1l, Lagrangian-to-
+// Eulerian remap, then T/omega/A-grid winds for the caller).
+void Dycore::step() {
+  if (nl.host_only) throw std::runtime_error("host-only dycore cannot step");
+  if (nl.k_split != 1) throw std::runtime_error("step: only k_split = 1 is supported");
+  const int npz = nl.npz, k1 = npz + 1, nq = nl.nq;
+  if (nq < 1) throw std::runtime_error("step: nq >= 1 required (tracer 0 is specific humidity)");
+  Ctx c = ctx();
+  const double bdt = nl.dt_atmos;
+  const double mdt = bdt / nl.k_split;
+  const double dt = mdt / nl.n_split, dt2 = 0.5 * dt;
+  const double ptop = ak[0];
+  const double* vert = vertical_dev();
+  const double* ak_dev = vert;
+  const double* bk_dev = vert + k1;
+  const double* dp_ref = vert + 2 * k1;
+
+  hipEvent_t ev[5];
+  for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+  HIP_CHECK(hipEventRecord(ev[0], st));
+
+  Field& u = need("u", npz);
+  Field& v = need("v", npz);
+  Field& w = need("w", npz);
+  Field& delz = need("delz", npz);
+  Field& pt = need("pt", npz);
+  Field& delp = need("delp", npz);
+  Field& q = need("q", nq * npz);
+  Field& phis = need("phis", 1);
+  auto S = [&](const char* n, int nk) { return field(n, nk).p; };
+  double* pe = S("pe", k1);
+  double* peln = S("peln", k1);
+  double* pk = S("pk", k1);
+  double* pkz = S("pkz", npz);
+  double* ps = S("ps", 1);
+  double* omga = S("omga", npz);
+  double* ua = S("ua", npz);
+  double* va = S("va", npz);
+  double* uc = S("uc", npz);
+  double* vc = S("vc", npz);
+  double* mfx = S("mfx", npz);
+  double* mfy = S("mfy", npz);
+  double* cx = S("cx", npz);
+  double* cy = S("cy", npz);
+  double* dp1 = S("dp1", npz);
+
+  fv_prep(c, npz, nq, delp.p, delz.p, q.p, pt.p, pkz);
+  copy_levels(c, field_elems(npz), delp.p, dp1);
+  for (double* x : {mfx, mfy, cx, cy}) fill_field(c, field_elems(npz), 0.0, x);
+
+  // ---- dyn_core ----
+  double* zh = S("zh", k1);
+  double* gzc = S("_gzc", k1);
+  double* pef = S("_pef", k1);
+  double* ppe = S("ppe", k1);
+  double* pk3 = S("_pk3", k1);
+  double* gz = S("_gz", k1);
+  double* ws = S("ws", 1);
+  NhScratch nsc;
+  for (int n = 0; n < 14; ++n) nsc.s[n] = S(("_nh" + std::to_string(n)).c_str(), k1);
+
+  CswArgs ca{};
+  ca.npz = npz;
+  ca.dt2 = dt2;
+  ca.delp = delp.p; ca.pt = pt.p; ca.w = w.p; ca.u = u.p; ca.v = v.p;
+  ca.uc = uc; ca.vc = vc; ca.ua = ua; ca.va = va;
+  ca.ut = S("_ut", npz); ca.vt = S("_vt", npz);
+  ca.delpc = S("_delpc", npz); ca.ptc = S("_ptc", npz); ca.wc = S("_wc", npz);
+  ca.utmp = S("_cs_utmp", npz); ca.vtmp = S("_cs_vtmp", npz); ca.ke = S("_cs_ke", npz); ca.vort = S("_cs_vort", npz);
+
+  DswArgs da{};
+  da.npz = npz;
+  da.dt = dt; da.dddmp = nl.dddmp; da.d2_bg = nl.d2_bg;
+  da.hord_mt = nl.hord_mt; da.hord_vt = nl.hord_vt; da.hord_tm = nl.hord_tm; da.hord_dp = nl.hord_dp;
+  da.delp = delp.p; da.pt = pt.p; da.w = w.p; da.u = u.p; da.v = v.p;
+  da.uc = uc; da.vc = vc; da.ua = ua; da.va = va;
+  da.crx = S("crx", npz); da.cry = S("cry", npz); da.xfx = S("xfx", npz); da.yfx = S("yfx", npz);
+  da.cx = cx; da.cy = cy; da.mfx = mfx; da.mfy = mfy;
+  da.ut = S("_ds_ut", npz); da.vt = S("_ds_vt", npz); da.ra_x = S("_ds_ra_x", npz); da.ra_y = S("_ds_ra_y", npz);
+  da.fx = S("_ds_fx", npz); da.fy = S("_ds_fy", npz); da.gwx = S("_ds_gwx", npz); da.gwy = S("_ds_gwy", npz);
+  da.gtx = S("_ds_gtx", npz); da.gty = S("_ds_gty", npz); da.ke = S("_ds_ke", npz); da.vort = S("_ds_vort", npz);
+  da.tp_fx2 = S("_tp1_fx2", npz); da.tp_fy2 = S("_tp1_fy2", npz); da.tp_qi = S("_tp1_qi", npz);
+  da.tp_qj = S("_tp1_qj", npz);
+
+  UdzdArgs za{};
+  za.npz = npz;
+  za.hord = nl.hord_tm;
+  za.dp0 = dp_ref;
+  za.crx = da.crx; za.cry = da.cry; za.xfx = da.xfx; za.yfx = da.yfx;
+  za.crx_e = S("_ud_crx", k1); za.cry_e = S("_ud_cry", k1); za.xfx_e = S("_ud_xfx", k1); za.yfx_e = S("_ud_yfx", k1);
+  za.ra_x = S("_ud_ra_x", k1); za.ra_y = S("_ud_ra_y", k1); za.fx = S("_ud_fx", k1); za.fy = S("_ud_fy", k1);
+  za.gam = S("_ud_gam", k1);
+  za.zh = zh;
+  za.tp_fx2 = S("_tp2_fx2", k1); za.tp_fy2 = S("_tp2_fy2", k1); za.tp_qi = S("_tp2_qi", k1);
+  za.tp_qj = S("_tp2_qj", k1);
+
+  Riem3Args ra{};
+  ra.npz = npz;
+  ra.dt = dt; ra.ptop = ptop; ra.p_fac = nl.p_fac; ra.dz_min = nl.dz_min;
+  ra.delp = delp.p; ra.pt = pt.p; ra.phis = phis.p;
+  ra.w = w.p; ra.delz = delz.p; ra.zh = zh; ra.ppe = ppe; ra.pk3 = pk3; ra.pe = pe; ra.peln = peln; ra.pk = pk;
+  ra.ws = ws;
+
+  NhPgArgs pa{};
+  pa.npz = npz;
+  pa.dt = dt; pa.ptop = ptop;
+  pa.pp = ppe; pa.pk3 = pk3; pa.gz = gz; pa.delp = delp.p;
+  pa.ppb = S("_pg_pp", k1); pa.pkb = S("_pg_pk", k1); pa.gzb = S("_pg_gz", k1); pa.wk1 = S("_pg_wk", npz);
+  pa.qx = S("_pg_qx", k1); pa.qy = S("_pg_qy", k1);
+  pa.u = u.p; pa.v = v.p;
+
+  halo_update({{"u", 'd'}, {"v", 'd'}, {"delp", 'c'}, {"pt", 'c'}, {"w", 'c'}, {"phis", 'c'}});
+  zh_init(c, npz, phis.p, delz.p, zh);
+  halo_update({{"zh", 'c'}});
+  for (int it = 0; it < nl.n_split; ++it) {
+    const bool last = it == nl.n_split - 1;
+    c_sw(c, ca);
+    update_dz_c(c, npz, dp_ref, ca.ut, ca.vt, zh, gzc);
+    riem_solver_c(c, npz, dt2, ptop, nl.p_fac, nl.dz_min, ca.delpc, ca.ptc, ca.wc, phis.p, gzc, pef, nsc);
+    p_grad_c(c, npz, dt2, ca.delpc, pef, gzc, uc, vc);
+    halo_update({{"uc", 'C'}, {"vc", 'C'}});
+    d_sw(c, da);
+    halo_update({{"delp", 'c'}, {"pt", 'c'}});
+    update_dz_d(c, za);
+    ra.last_call = last ? 1 : 0;
+    riem_solver3(c, ra, nsc);
+    halo_update({{"zh", 'c'}, {"ppe", 'c'}, {"w", 'c'}});
+    pk3_pe_halo(c, npz, ptop, last, delp.p, pk3, pe);
+    scale_field(c, field_elems(k1), Constants::grav, zh, gz);
+    nh_p_grad(c, pa);
+    if (!last) halo_update({{"u", 'd'}, {"v", 'd'}});
+  }
+  HIP_CHECK(hipEventRecord(ev[1], st));
+
+  // ---- tracer transport with the accumulated mass fluxes ----
+  tracer_2d(nq, mdt);
+  HIP_CHECK(hipEventRecord(ev[2], st));
+
+  // ---- vertical remap to the hybrid Eulerian coordinate ----
+  RemapState rs{pe, peln, pk, pkz, delp.p, delz.p, pt.p, w.p, q.p, u.p, v.p, ps, ws};
+  RemapScratch rsc;
+  for (int n = 0; n < 11; ++n) rsc.s[n] = S(("_rm" + std::to_string(n)).c_str(), k1);
+  lagrangian_to_eulerian(c, npz, nq, ptop, nl.fill != 0, ak_dev, bk_dev, rs, rsc);
+  HIP_CHECK(hipEventRecord(ev[3], st));
+
+  // ---- exit: T, omega, A-grid winds ----
+  fv_wrapup(c, npz, nq, q.p, delp.p, delz.p, w.p, pt.p, omga);
+  halo_update({{"u", 'd'}, {"v", 'd'}});
+  c2l_ord4(c, npz, u.p, v.p, ua, va);
+  HIP_CHECK(hipEventRecord(ev[4], st));
+  HIP_CHECK(hipEventSynchronize(ev[4]));
+  const char* names[4] = {"dyn_core", "tracer_2d", "remap", "exit"};
+  for (int n = 0; n < 4; ++n) {
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, ev[n], ev[n + 1]));
+    timers[names[n]] += ms;
+  }
+  float tot = 0;
+  HIP_CHECK(hipEventElapsedTime(&tot, ev[0], ev[4]));
+  timers["fv_dynamics"] += tot;
+  timers["steps"] += 1;
+  if (ktimer_enabled()) ktimer_flush();
+  for (auto& e : ev) (void)hipEventDestroy(e);
+}
 
 }  // namespace gtfv3

@@ -48,6 +48,8 @@ class Dycore {
 
   Field& field(const std::string& name, int nk);  // get or create (zeroed)
   Field* find(const std::string& name);
+  Field& need(const std::string& name, int nk);  // existing field, level count checked
+  const double* vertical_dev();                  // ak | bk | dp_ref on device
   Ctx ctx() const;
   long field_elems(int nk) const { return (long)d.nsub * nk * d.plane; }
 

@@ -215,7 +215,7 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
       foff[f] = off;
       int n = n_send_[F.kind];
       if (n) {
-        hipLaunchKernelGGL(halo_pack_kernel, dim3(cdiv(n, 256), F.nk), dim3(256), 0, stream,
+        GT_LAUNCH(halo_pack_kernel, dim3(cdiv(n, 256), F.nk), dim3(256), 0, stream,
                            d_send_[F.kind], n, F.nk, d_.plane, F.p[0], F.p[1] ? F.p[1] : F.p[0],
                            sendbuf_ + off);
         HIP_LAUNCH_CHECK();
@@ -244,7 +244,7 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
     const HaloField& F = fields[f];
     int n = n_local_[F.kind];
     if (!n) continue;
-    hipLaunchKernelGGL(halo_local_kernel, dim3(cdiv(n, 256), F.nk), dim3(256), 0, stream, d_local_[F.kind], n,
+    GT_LAUNCH(halo_local_kernel, dim3(cdiv(n, 256), F.nk), dim3(256), 0, stream, d_local_[F.kind], n,
                        F.nk, d_.plane, F.p[0], F.p[1] ? F.p[1] : F.p[0]);
     HIP_LAUNCH_CHECK();
   }
@@ -253,7 +253,7 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
       const HaloField& F = fields[f];
       int n = n_recv_[F.kind];
       if (!n) continue;
-      hipLaunchKernelGGL(halo_unpack_kernel, dim3(cdiv(n, 256), F.nk), dim3(256), 0, stream, d_recv_[F.kind], n,
+      GT_LAUNCH(halo_unpack_kernel, dim3(cdiv(n, 256), F.nk), dim3(256), 0, stream, d_recv_[F.kind], n,
                          F.nk, d_.plane, F.p[0], F.p[1] ? F.p[1] : F.p[0], recvbuf_ + foff[f]);
       HIP_LAUNCH_CHECK();
     }

@@ -2,6 +2,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <map>
 #include <stdexcept>
 #include <string>
 
@@ -25,5 +26,37 @@ __host__ __device__ inline long pidx(const Dims& d, int i, int j) {
 }
 
 inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
+
+// Optional per-kernel timing: when enabled, every GT_LAUNCH brackets its kernel
+// with a pair of HIP events on the launch stream; ktimer_flush() (after a stream
+// sync) folds them into per-kernel totals.  Off by default: zero cost then.
+struct KernelStat {
+  double ms = 0.0;
+  long launches = 0;
+};
+bool ktimer_enabled();
+void ktimer_enable(bool on);
+void ktimer_begin(const char* name, hipStream_t s);
+void ktimer_end(hipStream_t s);
+void ktimer_flush();
+void ktimer_reset();
+const std::map<std::string, KernelStat>& ktimer_stats();
+
+struct KScope {
+  bool on;
+  hipStream_t s;
+  KScope(const char* n, hipStream_t st) : on(ktimer_enabled()), s(st) {
+    if (on) ktimer_begin(n, s);
+  }
+  ~KScope() {
+    if (on) ktimer_end(s);
+  }
+};
+
+#define GT_LAUNCH(kern, grid, block, shm, st, ...)        \
+  do {                                                    \
+    ::gtfv3::KScope kscope_(#kern, st);                   \
+    hipLaunchKernelGGL(kern, grid, block, shm, st, __VA_ARGS__); \
+  } while (0)
 
 }  // namespace gtfv3

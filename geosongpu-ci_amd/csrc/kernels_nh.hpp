@@ -1,0 +1,62 @@
+// kernels_nh.hpp — launchers of the non-hydrostatic (nh.hip) and remap (remap.hip) kernels.
+#pragma once
+#include "kernels.hpp"
+
+namespace gtfv3 {
+
+// per-column work planes (each npz+1 levels, [sub][k][plane])
+struct NhScratch {
+  double* s[14];
+};
+
+void update_dz_c(const Ctx& c, int npz, const double* dp0, const double* ut, const double* vt, const double* gz,
+                 double* gz_out);
+// clamp + ws + SIM1 on the C-grid half step; gz: heights in, geopotential out
+void riem_solver_c(const Ctx& c, int npz, double dt2, double ptop, double p_fac, double dz_min, const double* delpc,
+                   const double* ptc, const double* wc, const double* phis, double* gz, double* pef,
+                   const NhScratch& sc);
+void p_grad_c(const Ctx& c, int npz, double dt2, const double* delpc, const double* pkc, const double* gz, double* uc,
+              double* vc);
+
+struct UdzdArgs {
+  int npz, hord;
+  const double* dp0;
+  const double *crx, *cry, *xfx, *yfx;
+  double *crx_e, *cry_e, *xfx_e, *yfx_e, *ra_x, *ra_y, *fx, *fy, *gam;
+  double* zh;
+  double *tp_fx2, *tp_fy2, *tp_qi, *tp_qj;
+};
+void update_dz_d(const Ctx& c, const UdzdArgs& a);
+
+struct Riem3Args {
+  int npz;
+  double dt, ptop, p_fac, dz_min;
+  int last_call;
+  const double *delp, *pt, *phis;
+  double *w, *delz, *zh, *ppe, *pk3, *pe, *peln, *pk;
+  double* ws;  // surface w (dz/dt of the ground), consumed by the remap; may be null
+};
+void riem_solver3(const Ctx& c, const Riem3Args& a, const NhScratch& sc);
+void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* delp, double* pk3, double* pe);
+void a2b_ord4(const Ctx& c, int nk, const double* q, double* qout, double* qx, double* qy);
+
+struct NhPgArgs {
+  int npz;
+  double dt, ptop;
+  const double *pp, *pk3, *gz, *delp;
+  double *ppb, *pkb, *gzb, *wk1, *qx, *qy;
+  double *u, *v;
+};
+void nh_p_grad(const Ctx& c, const NhPgArgs& a);
+void scale_field(const Ctx& c, long n, double a, const double* x, double* y);
+
+struct RemapState {
+  double *pe, *peln, *pk, *pkz, *delp, *delz, *pt, *w, *q, *u, *v, *ps, *ws;
+};
+struct RemapScratch {
+  double* s[11];
+};
+void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fill, const double* ak_dev,
+                            const double* bk_dev, const RemapState& S, const RemapScratch& R);
+
+}  // namespace gtfv3

@@ -1,0 +1,189 @@
+// misc.hip — pointwise pieces of fv_dynamics on gfx950: entry conversion to
+// virtual potential temperature + pkz, zh from delz, exit conversion (T, omega),
+// cubed_to_latlon (c2l_ord4) and the Held & Suarez (1994) forcing of GEOShs.
+#include "kernels_misc.hpp"
+#include "stencil_common.hpp"
+
+namespace gtfv3 {
+namespace {
+
+constexpr double GRAV = Constants::grav;
+constexpr double RDGAS = Constants::rdgas;
+constexpr double KAPPA = Constants::kappa;
+constexpr double ZVIR = Constants::zvir;
+
+#define KSETUP3(nk_)                                                 \
+  int i, j;                                                          \
+  if (!thread_point(L, i, j)) return;                                \
+  const int z = blockIdx.z, s = z / (nk_);                           \
+  const SubInfo sub = subs[s];                                       \
+  const int N = sub.N;                                               \
+  const int I = i + sub.ioff, J = j + sub.joff;                      \
+  const long zo = (long)z * d.plane;                                 \
+  const long o = pidx(d, i, j);                                      \
+  (void)I; (void)J; (void)N; (void)zo;
+#define MT(name) met(M, d, name, s)
+#define AT(arr, di, dj) arr[zo + o + (long)(dj) * d.pitch + (di)]
+#define MA(arr, di, dj) arr[o + (long)(dj) * d.pitch + (di)]
+
+// fv_dynamics entry: pkz from the non-hydrostatic state, pt -> virtual potential temperature
+__global__ void __launch_bounds__(256) prep_k(Dims d, const SubInfo* __restrict__ subs, int npz, int nq,
+                                              const double* __restrict__ delp, const double* __restrict__ delz,
+                                              const double* __restrict__ q, double* __restrict__ pt,
+                                              double* __restrict__ pkz) {
+  Launch2D L{0, 0, d.nx, d.ny};
+  KSETUP3(npz)
+  const int k = z % npz;
+  const double rdg = -RDGAS * (1.0 / GRAV);
+  const double qv = q[((long)s * nq * npz + k) * d.plane + o];  // tracer 0 = specific humidity
+  const double dp1 = ZVIR * qv;
+  double pk = exp(KAPPA * log(rdg * AT(delp, 0, 0) * AT(pt, 0, 0) * (1.0 + dp1) / AT(delz, 0, 0)));
+  AT(pkz, 0, 0) = pk;
+  AT(pt, 0, 0) = AT(pt, 0, 0) * (1.0 + dp1) / pk;
+}
+
+// zh (interface heights) from delz and the surface height
+__global__ void __launch_bounds__(256) zh_init_k(Dims d, int npz, const double* __restrict__ phis,
+                                                 const double* __restrict__ delz, double* __restrict__ zh) {
+  Launch2D L{0, 0, d.nx, d.ny};
+  int i, j;
+  if (!thread_point(L, i, j)) return;
+  const int s = blockIdx.z;
+  const long o = pidx(d, i, j);
+  double* Z = zh + (long)s * (npz + 1) * d.plane + o;
+  const double* DZ = delz + (long)s * npz * d.plane + o;
+  double zc = phis[(long)s * d.plane + o] * (1.0 / GRAV);
+  Z[(long)npz * d.plane] = zc;
+  for (int k = npz - 1; k >= 0; --k) {
+    zc = zc - DZ[(long)k * d.plane];
+    Z[(long)k * d.plane] = zc;
+  }
+}
+
+// fv_dynamics exit: T_v -> T and omega from w
+__global__ void __launch_bounds__(256) wrapup_k(Dims d, const SubInfo* __restrict__ subs, int npz, int nq,
+                                                const double* __restrict__ q, const double* __restrict__ delp,
+                                                const double* __restrict__ delz, const double* __restrict__ w,
+                                                double* __restrict__ pt, double* __restrict__ omga) {
+  Launch2D L{0, 0, d.nx, d.ny};
+  KSETUP3(npz)
+  const int k = z % npz;
+  const double qv = q[((long)s * nq * npz + k) * d.plane + o];
+  AT(pt, 0, 0) = AT(pt, 0, 0) / (1.0 + ZVIR * qv);
+  AT(omga, 0, 0) = AT(delp, 0, 0) / AT(delz, 0, 0) * AT(w, 0, 0);
+}
+
+// cubed_to_latlon: c2l_ord4 (4-point Lagrange in the interior, 2nd order at tile edges)
+__global__ void __launch_bounds__(256) c2l_k(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                             int npz, const double* __restrict__ u, const double* __restrict__ v,
+                                             double* __restrict__ ua, double* __restrict__ va) {
+  Launch2D L{0, 0, d.nx, d.ny};
+  KSETUP3(npz)
+  const double C1 = 1.125, C2 = -0.125;
+  const double* dx = MT(M_DX);
+  const double* dy = MT(M_DY);
+  double ut = C2 * (AT(u, 0, -1) + AT(u, 0, 2)) + C1 * (AT(u, 0, 0) + AT(u, 0, 1));
+  double vt = C2 * (AT(v, -1, 0) + AT(v, 2, 0)) + C1 * (AT(v, 0, 0) + AT(v, 1, 0));
+  if (J == 0 || J == N - 1) {
+    vt = 2.0 * (AT(v, 0, 0) * MA(dy, 0, 0) + AT(v, 1, 0) * MA(dy, 1, 0)) / (MA(dy, 0, 0) + MA(dy, 1, 0));
+    ut = 2.0 * (AT(u, 0, 0) * MA(dx, 0, 0) + AT(u, 0, 1) * MA(dx, 0, 1)) / (MA(dx, 0, 0) + MA(dx, 0, 1));
+  }
+  if (I == 0 || I == N - 1) {
+    ut = 2.0 * (AT(u, 0, 0) * MA(dx, 0, 0) + AT(u, 0, 1) * MA(dx, 0, 1)) / (MA(dx, 0, 0) + MA(dx, 0, 1));
+    vt = 2.0 * (AT(v, 0, 0) * MA(dy, 0, 0) + AT(v, 1, 0) * MA(dy, 1, 0)) / (MA(dy, 0, 0) + MA(dy, 1, 0));
+  }
+  AT(ua, 0, 0) = MA(MT(M_A11), 0, 0) * ut + MA(MT(M_A12), 0, 0) * vt;
+  AT(va, 0, 0) = MA(MT(M_A21), 0, 0) * ut + MA(MT(M_A22), 0, 0) * vt;
+}
+
+// Held & Suarez (1994) forcing, implicit in time: Newtonian cooling of T towards
+// T_eq(lat, p) and Rayleigh friction of the D-grid winds in the boundary layer.
+__global__ void __launch_bounds__(256) hs_k(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                            int npz, double dt, const double* __restrict__ pe,
+                                            double* __restrict__ pt, double* __restrict__ u, double* __restrict__ v) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KSETUP3(npz)
+  const int k = z % npz;
+  const double p0 = 1.0e5, sigb = 0.7;
+  const double ka = 1.0 / (40.0 * 86400.0), ks = 1.0 / (4.0 * 86400.0), kf = 1.0 / 86400.0;
+  const double dty = 60.0, dthz = 10.0;
+  const long e0 = ((long)s * (npz + 1) + k) * d.plane;
+  const long e1 = e0 + d.plane;
+  const long es = ((long)s * (npz + 1) + npz) * d.plane;
+  auto sigma = [&](long off) { return 0.5 * (pe[e0 + off] + pe[e1 + off]) / pe[es + off]; };
+  if (i < d.nx && j < d.ny) {
+    const double lat = MA(MT(M_LAT), 0, 0);
+    const double sl = sin(lat), cl = cos(lat);
+    const double pm = 0.5 * (pe[e0 + o] + pe[e1 + o]);
+    const double sg = pm / pe[es + o];
+    const double teq = fmax(200.0, (315.0 - dty * sl * sl - dthz * log(pm / p0) * cl * cl) * exp(KAPPA * log(pm / p0)));
+    const double kt = ka + (ks - ka) * fmax(0.0, (sg - sigb) / (1.0 - sigb)) * cl * cl * cl * cl;
+    AT(pt, 0, 0) = (AT(pt, 0, 0) + dt * kt * teq) / (1.0 + dt * kt);
+  }
+  if (i < d.nx) {  // u on x-edges: sigma averaged over the two adjacent cells
+    const double sg = 0.5 * (sigma(o) + sigma(o - d.pitch));
+    const double kv = kf * fmax(0.0, (sg - sigb) / (1.0 - sigb));
+    AT(u, 0, 0) = AT(u, 0, 0) / (1.0 + dt * kv);
+  }
+  if (j < d.ny) {
+    const double sg = 0.5 * (sigma(o) + sigma(o - 1));
+    const double kv = kf * fmax(0.0, (sg - sigb) / (1.0 - sigb));
+    AT(v, 0, 0) = AT(v, 0, 0) / (1.0 + dt * kv);
+  }
+}
+
+__global__ void fill_k(long n, double a, double* __restrict__ x) {
+  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long stride = (long)gridDim.x * blockDim.x;
+  for (; t < n; t += stride) x[t] = a;
+}
+
+inline dim3 g2(const Dims& d, const Launch2D& L, int nz) { return dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), nz); }
+
+}  // namespace
+
+void fv_prep(const Ctx& c, int npz, int nq, const double* delp, const double* delz, const double* q, double* pt,
+             double* pkz) {
+  const Dims& d = c.d;
+  Launch2D L{0, 0, d.nx, d.ny};
+  GT_LAUNCH(prep_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nq, delp, delz, q, pt,
+                     pkz);
+  HIP_LAUNCH_CHECK();
+}
+
+void zh_init(const Ctx& c, int npz, const double* phis, const double* delz, double* zh) {
+  const Dims& d = c.d;
+  Launch2D L{0, 0, d.nx, d.ny};
+  GT_LAUNCH(zh_init_k, g2(d, L, d.nsub), dim3(BX, BY), 0, c.st, d, npz, phis, delz, zh);
+  HIP_LAUNCH_CHECK();
+}
+
+void fv_wrapup(const Ctx& c, int npz, int nq, const double* q, const double* delp, const double* delz,
+               const double* w, double* pt, double* omga) {
+  const Dims& d = c.d;
+  Launch2D L{0, 0, d.nx, d.ny};
+  GT_LAUNCH(wrapup_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nq, q, delp, delz, w,
+                     pt, omga);
+  HIP_LAUNCH_CHECK();
+}
+
+void c2l_ord4(const Ctx& c, int npz, const double* u, const double* v, double* ua, double* va) {
+  const Dims& d = c.d;
+  Launch2D L{0, 0, d.nx, d.ny};
+  GT_LAUNCH(c2l_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, u, v, ua, va);
+  HIP_LAUNCH_CHECK();
+}
+
+void held_suarez(const Ctx& c, int npz, double dt, const double* pe, double* pt, double* u, double* v) {
+  const Dims& d = c.d;
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  GT_LAUNCH(hs_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt, pe, pt, u, v);
+  HIP_LAUNCH_CHECK();
+}
+
+void fill_field(const Ctx& c, long n, double a, double* x) {
+  GT_LAUNCH(fill_k, dim3(cdiv(n, 256) < 8192 ? cdiv(n, 256) : 8192), dim3(256), 0, c.st, n, a, x);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // namespace gtfv3

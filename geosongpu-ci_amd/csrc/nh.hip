@@ -1,0 +1,666 @@
+// nh.hip — non-hydrostatic pieces of dyn_core on gfx950: update_dz_c,
+// riem_solver_c / riem_solver3 (SIM1 semi-implicit vertical acoustic solve),
+// p_grad_c, edge_profile + update_dz_d, pk3_halo / pe_halo, a2b_ord4, nh_p_grad.
+// Column kernels put one (i,j) column per lane: a wavefront covers 64 consecutive
+// i, so every k-plane access is coalesced; per-column work arrays are planes of
+// scratch fields (same [sub][k][plane] layout).
+#include "kernels_nh.hpp"
+#include "stencil_common.hpp"
+
+namespace gtfv3 {
+namespace {
+
+constexpr double GRAV = Constants::grav;
+constexpr double RDGAS = Constants::rdgas;
+constexpr double KAPPA = Constants::kappa;
+constexpr double R3 = 1.0 / 3.0;
+
+#define KSETUP2(nk_)                                                 \
+  int i, j;                                                          \
+  if (!thread_point(L, i, j)) return;                                \
+  const int z = blockIdx.z, s = z / (nk_);                           \
+  const SubInfo sub = subs[s];                                       \
+  const int N = sub.N;                                               \
+  const int I = i + sub.ioff, J = j + sub.joff;                      \
+  const long zo = (long)z * d.plane;                                 \
+  const long o = pidx(d, i, j);                                      \
+  (void)I; (void)J; (void)N; (void)zo;
+#define MT(name) met(M, d, name, s)
+#define AT(arr, di, dj) arr[zo + o + (long)(dj) * d.pitch + (di)]
+#define MA(arr, di, dj) arr[o + (long)(dj) * d.pitch + (di)]
+
+// strided column view
+struct Col {
+  double* p;
+  long st;
+  __device__ __forceinline__ double& operator[](int k) const { return p[(long)k * st]; }
+};
+__device__ __forceinline__ Col col(double* f, const Dims& d, int s, int nk, long o) {
+  return Col{f + (long)s * nk * d.plane + o, d.plane};
+}
+__device__ __forceinline__ Col ccol(const double* f, const Dims& d, int s, int nk, long o) {
+  return Col{const_cast<double*>(f) + (long)s * nk * d.plane + o, d.plane};
+}
+
+struct SimScratch {
+  Col pl, w1, g_rat, bb, dd, gam, pp, aa, pe;
+};
+
+// SIM1_solver (a_imp = 1, no moist cappa); arrays indexed by layer / interface
+__device__ void sim1(double dt, double gama, double kappa, int km, const Col& dm2, const Col& pm2, const Col& pem,
+                     const Col& w2, const Col& dz2, const Col& pt2, double ws, double p_fac, const SimScratch& S) {
+  const double t1g = gama * 2.0 * dt * dt;
+  const double rdt = 1.0 / dt;
+  const double capa1 = kappa - 1.0;
+  for (int k = 0; k < km; ++k) {
+    S.pl[k] = exp(gama * log(-dm2[k] / dz2[k] * RDGAS * pt2[k])) - pm2[k];
+    S.w1[k] = w2[k];
+  }
+  for (int k = 0; k < km - 1; ++k) {
+    double g = dm2[k] / dm2[k + 1];
+    S.g_rat[k] = g;
+    S.bb[k] = 2.0 * (1.0 + g);
+    S.dd[k] = 3.0 * (S.pl[k] + g * S.pl[k + 1]);
+  }
+  double bet = S.bb[0];
+  S.pp[0] = 0.0;
+  S.pp[1] = S.dd[0] / bet;
+  S.bb[km - 1] = 2.0;
+  S.dd[km - 1] = 3.0 * S.pl[km - 1];
+  for (int k = 1; k < km; ++k) {
+    double gm = S.g_rat[k - 1] / bet;
+    S.gam[k] = gm;
+    bet = S.bb[k] - gm;
+    S.pp[k + 1] = (S.dd[k] - S.pp[k]) / bet;
+  }
+  for (int k = km - 1; k > 0; --k) S.pp[k] = S.pp[k] - S.gam[k] * S.pp[k + 1];
+  for (int k = 1; k < km; ++k) S.aa[k] = t1g / (dz2[k - 1] + dz2[k]) * (pem[k] + S.pp[k]);
+  bet = dm2[0] - S.aa[1];
+  w2[0] = (dm2[0] * S.w1[0] + dt * S.pp[1]) / bet;
+  for (int k = 1; k < km - 1; ++k) {
+    double gm = S.aa[k] / bet;
+    S.gam[k] = gm;
+    bet = dm2[k] - (S.aa[k] + S.aa[k + 1] + S.aa[k] * gm);
+    w2[k] = (dm2[k] * S.w1[k] + dt * (S.pp[k + 1] - S.pp[k]) - S.aa[k] * w2[k - 1]) / bet;
+  }
+  double p1 = t1g / dz2[km - 1] * (pem[km] + S.pp[km]);
+  S.gam[km - 1] = S.aa[km - 1] / bet;
+  bet = dm2[km - 1] - (S.aa[km - 1] + p1 + S.aa[km - 1] * S.gam[km - 1]);
+  w2[km - 1] = (dm2[km - 1] * S.w1[km - 1] + dt * (S.pp[km] - S.pp[km - 1]) - p1 * ws - S.aa[km - 1] * w2[km - 2]) / bet;
+  for (int k = km - 2; k >= 0; --k) w2[k] = w2[k] - S.gam[k + 1] * w2[k + 1];
+  S.pe[0] = 0.0;
+  for (int k = 0; k < km; ++k) S.pe[k + 1] = S.pe[k] + dm2[k] * (w2[k] - S.w1[k]) * rdt;
+  p1 = (S.pe[km - 1] + 2.0 * S.pe[km]) * R3;
+  dz2[km - 1] = -dm2[km - 1] * RDGAS * pt2[km - 1] * exp(capa1 * log(fmax(p_fac * pm2[km - 1], p1 + pm2[km - 1])));
+  for (int k = km - 2; k >= 0; --k) {
+    p1 = (S.pe[k] + S.bb[k] * S.pe[k + 1] + S.g_rat[k] * S.pe[k + 2]) * R3 - S.g_rat[k] * p1;
+    dz2[k] = -dm2[k] * RDGAS * pt2[k] * exp(capa1 * log(fmax(p_fac * pm2[k], p1 + pm2[k])));
+  }
+}
+
+__device__ __forceinline__ SimScratch scratch_cols(const NhScratch& sc, const Dims& d, int s, int nk1, long o) {
+  SimScratch S;
+  S.pl = col(sc.s[0], d, s, nk1, o);
+  S.w1 = col(sc.s[1], d, s, nk1, o);
+  S.g_rat = col(sc.s[2], d, s, nk1, o);
+  S.bb = col(sc.s[3], d, s, nk1, o);
+  S.dd = col(sc.s[4], d, s, nk1, o);
+  S.gam = col(sc.s[5], d, s, nk1, o);
+  S.pp = col(sc.s[6], d, s, nk1, o);
+  S.aa = col(sc.s[7], d, s, nk1, o);
+  S.pe = col(sc.s[8], d, s, nk1, o);
+  return S;
+}
+
+// ---------------- update_dz_c (per interface level, out of place) ----------------
+__global__ void __launch_bounds__(256) udzc_k(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                              int npz, const double* __restrict__ dp0, const double* __restrict__ ut,
+                                              const double* __restrict__ vt, const double* __restrict__ gz,
+                                              double* __restrict__ gzo) {
+  Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
+  KSETUP2(npz + 1)
+  const int k = z % (npz + 1);
+  const int km = npz;
+  // xfx / yfx at faces (0: own, 1: +1 neighbour)
+  auto flux_lvl = [&](const double* a, long off) -> double {
+    const long b = (long)s * npz * d.plane + off;
+    if (k == 0) {
+      double top_ratio = dp0[0] / (dp0[1] + dp0[0]);
+      return a[b] + (a[b] - a[b + d.plane]) * top_ratio;
+    } else if (k == km) {
+      double bot_ratio = dp0[km - 1] / (dp0[km - 2] + dp0[km - 1]);
+      const double* c = a + (long)(km - 1) * d.plane;
+      return c[b] + (c[b] - c[b - d.plane]) * bot_ratio;
+    } else {
+      double int_ratio = 1.0 / (dp0[k - 1] + dp0[k]);
+      const double* c = a + (long)k * d.plane;
+      return (dp0[k] * c[b - d.plane] + dp0[k - 1] * c[b]) * int_ratio;
+    }
+  };
+  const double* g = gz + zo;
+  double xf0 = flux_lvl(ut, o), xf1 = flux_lvl(ut, o + 1);
+  double yf0 = flux_lvl(vt, o), yf1 = flux_lvl(vt, o + d.pitch);
+  double fx0 = xf0 * (xf0 > 0.0 ? g[cc_off(d, sub, i - 1, j, 1)] : g[cc_off(d, sub, i, j, 1)]);
+  double fx1 = xf1 * (xf1 > 0.0 ? g[cc_off(d, sub, i, j, 1)] : g[cc_off(d, sub, i + 1, j, 1)]);
+  double fy0 = yf0 * (yf0 > 0.0 ? g[cc_off(d, sub, i, j - 1, 2)] : g[cc_off(d, sub, i, j, 2)]);
+  double fy1 = yf1 * (yf1 > 0.0 ? g[cc_off(d, sub, i, j, 2)] : g[cc_off(d, sub, i, j + 1, 2)]);
+  const double area = MA(MT(M_AREA), 0, 0);
+  const double gc = g[cc_off(d, sub, i, j, 2)];
+  gzo[zo + o] = (gc * area + fx0 - fx1 + fy0 - fy1) / (area + xf0 - xf1 + yf0 - yf1);
+}
+
+// dz clamp + ws + riem_solver_c, one column per lane on cells [-1,nx]x[-1,ny]
+__global__ void __launch_bounds__(256) riem_c_k(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                                int npz, double dt2, double ptop, double p_fac, double dz_min,
+                                                const double* __restrict__ delpc, const double* __restrict__ ptc,
+                                                const double* __restrict__ wc, const double* __restrict__ phis,
+                                                double* __restrict__ gz, double* __restrict__ pef, NhScratch sc) {
+  Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
+  int i, j;
+  if (!thread_point(L, i, j)) return;
+  const int s = blockIdx.z;
+  const long o = pidx(d, i, j);
+  const int km = npz, k1 = npz + 1;
+  Col G = col(gz, d, s, k1, o), PF = col(pef, d, s, k1, o);
+  Col DPC = ccol(delpc, d, s, km, o), PTC = ccol(ptc, d, s, km, o), WC = ccol(wc, d, s, km, o);
+  const double hs = phis[(long)s * d.plane + o];
+  const double zs = hs * (1.0 / GRAV);
+  const double ws = (zs - G[km]) * (1.0 / dt2);
+  for (int k = km - 1; k >= 0; --k) G[k] = fmax(G[k], G[k + 1] + dz_min);
+  SimScratch S = scratch_cols(sc, d, s, k1, o);
+  Col PEM = col(sc.s[9], d, s, k1, o), DM = col(sc.s[10], d, s, k1, o), PM2 = col(sc.s[11], d, s, k1, o),
+      DZ2 = col(sc.s[12], d, s, k1, o), W2 = col(sc.s[13], d, s, k1, o);
+  PEM[0] = ptop;
+  for (int k = 1; k <= km; ++k) PEM[k] = PEM[k - 1] + DPC[k - 1];
+  for (int k = 0; k < km; ++k) {
+    DZ2[k] = G[k + 1] - G[k];
+    PM2[k] = DPC[k] / log(PEM[k + 1] / PEM[k]);
+    DM[k] = DPC[k] * (1.0 / GRAV);
+    W2[k] = WC[k];
+  }
+  const double gama = 1.0 / (1.0 - KAPPA);
+  sim1(dt2, gama, KAPPA, km, DM, PM2, PEM, W2, DZ2, PTC, ws, p_fac, S);
+  PF[0] = ptop;
+  for (int k = 1; k <= km; ++k) PF[k] = S.pe[k] + PEM[k];
+  G[km] = hs;
+  for (int k = km - 1; k >= 0; --k) G[k] = G[k + 1] - DZ2[k] * GRAV;
+}
+
+// C-grid pressure gradient (non-hydrostatic: wk = delpc)
+__global__ void __launch_bounds__(256) pgradc_k(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                                int npz, double dt2, const double* __restrict__ delpc,
+                                                const double* __restrict__ pkc, const double* __restrict__ gz,
+                                                double* __restrict__ uc, double* __restrict__ vc) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KSETUP2(npz)
+  const int k = z % npz;
+  const long p0 = ((long)s * (npz + 1) + k) * d.plane + o;  // interface k
+  const long p1 = p0 + d.plane;                             // interface k+1
+  if (j < d.ny) {
+    const long w = -1;
+    double wsum = AT(delpc, -1, 0) + AT(delpc, 0, 0);
+    AT(uc, 0, 0) = AT(uc, 0, 0) + dt2 * MA(MT(M_RDXC), 0, 0) / wsum *
+                                      ((gz[p1 + w] - gz[p0]) * (pkc[p1] - pkc[p0 + w]) +
+                                       (gz[p0 + w] - gz[p1]) * (pkc[p1 + w] - pkc[p0]));
+  }
+  if (i < d.nx) {
+    const long w = -d.pitch;
+    double wsum = AT(delpc, 0, -1) + AT(delpc, 0, 0);
+    AT(vc, 0, 0) = AT(vc, 0, 0) + dt2 * MA(MT(M_RDYC), 0, 0) / wsum *
+                                      ((gz[p1 + w] - gz[p0]) * (pkc[p1] - pkc[p0 + w]) +
+                                       (gz[p0 + w] - gz[p1]) * (pkc[p1 + w] - pkc[p0]));
+  }
+}
+
+// edge_profile of (crx, xfx) on x-face columns and (cry, yfx) on y-face columns
+__device__ void edge_profile_col(const Col& q, const Col& qe, const Col& gam, const double* dp0, int km) {
+  double g0 = dp0[1] / dp0[0];
+  double xt1 = 2.0 * g0 * (g0 + 1.0);
+  double bet = g0 * (g0 + 0.5);
+  qe[0] = (xt1 * q[0] + q[1]) / bet;
+  gam[0] = (1.0 + g0 * (g0 + 1.5)) / bet;
+  double gk = g0;
+  for (int k = 1; k < km; ++k) {
+    gk = dp0[k - 1] / dp0[k];
+    bet = 2.0 + 2.0 * gk - gam[k - 1];
+    qe[k] = (3.0 * (q[k - 1] + gk * q[k]) - qe[k - 1]) / bet;
+    gam[k] = gk / bet;
+  }
+  double a_bot = 1.0 + gk * (gk + 1.5);
+  xt1 = 2.0 * gk * (gk + 1.0);
+  double xt2 = gk * (gk + 0.5) - a_bot * gam[km - 1];
+  qe[km] = (xt1 * q[km - 1] + q[km - 2] - a_bot * qe[km - 1]) / xt2;
+  for (int k = km - 1; k >= 0; --k) qe[k] = qe[k] - gam[k] * qe[k + 1];
+}
+
+__global__ void __launch_bounds__(256) edge_prof_k(Dims d, int npz, const double* __restrict__ dp0,
+                                                   const double* __restrict__ crx, const double* __restrict__ xfx,
+                                                   const double* __restrict__ cry, const double* __restrict__ yfx,
+                                                   double* __restrict__ crx_e, double* __restrict__ xfx_e,
+                                                   double* __restrict__ cry_e, double* __restrict__ yfx_e,
+                                                   double* __restrict__ gam_scr) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  int i, j;
+  if (!thread_point(L, i, j)) return;
+  const int s = blockIdx.z;
+  const long o = pidx(d, i, j);
+  const int km = npz, k1 = npz + 1;
+  Col G = col(gam_scr, d, s, k1, o);
+  if (i >= 0 && i <= d.nx && j <= d.ny + NG - 1) {
+    edge_profile_col(ccol(crx, d, s, km, o), col(crx_e, d, s, k1, o), G, dp0, km);
+    edge_profile_col(ccol(xfx, d, s, km, o), col(xfx_e, d, s, k1, o), G, dp0, km);
+  }
+  if (j >= 0 && j <= d.ny && i <= d.nx + NG - 1) {
+    edge_profile_col(ccol(cry, d, s, km, o), col(cry_e, d, s, k1, o), G, dp0, km);
+    edge_profile_col(ccol(yfx, d, s, km, o), col(yfx_e, d, s, k1, o), G, dp0, km);
+  }
+}
+
+// ra_x, ra_y for the interface-level transport of zh
+__global__ void __launch_bounds__(256) ra_k(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                            int nk, const double* __restrict__ xfx, const double* __restrict__ yfx,
+                                            double* __restrict__ ra_x, double* __restrict__ ra_y) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
+  KSETUP2(nk)
+  const double area = MA(MT(M_AREA), 0, 0);
+  AT(ra_y, 0, 0) = (j >= 0 && j < d.ny) ? area + AT(yfx, 0, 0) - AT(yfx, 0, 1) : 0.0;
+  AT(ra_x, 0, 0) = (i >= 0 && i < d.nx) ? area + AT(xfx, 0, 0) - AT(xfx, 1, 0) : 0.0;
+}
+
+// zh update from the transported fluxes (compute cells, all interfaces)
+__global__ void __launch_bounds__(256) zh_update_k(Dims d, const SubInfo* __restrict__ subs,
+                                                   const double* __restrict__ M, int nk, const double* __restrict__ fx,
+                                                   const double* __restrict__ fy, const double* __restrict__ ra_x,
+                                                   const double* __restrict__ ra_y, double* __restrict__ zh) {
+  Launch2D L{0, 0, d.nx, d.ny};
+  KSETUP2(nk)
+  const double area = MA(MT(M_AREA), 0, 0);
+  AT(zh, 0, 0) = (AT(zh, 0, 0) * area + AT(fx, 0, 0) - AT(fx, 1, 0) + AT(fy, 0, 0) - AT(fy, 0, 1)) /
+                 (AT(ra_x, 0, 0) + AT(ra_y, 0, 0) - area);
+}
+
+// update_dz_d clamp + ws + riem_solver3 on compute columns
+__global__ void __launch_bounds__(256) riem3_k(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                               int npz, double dt, double ptop, double p_fac, double dz_min,
+                                               int last_call, const double* __restrict__ delp,
+                                               const double* __restrict__ pt, const double* __restrict__ phis,
+                                               double* __restrict__ w, double* __restrict__ delz,
+                                               double* __restrict__ zh, double* __restrict__ ppe,
+                                               double* __restrict__ pk3, double* __restrict__ pe,
+                                               double* __restrict__ peln, double* __restrict__ pk, double* __restrict__ wsout,
+                                               NhScratch sc) {
+  Launch2D L{0, 0, d.nx, d.ny};
+  int i, j;
+  if (!thread_point(L, i, j)) return;
+  const int s = blockIdx.z;
+  const long o = pidx(d, i, j);
+  const int km = npz, k1 = npz + 1;
+  Col Z = col(zh, d, s, k1, o);
+  const double zs = phis[(long)s * d.plane + o] * (1.0 / GRAV);
+  const double ws = (zs - Z[km]) * (1.0 / dt);
+  if (wsout) wsout[(long)s * d.plane + o] = ws;
+  for (int k = km - 1; k >= 0; --k) Z[k] = fmax(Z[k], Z[k + 1] + dz_min);
+  SimScratch S = scratch_cols(sc, d, s, k1, o);
+  Col PEM = col(sc.s[9], d, s, k1, o), DM = col(sc.s[10], d, s, k1, o), PM2 = col(sc.s[11], d, s, k1, o),
+      DZ2 = col(sc.s[12], d, s, k1, o), PLN = col(sc.s[13], d, s, k1, o);
+  Col DP = ccol(delp, d, s, km, o), PT = ccol(pt, d, s, km, o), W = col(w, d, s, km, o);
+  Col PK3 = col(pk3, d, s, k1, o);
+  const double peln1 = log(ptop);
+  const double ptk = exp(KAPPA * peln1);
+  PEM[0] = ptop;
+  PLN[0] = peln1;
+  PK3[0] = ptk;
+  for (int k = 1; k <= km; ++k) {
+    PEM[k] = PEM[k - 1] + DP[k - 1];
+    PLN[k] = log(PEM[k]);
+    PK3[k] = exp(KAPPA * PLN[k]);
+  }
+  for (int k = 0; k < km; ++k) {
+    PM2[k] = DP[k] / (PLN[k + 1] - PLN[k]);
+    DM[k] = DP[k] * (1.0 / GRAV);
+    DZ2[k] = Z[k + 1] - Z[k];
+  }
+  const double gama = 1.0 / (1.0 - KAPPA);
+  sim1(dt, gama, KAPPA, km, DM, PM2, PEM, W, DZ2, PT, ws, p_fac, S);
+  Col DZ = col(delz, d, s, km, o), PP = col(ppe, d, s, k1, o);
+  for (int k = 0; k < km; ++k) DZ[k] = DZ2[k];
+  if (last_call) {
+    Col PE = col(pe, d, s, k1, o), PL = col(peln, d, s, k1, o), PK = col(pk, d, s, k1, o);
+    for (int k = 0; k <= km; ++k) {
+      PL[k] = PLN[k];
+      PK[k] = PK3[k];
+      PE[k] = PEM[k];
+    }
+  }
+  for (int k = 0; k <= km; ++k) PP[k] = S.pe[k];
+  Z[km] = zs;
+  for (int k = km - 1; k >= 0; --k) Z[k] = Z[k + 1] - DZ2[k];
+}
+
+// pk3 on the 2-wide halo ring and pe on the 1-wide ring (from the halo-updated delp)
+__global__ void __launch_bounds__(256) pk3_pe_halo_k(Dims d, int npz, double ptop, int do_pe,
+                                                     const double* __restrict__ delp, double* __restrict__ pk3,
+                                                     double* __restrict__ pe) {
+  Launch2D L{-2, -2, d.nx + 4, d.ny + 4};
+  int i, j;
+  if (!thread_point(L, i, j)) return;
+  if (i >= 0 && i < d.nx && j >= 0 && j < d.ny) return;
+  const int s = blockIdx.z;
+  const long o = pidx(d, i, j);
+  const int km = npz, k1 = npz + 1;
+  Col DP = ccol(delp, d, s, km, o), PK = col(pk3, d, s, k1, o);
+  const bool ring1 = i >= -1 && i <= d.nx && j >= -1 && j <= d.ny;
+  Col PE = col(pe, d, s, k1, o);
+  double pei = ptop;
+  if (do_pe && ring1) PE[0] = ptop;
+  for (int k = 0; k < km; ++k) {
+    pei = pei + DP[k];
+    PK[k + 1] = exp(KAPPA * log(pei));
+    if (do_pe && ring1) PE[k + 1] = pei;
+  }
+}
+
+// ---------------- a2b_ord4 (3 passes) ----------------
+constexpr double B1 = 7.0 / 12.0, B2 = -1.0 / 12.0;
+constexpr double AA1 = 0.5625, AA2 = -0.0625;
+constexpr double AC1 = 2.0 / 3.0, AC2 = -1.0 / 6.0;
+
+__global__ void __launch_bounds__(256) a2b_qxqy_k(Dims d, const SubInfo* __restrict__ subs,
+                                                  const double* __restrict__ M, int nk, const double* __restrict__ q,
+                                                  double* __restrict__ qx, double* __restrict__ qy) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  KSETUP2(nk)
+  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+  const double* dxa = MT(M_DXA);
+  const double* dya = MT(M_DYA);
+  double vx = 0.0, vy = 0.0;
+  const bool rows = J >= max(0, jo - 2) && J <= min(N - 1, jo + ny + 1);
+  if (rows) {
+    auto gen = [&](int di) {
+      return B2 * (AT(q, di - 2, 0) + AT(q, di + 1, 0)) + B1 * (AT(q, di - 1, 0) + AT(q, di, 0));
+    };
+    if (I == 0) {
+      double gr = MA(dxa, 1, 0) / MA(dxa, 0, 0);
+      vx = 0.5 * ((2.0 + gr) * (AT(q, -1, 0) + AT(q, 0, 0)) - (AT(q, -2, 0) + AT(q, 1, 0))) / (1.0 + gr);
+    } else if (I == N) {
+      double gr = MA(dxa, -2, 0) / MA(dxa, -1, 0);
+      vx = 0.5 * ((2.0 + gr) * (AT(q, -1, 0) + AT(q, 0, 0)) - (AT(q, -2, 0) + AT(q, 1, 0))) / (1.0 + gr);
+    } else if (I == 1) {
+      double g1 = MA(dxa, 0, 0) / MA(dxa, -1, 0);
+      double gw = MA(dxa, 0, 0) / MA(dxa, -1, 0);  // ratio at the edge I = 0: dxa(1)/dxa(0)
+      double qx0 = 0.5 * ((2.0 + gw) * (AT(q, -2, 0) + AT(q, -1, 0)) - (AT(q, -3, 0) + AT(q, 0, 0))) / (1.0 + gw);
+      vx = (3.0 * (g1 * AT(q, -1, 0) + AT(q, 0, 0)) - (g1 * qx0 + gen(1))) / (2.0 + 2.0 * g1);
+    } else if (I == N - 1) {
+      double g1 = MA(dxa, -1, 0) / MA(dxa, 0, 0);
+      double ge = MA(dxa, -1, 0) / MA(dxa, 0, 0);  // ratio at the edge I = N: dxa(N-2)/dxa(N-1)
+      double qxN = 0.5 * ((2.0 + ge) * (AT(q, 0, 0) + AT(q, 1, 0)) - (AT(q, -1, 0) + AT(q, 2, 0))) / (1.0 + ge);
+      vx = (3.0 * (AT(q, -1, 0) + g1 * AT(q, 0, 0)) - (g1 * qxN + gen(-1))) / (2.0 + 2.0 * g1);
+    } else if (I >= max(2, io) && I <= min(N - 2, io + nx)) {
+      vx = gen(0);
+    }
+  }
+  const bool cols = I >= max(0, io - 2) && I <= min(N - 1, io + nx + 1);
+  if (cols) {
+    auto gen = [&](int dj) {
+      return B2 * (AT(q, 0, dj - 2) + AT(q, 0, dj + 1)) + B1 * (AT(q, 0, dj - 1) + AT(q, 0, dj));
+    };
+    if (J == 0) {
+      double gr = MA(dya, 0, 1) / MA(dya, 0, 0);
+      vy = 0.5 * ((2.0 + gr) * (AT(q, 0, -1) + AT(q, 0, 0)) - (AT(q, 0, -2) + AT(q, 0, 1))) / (1.0 + gr);
+    } else if (J == N) {
+      double gr = MA(dya, 0, -2) / MA(dya, 0, -1);
+      vy = 0.5 * ((2.0 + gr) * (AT(q, 0, -1) + AT(q, 0, 0)) - (AT(q, 0, -2) + AT(q, 0, 1))) / (1.0 + gr);
+    } else if (J == 1) {
+      double g1 = MA(dya, 0, 0) / MA(dya, 0, -1);
+      double gs = MA(dya, 0, 0) / MA(dya, 0, -1);
+      double qy0 = 0.5 * ((2.0 + gs) * (AT(q, 0, -2) + AT(q, 0, -1)) - (AT(q, 0, -3) + AT(q, 0, 0))) / (1.0 + gs);
+      vy = (3.0 * (g1 * AT(q, 0, -1) + AT(q, 0, 0)) - (g1 * qy0 + gen(1))) / (2.0 + 2.0 * g1);
+    } else if (J == N - 1) {
+      double g1 = MA(dya, 0, -1) / MA(dya, 0, 0);
+      double gn = MA(dya, 0, -1) / MA(dya, 0, 0);
+      double qyN = 0.5 * ((2.0 + gn) * (AT(q, 0, 0) + AT(q, 0, 1)) - (AT(q, 0, -1) + AT(q, 0, 2))) / (1.0 + gn);
+      vy = (3.0 * (AT(q, 0, -1) + g1 * AT(q, 0, 0)) - (g1 * qyN + gen(-1))) / (2.0 + 2.0 * g1);
+    } else if (J >= max(2, jo) && J <= min(N - 2, jo + ny)) {
+      vy = gen(0);
+    }
+  }
+  AT(qx, 0, 0) = vx;
+  AT(qy, 0, 0) = vy;
+}
+
+// qout on cube corners and tile-edge lines
+__global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restrict__ subs,
+                                                  const double* __restrict__ M, int nk, const double* __restrict__ cw,
+                                                  const double* __restrict__ q, const double* __restrict__ qx,
+                                                  const double* __restrict__ qy, double* __restrict__ qout) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KSETUP2(nk)
+  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+  // cube corner value (extrapolation from the three faces)
+  auto corner_val = [&](int c) {
+    const int pr[4][3][4] = {{{0, 0, 1, 1}, {-1, 0, -2, 1}, {0, -1, 1, -2}},
+                             {{N - 1, 0, N - 2, 1}, {N - 1, -1, N - 2, -2}, {N, 0, N + 1, 1}},
+                             {{N - 1, N - 1, N - 2, N - 2}, {N, N - 1, N + 1, N - 2}, {N - 1, N, N - 2, N + 1}},
+                             {{0, N - 1, 1, N - 2}, {-1, N - 1, -2, N - 2}, {0, N, 1, N + 1}}};
+    double acc = 0.0;
+    for (int r = 0; r < 3; ++r) {
+      double q1 = q[zo + pidx(d, pr[c][r][0] - io, pr[c][r][1] - jo)];
+      double q2 = q[zo + pidx(d, pr[c][r][2] - io, pr[c][r][3] - jo)];
+      double e = q1 + cw[(long)s * 12 + c * 3 + r] * (q1 - q2);
+      acc = r == 0 ? e : acc + e;
+    }
+    return acc * R3;
+  };
+  auto gq = [&](const double* a, int Ig, int Jg) { return a[zo + pidx(d, Ig - io, Jg - jo)]; };
+  auto colv = [&](int Ig, int Jg) {  // W/E edge generic
+    return AA2 * (gq(qx, Ig, Jg - 2) + gq(qx, Ig, Jg + 1)) + AA1 * (gq(qx, Ig, Jg - 1) + gq(qx, Ig, Jg));
+  };
+  auto rowv = [&](int Ig, int Jg) {
+    return AA2 * (gq(qy, Ig - 2, Jg) + gq(qy, Ig + 1, Jg)) + AA1 * (gq(qy, Ig - 1, Jg) + gq(qy, Ig, Jg));
+  };
+  auto edge_or_corner = [&](int Ig, int Jg) -> double {  // value of qout at a tile-edge point (recursive-free)
+    if (Ig == 0 && Jg == 0) return corner_val(0);
+    if (Ig == N && Jg == 0) return corner_val(1);
+    if (Ig == N && Jg == N) return corner_val(2);
+    if (Ig == 0 && Jg == N) return corner_val(3);
+    if (Ig == 0 || Ig == N) return colv(Ig, Jg);
+    return rowv(Ig, Jg);
+  };
+  double val;
+  bool set = true;
+  if ((I == 0 || I == N) && (J == 0 || J == N)) val = edge_or_corner(I, J);
+  else if ((I == 0 && io == 0) || (I == N && io + nx == N)) {
+    if (J == 1 && jo == 0) val = AC1 * (gq(qx, I, 0) + gq(qx, I, 1)) + AC2 * (edge_or_corner(I, 0) + colv(I, 2));
+    else if (J == N - 1 && jo + ny == N)
+      val = AC1 * (gq(qx, I, N - 2) + gq(qx, I, N - 1)) + AC2 * (colv(I, N - 2) + edge_or_corner(I, N));
+    else if (J >= max(2, jo) && J <= min(N - 2, jo + ny)) val = colv(I, J);
+    else set = false;
+  } else if ((J == 0 && jo == 0) || (J == N && jo + ny == N)) {
+    if (I == 1 && io == 0) val = AC1 * (gq(qy, 0, J) + gq(qy, 1, J)) + AC2 * (edge_or_corner(0, J) + rowv(2, J));
+    else if (I == N - 1 && io + nx == N)
+      val = AC1 * (gq(qy, N - 2, J) + gq(qy, N - 1, J)) + AC2 * (rowv(N - 2, J) + edge_or_corner(N, J));
+    else if (I >= max(2, io) && I <= min(N - 2, io + nx)) val = rowv(I, J);
+    else set = false;
+  } else {
+    set = false;
+  }
+  if (set) AT(qout, 0, 0) = val;
+}
+
+// interior qout = 0.5 * (qxx + qyy)
+__global__ void __launch_bounds__(256) a2b_inner_k(Dims d, const SubInfo* __restrict__ subs, int nk,
+                                                   const double* __restrict__ qx, const double* __restrict__ qy,
+                                                   double* __restrict__ qout) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KSETUP2(nk)
+  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+  const bool icols = I >= max(1, io) && I <= min(N - 1, io + nx);
+  const bool jrows = J >= max(1, jo) && J <= min(N - 1, jo + ny);
+  if (!(icols && jrows)) return;
+  auto qxx_gen = [&](int dj) {
+    return AA2 * (AT(qx, 0, dj - 2) + AT(qx, 0, dj + 1)) + AA1 * (AT(qx, 0, dj - 1) + AT(qx, 0, dj));
+  };
+  auto qyy_gen = [&](int di) {
+    return AA2 * (AT(qy, di - 2, 0) + AT(qy, di + 1, 0)) + AA1 * (AT(qy, di - 1, 0) + AT(qy, di, 0));
+  };
+  double qxx, qyy;
+  if (J == 1) qxx = AC1 * (AT(qx, 0, -1) + AT(qx, 0, 0)) + AC2 * (AT(qout, 0, -1) + qxx_gen(1));
+  else if (J == N - 1) qxx = AC1 * (AT(qx, 0, -1) + AT(qx, 0, 0)) + AC2 * (AT(qout, 0, 1) + qxx_gen(-1));
+  else qxx = qxx_gen(0);
+  if (I == 1) qyy = AC1 * (AT(qy, -1, 0) + AT(qy, 0, 0)) + AC2 * (AT(qout, -1, 0) + qyy_gen(1));
+  else if (I == N - 1) qyy = AC1 * (AT(qy, -1, 0) + AT(qy, 0, 0)) + AC2 * (AT(qout, 1, 0) + qyy_gen(-1));
+  else qyy = qyy_gen(0);
+  AT(qout, 0, 0) = 0.5 * (qxx + qyy);
+}
+
+// non-hydrostatic pressure gradient on the D-grid winds (u, v arrive x dx, dy)
+__global__ void __launch_bounds__(256) nhpgrad_k(Dims d, const SubInfo* __restrict__ subs,
+                                                 const double* __restrict__ M, int npz, double dt, double ptk,
+                                                 const double* __restrict__ ppb, const double* __restrict__ gzb,
+                                                 const double* __restrict__ pkb, const double* __restrict__ wk1,
+                                                 double* __restrict__ u, double* __restrict__ v) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KSETUP2(npz)
+  const int k = z % npz;
+  const long p0 = ((long)s * (npz + 1) + k) * d.plane + o;
+  const long p1 = p0 + d.plane;
+  // level-0 interface values are the model-top constants (pp = 0, pk = ptop**kappa)
+  const double pk0 = k == 0 ? ptk : pkb[p0];
+  const double pp0 = k == 0 ? 0.0 : ppb[p0];
+  if (i < d.nx) {
+    const long e = 1;
+    const double pk0e = k == 0 ? ptk : pkb[p0 + e];
+    const double pp0e = k == 0 ? 0.0 : ppb[p0 + e];
+    double wk0 = pkb[p1] - pk0, wke = pkb[p1 + e] - pk0e;
+    double du1 = dt / (wk0 + wke) *
+                 ((gzb[p1] - gzb[p0 + e]) * (pkb[p1 + e] - pk0) + (gzb[p0] - gzb[p1 + e]) * (pkb[p1] - pk0e));
+    AT(u, 0, 0) = (AT(u, 0, 0) + du1 +
+                   dt / (AT(wk1, 0, 0) + AT(wk1, 1, 0)) *
+                       ((gzb[p1] - gzb[p0 + e]) * (ppb[p1 + e] - pp0) + (gzb[p0] - gzb[p1 + e]) * (ppb[p1] - pp0e))) *
+                  MA(MT(M_RDX), 0, 0);
+  }
+  if (j < d.ny) {
+    const long e = d.pitch;
+    const double pk0e = k == 0 ? ptk : pkb[p0 + e];
+    const double pp0e = k == 0 ? 0.0 : ppb[p0 + e];
+    double wk0 = pkb[p1] - pk0, wke = pkb[p1 + e] - pk0e;
+    double dv1 = dt / (wk0 + wke) *
+                 ((gzb[p1] - gzb[p0 + e]) * (pkb[p1 + e] - pk0) + (gzb[p0] - gzb[p1 + e]) * (pkb[p1] - pk0e));
+    AT(v, 0, 0) = (AT(v, 0, 0) + dv1 +
+                   dt / (AT(wk1, 0, 0) + AT(wk1, 0, 1)) *
+                       ((gzb[p1] - gzb[p0 + e]) * (ppb[p1 + e] - pp0) + (gzb[p0] - gzb[p1 + e]) * (ppb[p1] - pp0e))) *
+                  MA(MT(M_RDY), 0, 0);
+  }
+}
+
+__global__ void scale_k(long n, double a, const double* __restrict__ x, double* __restrict__ y) {
+  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long stride = (long)gridDim.x * blockDim.x;
+  for (; t < n; t += stride) y[t] = a * x[t];
+}
+
+inline dim3 g2(const Dims& d, const Launch2D& L, int nz) { return dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), nz); }
+
+}  // namespace
+
+void update_dz_c(const Ctx& c, int npz, const double* dp0, const double* ut, const double* vt, const double* gz,
+                 double* gz_out) {
+  const Dims& d = c.d;
+  Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
+  GT_LAUNCH(udzc_k, g2(d, L, d.nsub * (npz + 1)), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dp0, ut, vt,
+                     gz, gz_out);
+  HIP_LAUNCH_CHECK();
+}
+
+void riem_solver_c(const Ctx& c, int npz, double dt2, double ptop, double p_fac, double dz_min, const double* delpc,
+                   const double* ptc, const double* wc, const double* phis, double* gz, double* pef,
+                   const NhScratch& sc) {
+  const Dims& d = c.d;
+  Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
+  GT_LAUNCH(riem_c_k, g2(d, L, d.nsub), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt2, ptop, p_fac,
+                     dz_min, delpc, ptc, wc, phis, gz, pef, sc);
+  HIP_LAUNCH_CHECK();
+}
+
+void p_grad_c(const Ctx& c, int npz, double dt2, const double* delpc, const double* pkc, const double* gz, double* uc,
+              double* vc) {
+  const Dims& d = c.d;
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  GT_LAUNCH(pgradc_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt2, delpc, pkc,
+                     gz, uc, vc);
+  HIP_LAUNCH_CHECK();
+}
+
+void update_dz_d(const Ctx& c, const UdzdArgs& a) {
+  const Dims& d = c.d;
+  const int k1 = a.npz + 1;
+  Launch2D Lf{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  GT_LAUNCH(edge_prof_k, g2(d, Lf, d.nsub), dim3(BX, BY), 0, c.st, d, a.npz, a.dp0, a.crx, a.xfx, a.cry,
+                     a.yfx, a.crx_e, a.xfx_e, a.cry_e, a.yfx_e, a.gam);
+  HIP_LAUNCH_CHECK();
+  Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
+  GT_LAUNCH(ra_k, g2(d, Lr, d.nsub * k1), dim3(BX, BY), 0, c.st, d, c.subs, c.met, k1, a.xfx_e, a.yfx_e,
+                     a.ra_x, a.ra_y);
+  HIP_LAUNCH_CHECK();
+  TpArgs t{};
+  t.q = a.zh; t.nt = 1; t.nk = k1;
+  t.crx = a.crx_e; t.cry = a.cry_e; t.xfx = a.xfx_e; t.yfx = a.yfx_e; t.ra_x = a.ra_x; t.ra_y = a.ra_y;
+  t.mfx = nullptr; t.mfy = nullptr; t.fx = a.fx; t.fy = a.fy;
+  t.fx2 = a.tp_fx2; t.fy2 = a.tp_fy2; t.qi = a.tp_qi; t.qj = a.tp_qj; t.ord = a.hord;
+  fv_tp_2d(c, t);
+  Launch2D Li{0, 0, d.nx, d.ny};
+  GT_LAUNCH(zh_update_k, g2(d, Li, d.nsub * k1), dim3(BX, BY), 0, c.st, d, c.subs, c.met, k1, a.fx, a.fy,
+                     a.ra_x, a.ra_y, a.zh);
+  HIP_LAUNCH_CHECK();
+}
+
+void riem_solver3(const Ctx& c, const Riem3Args& a, const NhScratch& sc) {
+  const Dims& d = c.d;
+  Launch2D L{0, 0, d.nx, d.ny};
+  GT_LAUNCH(riem3_k, g2(d, L, d.nsub), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.ptop, a.p_fac,
+                     a.dz_min, a.last_call, a.delp, a.pt, a.phis, a.w, a.delz, a.zh, a.ppe, a.pk3, a.pe, a.peln, a.pk,
+                     a.ws, sc);
+  HIP_LAUNCH_CHECK();
+}
+
+void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* delp, double* pk3, double* pe) {
+  const Dims& d = c.d;
+  Launch2D L{-2, -2, d.nx + 4, d.ny + 4};
+  GT_LAUNCH(pk3_pe_halo_k, g2(d, L, d.nsub), dim3(BX, BY), 0, c.st, d, npz, ptop, do_pe ? 1 : 0, delp, pk3,
+                     pe);
+  HIP_LAUNCH_CHECK();
+}
+
+void a2b_ord4(const Ctx& c, int nk, const double* q, double* qout, double* qx, double* qy) {
+  const Dims& d = c.d;
+  Launch2D Lf{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  GT_LAUNCH(a2b_qxqy_k, g2(d, Lf, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, c.met, nk, q, qx, qy);
+  HIP_LAUNCH_CHECK();
+  Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
+  GT_LAUNCH(a2b_edge_k, g2(d, Lc, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, c.met, nk, c.cornerw, q,
+                     qx, qy, qout);
+  HIP_LAUNCH_CHECK();
+  GT_LAUNCH(a2b_inner_k, g2(d, Lc, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, nk, qx, qy, qout);
+  HIP_LAUNCH_CHECK();
+}
+
+void nh_p_grad(const Ctx& c, const NhPgArgs& a) {
+  const Dims& d = c.d;
+  const int k1 = a.npz + 1;
+  a2b_ord4(c, k1, a.pp, a.ppb, a.qx, a.qy);
+  a2b_ord4(c, k1, a.pk3, a.pkb, a.qx, a.qy);
+  a2b_ord4(c, k1, a.gz, a.gzb, a.qx, a.qy);
+  a2b_ord4(c, a.npz, a.delp, a.wk1, a.qx, a.qy);
+  const double ptk = exp(Constants::kappa * log(a.ptop));
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  GT_LAUNCH(nhpgrad_k, g2(d, L, d.nsub * a.npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, ptk,
+                     a.ppb, a.gzb, a.pkb, a.wk1, a.u, a.v);
+  HIP_LAUNCH_CHECK();
+}
+
+void scale_field(const Ctx& c, long n, double a, const double* x, double* y) {
+  GT_LAUNCH(scale_k, dim3(cdiv(n, 256) < 8192 ? cdiv(n, 256) : 8192), dim3(256), 0, c.st, n, a, x, y);
+  HIP_LAUNCH_CHECK();
+}
+
+}  // namespace gtfv3

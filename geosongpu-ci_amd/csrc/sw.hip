@@ -580,22 +580,22 @@ void c_sw(const Ctx& c, const CswArgs& a) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  hipLaunchKernelGGL(cs_tmp, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.utmp,
+  GT_LAUNCH(cs_tmp, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.utmp,
                      a.vtmp, a.ua, a.va);
   HIP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(cs_corner_fix, dim3(nz), dim3(64), 0, c.st, d, c.subs, a.npz, a.utmp, a.vtmp, a.ua, a.va);
+  GT_LAUNCH(cs_corner_fix, dim3(nz), dim3(64), 0, c.st, d, c.subs, a.npz, a.utmp, a.vtmp, a.ua, a.va);
   HIP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(cs_cgrid, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
+  GT_LAUNCH(cs_cgrid, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
                      a.utmp, a.vtmp, a.ua, a.va, a.uc, a.vc, a.ut, a.vt);
   HIP_LAUNCH_CHECK();
   Launch2D Lt{-1, -1, d.nx + 2, d.ny + 2};
-  hipLaunchKernelGGL(cs_transport_ke, g2(d, Lt, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.delp,
+  GT_LAUNCH(cs_transport_ke, g2(d, Lt, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.delp,
                      a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke);
   HIP_LAUNCH_CHECK();
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
-  hipLaunchKernelGGL(cs_vort, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.vort);
+  GT_LAUNCH(cs_vort, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.vort);
   HIP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(cs_update, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
+  GT_LAUNCH(cs_update, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
                      a.vort, a.ke, a.uc, a.vc);
   HIP_LAUNCH_CHECK();
 }
@@ -604,17 +604,17 @@ void d_sw(const Ctx& c, const DswArgs& a) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  hipLaunchKernelGGL(ds_utvt1, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.uc, a.vc,
+  GT_LAUNCH(ds_utvt1, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.uc, a.vc,
                      a.ut, a.vt);
   HIP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ds_utvt2, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.ut,
+  GT_LAUNCH(ds_utvt2, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.ut,
                      a.vt);
   HIP_LAUNCH_CHECK();
-  hipLaunchKernelGGL(ds_courant, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.ut, a.vt,
+  GT_LAUNCH(ds_courant, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.ut, a.vt,
                      a.crx, a.cry, a.xfx, a.yfx);
   HIP_LAUNCH_CHECK();
   Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  hipLaunchKernelGGL(ds_ra, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.xfx, a.yfx, a.ra_x,
+  GT_LAUNCH(ds_ra, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.xfx, a.yfx, a.ra_x,
                      a.ra_y);
   HIP_LAUNCH_CHECK();
   TpArgs t{};
@@ -625,7 +625,7 @@ void d_sw(const Ctx& c, const DswArgs& a) {
   // mass fluxes
   t.q = a.delp; t.mfx = nullptr; t.mfy = nullptr; t.fx = a.fx; t.fy = a.fy; t.ord = a.hord_dp;
   fv_tp_2d(c, t);
-  hipLaunchKernelGGL(ds_accum, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, a.npz, a.crx, a.cry, a.fx, a.fy,
+  GT_LAUNCH(ds_accum, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, a.npz, a.crx, a.cry, a.fx, a.fy,
                      a.cx, a.cy, a.mfx, a.mfy);
   HIP_LAUNCH_CHECK();
   // w and pt with the mass fluxes
@@ -635,21 +635,21 @@ void d_sw(const Ctx& c, const DswArgs& a) {
   t.q = a.pt; t.fx = a.gtx; t.fy = a.gty; t.ord = a.hord_tm;
   fv_tp_2d(c, t);
   Launch2D Li{0, 0, d.nx, d.ny};
-  hipLaunchKernelGGL(ds_thermo, g2(d, Li, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.fx, a.fy, a.gwx,
+  GT_LAUNCH(ds_thermo, g2(d, Li, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.fx, a.fy, a.gwx,
                      a.gwy, a.gtx, a.gty, a.delp, a.pt, a.w);
   HIP_LAUNCH_CHECK();
   // kinetic energy (+ divergence damping) at corners
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
-  hipLaunchKernelGGL(ds_ke, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.hord_mt, a.dddmp,
+  GT_LAUNCH(ds_ke, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.hord_mt, a.dddmp,
                      a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke);
   HIP_LAUNCH_CHECK();
   // vorticity transport
-  hipLaunchKernelGGL(ds_vort, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.vort);
+  GT_LAUNCH(ds_vort, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.vort);
   HIP_LAUNCH_CHECK();
   t.mfx = nullptr; t.mfy = nullptr;
   t.q = a.vort; t.fx = a.gwx; t.fy = a.gwy; t.ord = a.hord_vt;
   fv_tp_2d(c, t);
-  hipLaunchKernelGGL(ds_uv, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.ke, a.gwx, a.gwy, a.u,
+  GT_LAUNCH(ds_uv, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.ke, a.gwx, a.gwy, a.u,
                      a.v);
   HIP_LAUNCH_CHECK();
 }

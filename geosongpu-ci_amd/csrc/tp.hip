@@ -259,15 +259,15 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
   const Dims& d = c.d;
   long nz = (long)d.nsub * a.nt * a.nk;
   Launch2D L1{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  hipLaunchKernelGGL(tp_pass1, grid_for(L1, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.q, a.nt, a.nk, a.crx,
+  GT_LAUNCH(tp_pass1, grid_for(L1, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.q, a.nt, a.nk, a.crx,
                      a.cry, a.fx2, a.fy2, a.ord, (int)nz);
   HIP_LAUNCH_CHECK();
   Launch2D L2{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  hipLaunchKernelGGL(tp_pass2, grid_for(L2, nz), dim3(BX, BY), 0, c.st, d, c.met, a.q, a.nt, a.nk, a.xfx, a.yfx,
+  GT_LAUNCH(tp_pass2, grid_for(L2, nz), dim3(BX, BY), 0, c.st, d, c.met, a.q, a.nt, a.nk, a.xfx, a.yfx,
                      a.ra_x, a.ra_y, a.fx2, a.fy2, a.qi, a.qj, (int)nz);
   HIP_LAUNCH_CHECK();
   Launch2D L3{0, 0, d.nx + 1, d.ny + 1};
-  hipLaunchKernelGGL(tp_pass3, grid_for(L3, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.nt, a.nk, a.crx, a.cry,
+  GT_LAUNCH(tp_pass3, grid_for(L3, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.nt, a.nk, a.crx, a.cry,
                      a.mfx ? a.mfx : a.xfx, a.mfy ? a.mfy : a.yfx, a.fx2, a.fy2, a.qi, a.qj, a.fx, a.fy, a.ord,
                      (int)nz);
   HIP_LAUNCH_CHECK();
@@ -279,7 +279,7 @@ void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, doub
   (void)ra_x; (void)ra_y;
   HIP_CHECK(hipMemsetAsync(cmax_dev, 0, sizeof(double) * npz, c.st));
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  hipLaunchKernelGGL(tracer_prep_k, dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
+  GT_LAUNCH(tracer_prep_k, dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
                      c.met, npz, cx, cy, xfx, yfx, cmax_dev);
   HIP_LAUNCH_CHECK();
 }
@@ -288,18 +288,18 @@ void tracer_split(const Ctx& c, int npz, const int* nsplt_dev, double* cx, doubl
                   double* mfx, double* mfy, double* ra_x, double* ra_y) {
   const Dims& d = c.d;
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  hipLaunchKernelGGL(tracer_split_k, dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
+  GT_LAUNCH(tracer_split_k, dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
                      c.met, npz, nsplt_dev, cx, cy, xfx, yfx, mfx, mfy, ra_x, ra_y);
   HIP_LAUNCH_CHECK();
   Launch2D L2{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  hipLaunchKernelGGL(tracer_ra_k, dim3(cdiv(L2.ni, BX), cdiv(L2.nj, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
+  GT_LAUNCH(tracer_ra_k, dim3(cdiv(L2.ni, BX), cdiv(L2.nj, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
                      c.met, npz, xfx, yfx, ra_x, ra_y);
   HIP_LAUNCH_CHECK();
 }
 
 void tracer_dp2(const Ctx& c, int npz, const double* dp1, const double* mfx, const double* mfy, double* dp2) {
   const Dims& d = c.d;
-  hipLaunchKernelGGL(tracer_dp2_k, dim3(cdiv(d.nx, BX), cdiv(d.ny, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
+  GT_LAUNCH(tracer_dp2_k, dim3(cdiv(d.nx, BX), cdiv(d.ny, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
                      c.met, npz, dp1, mfx, mfy, dp2);
   HIP_LAUNCH_CHECK();
 }
@@ -309,13 +309,13 @@ void tracer_update(const Ctx& c, int npz, int nq, double* q, const double* qn, c
   (void)qn;
   const Dims& d = c.d;
   long nz = (long)d.nsub * nq * npz;
-  hipLaunchKernelGGL(tracer_update_k, dim3(cdiv(d.nx, BX), cdiv(d.ny, BY), (unsigned)(nz < ZMAX ? nz : ZMAX)),
+  GT_LAUNCH(tracer_update_k, dim3(cdiv(d.nx, BX), cdiv(d.ny, BY), (unsigned)(nz < ZMAX ? nz : ZMAX)),
                      dim3(BX, BY), 0, c.st, d, c.met, npz, nq, q, dp1, dp2, fx, fy, nsplt_dev, it, (int)nz);
   HIP_LAUNCH_CHECK();
 }
 
 void copy_levels(const Ctx& c, long n, const double* src, double* dst) {
-  hipLaunchKernelGGL(copy_k, dim3(cdiv(n, 256) < 8192 ? cdiv(n, 256) : 8192), dim3(256), 0, c.st, n, src, dst);
+  GT_LAUNCH(copy_k, dim3(cdiv(n, 256) < 8192 ? cdiv(n, 256) : 8192), dim3(256), 0, c.st, n, src, dst);
   HIP_LAUNCH_CHECK();
 }
 

@@ -131,6 +131,21 @@ class Domain:
     def stream(self):
         return lib().gtfv3_stream(self.h)
 
+    def kernel_timing(self, on=True):
+        check(lib().gtfv3_kernel_timing(self.h, 1 if on else 0))
+
+    def kernel_stats(self):
+        """{kernel: (total_ms, launches)} since kernel_timing(True)"""
+        buf = ctypes.create_string_buffer(1 << 16)
+        check(lib().gtfv3_kernel_stats(self.h, buf, 1 << 16))
+        out = {}
+        for item in buf.value.decode().split(";"):
+            if "=" in item:
+                k, v = item.split("=")
+                ms, n = v.split(",")
+                out[k] = (float(ms), int(n))
+        return out
+
     def timers(self):
         buf = ctypes.create_string_buffer(8192)
         check(lib().gtfv3_timers(self.h, buf, 8192))

@@ -60,6 +60,10 @@ int gtfv3_sync(void* h);
 void* gtfv3_stream(void* h);
 /* accumulated per-phase timers (ms), "name=value;..." into buf */
 int gtfv3_timers(void* h, char* buf, int len);
+/* per-kernel HIP-event timing (off by default); enabling resets the statistics */
+int gtfv3_kernel_timing(void* h, int on);
+/* per-kernel totals since enabling, "kernel=ms,launches;..." into buf */
+int gtfv3_kernel_stats(void* h, char* buf, int len);
 
 #ifdef __cplusplus
 }

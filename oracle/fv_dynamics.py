@@ -1,0 +1,218 @@
+"""Oracle: one fv_dynamics call (non-hydrostatic FV3 as configured by the GEOS
+Held-Suarez namelist) composed from the oracle pieces — TEST INFRASTRUCTURE ONLY.
+
+Sequence (FV3 fv_dynamics.F90 -> dyn_core.F90 -> tracer_2d_1l -> Lagrangian_to_Eulerian
+-> cubed_to_latlon, the call stack of SURVEY.md §8(a)):
+
+  entry      pkz from the nh state, pt -> virtual potential temperature, dp1 = delp
+  dyn_core   n_split acoustic sub-steps of
+               c_sw, update_dz_c, riem_solver_c, p_grad_c,
+               d_sw, update_dz_d, riem_solver3, pk3/pe halo, nh_p_grad
+  tracers    tracer_2d_1l with the accumulated mass fluxes and Courant numbers
+  remap      Lagrangian_to_Eulerian (kord 9, T_v in log p)
+  exit       T = T_v / (1 + zvir q), omega = delp / delz * w, A-grid winds (c2l_ord4)
+
+All arrays are (nsub, nk, nj, pitch) in the product's HBM layout; sub-domains are
+the single-rank Layout order.  The halo fills are the oracle's own (halo.py).
+"""
+import numpy as np
+
+from . import NG
+from . import fv_mapz, nh_core, sw_core, tp_core
+from .halo import Layout, fill_scalar, fill_vector
+from .util import Plane, sh
+
+np.seterr(all="ignore")
+
+GRAV = nh_core.GRAV
+RDGAS = nh_core.RDGAS
+KAPPA = nh_core.KAPPA
+ZVIR = (8314.47 / 18.015) / (8314.47 / 28.965) - 1.0
+
+
+class Grid:
+    """Everything the oracle needs about the decomposition and metrics."""
+
+    def __init__(self, N, lx, ly, ms, corner_w, da_min_c, nj, pitch):
+        self.layout = Layout(N, lx, ly)
+        self.subs = self.layout.subs()
+        self.nx, self.ny = self.layout.nx, self.layout.ny
+        self.ms = ms
+        self.corner_w = corner_w
+        self.da_min_c = da_min_c
+        self.P = [Plane(s, self.nx, self.ny, nj, pitch) for s in self.subs]
+
+    @property
+    def nsub(self):
+        return len(self.subs)
+
+
+def _halo(g, st, items):
+    """items: list of (name, kind) as in Dycore::halo_update; vector kinds take two names"""
+    n = 0
+    while n < len(items):
+        name, k = items[n]
+        if k == "c":
+            fill_scalar(st[name], g.layout, "cell")
+        elif k == "b":
+            fill_scalar(st[name], g.layout, "corner")
+        else:
+            fill_vector(st[name], st[items[n + 1][0]], g.layout, {"d": "dgrid", "C": "cgrid", "a": "agrid"}[k])
+            n += 1
+        n += 1
+
+
+def c2l_ord4(u, v, m, P):
+    """cubed_to_latlon, 4th order (FV3 fv_grid_utils c2l_ord4): D-grid (u, v) -> A-grid (ua, va)
+    on compute cells; 2nd-order distance-weighted averages on the tile-edge rows/columns."""
+    N, I, J = P.N, P.I, P.J
+    c1, c2 = 1.125, -0.125
+    dx, dy = m["dx"], m["dy"]
+    ut = c2 * (sh(u, 0, -1) + sh(u, 0, 2)) + c1 * (u + sh(u, 0, 1))
+    vt = c2 * (sh(v, -1, 0) + sh(v, 2, 0)) + c1 * (v + sh(v, 1, 0))
+    row = (J == 0) | (J == N - 1)
+    vt_e = 2.0 * (v * dy + sh(v, 1, 0) * sh(dy, 1, 0)) / (dy + sh(dy, 1, 0))
+    ut_e = 2.0 * (u * dx + sh(u, 0, 1) * sh(dx, 0, 1)) / (dx + sh(dx, 0, 1))
+    vt = np.where(row, vt_e, vt)
+    ut = np.where(row, ut_e, ut)
+    col = (I == 0) | (I == N - 1)
+    ut = np.where(col, ut_e, ut)
+    vt = np.where(col, vt_e, vt)
+    ua = m["a11"] * ut + m["a12"] * vt
+    va = m["a21"] * ut + m["a22"] * vt
+    comp = P.reg(0, P.nx - 1, 0, P.ny - 1)
+    return np.where(comp, ua, 0.0), np.where(comp, va, 0.0)
+
+
+def fv_dynamics(st, ak, bk, g, nl):
+    """One fv_dynamics call.  st: dict name -> array; updated and returned (new dict).
+
+    Required inputs: u, v, w, delz, pt (T), delp, q (nq*npz levels, tracer 0 = sphum), phis.
+    nl: dict with n_split, dt_atmos, hord_mt/vt/tm/dp/tr, dddmp, d2_bg, p_fac, dz_min, fill, nq.
+    """
+    st = {k: v.copy() for k, v in st.items()}
+    nsub, nx, ny = g.nsub, g.nx, g.ny
+    npz = st["delp"].shape[1]
+    k1 = npz + 1
+    nq = nl["nq"]
+    shp = st["delp"].shape
+    shp1 = (nsub, k1) + shp[2:]
+    shp0 = (nsub, 1) + shp[2:]
+    for name, s_ in (("pe", shp1), ("peln", shp1), ("pk", shp1), ("pkz", shp), ("ps", shp0), ("omga", shp),
+                     ("ua", shp), ("va", shp), ("uc", shp), ("vc", shp), ("mfx", shp), ("mfy", shp), ("cx", shp),
+                     ("cy", shp), ("zh", shp1), ("ppe", shp1), ("pk3", shp1), ("ws", shp0)):
+        if name not in st:
+            st[name] = np.zeros(s_)
+    bdt = nl["dt_atmos"]
+    dt = bdt / nl["n_split"]
+    dt2 = 0.5 * dt
+    ptop = ak[0]
+    dp0 = nh_core.dp_ref(ak, bk)
+    comp = [P.reg(0, nx - 1, 0, ny - 1) for P in g.P]
+    q0 = st["q"][:, :npz]
+
+    # ---- entry ----
+    rdg = -RDGAS * (1.0 / GRAV)
+    for s in range(nsub):
+        dp1 = ZVIR * q0[s]
+        pk = np.exp(KAPPA * np.log(rdg * st["delp"][s] * st["pt"][s] * (1.0 + dp1) / st["delz"][s]))
+        st["pkz"][s] = np.where(comp[s], pk, st["pkz"][s])
+        st["pt"][s] = np.where(comp[s], st["pt"][s] * (1.0 + dp1) / pk, st["pt"][s])
+    st["dp1"] = st["delp"].copy()
+    for name in ("mfx", "mfy", "cx", "cy"):
+        st[name][:] = 0.0
+
+    # ---- dyn_core ----
+    _halo(g, st, [("u", "d"), ("v", "d"), ("delp", "c"), ("pt", "c"), ("w", "c"), ("phis", "c")])
+    zs = [st["phis"][s, 0] * (1.0 / GRAV) for s in range(nsub)]
+    for s in range(nsub):
+        zc = zs[s]
+        z = st["zh"][s]
+        z[npz] = np.where(comp[s], zc, z[npz])
+        for k in range(npz - 1, -1, -1):
+            z[k] = np.where(comp[s], z[k + 1] - st["delz"][s, k], z[k])
+    _halo(g, st, [("zh", "c")])
+    ords = (nl["hord_mt"], nl["hord_vt"], nl["hord_tm"], nl["hord_dp"])
+    for it in range(nl["n_split"]):
+        last = it == nl["n_split"] - 1
+        cs = []
+        for s in range(nsub):
+            m, sub, P = g.ms[s], g.subs[s], g.P[s]
+            c = sw_core.c_sw(st["delp"][s], st["pt"][s], st["u"][s], st["v"][s], st["w"][s], sub, m, nx, ny, dt2)
+            gzc, ws = nh_core.update_dz_c(c["ut"], c["vt"], st["zh"][s], zs[s], sub, m, nx, ny, dp0, dt2,
+                                          nl["dz_min"])
+            reg = P.reg(-1, nx, -1, ny)
+            pef, gzc = nh_core.riem_solver_c(dt2, c["delpc"], c["ptc"], c["wc"], gzc, st["phis"][s, 0], ws, ptop,
+                                             nl["p_fac"], reg)
+            uc, vc = nh_core.p_grad_c(c["uc"], c["vc"], c["delpc"], pef, gzc, m, P, dt2)
+            st["uc"][s], st["vc"][s], st["ua"][s], st["va"][s] = uc, vc, c["ua"], c["va"]
+            cs.append(c)
+        _halo(g, st, [("uc", "C"), ("vc", "C")])
+        ds = []
+        for s in range(nsub):
+            m, sub, P = g.ms[s], g.subs[s], g.P[s]
+            r = sw_core.d_sw(st["delp"][s], st["pt"][s], st["u"][s], st["v"][s], st["w"][s], st["uc"][s],
+                             st["vc"][s], st["ua"][s], st["va"][s], sub, m, nx, ny, dt, ords, nl["dddmp"],
+                             nl["d2_bg"], g.da_min_c)
+            for name in ("delp", "pt", "w", "u", "v"):
+                st[name][s] = r[name]
+            st["cx"][s] = np.where(P.reg(0, nx, -NG, ny + NG - 1), st["cx"][s] + r["crx"], st["cx"][s])
+            st["cy"][s] = np.where(P.reg(-NG, nx + NG - 1, 0, ny), st["cy"][s] + r["cry"], st["cy"][s])
+            st["mfx"][s] = np.where(P.reg(0, nx, 0, ny - 1), st["mfx"][s] + r["fx"], st["mfx"][s])
+            st["mfy"][s] = np.where(P.reg(0, nx - 1, 0, ny), st["mfy"][s] + r["fy"], st["mfy"][s])
+            ds.append(r)
+        _halo(g, st, [("delp", "c"), ("pt", "c")])
+        for s in range(nsub):
+            m, sub, P = g.ms[s], g.subs[s], g.P[s]
+            r = ds[s]
+            zh, ws = nh_core.update_dz_d(st["zh"][s], r["crx"], r["cry"], r["xfx"], r["yfx"], zs[s], sub, m, nx, ny,
+                                         dp0, dt, nl["hord_tm"], nl["dz_min"])
+            o = nh_core.riem_solver3(dt, st["delp"][s], st["pt"][s], st["w"][s], zh, zs[s], ws, ptop, nl["p_fac"],
+                                     comp[s], last)
+            st["w"][s] = o["w"]
+            st["delz"][s] = np.where(comp[s], o["delz"], st["delz"][s])
+            st["zh"][s] = o["zh"]
+            st["ppe"][s] = np.where(comp[s], o["ppe"], st["ppe"][s])
+            st["pk3"][s] = np.where(comp[s], o["pk3"], st["pk3"][s])
+            st["ws"][s, 0] = np.where(comp[s], ws, st["ws"][s, 0])
+            if last:
+                for name in ("pe", "peln", "pk"):
+                    st[name][s] = np.where(comp[s], o[name], st[name][s])
+        _halo(g, st, [("zh", "c"), ("ppe", "c"), ("w", "c")])
+        for s in range(nsub):
+            P = g.P[s]
+            st["pk3"][s] = nh_core.pk3_halo(st["pk3"][s], st["delp"][s], ptop, P)
+            if last:
+                st["pe"][s] = nh_core.pe_halo(st["pe"][s], st["delp"][s], ptop, P)
+        for s in range(nsub):
+            m, P = g.ms[s], g.P[s]
+            gz = st["zh"][s] * GRAV
+            st["u"][s], st["v"][s] = nh_core.nh_p_grad(st["u"][s], st["v"][s], st["ppe"][s], gz, st["delp"][s],
+                                                       st["pk3"][s], dt, ptop, P, m, g.corner_w[s])
+        if not last:
+            _halo(g, st, [("u", "d"), ("v", "d")])
+
+    # ---- tracer transport ----
+    st["q"], nsplt = tp_core.tracer_2d_1l(st["q"], st["dp1"], st["mfx"], st["mfy"], st["cx"], st["cy"], g.subs,
+                                          g.ms, nx, ny, npz, nq, nl["hord_tr"],
+                                          lambda a: fill_scalar(a, g.layout, "cell"))
+
+    # ---- vertical remap ----
+    keys = ("pe", "peln", "pk", "pkz", "delp", "delz", "pt", "w", "q", "u", "v", "ps")
+    for s in range(nsub):
+        sub_st = {k: st[k][s] for k in keys}
+        sub_st["ws"] = st["ws"][s, 0]
+        o = fv_mapz.lagrangian_to_eulerian(sub_st, ak, bk, ptop, nq, nl["fill"], g.P[s])
+        for k in keys:
+            st[k][s] = o[k]
+
+    # ---- exit ----
+    for s in range(nsub):
+        q0s = st["q"][s, :npz]
+        st["pt"][s] = np.where(comp[s], st["pt"][s] / (1.0 + ZVIR * q0s), st["pt"][s])
+        st["omga"][s] = np.where(comp[s], st["delp"][s] / st["delz"][s] * st["w"][s], st["omga"][s])
+    _halo(g, st, [("u", "d"), ("v", "d")])
+    for s in range(nsub):
+        st["ua"][s], st["va"][s] = c2l_ord4(st["u"][s], st["v"][s], g.ms[s], g.P[s])
+    st["_nsplt"] = nsplt
+    return st

@@ -93,50 +93,81 @@ class Layout:
         raise AssertionError("no owner")
 
 
-def fill_scalar(fields, layout, stagger="cell"):
-    """fields: array (nsub_total, nk, nj, pitch) in HBM layout; halos overwritten in place."""
+def _scalar_table(layout, stagger):
+    """(dst g, j, i), (src g, j, i) slot lists for one stagger; src g = -1 -> zero-fill"""
+    key = ("s", layout.N, layout.lx, layout.ly, stagger)
+    if key in _TABLES:
+        return _TABLES[key]
     dx2, dy2 = STAGGER[stagger]
     sx = 1 if stagger in ("yedge", "corner") else 0
     sy = 1 if stagger in ("xedge", "corner") else 0
     nx, ny = layout.nx, layout.ny
-    src = fields.copy()
+    dst, src = [], []
     for g, sd in enumerate(layout.subs()):
         for j in range(-NG, ny + NG + sy):
             for i in range(-NG, nx + NG + sx):
                 if 0 <= i <= nx - 1 + sx and 0 <= j <= ny - 1 + sy:
                     continue
                 loc = locate(sd["tile"], 2 * (i + sd["ioff"]) + dx2, 2 * (j + sd["joff"]) + dy2, layout.N)
+                dst.append((g, j + NG, i + NG))
                 if loc is None:
-                    fields[g, :, j + NG, i + NG] = 0.0
+                    src.append((-1, 0, 0))
                     continue
                 gs, ii, jj = layout.owner(loc[0], loc[1], loc[2])
-                fields[g, :, j + NG, i + NG] = src[gs, :, jj + NG, ii + NG]
+                src.append((gs, jj + NG, ii + NG))
+    t = (np.array(dst).T, np.array(src).T)
+    _TABLES[key] = t
+    return t
+
+
+_TABLES = {}
+
+
+def fill_scalar(fields, layout, stagger="cell"):
+    """fields: array (nsub_total, nk, nj, pitch) in HBM layout; halos overwritten in place."""
+    (dg, dj, di), (sg, sj, si) = _scalar_table(layout, stagger)
+    vals = fields[sg, :, sj, si]
+    vals[sg < 0] = 0.0
+    fields[dg, :, dj, di] = vals
     return fields
 
 
-def fill_vector(fx, fy, layout, kind="dgrid"):
-    """Vector pair halo fill with rotation of components across rotated tile edges."""
-    sx_, sy_ = VECTOR[kind]
-    srcs = (fx.copy(), fy.copy())
-    dsts = (fx, fy)
+def _vector_table(layout, kind):
+    key = ("v", layout.N, layout.lx, layout.ly, kind)
+    if key in _TABLES:
+        return _TABLES[key]
+    out = []
     nx, ny = layout.nx, layout.ny
-    for c, st in enumerate((sx_, sy_)):
+    for c, st in enumerate(VECTOR[kind]):
         dx2, dy2 = STAGGER[st]
         sx = 1 if st in ("yedge", "corner") else 0
         sy = 1 if st in ("xedge", "corner") else 0
+        dst, src = [], []
         for g, sd in enumerate(layout.subs()):
             for j in range(-NG, ny + NG + sy):
                 for i in range(-NG, nx + NG + sx):
                     if 0 <= i <= nx - 1 + sx and 0 <= j <= ny - 1 + sy:
                         continue
                     loc = locate(sd["tile"], 2 * (i + sd["ioff"]) + dx2, 2 * (j + sd["joff"]) + dy2, layout.N)
+                    dst.append((g, j + NG, i + NG))
                     if loc is None:
-                        dsts[c][g, :, j + NG, i + NG] = 0.0
+                        src.append((-1, 0, 0, 0, 0))
                         continue
                     dxd, dyd = (1, 0) if c == 0 else (0, 1)
                     ox, oy = _rot(loc[3], dxd, dyd)
-                    sc = 0 if ox != 0 else 1
-                    sign = ox + oy
                     gs, ii, jj = layout.owner(loc[0], loc[1], loc[2])
-                    dsts[c][g, :, j + NG, i + NG] = sign * srcs[sc][gs, :, jj + NG, ii + NG]
+                    src.append((gs, jj + NG, ii + NG, 0 if ox != 0 else 1, ox + oy))
+        out.append((np.array(dst).T, np.array(src).T))
+    _TABLES[key] = out
+    return out
+
+
+def fill_vector(fx, fy, layout, kind="dgrid"):
+    """Vector pair halo fill with rotation of components across rotated tile edges."""
+    srcs = (fx.copy(), fy.copy())
+    dsts = (fx, fy)
+    for c, ((dg, dj, di), (sg, sj, si, sc, sign)) in enumerate(_vector_table(layout, kind)):
+        vals = np.where(sc[:, None] == 0, srcs[0][sg, :, sj, si], srcs[1][sg, :, sj, si]) * sign[:, None]
+        vals[sg < 0] = 0.0
+        dsts[c][dg, :, dj, di] = vals
     return fx, fy
