@@ -34,7 +34,21 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 # Algorithmic HBM bytes per launch of the kernels that can dominate a step:
 # distinct fp64 fields read + written once over the kernel's domain (see DESIGN.md
 # "Kernels").  c = cells per level over the launch's sub-domains, L = levels.
-KERNEL_BYTES = {}
+def _cols(d, ring=0):
+    return d.nsub * (d.nx + 2 * ring) * (d.ny + 2 * ring)
+
+
+KERNEL_BYTES = {
+    # riem_solver3 (+ update_dz_d clamp): read zh(L+1) delp pt w phis, write w delz zh ppe pk3 ws
+    # (pe/peln/pk on the last acoustic sub-step only are not counted: a lower bound)
+    "riem3_k": lambda d: 8 * _cols(d) * ((d.npz + 1) + 3 * d.npz + 1 + 2 * d.npz + 3 * (d.npz + 1) + 1),
+    # riem_solver_c on the 1-ring: read delpc ptc wc gz(L+1) phis, write gz(L+1) pef(L+1)
+    "riem_c_k": lambda d: 8 * _cols(d, 1) * (3 * d.npz + (d.npz + 1) + 1 + 2 * (d.npz + 1)),
+    # Lagrangian_to_Eulerian scalars: read pe peln (L+1) delp delz pt w q ws, write pt delp delz w q pk
+    # peln (L+1) pkz ps
+    "remap_scalar_k": lambda d: 8 * _cols(d) * ((2 * (d.npz + 1) + 4 * d.npz + d.nq * d.npz + 1)
+                                                + (4 * d.npz + d.nq * d.npz + 2 * (d.npz + 1) + d.npz + 1)),
+}
 
 
 def layout_for(n):

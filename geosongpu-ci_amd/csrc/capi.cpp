@@ -223,6 +223,18 @@ int gtfv3_halo_table(void* h, int kind, int* out, int cap) {
   }
 }
 
+int gtfv3_halo_remote(void* h, int kind, int dir, int* out, int cap) {
+  try {
+    std::vector<int> t = D(h)->halo.remote_table(kind, dir);
+    int n = (int)t.size() / 6;
+    if (out && cap >= (int)t.size()) std::memcpy(out, t.data(), sizeof(int) * t.size());
+    return n;
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return -1;
+  }
+}
+
 int gtfv3_halo_update(void* h, const char* spec) {
   API_TRY
   std::vector<std::pair<std::string, char>> items;

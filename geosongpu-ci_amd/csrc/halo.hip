@@ -138,6 +138,8 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
     n_local_[kind] = (int)h_local_[kind].size();
     n_send_[kind] = (int)hs.size();
     n_recv_[kind] = (int)hr.size();
+    h_send_[kind] = hs;
+    h_recv_[kind] = hr;
     if (!device) continue;
     if (n_local_[kind]) {
       HIP_CHECK(hipMalloc(&d_local_[kind], sizeof(HaloEntry) * n_local_[kind]));
@@ -160,6 +162,19 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
     HIP_CHECK(hipMalloc(&sendbuf_, sizeof(double) * buf_elems_));
     HIP_CHECK(hipMalloc(&recvbuf_, sizeof(double) * buf_elems_));
   }
+}
+
+std::vector<int> HaloExchanger::remote_table(int kind, int dir) const {
+  const auto& t = dir == 0 ? h_send_[kind] : h_recv_[kind];
+  const auto& starts = dir == 0 ? send_peer_start_[kind] : recv_peer_start_[kind];
+  const auto& counts = dir == 0 ? send_peer_count_[kind] : recv_peer_count_[kind];
+  std::vector<int> out;
+  for (int p = 0; p < (int)starts.size(); ++p)
+    for (int e = starts[p]; e < starts[p] + counts[p]; ++e) {
+      const PackEntry& h = t[e];
+      out.insert(out.end(), {h.sub, h.off, h.comp, h.sign, e - starts[p], p});
+    }
+  return out;
 }
 
 namespace {

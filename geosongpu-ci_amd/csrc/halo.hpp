@@ -46,6 +46,8 @@ class HaloExchanger {
   void exchange(const HaloField* fields, int nf, hipStream_t stream);
   // host copies of tables for tests
   const std::vector<HaloEntry>& local_table(int kind) const { return h_local_[kind]; }
+  // remote tables (dir 0: send/pack, 1: recv/unpack) as (sub, off, comp, sign, pos_in_peer_segment, peer)
+  std::vector<int> remote_table(int kind, int dir) const;
   int nranks() const { return nranks_; }
 
  private:
@@ -53,6 +55,7 @@ class HaloExchanger {
   int rank_ = 0, nranks_ = 1;
   ncclComm_t comm_ = nullptr;
   std::vector<HaloEntry> h_local_[H_NKIND];
+  std::vector<PackEntry> h_send_[H_NKIND], h_recv_[H_NKIND];
   HaloEntry* d_local_[H_NKIND] = {};
   int n_local_[H_NKIND] = {};
   // remote: per kind, concatenated over peers

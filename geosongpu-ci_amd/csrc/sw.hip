@@ -45,15 +45,18 @@ __global__ void __launch_bounds__(256) cs_tmp(Dims d, const SubInfo* __restrict_
   const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
   double ut = BIG, vt = BIG;
   if (i <= nx + NG - 1 && j <= ny + NG - 1) {
-    const bool rows = J >= max(2, jo - 1) && J <= min(N - 3, jo + ny);
-    const bool cols = I >= max(2, io - 1) && I <= min(N - 3, io + nx);
+    const bool rows = J >= max(3, jo - 1) && J <= min(N - 4, jo + ny);
+    const bool cols = I >= max(3, io - 1) && I <= min(N - 4, io + nx);
     if (rows) ut = A2 * (AT(u, 0, -1) + AT(u, 0, 2)) + A1 * (AT(u, 0, 0) + AT(u, 0, 1));
     if (cols) vt = A2 * (AT(v, -1, 0) + AT(v, 2, 0)) + A1 * (AT(v, 0, 0) + AT(v, 1, 0));
+    // tile-edge zones (npt = 4: three cells, the halo width) wherever the halo reaches them
+    const int jsd = jo - NG, jed = jo + ny + NG - 1, isd = io - NG, ied = io + nx + NG - 1;
+    const bool mid = J >= max(3, jsd) && J <= min(N - 4, jed);
     bool two = false;
-    if (jo == 0 && J >= jo - 3 && J <= 1) two = true;
-    if (jo + ny == N && J >= N - 2 && J <= jo + ny + 2) two = true;
-    if (rows && io == 0 && I >= io - 3 && I <= 1) two = true;
-    if (rows && io + nx == N && I >= N - 2 && I <= io + nx + 2) two = true;
+    if (J >= jsd && J <= 2) two = true;
+    if (J >= N - 3 && J <= jed) two = true;
+    if (mid && I >= isd && I <= 2) two = true;
+    if (mid && I >= N - 3 && I <= ied) two = true;
     if (two) {
       ut = 0.5 * (AT(u, 0, 0) + AT(u, 0, 1));
       vt = 0.5 * (AT(v, 0, 0) + AT(v, 1, 0));

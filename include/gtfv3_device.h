@@ -44,6 +44,10 @@ int gtfv3_get_scalars(void* h, double* out);
  * 4 A-grid): 6 ints per entry {dst_sub, dst_off, src_sub, src_off, comp, sign}; returns the
  * entry count (writes only when cap >= count). */
 int gtfv3_halo_table(void* h, int kind, int* out, int cap);
+/* cross-rank halo tables (dir 0 = pack/send, 1 = unpack/recv): entries of 6 ints
+ * (sub, plane offset, component, sign, position in the peer's segment, peer rank);
+ * returns the entry count (copies when cap >= 6*count) */
+int gtfv3_halo_remote(void* h, int kind, int dir, int* out, int cap);
 
 /* halo update, spec "name:kind,..." kind c=cell b=corner d=D-grid pair C=C-grid pair a=A-grid pair
  * (a pair lists x then y component, e.g. "u:d,v:d") */

@@ -34,31 +34,31 @@ def d2a2c_vect(u, v, P, m):
     utmp = np.full_like(u, BIG)
     vtmp = np.full_like(v, BIG)
     # interior
-    rows = (J >= max(2, jo - 1)) & (J <= min(N - 3, jo + ny)) & (P.li >= -NG) & (P.li <= nx + NG - 1)
+    rows = (J >= max(3, jo - 1)) & (J <= min(N - 4, jo + ny)) & (P.li >= -NG) & (P.li <= nx + NG - 1)
     utmp = np.where(rows, A2 * (sh(u, 0, -1) + sh(u, 0, 2)) + A1 * (u + sh(u, 0, 1)), utmp)
-    cols = (I >= max(2, io - 1)) & (I <= min(N - 3, io + nx)) & (P.lj >= -NG) & (P.lj <= ny + NG - 1)
+    cols = (I >= max(3, io - 1)) & (I <= min(N - 4, io + nx)) & (P.lj >= -NG) & (P.lj <= ny + NG - 1)
     vtmp = np.where(cols, A2 * (sh(v, -1, 0) + sh(v, 2, 0)) + A1 * (v + sh(v, 1, 0)), vtmp)
     u2 = 0.5 * (u + sh(u, 0, 1))
     v2 = 0.5 * (v + sh(v, 1, 0))
     allc = (P.li >= -NG) & (P.li <= nx + NG - 1)
     allr = (P.lj >= -NG) & (P.lj <= ny + NG - 1)
-    if jo == 0:  # south edge rows g in [jo-3, 1]
-        msk = allc & (J >= jo - 3) & (J <= 1)
-        utmp = np.where(msk, u2, utmp)
-        vtmp = np.where(msk, v2, vtmp)
-    if jo + ny == N:  # north edge rows g in [N-2, jo+ny+2]
-        msk = allc & (J >= N - 2) & (J <= jo + ny + 2)
-        utmp = np.where(msk, u2, utmp)
-        vtmp = np.where(msk, v2, vtmp)
-    midrows = (J >= max(2, jo - 1)) & (J <= min(N - 3, jo + ny))
-    if io == 0:
-        msk = midrows & (I >= io - 3) & (I <= 1)
-        utmp = np.where(msk, u2, utmp)
-        vtmp = np.where(msk, v2, vtmp)
-    if io + nx == N:
-        msk = midrows & (I >= N - 2) & (I <= io + nx + 2)
-        utmp = np.where(msk, u2, utmp)
-        vtmp = np.where(msk, v2, vtmp)
+    # tile-edge zones (npt = 4: three cells each side, matching the halo width so the
+    # zone reads the same from both tiles), applied wherever this sub-domain's halo reaches them
+    # (FV3: `js==1 .or. jsd<npt` etc.), so the result does not depend on the layout
+    jsd, jed, isd, ied = jo - NG, jo + ny + NG - 1, io - NG, io + nx + NG - 1
+    msk = allc & (J >= jsd) & (J <= 2)  # south edge rows
+    utmp = np.where(msk, u2, utmp)
+    vtmp = np.where(msk, v2, vtmp)
+    msk = allc & (J >= N - 3) & (J <= jed)  # north edge rows
+    utmp = np.where(msk, u2, utmp)
+    vtmp = np.where(msk, v2, vtmp)
+    midrows = (J >= max(3, jsd)) & (J <= min(N - 4, jed))
+    msk = midrows & (I >= isd) & (I <= 2)  # west edge columns
+    utmp = np.where(msk, u2, utmp)
+    vtmp = np.where(msk, v2, vtmp)
+    msk = midrows & (I >= N - 3) & (I <= ied)  # east edge columns
+    utmp = np.where(msk, u2, utmp)
+    vtmp = np.where(msk, v2, vtmp)
     del allr
     ua = np.zeros_like(u)
     va = np.zeros_like(v)

