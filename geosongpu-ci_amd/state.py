@@ -31,7 +31,7 @@ def hybrid_levels(npz=72, ptop=1.0, p_sig=2.0e4, ps_ref=1.0e5):
     lp = np.log(ptop) + (np.log(ps_ref) - np.log(ptop)) * x
     pref = np.exp(lp)
     pref[0], pref[-1] = ptop, ps_ref
-    bk = np.where(pref > p_sig, ((pref - p_sig) / (ps_ref - p_sig)) ** 1.2, 0.0)
+    bk = np.clip((pref - p_sig) / (ps_ref - p_sig), 0.0, None) ** 1.2
     bk[-1] = 1.0
     ak = pref - bk * ps_ref
     ak[-1] = 0.0
@@ -40,7 +40,8 @@ def hybrid_levels(npz=72, ptop=1.0, p_sig=2.0e4, ps_ref=1.0e5):
 
 
 def _unit(v):
-    return v / np.linalg.norm(v, axis=-1, keepdims=True)
+    n = np.linalg.norm(v, axis=-1, keepdims=True)
+    return v / np.where(n > 0.0, n, 1.0)
 
 
 def _latlon(p):
