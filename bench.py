@@ -51,6 +51,20 @@ KERNEL_BYTES = {
 }
 
 
+def pmc_traffic(kernel):
+    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+    (profiles/rNN_pmc_traffic.json, made by tools/pmc_summary.py from separate
+    FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this same command); None if absent."""
+    import glob
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_traffic.json")))
+    for f in reversed(files):
+        with open(f) as fh:
+            t = json.load(fh)
+        if kernel in t:
+            return t[kernel]["traffic_bytes"], os.path.basename(f)
+    return None, None
+
+
 def layout_for(n):
     """(layout_x, layout_y) for n ranks: 6*lx*ly sub-domains divisible by n"""
     return {1: (1, 1), 2: (1, 1), 3: (1, 1), 6: (1, 1), 4: (1, 2), 8: (2, 2), 12: (1, 2), 24: (2, 2)}.get(n, (2, 2))
@@ -169,9 +183,10 @@ def main():
         if fn is not None:
             b = fn(d)
             ach = b / (avg_ms * 1e-3) / 1e9
+            traffic, src = pmc_traffic(name)
             roof = dict(bound="hbm", kernel=name, achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=ach / HBM_PEAK_GBS, traffic=None, bytes_per_launch=b, avg_ms=avg_ms,
-                        share_of_step=tot / (ms_step * a.steps))
+                        frac=ach / HBM_PEAK_GBS, traffic=traffic, traffic_source=src, bytes_per_launch=b,
+                        avg_ms=avg_ms, share_of_step=tot / (ms_step * a.steps))
         else:
             roof = dict(bound="hbm", kernel=name, achieved=None, peak=HBM_PEAK_GBS, unit="GB/s", frac=None,
                         traffic=None, avg_ms=avg_ms, share_of_step=tot / (ms_step * a.steps))

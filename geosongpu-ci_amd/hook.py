@@ -1,0 +1,80 @@
+"""Python mirror of the generated `geos_gtfv3` hook (reference:
+src/tcn/py_ftn_interface/templates/hook.py.jinja2:11-34,74), backed by the HIP
+library instead of an embedded Python dycore.
+
+    from geosongpu_ci_amd.hook import geos_gtfv3
+    geos_gtfv3.init(comm=0, npx=181, npy=181, npz=72, ntiles=6, is_=1, ie=180, ...)
+    geos_gtfv3.run(comm=0, ..., u=u, v=v, ...)     # arrays in Fortran layout, updated in place
+    geos_gtfv3.finalize()
+
+Arrays are what the reference hook receives from FortranPythonConversion.fortran_to_python
+(data_conversion.py:134-148): zero-copy views of Fortran buffers with i fastest,
+i.e. Fortran-ordered numpy arrays of the FV3 shapes listed in SURVEY.md §8(b)
+(`pe` and `peln` are (i, k, j)).  With GTFV3_BRIDGE_TILES_PER_RANK=6 (all six tiles
+on one GPU, one process) every array carries a trailing tile axis of length 6.
+
+The keyword `is` of the reference argument list is spelled `is_` here (Python
+keyword); `is` is also accepted through **kwargs.
+"""
+import ctypes
+
+import numpy as np
+
+from ._lib import lib
+
+INIT_ARGS = ("comm", "npx", "npy", "npz", "ntiles", "is", "ie", "js", "je", "isd", "ied", "jsd", "jed", "bdt",
+             "nq_tot")
+RUN_SCALARS = INIT_ARGS + ("ng", "ptop", "ks", "layout_1", "layout_2", "adiabatic")
+RUN_ARRAYS = ("ak", "bk", "u", "v", "w", "delz", "pt", "delp", "q", "ps", "pe", "pk", "peln", "pkz", "phis",
+              "q_con", "omga", "ua", "va", "uc", "vc", "mfx", "mfy", "cx", "cy", "diss_est")
+FLOATS = ("bdt", "ptop")
+
+
+def _norm(kwargs):
+    if "is_" in kwargs:
+        kwargs = dict(kwargs)
+        kwargs["is"] = kwargs.pop("is_")
+    return kwargs
+
+
+def _scalar_args(kw, names):
+    out = []
+    for n in names:
+        v = kw[n]
+        if n == "comm":
+            out.append(ctypes.c_void_p(int(v)))
+        elif n in FLOATS:
+            out.append(ctypes.c_float(float(v)))
+        else:
+            out.append(ctypes.c_int(int(v)))
+    return out
+
+
+class GEOS_GTFV3:
+    """init / run / finalize with the reference hook's argument names and order."""
+
+    def init(self, **kwargs):
+        kw = _norm(kwargs)
+        lib().geos_gtfv3_init_c(*_scalar_args(kw, INIT_ARGS))
+
+    def run(self, **kwargs):
+        kw = _norm(kwargs)
+        arrs = []
+        dtype = np.asarray(kw["u"]).dtype
+        if dtype not in (np.float32, np.float64):
+            raise TypeError("geos_gtfv3.run: state arrays must be float32 or float64")
+        ct = ctypes.c_double if dtype == np.float64 else ctypes.c_float
+        for n in RUN_ARRAYS:
+            a = kw[n]
+            if not (isinstance(a, np.ndarray) and a.dtype == dtype and (a.flags.f_contiguous or a.ndim == 1)):
+                raise TypeError(f"geos_gtfv3.run: {n} must be a Fortran-contiguous {dtype} array "
+                                "(in-place update of the caller's buffer)")
+            arrs.append(a.ctypes.data_as(ctypes.POINTER(ct)))
+        fn = lib().geos_gtfv3_run_f64_c if dtype == np.float64 else lib().geos_gtfv3_run_c
+        fn(*_scalar_args(kw, RUN_SCALARS), *arrs)
+
+    def finalize(self):
+        lib().geos_gtfv3_finalize_c()
+
+
+geos_gtfv3 = GEOS_GTFV3()

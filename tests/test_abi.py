@@ -1,5 +1,7 @@
 """The C-ABI library loads and exports every symbol include/*.h declares (CPU)."""
 import ctypes
+
+import numpy as np
 import os
 import re
 
@@ -49,3 +51,13 @@ def test_last_error_channel(pkg):
     buf = ctypes.create_string_buffer(256)
     n = lib.geos_gtfv3_last_error(buf, 256)
     assert n > 0 and b"bogus_key" in buf.value
+
+
+def test_layout_rule_matches_reference():
+    """numpy restatement of data_conversion.py:141/184 == Fortran-ordered arrays"""
+    dim = [5, 4, 3]
+    flat = np.arange(np.prod(dim), dtype=np.float64)
+    view = flat.reshape(tuple(reversed(dim))).transpose()
+    assert view.shape == tuple(dim) and view.flags.f_contiguous
+    assert view[1, 0, 0] == 1.0 and view[0, 1, 0] == dim[0] and view[0, 0, 1] == dim[0] * dim[1]
+    np.testing.assert_array_equal(view.flatten(order="F"), flat)
