@@ -377,7 +377,7 @@ void Dycore::step() {
   // ---- vertical remap to the hybrid Eulerian coordinate ----
   RemapState rs{pe, peln, pk, pkz, delp.p, delz.p, pt.p, w.p, q.p, u.p, v.p, ps, ws};
   RemapScratch rsc;
-  for (int n = 0; n < 11; ++n) rsc.s[n] = S(("_rm" + std::to_string(n)).c_str(), k1);
+  for (int n = 0; n < 3; ++n) rsc.s[n] = S(("_rmj" + std::to_string(n)).c_str(), remap_jobs(nq) * k1);
   lagrangian_to_eulerian(c, npz, nq, ptop, nl.fill != 0, ak_dev, bk_dev, rs, rsc);
   HIP_CHECK(hipEventRecord(ev[3], st));
 

@@ -54,8 +54,9 @@ struct RemapState {
   double *pe, *peln, *pk, *pkz, *delp, *delz, *pt, *w, *q, *u, *v, *ps, *ws;
 };
 struct RemapScratch {
-  double* s[11];
+  double* s[3];  // q edges, gam, source copy: remap_jobs(nq) * (npz+1) levels each
 };
+int remap_jobs(int nq);
 void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fill, const double* ak_dev,
                             const double* bk_dev, const RemapState& S, const RemapScratch& R);
 

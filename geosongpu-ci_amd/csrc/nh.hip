@@ -10,8 +10,6 @@
 namespace gtfv3 {
 namespace {
 
-constexpr double GRAV = Constants::grav;
-constexpr double RDGAS = Constants::rdgas;
 constexpr double KAPPA = Constants::kappa;
 constexpr double R3 = 1.0 / 3.0;
 
@@ -40,76 +38,6 @@ __device__ __forceinline__ Col col(double* f, const Dims& d, int s, int nk, long
 }
 __device__ __forceinline__ Col ccol(const double* f, const Dims& d, int s, int nk, long o) {
   return Col{const_cast<double*>(f) + (long)s * nk * d.plane + o, d.plane};
-}
-
-struct SimScratch {
-  Col pl, w1, g_rat, bb, dd, gam, pp, aa, pe;
-};
-
-// SIM1_solver (a_imp = 1, no moist cappa); arrays indexed by layer / interface
-__device__ void sim1(double dt, double gama, double kappa, int km, const Col& dm2, const Col& pm2, const Col& pem,
-                     const Col& w2, const Col& dz2, const Col& pt2, double ws, double p_fac, const SimScratch& S) {
-  const double t1g = gama * 2.0 * dt * dt;
-  const double rdt = 1.0 / dt;
-  const double capa1 = kappa - 1.0;
-  for (int k = 0; k < km; ++k) {
-    S.pl[k] = exp(gama * log(-dm2[k] / dz2[k] * RDGAS * pt2[k])) - pm2[k];
-    S.w1[k] = w2[k];
-  }
-  for (int k = 0; k < km - 1; ++k) {
-    double g = dm2[k] / dm2[k + 1];
-    S.g_rat[k] = g;
-    S.bb[k] = 2.0 * (1.0 + g);
-    S.dd[k] = 3.0 * (S.pl[k] + g * S.pl[k + 1]);
-  }
-  double bet = S.bb[0];
-  S.pp[0] = 0.0;
-  S.pp[1] = S.dd[0] / bet;
-  S.bb[km - 1] = 2.0;
-  S.dd[km - 1] = 3.0 * S.pl[km - 1];
-  for (int k = 1; k < km; ++k) {
-    double gm = S.g_rat[k - 1] / bet;
-    S.gam[k] = gm;
-    bet = S.bb[k] - gm;
-    S.pp[k + 1] = (S.dd[k] - S.pp[k]) / bet;
-  }
-  for (int k = km - 1; k > 0; --k) S.pp[k] = S.pp[k] - S.gam[k] * S.pp[k + 1];
-  for (int k = 1; k < km; ++k) S.aa[k] = t1g / (dz2[k - 1] + dz2[k]) * (pem[k] + S.pp[k]);
-  bet = dm2[0] - S.aa[1];
-  w2[0] = (dm2[0] * S.w1[0] + dt * S.pp[1]) / bet;
-  for (int k = 1; k < km - 1; ++k) {
-    double gm = S.aa[k] / bet;
-    S.gam[k] = gm;
-    bet = dm2[k] - (S.aa[k] + S.aa[k + 1] + S.aa[k] * gm);
-    w2[k] = (dm2[k] * S.w1[k] + dt * (S.pp[k + 1] - S.pp[k]) - S.aa[k] * w2[k - 1]) / bet;
-  }
-  double p1 = t1g / dz2[km - 1] * (pem[km] + S.pp[km]);
-  S.gam[km - 1] = S.aa[km - 1] / bet;
-  bet = dm2[km - 1] - (S.aa[km - 1] + p1 + S.aa[km - 1] * S.gam[km - 1]);
-  w2[km - 1] = (dm2[km - 1] * S.w1[km - 1] + dt * (S.pp[km] - S.pp[km - 1]) - p1 * ws - S.aa[km - 1] * w2[km - 2]) / bet;
-  for (int k = km - 2; k >= 0; --k) w2[k] = w2[k] - S.gam[k + 1] * w2[k + 1];
-  S.pe[0] = 0.0;
-  for (int k = 0; k < km; ++k) S.pe[k + 1] = S.pe[k] + dm2[k] * (w2[k] - S.w1[k]) * rdt;
-  p1 = (S.pe[km - 1] + 2.0 * S.pe[km]) * R3;
-  dz2[km - 1] = -dm2[km - 1] * RDGAS * pt2[km - 1] * exp(capa1 * log(fmax(p_fac * pm2[km - 1], p1 + pm2[km - 1])));
-  for (int k = km - 2; k >= 0; --k) {
-    p1 = (S.pe[k] + S.bb[k] * S.pe[k + 1] + S.g_rat[k] * S.pe[k + 2]) * R3 - S.g_rat[k] * p1;
-    dz2[k] = -dm2[k] * RDGAS * pt2[k] * exp(capa1 * log(fmax(p_fac * pm2[k], p1 + pm2[k])));
-  }
-}
-
-__device__ __forceinline__ SimScratch scratch_cols(const NhScratch& sc, const Dims& d, int s, int nk1, long o) {
-  SimScratch S;
-  S.pl = col(sc.s[0], d, s, nk1, o);
-  S.w1 = col(sc.s[1], d, s, nk1, o);
-  S.g_rat = col(sc.s[2], d, s, nk1, o);
-  S.bb = col(sc.s[3], d, s, nk1, o);
-  S.dd = col(sc.s[4], d, s, nk1, o);
-  S.gam = col(sc.s[5], d, s, nk1, o);
-  S.pp = col(sc.s[6], d, s, nk1, o);
-  S.aa = col(sc.s[7], d, s, nk1, o);
-  S.pe = col(sc.s[8], d, s, nk1, o);
-  return S;
 }
 
 // ---------------- update_dz_c (per interface level, out of place) ----------------
@@ -147,43 +75,6 @@ __global__ void __launch_bounds__(256) udzc_k(Dims d, const SubInfo* __restrict_
   const double area = MA(MT(M_AREA), 0, 0);
   const double gc = g[cc_off(d, sub, i, j, 2)];
   gzo[zo + o] = (gc * area + fx0 - fx1 + fy0 - fy1) / (area + xf0 - xf1 + yf0 - yf1);
-}
-
-// dz clamp + ws + riem_solver_c, one column per lane on cells [-1,nx]x[-1,ny]
-__global__ void __launch_bounds__(256) riem_c_k(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
-                                                int npz, double dt2, double ptop, double p_fac, double dz_min,
-                                                const double* __restrict__ delpc, const double* __restrict__ ptc,
-                                                const double* __restrict__ wc, const double* __restrict__ phis,
-                                                double* __restrict__ gz, double* __restrict__ pef, NhScratch sc) {
-  Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
-  int i, j;
-  if (!thread_point(L, i, j)) return;
-  const int s = blockIdx.z;
-  const long o = pidx(d, i, j);
-  const int km = npz, k1 = npz + 1;
-  Col G = col(gz, d, s, k1, o), PF = col(pef, d, s, k1, o);
-  Col DPC = ccol(delpc, d, s, km, o), PTC = ccol(ptc, d, s, km, o), WC = ccol(wc, d, s, km, o);
-  const double hs = phis[(long)s * d.plane + o];
-  const double zs = hs * (1.0 / GRAV);
-  const double ws = (zs - G[km]) * (1.0 / dt2);
-  for (int k = km - 1; k >= 0; --k) G[k] = fmax(G[k], G[k + 1] + dz_min);
-  SimScratch S = scratch_cols(sc, d, s, k1, o);
-  Col PEM = col(sc.s[9], d, s, k1, o), DM = col(sc.s[10], d, s, k1, o), PM2 = col(sc.s[11], d, s, k1, o),
-      DZ2 = col(sc.s[12], d, s, k1, o), W2 = col(sc.s[13], d, s, k1, o);
-  PEM[0] = ptop;
-  for (int k = 1; k <= km; ++k) PEM[k] = PEM[k - 1] + DPC[k - 1];
-  for (int k = 0; k < km; ++k) {
-    DZ2[k] = G[k + 1] - G[k];
-    PM2[k] = DPC[k] / log(PEM[k + 1] / PEM[k]);
-    DM[k] = DPC[k] * (1.0 / GRAV);
-    W2[k] = WC[k];
-  }
-  const double gama = 1.0 / (1.0 - KAPPA);
-  sim1(dt2, gama, KAPPA, km, DM, PM2, PEM, W2, DZ2, PTC, ws, p_fac, S);
-  PF[0] = ptop;
-  for (int k = 1; k <= km; ++k) PF[k] = S.pe[k] + PEM[k];
-  G[km] = hs;
-  for (int k = km - 1; k >= 0; --k) G[k] = G[k + 1] - DZ2[k] * GRAV;
 }
 
 // C-grid pressure gradient (non-hydrostatic: wk = delpc)
@@ -277,64 +168,6 @@ __global__ void __launch_bounds__(256) zh_update_k(Dims d, const SubInfo* __rest
   const double area = MA(MT(M_AREA), 0, 0);
   AT(zh, 0, 0) = (AT(zh, 0, 0) * area + AT(fx, 0, 0) - AT(fx, 1, 0) + AT(fy, 0, 0) - AT(fy, 0, 1)) /
                  (AT(ra_x, 0, 0) + AT(ra_y, 0, 0) - area);
-}
-
-// update_dz_d clamp + ws + riem_solver3 on compute columns
-__global__ void __launch_bounds__(256) riem3_k(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
-                                               int npz, double dt, double ptop, double p_fac, double dz_min,
-                                               int last_call, const double* __restrict__ delp,
-                                               const double* __restrict__ pt, const double* __restrict__ phis,
-                                               double* __restrict__ w, double* __restrict__ delz,
-                                               double* __restrict__ zh, double* __restrict__ ppe,
-                                               double* __restrict__ pk3, double* __restrict__ pe,
-                                               double* __restrict__ peln, double* __restrict__ pk, double* __restrict__ wsout,
-                                               NhScratch sc) {
-  Launch2D L{0, 0, d.nx, d.ny};
-  int i, j;
-  if (!thread_point(L, i, j)) return;
-  const int s = blockIdx.z;
-  const long o = pidx(d, i, j);
-  const int km = npz, k1 = npz + 1;
-  Col Z = col(zh, d, s, k1, o);
-  const double zs = phis[(long)s * d.plane + o] * (1.0 / GRAV);
-  const double ws = (zs - Z[km]) * (1.0 / dt);
-  if (wsout) wsout[(long)s * d.plane + o] = ws;
-  for (int k = km - 1; k >= 0; --k) Z[k] = fmax(Z[k], Z[k + 1] + dz_min);
-  SimScratch S = scratch_cols(sc, d, s, k1, o);
-  Col PEM = col(sc.s[9], d, s, k1, o), DM = col(sc.s[10], d, s, k1, o), PM2 = col(sc.s[11], d, s, k1, o),
-      DZ2 = col(sc.s[12], d, s, k1, o), PLN = col(sc.s[13], d, s, k1, o);
-  Col DP = ccol(delp, d, s, km, o), PT = ccol(pt, d, s, km, o), W = col(w, d, s, km, o);
-  Col PK3 = col(pk3, d, s, k1, o);
-  const double peln1 = log(ptop);
-  const double ptk = exp(KAPPA * peln1);
-  PEM[0] = ptop;
-  PLN[0] = peln1;
-  PK3[0] = ptk;
-  for (int k = 1; k <= km; ++k) {
-    PEM[k] = PEM[k - 1] + DP[k - 1];
-    PLN[k] = log(PEM[k]);
-    PK3[k] = exp(KAPPA * PLN[k]);
-  }
-  for (int k = 0; k < km; ++k) {
-    PM2[k] = DP[k] / (PLN[k + 1] - PLN[k]);
-    DM[k] = DP[k] * (1.0 / GRAV);
-    DZ2[k] = Z[k + 1] - Z[k];
-  }
-  const double gama = 1.0 / (1.0 - KAPPA);
-  sim1(dt, gama, KAPPA, km, DM, PM2, PEM, W, DZ2, PT, ws, p_fac, S);
-  Col DZ = col(delz, d, s, km, o), PP = col(ppe, d, s, k1, o);
-  for (int k = 0; k < km; ++k) DZ[k] = DZ2[k];
-  if (last_call) {
-    Col PE = col(pe, d, s, k1, o), PL = col(peln, d, s, k1, o), PK = col(pk, d, s, k1, o);
-    for (int k = 0; k <= km; ++k) {
-      PL[k] = PLN[k];
-      PK[k] = PK3[k];
-      PE[k] = PEM[k];
-    }
-  }
-  for (int k = 0; k <= km; ++k) PP[k] = S.pe[k];
-  Z[km] = zs;
-  for (int k = km - 1; k >= 0; --k) Z[k] = Z[k + 1] - DZ2[k];
 }
 
 // pk3 on the 2-wide halo ring and pe on the 1-wide ring (from the halo-updated delp)
@@ -572,16 +405,6 @@ void update_dz_c(const Ctx& c, int npz, const double* dp0, const double* ut, con
   HIP_LAUNCH_CHECK();
 }
 
-void riem_solver_c(const Ctx& c, int npz, double dt2, double ptop, double p_fac, double dz_min, const double* delpc,
-                   const double* ptc, const double* wc, const double* phis, double* gz, double* pef,
-                   const NhScratch& sc) {
-  const Dims& d = c.d;
-  Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
-  GT_LAUNCH(riem_c_k, g2(d, L, d.nsub), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt2, ptop, p_fac,
-                     dz_min, delpc, ptc, wc, phis, gz, pef, sc);
-  HIP_LAUNCH_CHECK();
-}
-
 void p_grad_c(const Ctx& c, int npz, double dt2, const double* delpc, const double* pkc, const double* gz, double* uc,
               double* vc) {
   const Dims& d = c.d;
@@ -611,15 +434,6 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
   Launch2D Li{0, 0, d.nx, d.ny};
   GT_LAUNCH(zh_update_k, g2(d, Li, d.nsub * k1), dim3(BX, BY), 0, c.st, d, c.subs, c.met, k1, a.fx, a.fy,
                      a.ra_x, a.ra_y, a.zh);
-  HIP_LAUNCH_CHECK();
-}
-
-void riem_solver3(const Ctx& c, const Riem3Args& a, const NhScratch& sc) {
-  const Dims& d = c.d;
-  Launch2D L{0, 0, d.nx, d.ny};
-  GT_LAUNCH(riem3_k, g2(d, L, d.nsub), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.ptop, a.p_fac,
-                     a.dz_min, a.last_call, a.delp, a.pt, a.phis, a.w, a.delz, a.zh, a.ppe, a.pk3, a.pe, a.peln, a.pk,
-                     a.ws, sc);
   HIP_LAUNCH_CHECK();
 }
 

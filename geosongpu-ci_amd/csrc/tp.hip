@@ -183,7 +183,7 @@ __global__ void __launch_bounds__(256) tracer_split_k(Dims d, const double* __re
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   int i, j;
   if (!thread_point(L, i, j)) return;
-  const int z = blockIdx.z, k = z % npz, s = z / npz;
+  const int z = blockIdx.z, k = z % npz;
   const long fo = (long)z * d.plane;
   const long o = pidx(d, i, j);
   const int ns = nsplt[k];
