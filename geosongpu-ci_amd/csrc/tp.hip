@@ -1,11 +1,10 @@
 // tp.hip — fv_tp_2d (Lin & Rood 1996 two-dimensional flux-form PPM transport,
 // FV3 tp_core) and the tracer_2d_1l pieces (FV3 fv_tracer2d), HIP for gfx950.
 //
-// fv_tp_2d is split in three plane-parallel passes so every pass is a pure
-// streaming stencil (HBM-bound, no MFMA):
-//   pass 1  fx2 = xppm(q, crx) [x-corner-filled q]   fy2 = yppm(q, cry) [y-corner-filled q]
-//   pass 2  q_i = (q*area + yfx*fy2|j - yfx*fy2|j+1)/ra_y    q_j = (q*area + xfx*fx2|i - ...)/ra_x
-//   pass 3  fx = 0.5*(xppm(q_i) + fx2)*mfx     fy = 0.5*(yppm(q_j) + fy2)*mfy
+// fv_tp_2d (HBM-bound, no MFMA) is one fused LDS-tiled kernel computing, per tile:
+//   fx2 = xppm(q, crx) [x-corner-filled q]   fy2 = yppm(q, cry) [y-corner-filled q]
+//   q_i = (q*area + yfx*fy2|j - yfx*fy2|j+1)/ra_y    q_j = (q*area + xfx*fx2|i - ...)/ra_x
+//   fx = 0.5*(xppm(q_i) + fx2)*mfx     fy = 0.5*(yppm(q_j) + fy2)*mfy
 // Operation order inside each expression follows the Fortran so the fp64
 // numpy oracle (oracle/fv3.py) matches to the last bits.
 #include "kernels.hpp"
@@ -20,108 +19,143 @@ inline dim3 grid_for(const Launch2D& L, long nz) {
   return dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), (unsigned)(nz < ZMAX ? nz : ZMAX));
 }
 
-__global__ void __launch_bounds__(256) tp_pass1(Dims d, const SubInfo* __restrict__ subs,
-                                                const double* __restrict__ M, const double* __restrict__ q, int nt,
-                                                int nk, const double* __restrict__ crx,
-                                                const double* __restrict__ cry, double* __restrict__ fx2,
-                                                double* __restrict__ fy2, int ord, int nz) {
-  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  int i, j;
-  if (!thread_point(L, i, j)) return;
+// Fused fv_tp_2d: one workgroup = one TX x TY tile of one (sub-domain, level); the
+// corner-filled q tiles, the inner fluxes fx2 / fy2 and the advective updates
+// q_i / q_j all stay in LDS, so HBM sees q, the Courant numbers and area fluxes once
+// and the two output fluxes once (the unfused form round-tripped four scratch
+// fields).  Regions and expressions are exactly those of the three-pass form.
+constexpr int TX = 64, TY = 8, TBLOCK = 256;
+constexpr int QX_C = TX + 6, QX_R = TY + 5;   // q (x corner fill): cols i0-3..i0+TX+2, rows j0-3..j0+TY+1
+constexpr int QY_C = TX + 5, QY_R = TY + 6;   // q (y corner fill): cols i0-3..i0+TX+1, rows j0-3..j0+TY+2
+constexpr int FX_C = TX + 1, FX_R = TY + 5;   // fx2: edges i0..i0+TX, rows j0-3..j0+TY+1
+constexpr int FY_C = TX + 5, FY_R = TY + 1;   // fy2: cols i0-3..i0+TX+1, edges j0..j0+TY
+constexpr int QI_C = TX + 5, QI_R = TY;       // q_i: cols i0-3..i0+TX+1, rows j0..j0+TY-1
+constexpr int QJ_C = TX, QJ_R = TY + 5;       // q_j: cols i0..i0+TX-1, rows j0-3..j0+TY+1
+
+__global__ void __launch_bounds__(TBLOCK) tp_fused(Dims d, const SubInfo* __restrict__ subs,
+                                                   const double* __restrict__ M, const double* __restrict__ q, int nt,
+                                                   int nk, const double* __restrict__ crx,
+                                                   const double* __restrict__ cry, const double* __restrict__ xfx,
+                                                   const double* __restrict__ yfx, const double* __restrict__ ra_x,
+                                                   const double* __restrict__ ra_y, const double* __restrict__ mx,
+                                                   const double* __restrict__ my, double* __restrict__ fx,
+                                                   double* __restrict__ fy, int ord, int nz) {
+  __shared__ double QX[QX_R][QX_C];
+  __shared__ double QY[QY_R][QY_C];
+  __shared__ double FX2[FX_R][FX_C];
+  __shared__ double FY2[FY_R][FY_C];
+  __shared__ double QI[QI_R][QI_C];
+  __shared__ double QJ[QJ_R][QJ_C];
+  const int i0 = blockIdx.x * TX, j0 = blockIdx.y * TY;
+  const int tid = threadIdx.x;
+  const int nx = d.nx, ny = d.ny;
+  // cell halo only (not the +1 staggered row/column): copy_corners sources of points
+  // beyond it would leave the plane
+  auto inplane = [&](int i, int j) { return i >= -NG && i < nx + NG && j >= -NG && j < ny + NG; };
   for (int z = blockIdx.z; z < nz; z += gridDim.z) {
     const int k = z % nk, s = z / nk / nt;
     const SubInfo sub = subs[s];
     const double* qq = q + (long)z * d.plane;
     const long fo = ((long)s * nk + k) * d.plane;
-    if (i >= 0 && i <= d.nx && j >= -NG && j <= d.ny + NG - 1) {
-      const double* dxa = met(M, d, M_DXA, s);
-      double qv[6], dx[6];
+    const long zo = (long)z * d.plane;
+    const double* dxa = met(M, d, M_DXA, s);
+    const double* dya = met(M, d, M_DYA, s);
+    const double* area = met(M, d, M_AREA, s);
+    __syncthreads();  // previous level's readers are done with the tiles
+    for (int p = tid; p < QX_R * QX_C; p += TBLOCK) {
+      const int r = p / QX_C, c = p % QX_C;
+      const int i = i0 - 3 + c, j = j0 - 3 + r;
+      QX[r][c] = inplane(i, j) ? qq[cc_off(d, sub, i, j, 1)] : 0.0;
+    }
+    for (int p = tid; p < QY_R * QY_C; p += TBLOCK) {
+      const int r = p / QY_C, c = p % QY_C;
+      const int i = i0 - 3 + c, j = j0 - 3 + r;
+      QY[r][c] = inplane(i, j) ? qq[cc_off(d, sub, i, j, 2)] : 0.0;
+    }
+    __syncthreads();
+    // inner fluxes: fx2 on x-edges i in [0, nx], rows [-3, ny+2]; fy2 on y-edges j in [0, ny], cols [-3, nx+2]
+    for (int p = tid; p < FX_R * FX_C; p += TBLOCK) {
+      const int r = p / FX_C, c = p % FX_C;
+      const int i = i0 + c, j = j0 - 3 + r;
+      double v = 0.0;
+      if (i >= 0 && i <= nx && j >= -NG && j <= ny + NG - 1) {
+        double qv[6], dx[6];
 #pragma unroll
-      for (int m = 0; m < 6; ++m) {
-        qv[m] = qq[cc_off(d, sub, i - 3 + m, j, 1)];
-        dx[m] = dxa[pidx(d, i - 3 + m, j)];
+        for (int m = 0; m < 6; ++m) {
+          qv[m] = QX[r][c + m];
+          dx[m] = dxa[pidx(d, i - 3 + m, j)];
+        }
+        v = ppm_flux_ord(ord, i + sub.ioff, sub.N, qv, dx, crx[fo + pidx(d, i, j)]);
       }
-      fx2[(long)z * d.plane + pidx(d, i, j)] = ppm_flux_ord(ord, i + sub.ioff, sub.N, qv, dx, crx[fo + pidx(d, i, j)]);
+      FX2[r][c] = v;
     }
-    if (j >= 0 && j <= d.ny && i >= -NG && i <= d.nx + NG - 1) {
-      const double* dya = met(M, d, M_DYA, s);
-      double qv[6], dy[6];
+    for (int p = tid; p < FY_R * FY_C; p += TBLOCK) {
+      const int r = p / FY_C, c = p % FY_C;
+      const int i = i0 - 3 + c, j = j0 + r;
+      double v = 0.0;
+      if (j >= 0 && j <= ny && i >= -NG && i <= nx + NG - 1) {
+        double qv[6], dy[6];
 #pragma unroll
-      for (int m = 0; m < 6; ++m) {
-        qv[m] = qq[cc_off(d, sub, i, j - 3 + m, 2)];
-        dy[m] = dya[pidx(d, i, j - 3 + m)];
+        for (int m = 0; m < 6; ++m) {
+          qv[m] = QY[r + m][c];
+          dy[m] = dya[pidx(d, i, j - 3 + m)];
+        }
+        v = ppm_flux_ord(ord, j + sub.joff, sub.N, qv, dy, cry[fo + pidx(d, i, j)]);
       }
-      fy2[(long)z * d.plane + pidx(d, i, j)] = ppm_flux_ord(ord, j + sub.joff, sub.N, qv, dy, cry[fo + pidx(d, i, j)]);
+      FY2[r][c] = v;
     }
-  }
-}
-
-__global__ void __launch_bounds__(256) tp_pass2(Dims d, const double* __restrict__ M, const double* __restrict__ q,
-                                                int nt, int nk, const double* __restrict__ xfx,
-                                                const double* __restrict__ yfx, const double* __restrict__ ra_x,
-                                                const double* __restrict__ ra_y, const double* __restrict__ fx2,
-                                                const double* __restrict__ fy2, double* __restrict__ qi,
-                                                double* __restrict__ qj, int nz) {
-  Launch2D L{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  int i, j;
-  if (!thread_point(L, i, j)) return;
-  for (int z = blockIdx.z; z < nz; z += gridDim.z) {
-    const int k = z % nk, s = z / nk / nt;
-    const long zo = (long)z * d.plane, fo = ((long)s * nk + k) * d.plane;
-    const double area = met(M, d, M_AREA, s)[pidx(d, i, j)];
-    const long o = pidx(d, i, j);
-    const double qv = q[zo + o];
-    if (j >= 0 && j < d.ny) {
-      const long on = pidx(d, i, j + 1);
-      double fyy0 = yfx[fo + o] * fy2[zo + o];
-      double fyy1 = yfx[fo + on] * fy2[zo + on];
-      qi[zo + o] = (qv * area + fyy0 - fyy1) / ra_y[fo + o];
+    __syncthreads();
+    // advective updates q_i (rows [0, ny)) and q_j (cols [0, nx))
+    for (int p = tid; p < QI_R * QI_C; p += TBLOCK) {
+      const int r = p / QI_C, c = p % QI_C;
+      const int i = i0 - 3 + c, j = j0 + r;
+      double v = 0.0;
+      if (j >= 0 && j < ny && i >= -NG && i < nx + NG) {
+        const long o = pidx(d, i, j), on = pidx(d, i, j + 1);
+        const double fyy0 = yfx[fo + o] * FY2[r][c];
+        const double fyy1 = yfx[fo + on] * FY2[r + 1][c];
+        v = (QY[r + 3][c] * area[o] + fyy0 - fyy1) / ra_y[fo + o];
+      }
+      QI[r][c] = v;
     }
-    if (i >= 0 && i < d.nx) {
-      const long oe = pidx(d, i + 1, j);
-      double fxx0 = xfx[fo + o] * fx2[zo + o];
-      double fxx1 = xfx[fo + oe] * fx2[zo + oe];
-      qj[zo + o] = (qv * area + fxx0 - fxx1) / ra_x[fo + o];
+    for (int p = tid; p < QJ_R * QJ_C; p += TBLOCK) {
+      const int r = p / QJ_C, c = p % QJ_C;
+      const int i = i0 + c, j = j0 - 3 + r;
+      double v = 0.0;
+      if (i >= 0 && i < nx && j >= -NG && j < ny + NG) {
+        const long o = pidx(d, i, j), oe = pidx(d, i + 1, j);
+        const double fxx0 = xfx[fo + o] * FX2[r][c];
+        const double fxx1 = xfx[fo + oe] * FX2[r][c + 1];
+        v = (QX[r][c + 3] * area[o] + fxx0 - fxx1) / ra_x[fo + o];
+      }
+      QJ[r][c] = v;
     }
-  }
-}
-
-__global__ void __launch_bounds__(256) tp_pass3(Dims d, const SubInfo* __restrict__ subs,
-                                                const double* __restrict__ M, int nt, int nk,
-                                                const double* __restrict__ crx, const double* __restrict__ cry,
-                                                const double* __restrict__ mx, const double* __restrict__ my,
-                                                const double* __restrict__ fx2, const double* __restrict__ fy2,
-                                                const double* __restrict__ qi, const double* __restrict__ qj,
-                                                double* __restrict__ fx, double* __restrict__ fy, int ord, int nz) {
-  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  int i, j;
-  if (!thread_point(L, i, j)) return;
-  for (int z = blockIdx.z; z < nz; z += gridDim.z) {
-    const int k = z % nk, s = z / nk / nt;
-    const SubInfo sub = subs[s];
-    const long zo = (long)z * d.plane, fo = ((long)s * nk + k) * d.plane;
-    const long o = pidx(d, i, j);
-    if (j < d.ny) {
-      const double* dxa = met(M, d, M_DXA, s);
-      double qv[6], dx[6];
+    __syncthreads();
+    // outer fluxes
+    for (int p = tid; p < TX * TY; p += TBLOCK) {
+      const int r = p / TX, c = p % TX;
+      const int i = i0 + c, j = j0 + r;
+      const long o = pidx(d, i, j);
+      if (j < ny && i <= nx) {
+        double qv[6], dx[6];
 #pragma unroll
-      for (int m = 0; m < 6; ++m) {
-        qv[m] = qi[zo + pidx(d, i - 3 + m, j)];
-        dx[m] = dxa[pidx(d, i - 3 + m, j)];
+        for (int m = 0; m < 6; ++m) {
+          qv[m] = QI[r][c + m];
+          dx[m] = dxa[pidx(d, i - 3 + m, j)];
+        }
+        const double f = ppm_flux_ord(ord, i + sub.ioff, sub.N, qv, dx, crx[fo + o]);
+        fx[zo + o] = 0.5 * (f + FX2[r + 3][c]) * mx[fo + o];
       }
-      double f = ppm_flux_ord(ord, i + sub.ioff, sub.N, qv, dx, crx[fo + o]);
-      fx[zo + o] = 0.5 * (f + fx2[zo + o]) * mx[fo + o];
-    }
-    if (i < d.nx) {
-      const double* dya = met(M, d, M_DYA, s);
-      double qv[6], dy[6];
+      if (i < nx && j <= ny) {
+        double qv[6], dy[6];
 #pragma unroll
-      for (int m = 0; m < 6; ++m) {
-        qv[m] = qj[zo + pidx(d, i, j - 3 + m)];
-        dy[m] = dya[pidx(d, i, j - 3 + m)];
+        for (int m = 0; m < 6; ++m) {
+          qv[m] = QJ[r + m][c];
+          dy[m] = dya[pidx(d, i, j - 3 + m)];
+        }
+        const double f = ppm_flux_ord(ord, j + sub.joff, sub.N, qv, dy, cry[fo + o]);
+        fy[zo + o] = 0.5 * (f + FY2[r][c + 3]) * my[fo + o];
       }
-      double f = ppm_flux_ord(ord, j + sub.joff, sub.N, qv, dy, cry[fo + o]);
-      fy[zo + o] = 0.5 * (f + fy2[zo + o]) * my[fo + o];
     }
   }
 }
@@ -258,18 +292,9 @@ __global__ void copy_k(long n, const double* __restrict__ a, double* __restrict_
 void fv_tp_2d(const Ctx& c, const TpArgs& a) {
   const Dims& d = c.d;
   long nz = (long)d.nsub * a.nt * a.nk;
-  Launch2D L1{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  GT_LAUNCH(tp_pass1, grid_for(L1, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.q, a.nt, a.nk, a.crx,
-                     a.cry, a.fx2, a.fy2, a.ord, (int)nz);
-  HIP_LAUNCH_CHECK();
-  Launch2D L2{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  GT_LAUNCH(tp_pass2, grid_for(L2, nz), dim3(BX, BY), 0, c.st, d, c.met, a.q, a.nt, a.nk, a.xfx, a.yfx,
-                     a.ra_x, a.ra_y, a.fx2, a.fy2, a.qi, a.qj, (int)nz);
-  HIP_LAUNCH_CHECK();
-  Launch2D L3{0, 0, d.nx + 1, d.ny + 1};
-  GT_LAUNCH(tp_pass3, grid_for(L3, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.nt, a.nk, a.crx, a.cry,
-                     a.mfx ? a.mfx : a.xfx, a.mfy ? a.mfy : a.yfx, a.fx2, a.fy2, a.qi, a.qj, a.fx, a.fy, a.ord,
-                     (int)nz);
+  dim3 g(cdiv(d.nx + 1, TX), cdiv(d.ny + 1, TY), (unsigned)(nz < ZMAX ? nz : ZMAX));
+  GT_LAUNCH(tp_fused, g, dim3(TBLOCK), 0, c.st, d, c.subs, c.met, a.q, a.nt, a.nk, a.crx, a.cry, a.xfx, a.yfx,
+            a.ra_x, a.ra_y, a.mfx ? a.mfx : a.xfx, a.mfy ? a.mfy : a.yfx, a.fx, a.fy, a.ord, (int)nz);
   HIP_LAUNCH_CHECK();
 }
 
