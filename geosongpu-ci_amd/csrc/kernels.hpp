@@ -26,6 +26,7 @@ struct TpArgs {
   double *fx, *fy;
   double *fx2, *fy2, *qi, *qj;  // scratch, same shape as q
   int ord;
+  int cfg = -1;  // tile variant (tuning); -1: default
 };
 void fv_tp_2d(const Ctx& c, const TpArgs& a);
 

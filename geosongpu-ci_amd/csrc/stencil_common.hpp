@@ -78,13 +78,17 @@ __device__ __forceinline__ double ppm_al(int g, int N, const double* q, const do
   return P1 * (q[1] + q[2]) + P2 * (q[0] + q[3]);
 }
 
+__device__ __forceinline__ double ppm_al_in(const double* q) { return P1 * (q[1] + q[2]) + P2 * (q[0] + q[3]); }
+
 // PPM flux through interface g for hord 5 / 6 (FV3 xppm/yppm, iord < 8 branch).
 //   q[0..5] = q(g-3) .. q(g+2); dx[0..5] = dxa at those cells; c = Courant number.
-template <int ORD>
+// EDGE = false: the caller guarantees g-1..g+1 are away from the tile edges, so only
+// the interior interface formula can apply (dx is not read).
+template <int ORD, bool EDGE = true>
 __device__ __forceinline__ double ppm_flux(int g, int N, const double* q, const double* dx, double c) {
-  double alm = ppm_al(g - 1, N, q + 0, dx + 0);
-  double al0 = ppm_al(g, N, q + 1, dx + 1);
-  double alp = ppm_al(g + 1, N, q + 2, dx + 2);
+  double alm = EDGE ? ppm_al(g - 1, N, q + 0, dx + 0) : ppm_al_in(q + 0);
+  double al0 = EDGE ? ppm_al(g, N, q + 1, dx + 1) : ppm_al_in(q + 1);
+  double alp = EDGE ? ppm_al(g + 1, N, q + 2, dx + 2) : ppm_al_in(q + 2);
   double blm = alm - q[2], brm = al0 - q[2], b0m = blm + brm;
   double bl0 = al0 - q[3], br0 = alp - q[3], b00 = bl0 + br0;
   bool sm, s0;
@@ -103,6 +107,11 @@ __device__ __forceinline__ double ppm_flux(int g, int N, const double* q, const 
     double fx1 = (1.0 + c) * (bl0 + c * b00);
     return q[3] + (smooth ? fx1 : 0.0);
   }
+}
+
+template <bool EDGE>
+__device__ __forceinline__ double ppm_flux_o(int ord, int g, int N, const double* q, const double* dx, double c) {
+  return ord == 5 ? ppm_flux<5, EDGE>(g, N, q, dx, c) : ppm_flux<6, EDGE>(g, N, q, dx, c);
 }
 
 __device__ __forceinline__ double ppm_flux_ord(int ord, int g, int N, const double* q, const double* dx, double c) {

@@ -45,6 +45,7 @@ std::map<std::string, Fn>& reg() {
          a.fx2 = dy.field("_tp_fx2", q.nk).p; a.fy2 = dy.field("_tp_fy2", q.nk).p;
          a.qi = dy.field("_tp_qi", q.nk).p; a.qj = dy.field("_tp_qj", q.nk).p;
          a.ord = ord;
+         a.cfg = p.size() > 2 ? (int)p[2] : -1;
          fv_tp_2d(dy.ctx(), a);
        }},
       // c_sw(delp, pt, w, u, v | uc, vc, ua, va, ut, vt, delpc, ptc, wc) params: dt2

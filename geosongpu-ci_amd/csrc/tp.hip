@@ -19,144 +19,173 @@ inline dim3 grid_for(const Launch2D& L, long nz) {
   return dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), (unsigned)(nz < ZMAX ? nz : ZMAX));
 }
 
-// Fused fv_tp_2d: one workgroup = one TX x TY tile of one (sub-domain, level); the
-// corner-filled q tiles, the inner fluxes fx2 / fy2 and the advective updates
-// q_i / q_j all stay in LDS, so HBM sees q, the Courant numbers and area fluxes once
-// and the two output fluxes once (the unfused form round-tripped four scratch
-// fields).  Regions and expressions are exactly those of the three-pass form.
-constexpr int TX = 64, TY = 8, TBLOCK = 256;
-constexpr int QX_C = TX + 6, QX_R = TY + 5;   // q (x corner fill): cols i0-3..i0+TX+2, rows j0-3..j0+TY+1
-constexpr int QY_C = TX + 5, QY_R = TY + 6;   // q (y corner fill): cols i0-3..i0+TX+1, rows j0-3..j0+TY+2
-constexpr int FX_C = TX + 1, FX_R = TY + 5;   // fx2: edges i0..i0+TX, rows j0-3..j0+TY+1
-constexpr int FY_C = TX + 5, FY_R = TY + 1;   // fy2: cols i0-3..i0+TX+1, edges j0..j0+TY
-constexpr int QI_C = TX + 5, QI_R = TY;       // q_i: cols i0-3..i0+TX+1, rows j0..j0+TY-1
-constexpr int QJ_C = TX, QJ_R = TY + 5;       // q_j: cols i0..i0+TX-1, rows j0-3..j0+TY+1
+// Fused fv_tp_2d: one workgroup = one 64 x 8 tile of one (sub-domain, level), 256
+// threads as 64 x 4 (a wavefront = one 64-wide tile row, so global row reads are
+// coalesced).  The corner-filled q tiles, the inner fluxes fx2 / fy2 and the
+// advective updates q_i / q_j all stay in LDS, so HBM sees q, the Courant numbers
+// and area fluxes once and the two output fluxes once (the unfused form round-
+// tripped four scratch fields).  Tiles away from the tile edges take the interior
+// PPM path (no edge-interface branches, no dxa reads) and tiles away from the cube
+// corners skip the copy_corners remap; regions and expressions are exactly those of
+// the three-pass form (FV3 fv_tp_2d).
+constexpr int TX = 64, TY = 8, TW = 4;
+constexpr int QX_C = TX + 6, QX_R = TY + 5;  // q (x corner fill): cols i0-3..i0+TX+2, rows j0-3..j0+TY+1
+constexpr int QY_C = TX + 5, QY_R = TY + 6;  // q (y corner fill): cols i0-3..i0+TX+1, rows j0-3..j0+TY+2
+constexpr int FX_C = TX + 1, FX_R = TY + 5;  // fx2: edges i0..i0+TX, rows j0-3..j0+TY+1
+constexpr int FY_C = TX + 5, FY_R = TY + 1;  // fy2: cols i0-3..i0+TX+1, edges j0..j0+TY
+constexpr int QI_C = TX + 5, QI_R = TY;      // q_i: cols i0-3..i0+TX+1, rows j0..j0+TY-1
+constexpr int QJ_C = TX, QJ_R = TY + 5;      // q_j: cols i0..i0+TX-1, rows j0-3..j0+TY+1
 
-__global__ void __launch_bounds__(TBLOCK) tp_fused(Dims d, const SubInfo* __restrict__ subs,
-                                                   const double* __restrict__ M, const double* __restrict__ q, int nt,
-                                                   int nk, const double* __restrict__ crx,
-                                                   const double* __restrict__ cry, const double* __restrict__ xfx,
-                                                   const double* __restrict__ yfx, const double* __restrict__ ra_x,
-                                                   const double* __restrict__ ra_y, const double* __restrict__ mx,
-                                                   const double* __restrict__ my, double* __restrict__ fx,
-                                                   double* __restrict__ fy, int ord, int nz) {
-  __shared__ double QX[QX_R][QX_C];
-  __shared__ double QY[QY_R][QY_C];
-  __shared__ double FX2[FX_R][FX_C];
-  __shared__ double FY2[FY_R][FY_C];
-  __shared__ double QI[QI_R][QI_C];
-  __shared__ double QJ[QJ_R][QJ_C];
-  const int i0 = blockIdx.x * TX, j0 = blockIdx.y * TY;
-  const int tid = threadIdx.x;
+struct TpTiles {
+  double QX[QX_R][QX_C];
+  double QY[QY_R][QY_C];
+  double FX2[FX_R][FX_C];
+  double FY2[FY_R][FY_C];
+  double QI[QI_R][QI_C];
+  double QJ[QJ_R][QJ_C];
+};
+
+struct TpK {
+  Dims d;
+  const SubInfo* subs;
+  const double *M, *q;
+  int nt, nk;
+  const double *crx, *cry, *xfx, *yfx, *ra_x, *ra_y, *mx, *my;
+  double *fx, *fy;
+  int ord, nz;
+};
+
+template <bool EX, bool EY, bool CORNER>
+__device__ void tp_tile(const TpK& a, TpTiles& T, int z, int i0, int j0) {
+  const Dims& d = a.d;
+  const int tx = threadIdx.x, ty = threadIdx.y, tid = ty * TX + tx;
   const int nx = d.nx, ny = d.ny;
+  const int k = z % a.nk, s = z / a.nk / a.nt;
+  const SubInfo sub = a.subs[s];
+  const double* qq = a.q + (long)z * d.plane;
+  const long fo = ((long)s * a.nk + k) * d.plane;
+  const long zo = (long)z * d.plane;
+  const double* dxa = met(a.M, d, M_DXA, s);
+  const double* dya = met(a.M, d, M_DYA, s);
+  const double* area = met(a.M, d, M_AREA, s);
+  const int ord = a.ord;
   // cell halo only (not the +1 staggered row/column): copy_corners sources of points
   // beyond it would leave the plane
   auto inplane = [&](int i, int j) { return i >= -NG && i < nx + NG && j >= -NG && j < ny + NG; };
-  for (int z = blockIdx.z; z < nz; z += gridDim.z) {
-    const int k = z % nk, s = z / nk / nt;
-    const SubInfo sub = subs[s];
-    const double* qq = q + (long)z * d.plane;
-    const long fo = ((long)s * nk + k) * d.plane;
-    const long zo = (long)z * d.plane;
-    const double* dxa = met(M, d, M_DXA, s);
-    const double* dya = met(M, d, M_DYA, s);
-    const double* area = met(M, d, M_AREA, s);
+  for (int p = tid; p < QX_R * QX_C; p += TX * TW) {
+    const int r = p / QX_C, c = p % QX_C;
+    const int i = i0 - 3 + c, j = j0 - 3 + r;
+    T.QX[r][c] = inplane(i, j) ? qq[CORNER ? cc_off(d, sub, i, j, 1) : pidx(d, i, j)] : 0.0;
+  }
+  for (int p = tid; p < QY_R * QY_C; p += TX * TW) {
+    const int r = p / QY_C, c = p % QY_C;
+    const int i = i0 - 3 + c, j = j0 - 3 + r;
+    T.QY[r][c] = inplane(i, j) ? qq[CORNER ? cc_off(d, sub, i, j, 2) : pidx(d, i, j)] : 0.0;
+  }
+  __syncthreads();
+  // inner fluxes: fx2 on x-edges i in [0, nx], rows [-3, ny+2]; fy2 on y-edges j in [0, ny], cols [-3, nx+2]
+  for (int p = tid; p < FX_R * FX_C; p += TX * TW) {
+    const int r = p / FX_C, c = p % FX_C;
+    const int i = i0 + c, j = j0 - 3 + r;
+    double v = 0.0;
+    if (i <= nx && j >= -NG && j <= ny + NG - 1) {
+      double qv[6], dx[6];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        qv[m] = T.QX[r][c + m];
+        dx[m] = EX ? dxa[pidx(d, i - 3 + m, j)] : 0.0;
+      }
+      v = ppm_flux_o<EX>(ord, i + sub.ioff, sub.N, qv, dx, a.crx[fo + pidx(d, i, j)]);
+    }
+    T.FX2[r][c] = v;
+  }
+  for (int p = tid; p < FY_R * FY_C; p += TX * TW) {
+    const int r = p / FY_C, c = p % FY_C;
+    const int i = i0 - 3 + c, j = j0 + r;
+    double v = 0.0;
+    if (j <= ny && i >= -NG && i <= nx + NG - 1) {
+      double qv[6], dy[6];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        qv[m] = T.QY[r + m][c];
+        dy[m] = EY ? dya[pidx(d, i, j - 3 + m)] : 0.0;
+      }
+      v = ppm_flux_o<EY>(ord, j + sub.joff, sub.N, qv, dy, a.cry[fo + pidx(d, i, j)]);
+    }
+    T.FY2[r][c] = v;
+  }
+  __syncthreads();
+  // advective updates q_i (rows [0, ny)) and q_j (cols [0, nx))
+  for (int p = tid; p < QI_R * QI_C; p += TX * TW) {
+    const int r = p / QI_C, c = p % QI_C;
+    const int i = i0 - 3 + c, j = j0 + r;
+    double v = 0.0;
+    if (j < ny && i >= -NG && i < nx + NG) {
+      const long o = pidx(d, i, j), on = pidx(d, i, j + 1);
+      const double fyy0 = a.yfx[fo + o] * T.FY2[r][c];
+      const double fyy1 = a.yfx[fo + on] * T.FY2[r + 1][c];
+      v = (T.QY[r + 3][c] * area[o] + fyy0 - fyy1) / a.ra_y[fo + o];
+    }
+    T.QI[r][c] = v;
+  }
+  for (int p = tid; p < QJ_R * QJ_C; p += TX * TW) {
+    const int r = p / QJ_C, c = p % QJ_C;
+    const int i = i0 + c, j = j0 - 3 + r;
+    double v = 0.0;
+    if (i < nx && j >= -NG && j < ny + NG) {
+      const long o = pidx(d, i, j), oe = pidx(d, i + 1, j);
+      const double fxx0 = a.xfx[fo + o] * T.FX2[r][c];
+      const double fxx1 = a.xfx[fo + oe] * T.FX2[r][c + 1];
+      v = (T.QX[r][c + 3] * area[o] + fxx0 - fxx1) / a.ra_x[fo + o];
+    }
+    T.QJ[r][c] = v;
+  }
+  __syncthreads();
+  // outer fluxes
+  for (int r = ty; r < TY; r += TW) {
+    const int c = tx;
+    const int i = i0 + c, j = j0 + r;
+    const long o = pidx(d, i, j);
+    if (j < ny && i <= nx) {
+      double qv[6], dx[6];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        qv[m] = T.QI[r][c + m];
+        dx[m] = EX ? dxa[pidx(d, i - 3 + m, j)] : 0.0;
+      }
+      const double f = ppm_flux_o<EX>(ord, i + sub.ioff, sub.N, qv, dx, a.crx[fo + o]);
+      a.fx[zo + o] = 0.5 * (f + T.FX2[r + 3][c]) * a.mx[fo + o];
+    }
+    if (i < nx && j <= ny) {
+      double qv[6], dy[6];
+#pragma unroll
+      for (int m = 0; m < 6; ++m) {
+        qv[m] = T.QJ[r + m][c];
+        dy[m] = EY ? dya[pidx(d, i, j - 3 + m)] : 0.0;
+      }
+      const double f = ppm_flux_o<EY>(ord, j + sub.joff, sub.N, qv, dy, a.cry[fo + o]);
+      a.fy[zo + o] = 0.5 * (f + T.FY2[r][c + 3]) * a.my[fo + o];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(TX * TW) tp_fused(TpK a) {
+  __shared__ TpTiles T;
+  const int i0 = blockIdx.x * TX, j0 = blockIdx.y * TY;
+  for (int z = blockIdx.z; z < a.nz; z += gridDim.z) {
+    const int s = z / a.nk / a.nt;
+    const SubInfo& sub = a.subs[s];
+    const int N = sub.N, I0 = i0 + sub.ioff, J0 = j0 + sub.joff;
+    // interfaces g-1..g+1 touched by this tile's fluxes: [I0-1, I0+TX+1] (x), [J0-1, J0+TY+1] (y)
+    const bool ex = !(I0 - 1 >= 2 && I0 + TX + 1 <= N - 2);
+    const bool ey = !(J0 - 1 >= 2 && J0 + TY + 1 <= N - 2);
+    const bool corner = (I0 - 3 < 0 || I0 + TX + 2 >= N) && (J0 - 3 < 0 || J0 + TY + 2 >= N);
     __syncthreads();  // previous level's readers are done with the tiles
-    for (int p = tid; p < QX_R * QX_C; p += TBLOCK) {
-      const int r = p / QX_C, c = p % QX_C;
-      const int i = i0 - 3 + c, j = j0 - 3 + r;
-      QX[r][c] = inplane(i, j) ? qq[cc_off(d, sub, i, j, 1)] : 0.0;
-    }
-    for (int p = tid; p < QY_R * QY_C; p += TBLOCK) {
-      const int r = p / QY_C, c = p % QY_C;
-      const int i = i0 - 3 + c, j = j0 - 3 + r;
-      QY[r][c] = inplane(i, j) ? qq[cc_off(d, sub, i, j, 2)] : 0.0;
-    }
-    __syncthreads();
-    // inner fluxes: fx2 on x-edges i in [0, nx], rows [-3, ny+2]; fy2 on y-edges j in [0, ny], cols [-3, nx+2]
-    for (int p = tid; p < FX_R * FX_C; p += TBLOCK) {
-      const int r = p / FX_C, c = p % FX_C;
-      const int i = i0 + c, j = j0 - 3 + r;
-      double v = 0.0;
-      if (i >= 0 && i <= nx && j >= -NG && j <= ny + NG - 1) {
-        double qv[6], dx[6];
-#pragma unroll
-        for (int m = 0; m < 6; ++m) {
-          qv[m] = QX[r][c + m];
-          dx[m] = dxa[pidx(d, i - 3 + m, j)];
-        }
-        v = ppm_flux_ord(ord, i + sub.ioff, sub.N, qv, dx, crx[fo + pidx(d, i, j)]);
-      }
-      FX2[r][c] = v;
-    }
-    for (int p = tid; p < FY_R * FY_C; p += TBLOCK) {
-      const int r = p / FY_C, c = p % FY_C;
-      const int i = i0 - 3 + c, j = j0 + r;
-      double v = 0.0;
-      if (j >= 0 && j <= ny && i >= -NG && i <= nx + NG - 1) {
-        double qv[6], dy[6];
-#pragma unroll
-        for (int m = 0; m < 6; ++m) {
-          qv[m] = QY[r + m][c];
-          dy[m] = dya[pidx(d, i, j - 3 + m)];
-        }
-        v = ppm_flux_ord(ord, j + sub.joff, sub.N, qv, dy, cry[fo + pidx(d, i, j)]);
-      }
-      FY2[r][c] = v;
-    }
-    __syncthreads();
-    // advective updates q_i (rows [0, ny)) and q_j (cols [0, nx))
-    for (int p = tid; p < QI_R * QI_C; p += TBLOCK) {
-      const int r = p / QI_C, c = p % QI_C;
-      const int i = i0 - 3 + c, j = j0 + r;
-      double v = 0.0;
-      if (j >= 0 && j < ny && i >= -NG && i < nx + NG) {
-        const long o = pidx(d, i, j), on = pidx(d, i, j + 1);
-        const double fyy0 = yfx[fo + o] * FY2[r][c];
-        const double fyy1 = yfx[fo + on] * FY2[r + 1][c];
-        v = (QY[r + 3][c] * area[o] + fyy0 - fyy1) / ra_y[fo + o];
-      }
-      QI[r][c] = v;
-    }
-    for (int p = tid; p < QJ_R * QJ_C; p += TBLOCK) {
-      const int r = p / QJ_C, c = p % QJ_C;
-      const int i = i0 + c, j = j0 - 3 + r;
-      double v = 0.0;
-      if (i >= 0 && i < nx && j >= -NG && j < ny + NG) {
-        const long o = pidx(d, i, j), oe = pidx(d, i + 1, j);
-        const double fxx0 = xfx[fo + o] * FX2[r][c];
-        const double fxx1 = xfx[fo + oe] * FX2[r][c + 1];
-        v = (QX[r][c + 3] * area[o] + fxx0 - fxx1) / ra_x[fo + o];
-      }
-      QJ[r][c] = v;
-    }
-    __syncthreads();
-    // outer fluxes
-    for (int p = tid; p < TX * TY; p += TBLOCK) {
-      const int r = p / TX, c = p % TX;
-      const int i = i0 + c, j = j0 + r;
-      const long o = pidx(d, i, j);
-      if (j < ny && i <= nx) {
-        double qv[6], dx[6];
-#pragma unroll
-        for (int m = 0; m < 6; ++m) {
-          qv[m] = QI[r][c + m];
-          dx[m] = dxa[pidx(d, i - 3 + m, j)];
-        }
-        const double f = ppm_flux_ord(ord, i + sub.ioff, sub.N, qv, dx, crx[fo + o]);
-        fx[zo + o] = 0.5 * (f + FX2[r + 3][c]) * mx[fo + o];
-      }
-      if (i < nx && j <= ny) {
-        double qv[6], dy[6];
-#pragma unroll
-        for (int m = 0; m < 6; ++m) {
-          qv[m] = QJ[r + m][c];
-          dy[m] = dya[pidx(d, i, j - 3 + m)];
-        }
-        const double f = ppm_flux_ord(ord, j + sub.joff, sub.N, qv, dy, cry[fo + o]);
-        fy[zo + o] = 0.5 * (f + FY2[r][c + 3]) * my[fo + o];
-      }
-    }
+    if (corner) tp_tile<true, true, true>(a, T, z, i0, j0);
+    else if (ex && ey) tp_tile<true, true, false>(a, T, z, i0, j0);
+    else if (ex) tp_tile<true, false, false>(a, T, z, i0, j0);
+    else if (ey) tp_tile<false, true, false>(a, T, z, i0, j0);
+    else tp_tile<false, false, false>(a, T, z, i0, j0);
   }
 }
 
@@ -292,9 +321,10 @@ __global__ void copy_k(long n, const double* __restrict__ a, double* __restrict_
 void fv_tp_2d(const Ctx& c, const TpArgs& a) {
   const Dims& d = c.d;
   long nz = (long)d.nsub * a.nt * a.nk;
+  TpK k{d, c.subs, c.met, a.q, a.nt, a.nk, a.crx, a.cry, a.xfx, a.yfx, a.ra_x, a.ra_y,
+        a.mfx ? a.mfx : a.xfx, a.mfy ? a.mfy : a.yfx, a.fx, a.fy, a.ord, (int)nz};
   dim3 g(cdiv(d.nx + 1, TX), cdiv(d.ny + 1, TY), (unsigned)(nz < ZMAX ? nz : ZMAX));
-  GT_LAUNCH(tp_fused, g, dim3(TBLOCK), 0, c.st, d, c.subs, c.met, a.q, a.nt, a.nk, a.crx, a.cry, a.xfx, a.yfx,
-            a.ra_x, a.ra_y, a.mfx ? a.mfx : a.xfx, a.mfy ? a.mfy : a.yfx, a.fx, a.fy, a.ord, (int)nz);
+  GT_LAUNCH(tp_fused, g, dim3(TX, TW), 0, c.st, k);
   HIP_LAUNCH_CHECK();
 }
 
