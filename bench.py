@@ -31,24 +31,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 
-# Algorithmic HBM bytes per launch of the kernels that can dominate a step:
-# distinct fp64 fields read + written once over the kernel's domain (see DESIGN.md
-# "Kernels").  c = cells per level over the launch's sub-domains, L = levels.
-def _cols(d, ring=0):
-    return d.nsub * (d.nx + 2 * ring) * (d.ny + 2 * ring)
-
-
-KERNEL_BYTES = {
-    # riem_solver3 (+ update_dz_d clamp): read zh(L+1) delp pt w phis, write w delz zh ppe pk3 ws
-    # (pe/peln/pk on the last acoustic sub-step only are not counted: a lower bound)
-    "riem3_k": lambda d: 8 * _cols(d) * ((d.npz + 1) + 3 * d.npz + 1 + 2 * d.npz + 3 * (d.npz + 1) + 1),
-    # riem_solver_c on the 1-ring: read delpc ptc wc gz(L+1) phis, write gz(L+1) pef(L+1)
-    "riem_c_k": lambda d: 8 * _cols(d, 1) * (3 * d.npz + (d.npz + 1) + 1 + 2 * (d.npz + 1)),
-    # Lagrangian_to_Eulerian scalars: read pe peln (L+1) delp delz pt w q ws, write pt delp delz w q pk
-    # peln (L+1) pkz ps
-    "remap_scalar_k": lambda d: 8 * _cols(d) * ((2 * (d.npz + 1) + 4 * d.npz + d.nq * d.npz + 1)
-                                                + (4 * d.npz + d.nq * d.npz + 2 * (d.npz + 1) + d.npz + 1)),
-}
+# Algorithmic HBM bytes come from the library: each launcher registers its
+# kernel's bytes per launch (distinct fields read + written once over the compute
+# domain; formulas in DESIGN.md §4) with the event timer.
 
 
 def pmc_traffic(kernel):
@@ -177,22 +162,18 @@ def main():
 
     roof = None
     if kstats:
-        name, (tot, n) = max(kstats.items(), key=lambda kv: kv[1][0])
+        name, (tot, n, byt) = max(kstats.items(), key=lambda kv: kv[1][0])
         avg_ms = tot / n
-        fn = KERNEL_BYTES.get(name)
-        if fn is not None:
-            b = fn(d)
-            ach = b / (avg_ms * 1e-3) / 1e9
-            traffic, src = pmc_traffic(name)
-            roof = dict(bound="hbm", kernel=name, achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
-                        frac=ach / HBM_PEAK_GBS, traffic=traffic, traffic_source=src, bytes_per_launch=b,
-                        avg_ms=avg_ms, share_of_step=tot / (ms_step * a.steps))
-        else:
-            roof = dict(bound="hbm", kernel=name, achieved=None, peak=HBM_PEAK_GBS, unit="GB/s", frac=None,
-                        traffic=None, avg_ms=avg_ms, share_of_step=tot / (ms_step * a.steps))
+        traffic, src = pmc_traffic(name)
+        ach = byt / (tot * 1e-3) / 1e9 if byt > 0 else None
+        roof = dict(bound="hbm", kernel=name, achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
+                    frac=ach / HBM_PEAK_GBS if ach else None, traffic=traffic, traffic_source=src,
+                    bytes_per_launch=byt / n if byt > 0 else None, avg_ms=avg_ms,
+                    share_of_step=tot / (ms_step * a.steps))
         if a.kernel_report and rank == 0:
             with open(a.kernel_report, "w") as f:
-                json.dump({k: dict(ms_total=v[0], launches=v[1], ms_per_step=v[0] / a.steps)
+                json.dump({k: dict(ms_total=v[0], launches=v[1], ms_per_step=v[0] / a.steps,
+                                   gbs=(v[2] / (v[0] * 1e-3) / 1e9) if v[2] > 0 else None)
                            for k, v in sorted(kstats.items(), key=lambda kv: -kv[1][0])}, f, indent=1)
 
     cpu = None

@@ -311,7 +311,8 @@ int gtfv3_kernel_stats(void* h, char* buf, int len) {
   gtfv3::ktimer_flush();
   std::string s;
   for (auto& kv : gtfv3::ktimer_stats())
-    s += kv.first + "=" + std::to_string(kv.second.ms) + "," + std::to_string(kv.second.launches) + ";";
+    s += kv.first + "=" + std::to_string(kv.second.ms) + "," + std::to_string(kv.second.launches) + "," +
+         std::to_string(kv.second.bytes) + ";";
   if (buf && len > 0) {
     std::strncpy(buf, s.c_str(), (size_t)len - 1);
     buf[len - 1] = 0;

@@ -33,11 +33,14 @@ inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
 struct KernelStat {
   double ms = 0.0;
   long launches = 0;
+  double bytes = 0.0;  // algorithmic HBM bytes of the timed launches (0: no formula)
 };
 bool ktimer_enabled();
 void ktimer_enable(bool on);
 void ktimer_begin(const char* name, hipStream_t s);
 void ktimer_end(hipStream_t s);
+// algorithmic bytes of the launch just issued (DESIGN.md §4 formulas); no-op when off
+void ktimer_bytes(double bytes);
 void ktimer_flush();
 void ktimer_reset();
 const std::map<std::string, KernelStat>& ktimer_stats();

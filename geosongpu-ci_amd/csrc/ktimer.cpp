@@ -9,6 +9,7 @@ namespace {
 struct Pending {
   const char* name;
   hipEvent_t b, e;
+  double bytes;
 };
 
 struct KTimer {
@@ -42,7 +43,7 @@ void ktimer_begin(const char* name, hipStream_t s) {
   KTimer& t = kt();
   hipEvent_t b = t.take();
   HIP_CHECK(hipEventRecord(b, s));
-  t.pending.push_back({name, b, nullptr});
+  t.pending.push_back({name, b, nullptr, 0.0});
 }
 
 void ktimer_end(hipStream_t s) {
@@ -50,6 +51,11 @@ void ktimer_end(hipStream_t s) {
   hipEvent_t e = t.take();
   HIP_CHECK(hipEventRecord(e, s));
   t.pending.back().e = e;
+}
+
+void ktimer_bytes(double bytes) {
+  KTimer& t = kt();
+  if (t.on && !t.pending.empty()) t.pending.back().bytes = bytes;
 }
 
 void ktimer_flush() {
@@ -62,6 +68,7 @@ void ktimer_flush() {
     KernelStat& k = t.stats[p.name];
     k.ms += ms;
     k.launches += 1;
+    k.bytes += p.bytes;
   }
   t.pending.clear();
   t.used = 0;

@@ -170,26 +170,38 @@ __global__ void __launch_bounds__(256) zh_update_k(Dims d, const SubInfo* __rest
                  (AT(ra_x, 0, 0) + AT(ra_y, 0, 0) - area);
 }
 
-// pk3 on the 2-wide halo ring and pe on the 1-wide ring (from the halo-updated delp)
+// pk3 on the 2-wide halo ring and pe on the 1-wide ring (from the halo-updated delp):
+// one lane per (ring column, level); each lane sums delp from the top in the same order
+// as the sequential column loop, so the values are identical
+__device__ __forceinline__ bool ring2_point(int t, int nx, int ny, int& i, int& j) {
+  const int w = nx + 4;
+  if (t < 2 * w) { i = t % w - 2; j = t / w - 2; return true; }            // rows -2, -1
+  t -= 2 * w;
+  if (t < 2 * w) { i = t % w - 2; j = ny + t / w; return true; }           // rows ny, ny+1
+  t -= 2 * w;
+  if (t < 2 * ny) { i = t % 2 - 2; j = t / 2; return true; }               // cols -2, -1
+  t -= 2 * ny;
+  if (t < 2 * ny) { i = nx + t % 2; j = t / 2; return true; }              // cols nx, nx+1
+  return false;
+}
+
 __global__ void __launch_bounds__(256) pk3_pe_halo_k(Dims d, int npz, double ptop, int do_pe,
                                                      const double* __restrict__ delp, double* __restrict__ pk3,
                                                      double* __restrict__ pe) {
-  Launch2D L{-2, -2, d.nx + 4, d.ny + 4};
   int i, j;
-  if (!thread_point(L, i, j)) return;
-  if (i >= 0 && i < d.nx && j >= 0 && j < d.ny) return;
-  const int s = blockIdx.z;
+  if (!ring2_point(blockIdx.x * blockDim.x + threadIdx.x, d.nx, d.ny, i, j)) return;
+  const int s = blockIdx.z / npz, k = blockIdx.z % npz;
   const long o = pidx(d, i, j);
   const int km = npz, k1 = npz + 1;
-  Col DP = ccol(delp, d, s, km, o), PK = col(pk3, d, s, k1, o);
+  const double* DP = delp + (long)s * km * d.plane + o;
   const bool ring1 = i >= -1 && i <= d.nx && j >= -1 && j <= d.ny;
-  Col PE = col(pe, d, s, k1, o);
   double pei = ptop;
-  if (do_pe && ring1) PE[0] = ptop;
-  for (int k = 0; k < km; ++k) {
-    pei = pei + DP[k];
-    PK[k + 1] = exp(KAPPA * log(pei));
-    if (do_pe && ring1) PE[k + 1] = pei;
+  for (int m = 0; m <= k; ++m) pei = pei + DP[(long)m * d.plane];
+  const long b1 = (long)s * k1 * d.plane + o;
+  pk3[b1 + (long)(k + 1) * d.plane] = exp(KAPPA * log(pei));
+  if (do_pe && ring1) {
+    pe[b1 + (long)(k + 1) * d.plane] = pei;
+    if (k == 0) pe[b1] = ptop;
   }
 }
 
@@ -266,8 +278,15 @@ __global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restr
                                                   const double* __restrict__ M, int nk, const double* __restrict__ cw,
                                                   const double* __restrict__ q, const double* __restrict__ qx,
                                                   const double* __restrict__ qy, double* __restrict__ qout) {
-  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  KSETUP2(nk)
+  // all targets lie on the tile-edge lines: one lane per line point
+  const int z = blockIdx.z, s = z / nk;
+  const SubInfo sub = subs[s];
+  int i, j;
+  if (!edge_line_point(blockIdx.x * blockDim.x + threadIdx.x, sub, 0, d.nx, 0, d.ny, i, j)) return;
+  const int N = sub.N;
+  const int I = i + sub.ioff, J = j + sub.joff;
+  const long zo = (long)z * d.plane;
+  const long o = pidx(d, i, j);
   const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
   // cube corner value (extrapolation from the three faces)
   auto corner_val = [&](int c) {
@@ -439,8 +458,8 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
 
 void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* delp, double* pk3, double* pe) {
   const Dims& d = c.d;
-  Launch2D L{-2, -2, d.nx + 4, d.ny + 4};
-  GT_LAUNCH(pk3_pe_halo_k, g2(d, L, d.nsub), dim3(BX, BY), 0, c.st, d, npz, ptop, do_pe ? 1 : 0, delp, pk3,
+  const int nring = 4 * (d.nx + 4) + 4 * d.ny;
+  GT_LAUNCH(pk3_pe_halo_k, dim3(cdiv(nring, 256), 1, d.nsub * npz), dim3(256), 0, c.st, d, npz, ptop, do_pe ? 1 : 0, delp, pk3,
                      pe);
   HIP_LAUNCH_CHECK();
 }
@@ -451,7 +470,7 @@ void a2b_ord4(const Ctx& c, int nk, const double* q, double* qout, double* qx, d
   GT_LAUNCH(a2b_qxqy_k, g2(d, Lf, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, c.met, nk, q, qx, qy);
   HIP_LAUNCH_CHECK();
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
-  GT_LAUNCH(a2b_edge_k, g2(d, Lc, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, c.met, nk, c.cornerw, q,
+  GT_LAUNCH(a2b_edge_k, dim3(cdiv(edge_line_count(0, d.nx, 0, d.ny), 256), 1, d.nsub * nk), dim3(256), 0, c.st, d, c.subs, c.met, nk, c.cornerw, q,
                      qx, qy, qout);
   HIP_LAUNCH_CHECK();
   GT_LAUNCH(a2b_inner_k, g2(d, Lc, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, nk, qx, qy, qout);

@@ -469,6 +469,9 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
   HIP_LAUNCH_CHECK();
   GT_LAUNCH(remap_job_k, dim3(cdiv(nce, BLOCK), a.njob, d.nsub), dim3(BLOCK), 0, c.st, a);
   HIP_LAUNCH_CHECK();
+  // algorithmic bytes per column: every job reads its field and writes it back (L each),
+  // pe (+ peln for T) read once, ws
+  ktimer_bytes(8.0 * nc * d.nsub * (2.0 * npz * a.njob + 2.0 * (npz + 1) + 1));
   GT_LAUNCH(remap_finish_k, dim3(cdiv(nc, BLOCK), d.nsub), dim3(BLOCK), 0, c.st, a);
   HIP_LAUNCH_CHECK();
 }

@@ -277,6 +277,11 @@ void launch_riem(const Ctx& c, const RiemArgs& a) {
   const int ncol = (c.d.nx + 2 * a.ring) * (c.d.ny + 2 * a.ring);
   GT_LAUNCH(riem_col_k, dim3(cdiv(ncol, BLOCK), c.d.nsub), dim3(BLOCK), 0, c.st, a);
   HIP_LAUNCH_CHECK();
+  // algorithmic bytes per column: C grid reads delpc ptc wc (L) gz (L+1) phis, writes gz pef (L+1);
+  // D grid reads zh (L+1) delp pt w (L) phis, writes w delz (L) zh ppe pk3 (L+1) ws (+ pe peln pk)
+  const double km = a.npz, k1 = a.npz + 1;
+  const double per = a.cgrid ? 3 * km + 3 * k1 + 1 : 5 * km + (4 + (a.last_call ? 3 : 0)) * k1 + 2;
+  ktimer_bytes(8.0 * ncol * c.d.nsub * per);
 }
 
 }  // namespace

@@ -62,6 +62,32 @@ __device__ __forceinline__ long cc_off(const Dims& d, const SubInfo& s, int i, i
   return pidx(d, i, j);
 }
 
+// Candidate points of the tile-edge lines I in {-1, 0, N-1, N} (any j in [jlo, jhi]) and
+// J in {-1, 0, N-1, N} (any i in [ilo, ihi]) of a sub-domain, enumerated by t in
+// [0, edge_line_count): kernels whose targets all lie on those lines launch this many
+// lanes per plane instead of the whole plane.  Points outside the ranges and the
+// duplicates of the second family return false.
+__host__ __device__ inline int edge_line_count(int ilo, int ihi, int jlo, int jhi) {
+  return 4 * (jhi - jlo + 1) + 4 * (ihi - ilo + 1);
+}
+__device__ inline bool edge_line_point(int t, const SubInfo& sub, int ilo, int ihi, int jlo, int jhi, int& i,
+                                       int& j) {
+  const int N = sub.N, nj = jhi - jlo + 1, ni = ihi - ilo + 1;
+  auto line = [&](int l) { return l == 0 ? -1 : (l == 1 ? 0 : (l == 2 ? N - 1 : N)); };
+  if (t < 4 * nj) {
+    i = line(t / nj) - sub.ioff;
+    j = jlo + t % nj;
+    return i >= ilo && i <= ihi;
+  }
+  t -= 4 * nj;
+  if (t >= 4 * ni) return false;
+  j = line(t / ni) - sub.joff;
+  i = ilo + t % ni;
+  const int I = i + sub.ioff;
+  if (I == -1 || I == 0 || I == N - 1 || I == N) return false;  // already a column-line point
+  return j >= jlo && j <= jhi;
+}
+
 // PPM constants (FV3 tp_core)
 constexpr double P1 = 7.0 / 12.0, P2 = -1.0 / 12.0;
 constexpr double C1 = -2.0 / 14.0, C2 = 11.0 / 14.0, C3 = 5.0 / 14.0;

@@ -321,8 +321,15 @@ struct CornerMap {
 __global__ void __launch_bounds__(256) ds_utvt2(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
                                                 int npz, const double* __restrict__ uc, const double* __restrict__ vc,
                                                 double* __restrict__ ut, double* __restrict__ vt) {
-  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  KSETUP(npz)
+  // all targets lie on the tile-edge lines: one lane per line point
+  const int z = blockIdx.z, s = z / npz;
+  const SubInfo sub = subs[s];
+  int i, j;
+  if (!edge_line_point(blockIdx.x * blockDim.x + threadIdx.x, sub, -NG, d.nx + NG, -NG, d.ny + NG, i, j)) return;
+  const int N = sub.N;
+  const int I = i + sub.ioff, J = j + sub.joff;
+  const long zo = (long)z * d.plane;
+  const long o = pidx(d, i, j);
   const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
   // cross terms
   bool has_vt = false, has_ut = false;
@@ -610,7 +617,7 @@ void d_sw(const Ctx& c, const DswArgs& a) {
   GT_LAUNCH(ds_utvt1, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.uc, a.vc,
                      a.ut, a.vt);
   HIP_LAUNCH_CHECK();
-  GT_LAUNCH(ds_utvt2, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.ut,
+  GT_LAUNCH(ds_utvt2, dim3(cdiv(edge_line_count(-NG, d.nx + NG, -NG, d.ny + NG), 256), 1, nz), dim3(256), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.ut,
                      a.vt);
   HIP_LAUNCH_CHECK();
   GT_LAUNCH(ds_courant, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.ut, a.vt,

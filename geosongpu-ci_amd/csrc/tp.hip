@@ -326,6 +326,10 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
   dim3 g(cdiv(d.nx + 1, TX), cdiv(d.ny + 1, TY), (unsigned)(nz < ZMAX ? nz : ZMAX));
   GT_LAUNCH(tp_fused, g, dim3(TX, TW), 0, c.st, k);
   HIP_LAUNCH_CHECK();
+  // algorithmic bytes: q read + fx, fy written per plane; crx cry xfx yfx ra_x ra_y (+ mfx mfy)
+  // read once per (sub-domain, level) however many tracers share them
+  const double cells = (double)d.nx * d.ny;
+  ktimer_bytes(8.0 * cells * (3.0 * nz + (double)d.nsub * a.nk * (6 + (a.mfx ? 2 : 0))));
 }
 
 void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, double* xfx, double* yfx, double* ra_x,

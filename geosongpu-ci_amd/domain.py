@@ -135,15 +135,15 @@ class Domain:
         check(lib().gtfv3_kernel_timing(self.h, 1 if on else 0))
 
     def kernel_stats(self):
-        """{kernel: (total_ms, launches)} since kernel_timing(True)"""
+        """{kernel: (total_ms, launches, algorithmic_bytes)} since kernel_timing(True)"""
         buf = ctypes.create_string_buffer(1 << 16)
         check(lib().gtfv3_kernel_stats(self.h, buf, 1 << 16))
         out = {}
         for item in buf.value.decode().split(";"):
             if "=" in item:
                 k, v = item.split("=")
-                ms, n = v.split(",")
-                out[k] = (float(ms), int(n))
+                ms, n, b = v.split(",")
+                out[k] = (float(ms), int(n), float(b))
         return out
 
     def timers(self):

@@ -50,10 +50,10 @@ def main():
         st = d.kernel_stats()
         d.kernel_timing(False)
         ms = {k: v[0] / v[1] for k, v in st.items()}
+        gb = {k: v[2] / (v[0] * 1e-3) / 1e9 for k, v in st.items()}
         cells = d.nsub * d.nx * d.ny * a.npz
         for k, v in ms.items():
-            gbs = 9 * 8 * cells / (v * 1e-3) / 1e9
-            print(f"cfg {cfg:2d} {k[:40]:40s} {v:.4f} ms  {gbs:7.1f} GB/s algorithmic  identical={same}", flush=True)
+            print(f"cfg {cfg:2d} {k[:40]:40s} {v:.4f} ms  {gb[k]:7.1f} GB/s algorithmic  identical={same}", flush=True)
 
 
 if __name__ == "__main__":
