@@ -103,47 +103,69 @@ __global__ void __launch_bounds__(256) pgradc_k(Dims d, const SubInfo* __restric
   }
 }
 
-// edge_profile of (crx, xfx) on x-face columns and (cry, yfx) on y-face columns
-__device__ void edge_profile_col(const Col& q, const Col& qe, const Col& gam, const double* dp0, int km) {
+// edge_profile of (crx, xfx) on x-face columns and (cry, yfx) on y-face columns.
+// The tridiagonal coefficients depend only on the reference thicknesses dp0, so the
+// elimination factors gam are computed once per workgroup into LDS (same expressions
+// as the per-column form) and each column only carries its edge values.
+__device__ void edge_profile_col(const Col& q, const Col& qe, const double* gam, const double* dp0, int km) {
   double g0 = dp0[1] / dp0[0];
   double xt1 = 2.0 * g0 * (g0 + 1.0);
   double bet = g0 * (g0 + 0.5);
-  qe[0] = (xt1 * q[0] + q[1]) / bet;
-  gam[0] = (1.0 + g0 * (g0 + 1.5)) / bet;
+  double qp = (xt1 * q[0] + q[1]) / bet;
+  qe[0] = qp;
   double gk = g0;
+  double qprev = q[0];
   for (int k = 1; k < km; ++k) {
     gk = dp0[k - 1] / dp0[k];
     bet = 2.0 + 2.0 * gk - gam[k - 1];
-    qe[k] = (3.0 * (q[k - 1] + gk * q[k]) - qe[k - 1]) / bet;
-    gam[k] = gk / bet;
+    const double qk = q[k];
+    qp = (3.0 * (qprev + gk * qk) - qp) / bet;
+    qe[k] = qp;
+    qprev = qk;
   }
   double a_bot = 1.0 + gk * (gk + 1.5);
   xt1 = 2.0 * gk * (gk + 1.0);
   double xt2 = gk * (gk + 0.5) - a_bot * gam[km - 1];
-  qe[km] = (xt1 * q[km - 1] + q[km - 2] - a_bot * qe[km - 1]) / xt2;
-  for (int k = km - 1; k >= 0; --k) qe[k] = qe[k] - gam[k] * qe[k + 1];
+  double x = (xt1 * qprev + q[km - 2] - a_bot * qp) / xt2;
+  qe[km] = x;
+  for (int k = km - 1; k >= 0; --k) {
+    x = qe[k] - gam[k] * x;
+    qe[k] = x;
+  }
 }
+
+constexpr int EP_KMAX = 256;
 
 __global__ void __launch_bounds__(256) edge_prof_k(Dims d, int npz, const double* __restrict__ dp0,
                                                    const double* __restrict__ crx, const double* __restrict__ xfx,
                                                    const double* __restrict__ cry, const double* __restrict__ yfx,
                                                    double* __restrict__ crx_e, double* __restrict__ xfx_e,
-                                                   double* __restrict__ cry_e, double* __restrict__ yfx_e,
-                                                   double* __restrict__ gam_scr) {
+                                                   double* __restrict__ cry_e, double* __restrict__ yfx_e) {
+  __shared__ double gam[EP_KMAX];
+  const int km = npz, k1 = npz + 1;
+  if (threadIdx.x == 0 && threadIdx.y == 0) {
+    double g0 = dp0[1] / dp0[0];
+    double bet = g0 * (g0 + 0.5);
+    gam[0] = (1.0 + g0 * (g0 + 1.5)) / bet;
+    for (int k = 1; k < km; ++k) {
+      double gk = dp0[k - 1] / dp0[k];
+      bet = 2.0 + 2.0 * gk - gam[k - 1];
+      gam[k] = gk / bet;
+    }
+  }
+  __syncthreads();
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   int i, j;
   if (!thread_point(L, i, j)) return;
   const int s = blockIdx.z;
   const long o = pidx(d, i, j);
-  const int km = npz, k1 = npz + 1;
-  Col G = col(gam_scr, d, s, k1, o);
   if (i >= 0 && i <= d.nx && j <= d.ny + NG - 1) {
-    edge_profile_col(ccol(crx, d, s, km, o), col(crx_e, d, s, k1, o), G, dp0, km);
-    edge_profile_col(ccol(xfx, d, s, km, o), col(xfx_e, d, s, k1, o), G, dp0, km);
+    edge_profile_col(ccol(crx, d, s, km, o), col(crx_e, d, s, k1, o), gam, dp0, km);
+    edge_profile_col(ccol(xfx, d, s, km, o), col(xfx_e, d, s, k1, o), gam, dp0, km);
   }
   if (j >= 0 && j <= d.ny && i <= d.nx + NG - 1) {
-    edge_profile_col(ccol(cry, d, s, km, o), col(cry_e, d, s, k1, o), G, dp0, km);
-    edge_profile_col(ccol(yfx, d, s, km, o), col(yfx_e, d, s, k1, o), G, dp0, km);
+    edge_profile_col(ccol(cry, d, s, km, o), col(cry_e, d, s, k1, o), gam, dp0, km);
+    edge_profile_col(ccol(yfx, d, s, km, o), col(yfx_e, d, s, k1, o), gam, dp0, km);
   }
 }
 
@@ -210,74 +232,76 @@ constexpr double B1 = 7.0 / 12.0, B2 = -1.0 / 12.0;
 constexpr double AA1 = 0.5625, AA2 = -0.0625;
 constexpr double AC1 = 2.0 / 3.0, AC2 = -1.0 / 6.0;
 
-__global__ void __launch_bounds__(256) a2b_qxqy_k(Dims d, const SubInfo* __restrict__ subs,
-                                                  const double* __restrict__ M, int nk, const double* __restrict__ q,
-                                                  double* __restrict__ qx, double* __restrict__ qy) {
-  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  KSETUP2(nk)
-  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
-  const double* dxa = MT(M_DXA);
-  const double* dya = MT(M_DYA);
-  double vx = 0.0, vy = 0.0;
-  const bool rows = J >= max(0, jo - 2) && J <= min(N - 1, jo + ny + 1);
-  if (rows) {
-    auto gen = [&](int di) {
-      return B2 * (AT(q, di - 2, 0) + AT(q, di + 1, 0)) + B1 * (AT(q, di - 1, 0) + AT(q, di, 0));
-    };
+// x- and y-interpolated values of a2b_ord4 at one point (the former qx / qy planes),
+// evaluated on the fly by the corner-value kernels so those planes never touch HBM.
+// Zero where the 3-pass form left them unset.
+struct A2bPoint {
+  const Dims& d;
+  const SubInfo& sub;
+  const double* q;   // plane of the level
+  const double* dxa;
+  const double* dya;
+  __device__ __forceinline__ double Q(int i, int j) const { return q[pidx(d, i, j)]; }
+  __device__ double qx(int i, int j) const {
+    const int N = sub.N, io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+    const int I = i + io, J = j + jo;
+    if (!(J >= max(0, jo - 2) && J <= min(N - 1, jo + ny + 1))) return 0.0;
+    auto gen = [&](int di) { return B2 * (Q(i + di - 2, j) + Q(i + di + 1, j)) + B1 * (Q(i + di - 1, j) + Q(i + di, j)); };
+    auto DX = [&](int di) { return dxa[pidx(d, i + di, j)]; };
     if (I == 0) {
-      double gr = MA(dxa, 1, 0) / MA(dxa, 0, 0);
-      vx = 0.5 * ((2.0 + gr) * (AT(q, -1, 0) + AT(q, 0, 0)) - (AT(q, -2, 0) + AT(q, 1, 0))) / (1.0 + gr);
+      double gr = DX(1) / DX(0);
+      return 0.5 * ((2.0 + gr) * (Q(i - 1, j) + Q(i, j)) - (Q(i - 2, j) + Q(i + 1, j))) / (1.0 + gr);
     } else if (I == N) {
-      double gr = MA(dxa, -2, 0) / MA(dxa, -1, 0);
-      vx = 0.5 * ((2.0 + gr) * (AT(q, -1, 0) + AT(q, 0, 0)) - (AT(q, -2, 0) + AT(q, 1, 0))) / (1.0 + gr);
+      double gr = DX(-2) / DX(-1);
+      return 0.5 * ((2.0 + gr) * (Q(i - 1, j) + Q(i, j)) - (Q(i - 2, j) + Q(i + 1, j))) / (1.0 + gr);
     } else if (I == 1) {
-      double g1 = MA(dxa, 0, 0) / MA(dxa, -1, 0);
-      double gw = MA(dxa, 0, 0) / MA(dxa, -1, 0);  // ratio at the edge I = 0: dxa(1)/dxa(0)
-      double qx0 = 0.5 * ((2.0 + gw) * (AT(q, -2, 0) + AT(q, -1, 0)) - (AT(q, -3, 0) + AT(q, 0, 0))) / (1.0 + gw);
-      vx = (3.0 * (g1 * AT(q, -1, 0) + AT(q, 0, 0)) - (g1 * qx0 + gen(1))) / (2.0 + 2.0 * g1);
+      double g1 = DX(0) / DX(-1);
+      double gw = DX(0) / DX(-1);  // ratio at the edge I = 0: dxa(1)/dxa(0)
+      double qx0 = 0.5 * ((2.0 + gw) * (Q(i - 2, j) + Q(i - 1, j)) - (Q(i - 3, j) + Q(i, j))) / (1.0 + gw);
+      return (3.0 * (g1 * Q(i - 1, j) + Q(i, j)) - (g1 * qx0 + gen(1))) / (2.0 + 2.0 * g1);
     } else if (I == N - 1) {
-      double g1 = MA(dxa, -1, 0) / MA(dxa, 0, 0);
-      double ge = MA(dxa, -1, 0) / MA(dxa, 0, 0);  // ratio at the edge I = N: dxa(N-2)/dxa(N-1)
-      double qxN = 0.5 * ((2.0 + ge) * (AT(q, 0, 0) + AT(q, 1, 0)) - (AT(q, -1, 0) + AT(q, 2, 0))) / (1.0 + ge);
-      vx = (3.0 * (AT(q, -1, 0) + g1 * AT(q, 0, 0)) - (g1 * qxN + gen(-1))) / (2.0 + 2.0 * g1);
+      double g1 = DX(-1) / DX(0);
+      double ge = DX(-1) / DX(0);  // ratio at the edge I = N: dxa(N-2)/dxa(N-1)
+      double qxN = 0.5 * ((2.0 + ge) * (Q(i, j) + Q(i + 1, j)) - (Q(i - 1, j) + Q(i + 2, j))) / (1.0 + ge);
+      return (3.0 * (Q(i - 1, j) + g1 * Q(i, j)) - (g1 * qxN + gen(-1))) / (2.0 + 2.0 * g1);
     } else if (I >= max(2, io) && I <= min(N - 2, io + nx)) {
-      vx = gen(0);
+      return gen(0);
     }
+    return 0.0;
   }
-  const bool cols = I >= max(0, io - 2) && I <= min(N - 1, io + nx + 1);
-  if (cols) {
-    auto gen = [&](int dj) {
-      return B2 * (AT(q, 0, dj - 2) + AT(q, 0, dj + 1)) + B1 * (AT(q, 0, dj - 1) + AT(q, 0, dj));
-    };
+  __device__ double qy(int i, int j) const {
+    const int N = sub.N, io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+    const int I = i + io, J = j + jo;
+    if (!(I >= max(0, io - 2) && I <= min(N - 1, io + nx + 1))) return 0.0;
+    auto gen = [&](int dj) { return B2 * (Q(i, j + dj - 2) + Q(i, j + dj + 1)) + B1 * (Q(i, j + dj - 1) + Q(i, j + dj)); };
+    auto DY = [&](int dj) { return dya[pidx(d, i, j + dj)]; };
     if (J == 0) {
-      double gr = MA(dya, 0, 1) / MA(dya, 0, 0);
-      vy = 0.5 * ((2.0 + gr) * (AT(q, 0, -1) + AT(q, 0, 0)) - (AT(q, 0, -2) + AT(q, 0, 1))) / (1.0 + gr);
+      double gr = DY(1) / DY(0);
+      return 0.5 * ((2.0 + gr) * (Q(i, j - 1) + Q(i, j)) - (Q(i, j - 2) + Q(i, j + 1))) / (1.0 + gr);
     } else if (J == N) {
-      double gr = MA(dya, 0, -2) / MA(dya, 0, -1);
-      vy = 0.5 * ((2.0 + gr) * (AT(q, 0, -1) + AT(q, 0, 0)) - (AT(q, 0, -2) + AT(q, 0, 1))) / (1.0 + gr);
+      double gr = DY(-2) / DY(-1);
+      return 0.5 * ((2.0 + gr) * (Q(i, j - 1) + Q(i, j)) - (Q(i, j - 2) + Q(i, j + 1))) / (1.0 + gr);
     } else if (J == 1) {
-      double g1 = MA(dya, 0, 0) / MA(dya, 0, -1);
-      double gs = MA(dya, 0, 0) / MA(dya, 0, -1);
-      double qy0 = 0.5 * ((2.0 + gs) * (AT(q, 0, -2) + AT(q, 0, -1)) - (AT(q, 0, -3) + AT(q, 0, 0))) / (1.0 + gs);
-      vy = (3.0 * (g1 * AT(q, 0, -1) + AT(q, 0, 0)) - (g1 * qy0 + gen(1))) / (2.0 + 2.0 * g1);
+      double g1 = DY(0) / DY(-1);
+      double gs = DY(0) / DY(-1);
+      double qy0 = 0.5 * ((2.0 + gs) * (Q(i, j - 2) + Q(i, j - 1)) - (Q(i, j - 3) + Q(i, j))) / (1.0 + gs);
+      return (3.0 * (g1 * Q(i, j - 1) + Q(i, j)) - (g1 * qy0 + gen(1))) / (2.0 + 2.0 * g1);
     } else if (J == N - 1) {
-      double g1 = MA(dya, 0, -1) / MA(dya, 0, 0);
-      double gn = MA(dya, 0, -1) / MA(dya, 0, 0);
-      double qyN = 0.5 * ((2.0 + gn) * (AT(q, 0, 0) + AT(q, 0, 1)) - (AT(q, 0, -1) + AT(q, 0, 2))) / (1.0 + gn);
-      vy = (3.0 * (AT(q, 0, -1) + g1 * AT(q, 0, 0)) - (g1 * qyN + gen(-1))) / (2.0 + 2.0 * g1);
+      double g1 = DY(-1) / DY(0);
+      double gn = DY(-1) / DY(0);
+      double qyN = 0.5 * ((2.0 + gn) * (Q(i, j) + Q(i, j + 1)) - (Q(i, j - 1) + Q(i, j + 2))) / (1.0 + gn);
+      return (3.0 * (Q(i, j - 1) + g1 * Q(i, j)) - (g1 * qyN + gen(-1))) / (2.0 + 2.0 * g1);
     } else if (J >= max(2, jo) && J <= min(N - 2, jo + ny)) {
-      vy = gen(0);
+      return gen(0);
     }
+    return 0.0;
   }
-  AT(qx, 0, 0) = vx;
-  AT(qy, 0, 0) = vy;
-}
+};
 
 // qout on cube corners and tile-edge lines
 __global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restrict__ subs,
                                                   const double* __restrict__ M, int nk, const double* __restrict__ cw,
-                                                  const double* __restrict__ q, const double* __restrict__ qx,
-                                                  const double* __restrict__ qy, double* __restrict__ qout) {
+                                                  const double* __restrict__ q, double* __restrict__ qout) {
   // all targets lie on the tile-edge lines: one lane per line point
   const int z = blockIdx.z, s = z / nk;
   const SubInfo sub = subs[s];
@@ -303,12 +327,14 @@ __global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restr
     }
     return acc * R3;
   };
-  auto gq = [&](const double* a, int Ig, int Jg) { return a[zo + pidx(d, Ig - io, Jg - jo)]; };
+  const A2bPoint P{d, sub, q + zo, met(M, d, M_DXA, s), met(M, d, M_DYA, s)};
+  auto gqx = [&](int Ig, int Jg) { return P.qx(Ig - io, Jg - jo); };
+  auto gqy = [&](int Ig, int Jg) { return P.qy(Ig - io, Jg - jo); };
   auto colv = [&](int Ig, int Jg) {  // W/E edge generic
-    return AA2 * (gq(qx, Ig, Jg - 2) + gq(qx, Ig, Jg + 1)) + AA1 * (gq(qx, Ig, Jg - 1) + gq(qx, Ig, Jg));
+    return AA2 * (gqx(Ig, Jg - 2) + gqx(Ig, Jg + 1)) + AA1 * (gqx(Ig, Jg - 1) + gqx(Ig, Jg));
   };
   auto rowv = [&](int Ig, int Jg) {
-    return AA2 * (gq(qy, Ig - 2, Jg) + gq(qy, Ig + 1, Jg)) + AA1 * (gq(qy, Ig - 1, Jg) + gq(qy, Ig, Jg));
+    return AA2 * (gqy(Ig - 2, Jg) + gqy(Ig + 1, Jg)) + AA1 * (gqy(Ig - 1, Jg) + gqy(Ig, Jg));
   };
   auto edge_or_corner = [&](int Ig, int Jg) -> double {  // value of qout at a tile-edge point (recursive-free)
     if (Ig == 0 && Jg == 0) return corner_val(0);
@@ -322,15 +348,15 @@ __global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restr
   bool set = true;
   if ((I == 0 || I == N) && (J == 0 || J == N)) val = edge_or_corner(I, J);
   else if ((I == 0 && io == 0) || (I == N && io + nx == N)) {
-    if (J == 1 && jo == 0) val = AC1 * (gq(qx, I, 0) + gq(qx, I, 1)) + AC2 * (edge_or_corner(I, 0) + colv(I, 2));
+    if (J == 1 && jo == 0) val = AC1 * (gqx(I, 0) + gqx(I, 1)) + AC2 * (edge_or_corner(I, 0) + colv(I, 2));
     else if (J == N - 1 && jo + ny == N)
-      val = AC1 * (gq(qx, I, N - 2) + gq(qx, I, N - 1)) + AC2 * (colv(I, N - 2) + edge_or_corner(I, N));
+      val = AC1 * (gqx(I, N - 2) + gqx(I, N - 1)) + AC2 * (colv(I, N - 2) + edge_or_corner(I, N));
     else if (J >= max(2, jo) && J <= min(N - 2, jo + ny)) val = colv(I, J);
     else set = false;
   } else if ((J == 0 && jo == 0) || (J == N && jo + ny == N)) {
-    if (I == 1 && io == 0) val = AC1 * (gq(qy, 0, J) + gq(qy, 1, J)) + AC2 * (edge_or_corner(0, J) + rowv(2, J));
+    if (I == 1 && io == 0) val = AC1 * (gqy(0, J) + gqy(1, J)) + AC2 * (edge_or_corner(0, J) + rowv(2, J));
     else if (I == N - 1 && io + nx == N)
-      val = AC1 * (gq(qy, N - 2, J) + gq(qy, N - 1, J)) + AC2 * (rowv(N - 2, J) + edge_or_corner(N, J));
+      val = AC1 * (gqy(N - 2, J) + gqy(N - 1, J)) + AC2 * (rowv(N - 2, J) + edge_or_corner(N, J));
     else if (I >= max(2, io) && I <= min(N - 2, io + nx)) val = rowv(I, J);
     else set = false;
   } else {
@@ -339,28 +365,53 @@ __global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restr
   if (set) AT(qout, 0, 0) = val;
 }
 
-// interior qout = 0.5 * (qxx + qyy)
-__global__ void __launch_bounds__(256) a2b_inner_k(Dims d, const SubInfo* __restrict__ subs, int nk,
-                                                   const double* __restrict__ qx, const double* __restrict__ qy,
-                                                   double* __restrict__ qout) {
-  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  KSETUP2(nk)
-  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+// interior qout = 0.5 * (qxx + qyy).  One 64 x 4 tile of corner points per workgroup:
+// the x-interpolants qx (rows j0-2..j0+5) and y-interpolants qy (cols i0-2..i0+65) the
+// tile needs are evaluated once into LDS, so the former qx / qy planes never touch HBM.
+constexpr int A2_TX = 64, A2_TY = 4;
+__global__ void __launch_bounds__(A2_TX * A2_TY) a2b_inner_k(Dims d, const SubInfo* __restrict__ subs,
+                                                             const double* __restrict__ M, int nk,
+                                                             const double* __restrict__ q, double* __restrict__ qout) {
+  __shared__ double QXs[A2_TY + 4][A2_TX];
+  __shared__ double QYs[A2_TY][A2_TX + 4];
+  const int tid = threadIdx.y * A2_TX + threadIdx.x;
+  const int i0 = blockIdx.x * A2_TX, j0 = blockIdx.y * A2_TY;
+  const int z = blockIdx.z, s = z / nk;
+  const SubInfo sub = subs[s];
+  const int N = sub.N, io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+  const long zo = (long)z * d.plane;
+  const A2bPoint P{d, sub, q + zo, met(M, d, M_DXA, s), met(M, d, M_DYA, s)};
+  // the interpolants are only evaluated where the 3-pass form defined them
+  auto cell_ok = [&](int i, int j) { return i >= -NG && i <= nx + NG && j >= -NG && j <= ny + NG; };
+  for (int p = tid; p < (A2_TY + 4) * A2_TX; p += A2_TX * A2_TY) {
+    const int r = p / A2_TX, c = p % A2_TX;
+    const int i = i0 + c, j = j0 - 2 + r;
+    QXs[r][c] = (i <= nx && cell_ok(i, j)) ? P.qx(i, j) : 0.0;
+  }
+  for (int p = tid; p < A2_TY * (A2_TX + 4); p += A2_TX * A2_TY) {
+    const int r = p / (A2_TX + 4), c = p % (A2_TX + 4);
+    const int i = i0 - 2 + c, j = j0 + r;
+    QYs[r][c] = (j <= ny && cell_ok(i, j)) ? P.qy(i, j) : 0.0;
+  }
+  __syncthreads();
+  const int c = threadIdx.x, r = threadIdx.y;
+  const int i = i0 + c, j = j0 + r;
+  if (i > nx || j > ny) return;
+  const int I = i + io, J = j + jo;
   const bool icols = I >= max(1, io) && I <= min(N - 1, io + nx);
   const bool jrows = J >= max(1, jo) && J <= min(N - 1, jo + ny);
   if (!(icols && jrows)) return;
-  auto qxx_gen = [&](int dj) {
-    return AA2 * (AT(qx, 0, dj - 2) + AT(qx, 0, dj + 1)) + AA1 * (AT(qx, 0, dj - 1) + AT(qx, 0, dj));
-  };
-  auto qyy_gen = [&](int di) {
-    return AA2 * (AT(qy, di - 2, 0) + AT(qy, di + 1, 0)) + AA1 * (AT(qy, di - 1, 0) + AT(qy, di, 0));
-  };
+  const long o = pidx(d, i, j);
+  auto QX = [&](int dj) { return QXs[r + 2 + dj][c]; };
+  auto QY = [&](int di) { return QYs[r][c + 2 + di]; };
+  auto qxx_gen = [&](int dj) { return AA2 * (QX(dj - 2) + QX(dj + 1)) + AA1 * (QX(dj - 1) + QX(dj)); };
+  auto qyy_gen = [&](int di) { return AA2 * (QY(di - 2) + QY(di + 1)) + AA1 * (QY(di - 1) + QY(di)); };
   double qxx, qyy;
-  if (J == 1) qxx = AC1 * (AT(qx, 0, -1) + AT(qx, 0, 0)) + AC2 * (AT(qout, 0, -1) + qxx_gen(1));
-  else if (J == N - 1) qxx = AC1 * (AT(qx, 0, -1) + AT(qx, 0, 0)) + AC2 * (AT(qout, 0, 1) + qxx_gen(-1));
+  if (J == 1) qxx = AC1 * (QX(-1) + QX(0)) + AC2 * (AT(qout, 0, -1) + qxx_gen(1));
+  else if (J == N - 1) qxx = AC1 * (QX(-1) + QX(0)) + AC2 * (AT(qout, 0, 1) + qxx_gen(-1));
   else qxx = qxx_gen(0);
-  if (I == 1) qyy = AC1 * (AT(qy, -1, 0) + AT(qy, 0, 0)) + AC2 * (AT(qout, -1, 0) + qyy_gen(1));
-  else if (I == N - 1) qyy = AC1 * (AT(qy, -1, 0) + AT(qy, 0, 0)) + AC2 * (AT(qout, 1, 0) + qyy_gen(-1));
+  if (I == 1) qyy = AC1 * (QY(-1) + QY(0)) + AC2 * (AT(qout, -1, 0) + qyy_gen(1));
+  else if (I == N - 1) qyy = AC1 * (QY(-1) + QY(0)) + AC2 * (AT(qout, 1, 0) + qyy_gen(-1));
   else qyy = qyy_gen(0);
   AT(qout, 0, 0) = 0.5 * (qxx + qyy);
 }
@@ -437,8 +488,9 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
   const Dims& d = c.d;
   const int k1 = a.npz + 1;
   Launch2D Lf{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  if (a.npz > EP_KMAX) throw std::runtime_error("update_dz_d: npz too large");
   GT_LAUNCH(edge_prof_k, g2(d, Lf, d.nsub), dim3(BX, BY), 0, c.st, d, a.npz, a.dp0, a.crx, a.xfx, a.cry,
-                     a.yfx, a.crx_e, a.xfx_e, a.cry_e, a.yfx_e, a.gam);
+            a.yfx, a.crx_e, a.xfx_e, a.cry_e, a.yfx_e);
   HIP_LAUNCH_CHECK();
   Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
   GT_LAUNCH(ra_k, g2(d, Lr, d.nsub * k1), dim3(BX, BY), 0, c.st, d, c.subs, c.met, k1, a.xfx_e, a.yfx_e,
@@ -465,16 +517,17 @@ void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* d
 }
 
 void a2b_ord4(const Ctx& c, int nk, const double* q, double* qout, double* qx, double* qy) {
+  (void)qx;
+  (void)qy;
   const Dims& d = c.d;
-  Launch2D Lf{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  GT_LAUNCH(a2b_qxqy_k, g2(d, Lf, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, c.met, nk, q, qx, qy);
+  // corner / tile-edge values first: the interior points next to the tile edges use them
+  GT_LAUNCH(a2b_edge_k, dim3(cdiv(edge_line_count(0, d.nx, 0, d.ny), 256), 1, d.nsub * nk), dim3(256), 0, c.st, d,
+            c.subs, c.met, nk, c.cornerw, q, qout);
   HIP_LAUNCH_CHECK();
-  Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
-  GT_LAUNCH(a2b_edge_k, dim3(cdiv(edge_line_count(0, d.nx, 0, d.ny), 256), 1, d.nsub * nk), dim3(256), 0, c.st, d, c.subs, c.met, nk, c.cornerw, q,
-                     qx, qy, qout);
+  GT_LAUNCH(a2b_inner_k, dim3(cdiv(d.nx + 1, A2_TX), cdiv(d.ny + 1, A2_TY), d.nsub * nk), dim3(A2_TX, A2_TY), 0,
+            c.st, d, c.subs, c.met, nk, q, qout);
   HIP_LAUNCH_CHECK();
-  GT_LAUNCH(a2b_inner_k, g2(d, Lc, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, nk, qx, qy, qout);
-  HIP_LAUNCH_CHECK();
+  ktimer_bytes(8.0 * d.nx * d.ny * d.nsub * nk * 2.0);  // q read, qout written
 }
 
 void nh_p_grad(const Ctx& c, const NhPgArgs& a) {
