@@ -72,6 +72,7 @@ Namelist parse_config(const char* cfg) {
     else if (k == "adiabatic") nl.adiabatic = ix != 0;
     else if (k == "ptop") nl.ptop = x;
     else if (k == "host_only") nl.host_only = ix != 0;
+    else if (k == "loopback") nl.loopback = ix;
     else throw std::runtime_error("unknown config key: " + k);
   }
   for (int h : {nl.hord_mt, nl.hord_vt, nl.hord_tm, nl.hord_dp, nl.hord_tr})

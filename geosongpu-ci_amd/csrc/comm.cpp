@@ -1,0 +1,176 @@
+// comm.cpp — NCCL (RCCL) and in-process loopback transports (comm.hpp).
+#include "comm.hpp"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <condition_variable>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <stdexcept>
+#include <vector>
+
+#include "hip_util.hpp"
+
+namespace gtfv3 {
+namespace {
+
+class NcclTransport : public Transport {
+ public:
+  NcclTransport(int nranks, int rank, const void* id_bytes) {
+    if (!id_bytes) throw std::runtime_error("multi-rank run needs an ncclUniqueId");
+    ncclUniqueId id;
+    std::memcpy(&id, id_bytes, sizeof(id));
+    if (ncclCommInitRank(&comm_, nranks, id, rank) != ncclSuccess) throw std::runtime_error("ncclCommInitRank failed");
+  }
+  ~NcclTransport() override {
+    if (comm_) ncclCommDestroy(comm_);
+  }
+  void group_start() override {
+    if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
+  }
+  void send(const double* buf, size_t n, int peer, hipStream_t st) override {
+    if (ncclSend(buf, n, ncclDouble, peer, comm_, st) != ncclSuccess) throw std::runtime_error("ncclSend failed");
+  }
+  void recv(double* buf, size_t n, int peer, hipStream_t st) override {
+    if (ncclRecv(buf, n, ncclDouble, peer, comm_, st) != ncclSuccess) throw std::runtime_error("ncclRecv failed");
+  }
+  void group_end(hipStream_t) override {
+    if (ncclGroupEnd() != ncclSuccess) throw std::runtime_error("ncclGroupEnd failed");
+  }
+  void allreduce_max(double* dev, int n, hipStream_t st) override {
+    if (ncclAllReduce(dev, dev, n, ncclDouble, ncclMax, comm_, st) != ncclSuccess)
+      throw std::runtime_error("ncclAllReduce failed");
+  }
+
+ private:
+  ncclComm_t comm_ = nullptr;
+};
+
+// ---- loopback ----
+struct Msg {
+  const double* p;
+  size_t n;
+};
+
+struct LoopGroup {
+  int nranks = 0;
+  std::mutex m;
+  std::condition_variable cv;
+  int arrived = 0;
+  long generation = 0;
+  std::vector<std::vector<std::vector<Msg>>> posts;  // [src][dst] in send order
+  std::vector<double> red;
+  int red_count = 0;
+
+  void barrier() {
+    std::unique_lock<std::mutex> lk(m);
+    const long gen = generation;
+    if (++arrived == nranks) {
+      arrived = 0;
+      ++generation;
+      cv.notify_all();
+    } else {
+      cv.wait(lk, [&] { return generation != gen; });
+    }
+  }
+};
+
+std::mutex g_groups_m;
+std::map<int, std::shared_ptr<LoopGroup>> g_groups;
+
+class LoopbackTransport : public Transport {
+ public:
+  LoopbackTransport(int group, int nranks, int rank) : rank_(rank) {
+    std::lock_guard<std::mutex> lk(g_groups_m);
+    auto& g = g_groups[group];
+    if (!g) {
+      g = std::make_shared<LoopGroup>();
+      g->nranks = nranks;
+      g->posts.assign(nranks, std::vector<std::vector<Msg>>(nranks));
+    }
+    if (g->nranks != nranks) throw std::runtime_error("loopback group size mismatch");
+    g_ = g;
+  }
+  void group_start() override {
+    sends_.clear();
+    recvs_.clear();
+  }
+  void send(const double* buf, size_t n, int peer, hipStream_t) override { sends_.push_back({peer, buf, n}); }
+  void recv(double* buf, size_t n, int peer, hipStream_t) override { recvs_.push_back({peer, buf, n}); }
+  void group_end(hipStream_t st) override {
+    HIP_CHECK(hipStreamSynchronize(st));  // packed buffers complete
+    {
+      std::lock_guard<std::mutex> lk(g_->m);
+      for (auto& s : sends_) g_->posts[rank_][s.peer].push_back({s.p, s.n});
+    }
+    g_->barrier();
+    std::vector<size_t> taken(g_->nranks, 0);
+    for (auto& r : recvs_) {
+      Msg msg;
+      {
+        std::lock_guard<std::mutex> lk(g_->m);
+        auto& q = g_->posts[r.peer][rank_];
+        if (taken[r.peer] >= q.size()) throw std::runtime_error("loopback: unmatched receive");
+        msg = q[taken[r.peer]++];
+      }
+      if (msg.n != r.n) throw std::runtime_error("loopback: message size mismatch");
+      HIP_CHECK(hipMemcpyAsync(const_cast<double*>(r.p), msg.p, sizeof(double) * r.n, hipMemcpyDeviceToDevice, st));
+    }
+    HIP_CHECK(hipStreamSynchronize(st));
+    g_->barrier();  // every receiver has copied: senders may reuse their buffers
+    {
+      std::lock_guard<std::mutex> lk(g_->m);
+      for (auto& v : g_->posts[rank_]) v.clear();
+    }
+    g_->barrier();
+  }
+  void allreduce_max(double* dev, int n, hipStream_t st) override {
+    std::vector<double> h(n);
+    HIP_CHECK(hipMemcpyAsync(h.data(), dev, sizeof(double) * n, hipMemcpyDeviceToHost, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    {
+      std::lock_guard<std::mutex> lk(g_->m);
+      if (g_->red_count == 0) g_->red = h;
+      else
+        for (int i = 0; i < n; ++i) g_->red[i] = std::max(g_->red[i], h[i]);
+      ++g_->red_count;
+    }
+    g_->barrier();
+    {
+      std::lock_guard<std::mutex> lk(g_->m);
+      h = g_->red;
+    }
+    g_->barrier();
+    {
+      std::lock_guard<std::mutex> lk(g_->m);
+      g_->red_count = 0;
+    }
+    HIP_CHECK(hipMemcpyAsync(dev, h.data(), sizeof(double) * n, hipMemcpyHostToDevice, st));
+    HIP_CHECK(hipStreamSynchronize(st));
+    g_->barrier();
+  }
+
+ private:
+  struct Pending {
+    int peer;
+    const double* p;
+    size_t n;
+  };
+  int rank_;
+  std::shared_ptr<LoopGroup> g_;
+  std::vector<Pending> sends_, recvs_;
+};
+
+}  // namespace
+
+std::unique_ptr<Transport> make_nccl_transport(int nranks, int rank, const void* nccl_id) {
+  return std::make_unique<NcclTransport>(nranks, rank, nccl_id);
+}
+
+std::unique_ptr<Transport> make_loopback_transport(int group, int nranks, int rank) {
+  return std::make_unique<LoopbackTransport>(group, nranks, rank);
+}
+
+}  // namespace gtfv3

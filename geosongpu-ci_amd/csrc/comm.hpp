@@ -1,0 +1,30 @@
+// comm.hpp — rank-to-rank transport behind the halo exchange and the single
+// reduction of a dycore step (the tracer Courant maximum).
+//  * NcclTransport: RCCL point-to-point send/recv (grouped) and allreduce(max) on the
+//    dycore stream — the production path, one process per GPU over xGMI.
+//  * LoopbackTransport: several ranks of one process on one device; messages are
+//    device-to-device copies through a shared mailbox with host barriers.  It runs the
+//    exact same tables and pack / unpack kernels, so multi-rank steps can be verified
+//    on a single GPU (tests/test_gpu_multirank.py).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <memory>
+
+namespace gtfv3 {
+
+class Transport {
+ public:
+  virtual ~Transport() = default;
+  virtual void group_start() = 0;
+  virtual void send(const double* buf, size_t n, int peer, hipStream_t st) = 0;
+  virtual void recv(double* buf, size_t n, int peer, hipStream_t st) = 0;
+  virtual void group_end(hipStream_t st) = 0;
+  virtual void allreduce_max(double* dev, int n, hipStream_t st) = 0;
+};
+
+std::unique_ptr<Transport> make_nccl_transport(int nranks, int rank, const void* nccl_id);
+std::unique_ptr<Transport> make_loopback_transport(int group, int nranks, int rank);
+
+}  // namespace gtfv3

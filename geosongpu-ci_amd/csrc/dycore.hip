@@ -46,11 +46,8 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
   HIP_CHECK(hipMemcpy(dcornerw, hm.corner_w.data(), sizeof(double) * hm.corner_w.size(), hipMemcpyHostToDevice));
 
   if (nranks > 1) {
-    if (!nccl_id) throw std::runtime_error("multi-rank run needs an ncclUniqueId");
-    ncclUniqueId id;
-    std::memcpy(&id, nccl_id, sizeof(id));
-    if (ncclCommInitRank(&comm, nranks, id, rank) != ncclSuccess) throw std::runtime_error("ncclCommInitRank failed");
-    halo.set_comm(comm);
+    comm = nl.loopback ? make_loopback_transport(nl.loopback, nranks, rank) : make_nccl_transport(nranks, rank, nccl_id);
+    halo.set_transport(comm.get());
   }
   halo.build(*cs, dc, d, max_nk, 8);
 }
@@ -60,7 +57,6 @@ Dycore::~Dycore() {
   if (dsubs) (void)hipFree(dsubs);
   if (dmet) (void)hipFree(dmet);
   if (dcornerw) (void)hipFree(dcornerw);
-  if (comm) ncclCommDestroy(comm);
   if (st) (void)hipStreamDestroy(st);
 }
 
@@ -141,9 +137,7 @@ void Dycore::halo_update(const std::vector<std::pair<std::string, char>>& items)
 }
 
 void Dycore::allreduce_max(double* dev, int n) {
-  if (!comm) return;
-  if (ncclAllReduce(dev, dev, n, ncclDouble, ncclMax, comm, st) != ncclSuccess)
-    throw std::runtime_error("ncclAllReduce failed");
+  if (comm) comm->allreduce_max(dev, n, st);
 }
 
 void Dycore::set_vertical(const double* ak_, const double* bk_, int ks_) {

@@ -10,6 +10,7 @@
 #include <string>
 #include <vector>
 
+#include "comm.hpp"
 #include "grid.hpp"
 #include "halo.hpp"
 #include "kernels.hpp"
@@ -40,7 +41,7 @@ class Dycore {
   double* dcornerw = nullptr;
   HaloExchanger halo;
   hipStream_t st = nullptr;
-  ncclComm_t comm = nullptr;
+  std::unique_ptr<Transport> comm;  // null for one rank
   std::map<std::string, Field> fields;
   std::vector<double> ak, bk;  // npz+1
   int ks = 0;

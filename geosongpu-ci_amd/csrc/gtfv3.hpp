@@ -50,6 +50,7 @@ struct Namelist {
   bool adiabatic = false;
   double ptop = 1.0;
   bool host_only = false;            // grid + tables only (CPU tests)
+  int loopback = 0;                  // >0: in-process multi-rank group id (single-GPU tests)
 };
 
 // One sub-domain (tile piece) owned by this rank.

@@ -238,22 +238,17 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
       off += (size_t)std::max(n_send_[F.kind], n_recv_[F.kind]) * F.nk;
     }
     if (off > buf_elems_) throw std::runtime_error("halo: exchange buffer too small");
-    if (ncclGroupStart() != ncclSuccess) throw std::runtime_error("ncclGroupStart failed");
+    if (!tr_) throw std::runtime_error("halo: multi-rank exchange without a transport");
+    tr_->group_start();
     for (int f = 0; f < nf; ++f) {
       const HaloField& F = fields[f];
       for (int p = 0; p < nranks_; ++p) {
         int ns = send_peer_count_[F.kind][p], nr = recv_peer_count_[F.kind][p];
-        if (ns)
-          if (ncclSend(sendbuf_ + foff[f] + (size_t)send_peer_start_[F.kind][p] * F.nk, (size_t)ns * F.nk,
-                       ncclDouble, p, comm_, stream) != ncclSuccess)
-            throw std::runtime_error("ncclSend failed");
-        if (nr)
-          if (ncclRecv(recvbuf_ + foff[f] + (size_t)recv_peer_start_[F.kind][p] * F.nk, (size_t)nr * F.nk,
-                       ncclDouble, p, comm_, stream) != ncclSuccess)
-            throw std::runtime_error("ncclRecv failed");
+        if (ns) tr_->send(sendbuf_ + foff[f] + (size_t)send_peer_start_[F.kind][p] * F.nk, (size_t)ns * F.nk, p, stream);
+        if (nr) tr_->recv(recvbuf_ + foff[f] + (size_t)recv_peer_start_[F.kind][p] * F.nk, (size_t)nr * F.nk, p, stream);
       }
     }
-    if (ncclGroupEnd() != ncclSuccess) throw std::runtime_error("ncclGroupEnd failed");
+    tr_->group_end(stream);
   }
   for (int f = 0; f < nf; ++f) {
     const HaloField& F = fields[f];

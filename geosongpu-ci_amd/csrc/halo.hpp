@@ -16,6 +16,7 @@
 
 #include <vector>
 
+#include "comm.hpp"
 #include "grid.hpp"
 
 namespace gtfv3 {
@@ -41,7 +42,7 @@ class HaloExchanger {
   HaloExchanger() = default;
   ~HaloExchanger();
   void build(const CubedSphere& cs, const Decomp& dc, const Dims& d, int max_nk, int max_fields, bool device = true);
-  void set_comm(ncclComm_t comm) { comm_ = comm; }
+  void set_transport(Transport* t) { tr_ = t; }
   // fill halos of all listed fields (enqueued on `stream`)
   void exchange(const HaloField* fields, int nf, hipStream_t stream);
   // host copies of tables for tests
@@ -53,7 +54,7 @@ class HaloExchanger {
  private:
   Dims d_{};
   int rank_ = 0, nranks_ = 1;
-  ncclComm_t comm_ = nullptr;
+  Transport* tr_ = nullptr;
   std::vector<HaloEntry> h_local_[H_NKIND];
   std::vector<PackEntry> h_send_[H_NKIND], h_recv_[H_NKIND];
   HaloEntry* d_local_[H_NKIND] = {};
