@@ -196,45 +196,61 @@ __device__ __forceinline__ void atomic_max_pos(double* addr, double v) {
   atomicMax(reinterpret_cast<unsigned long long*>(addr), (unsigned long long)__double_as_longlong(v));
 }
 
+// Each thread walks TP_RPT rows so one workgroup covers 4*TP_RPT rows of the plane:
+// the per-level Courant maximum then costs one atomic per workgroup (a few per level
+// and sub-domain) instead of one per wavefront.
+constexpr int TP_RPT = 12;
 __global__ void __launch_bounds__(256) tracer_prep_k(Dims d, const double* __restrict__ M, int npz,
                                                      const double* __restrict__ cx, const double* __restrict__ cy,
                                                      double* __restrict__ xfx, double* __restrict__ yfx,
                                                      double* __restrict__ cmax) {
-  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  int i, j;
-  bool act = thread_point(L, i, j);
+  __shared__ double wmax[4];
   const int z = blockIdx.z, k = z % npz, s = z / npz;
   const long fo = (long)z * d.plane;
+  const int i = blockIdx.x * BX + threadIdx.x - NG;
+  const double* dxa = met(M, d, M_DXA, s);
+  const double* dya = met(M, d, M_DYA, s);
+  const double* dx = met(M, d, M_DX, s);
+  const double* dy = met(M, d, M_DY, s);
   double cm = 0.0;
-  if (act) {
+  for (int rr = 0; rr < TP_RPT; ++rr) {
+    const int j = (blockIdx.y * TP_RPT + rr) * BY + threadIdx.y - NG;
+    if (i > d.nx + NG || j > d.ny + NG) continue;
     const long o = pidx(d, i, j);
     if (i >= 0 && i <= d.nx && j >= -NG && j <= d.ny + NG - 1) {
       double c = cx[fo + o];
       double v;
       if (c > 0.0)
-        v = c * met(M, d, M_DXA, s)[pidx(d, i - 1, j)] * met(M, d, M_DY, s)[o] * met(M, d, M_SIN3, s)[pidx(d, i - 1, j)];
+        v = c * dxa[pidx(d, i - 1, j)] * dy[o] * met(M, d, M_SIN3, s)[pidx(d, i - 1, j)];
       else
-        v = c * met(M, d, M_DXA, s)[o] * met(M, d, M_DY, s)[o] * met(M, d, M_SIN1, s)[o];
+        v = c * dxa[o] * dy[o] * met(M, d, M_SIN1, s)[o];
       xfx[fo + o] = v;
     }
     if (j >= 0 && j <= d.ny && i >= -NG && i <= d.nx + NG - 1) {
       double c = cy[fo + o];
       double v;
       if (c > 0.0)
-        v = c * met(M, d, M_DYA, s)[pidx(d, i, j - 1)] * met(M, d, M_DX, s)[o] * met(M, d, M_SIN4, s)[pidx(d, i, j - 1)];
+        v = c * dya[pidx(d, i, j - 1)] * dx[o] * met(M, d, M_SIN4, s)[pidx(d, i, j - 1)];
       else
-        v = c * met(M, d, M_DYA, s)[o] * met(M, d, M_DX, s)[o] * met(M, d, M_SIN2, s)[o];
+        v = c * dya[o] * dx[o] * met(M, d, M_SIN2, s)[o];
       yfx[fo + o] = v;
     }
     if (i >= 0 && i < d.nx && j >= 0 && j < d.ny) {
       double a = fmax(fabs(cx[fo + o]), fabs(cy[fo + o]));
       if (!(k + 1 < npz / 6)) a = a + 1.0 - met(M, d, M_SIN5, s)[o];
-      cm = a;
+      cm = fmax(cm, a);
     }
   }
-  // wave reduction then one atomic per wave
+  // wave reduction, workgroup reduction, one atomic per workgroup
   for (int off = 32; off > 0; off >>= 1) cm = fmax(cm, __shfl_xor(cm, off));
-  if ((threadIdx.x & 63) == 0) atomic_max_pos(&cmax[k], cm);
+  const int w = (threadIdx.y * BX + threadIdx.x) >> 6;
+  if ((threadIdx.x & 63) == 0) wmax[w] = cm;
+  __syncthreads();
+  if (threadIdx.x == 0 && threadIdx.y == 0) {
+    double m = wmax[0];
+    for (int q = 1; q < (BX * BY) / 64; ++q) m = fmax(m, wmax[q]);
+    atomic_max_pos(&cmax[k], m);
+  }
 }
 
 __global__ void __launch_bounds__(256) tracer_split_k(Dims d, const double* __restrict__ M, int npz,
@@ -338,7 +354,7 @@ void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, doub
   (void)ra_x; (void)ra_y;
   HIP_CHECK(hipMemsetAsync(cmax_dev, 0, sizeof(double) * npz, c.st));
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  GT_LAUNCH(tracer_prep_k, dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
+  GT_LAUNCH(tracer_prep_k, dim3(cdiv(L.ni, BX), cdiv(L.nj, BY * TP_RPT), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
                      c.met, npz, cx, cy, xfx, yfx, cmax_dev);
   HIP_LAUNCH_CHECK();
 }
