@@ -68,6 +68,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--kernel-report", default="", help="write per-kernel stats JSON here")
+    p.add_argument("--geos-log", default="", help="also write a GEOS-style log (geoslog.py) of K individually "
+                   "synchronised steps run after the timed region, for tcn.benchmark's parse_geos_log")
     return p.parse_args()
 
 
@@ -125,6 +127,7 @@ def main():
         dist.broadcast_object_list(obj, src=0)
         nccl_id = obj[0]
     lx, ly = layout_for(world)
+    t_init = time.perf_counter()
     d = pkg.Domain(rank, world, nccl_id, npx=a.npx, npz=a.npz, nq=a.nq, layout_x=lx, layout_y=ly, dt=a.dt)
     ak, bk, ks = state.hybrid_levels(a.npz)
     st = state.jablonowski_williamson(d, ak, bk)
@@ -132,6 +135,8 @@ def main():
     for k, v in st.items():
         d.upload(k, v)
     del st
+    torch.cuda.synchronize()
+    t_init = time.perf_counter() - t_init
 
     def barrier():
         torch.cuda.synchronize()
@@ -175,6 +180,23 @@ def main():
                 json.dump({k: dict(ms_total=v[0], launches=v[1], ms_per_step=v[0] / a.steps,
                                    gbs=(v[2] / (v[0] * 1e-3) / 1e9) if v[2] > 0 else None)
                            for k, v in sorted(kstats.items(), key=lambda kv: -kv[1][0])}, f, indent=1)
+
+    if a.geos_log:
+        d.kernel_timing(False)
+        per_step = []
+        for _ in range(a.steps):
+            barrier()
+            t1 = time.perf_counter()
+            d.step(1)
+            d.sync()
+            barrier()
+            per_step.append(time.perf_counter() - t1)
+        if rank == 0:
+            geoslog = importlib.import_module(pkg.__name__ + ".geoslog")
+            t_fin = time.perf_counter()
+            geoslog.write_geos_log(a.geos_log, npx=d.N + 1, npz=d.npz, layout_x=lx, layout_y=ly,
+                                   backend="hip-gfx950-f64", step_seconds=per_step, init_s=t_init,
+                                   run_s=sum(per_step), finalize_s=time.perf_counter() - t_fin)
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
