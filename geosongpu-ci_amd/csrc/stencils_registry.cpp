@@ -7,6 +7,8 @@
 
 #include "dycore.hpp"
 #include "kernels.hpp"
+#include "kernels_column.hpp"
+#include "kernels_misc.hpp"
 #include "kernels_sw.hpp"
 
 namespace gtfv3 {
@@ -85,6 +87,38 @@ std::map<std::string, Fn>& reg() {
          a.gtx = scr("_ds_gtx"); a.gty = scr("_ds_gty"); a.vort = scr("_ds_vort");
          a.tp_fx2 = scr("_tp1_fx2"); a.tp_fy2 = scr("_tp1_fy2"); a.tp_qi = scr("_tp1_qi"); a.tp_qj = scr("_tp1_qj");
          d_sw(dy.ctx(), a);
+       }},
+      // K-column primitives (dsl_patterns KATs): column_top(in | out)
+      {"column_top",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
+         need(f, 2, "column_top");
+         Field& in = F(dy, f[0]);
+         column_top(dy.ctx(), in.nk, in.p, dy.field(f[1], in.nk).p);
+       }},
+      // column_while_lt(in | out) params: thr
+      {"column_while_lt",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 2, "column_while_lt");
+         Field& in = F(dy, f[0]);
+         column_while_lt(dy.ctx(), in.nk, p.at(0), in.p, dy.field(f[1], in.nk).p);
+       }},
+      // column_gather_k(data, kmask, kidx2d | out2d): out2d keeps its value where no level matches
+      {"column_gather_k",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
+         need(f, 4, "column_gather_k");
+         Field& data = F(dy, f[0]);
+         Field& km = F(dy, f[1]);
+         Field& kidx = F(dy, f[2]);
+         if (km.nk != data.nk || kidx.nk != 1) throw std::runtime_error("column_gather_k: field shapes");
+         column_gather_k(dy.ctx(), data.nk, data.p, km.p, kidx.p, dy.field(f[3], 1).p);
+       }},
+      // Held-Suarez forcing: held_suarez(pe, pt, u, v) in place, params: dt
+      {"held_suarez",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 4, "held_suarez");
+         Field& pt = F(dy, f[1]);
+         if (F(dy, f[0]).nk != pt.nk + 1) throw std::runtime_error("held_suarez: pe must have npz+1 levels");
+         held_suarez(dy.ctx(), pt.nk, p.at(0), F(dy, f[0]).p, pt.p, F(dy, f[2]).p, F(dy, f[3]).p);
        }},
       // tracer_2d_1l: uses state fields q, dp1, cx, cy, mfx, mfy. params: nq
       {"tracer_2d_1l",
