@@ -38,21 +38,26 @@ struct RiemArgs {
   double *gam, *pp, *w2;  // scratch, L+1 planes each
 };
 
-// The column body takes every array as a distinct __restrict__ pointer: the arrays never
-// alias, and saying so lets the compiler hoist the loads of an unrolled group of levels
-// above the stores of the previous ones (one memory latency per group of levels instead
-// of one per level: the sweeps are otherwise a chain of dependent HBM / L2 round trips).
-__device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, double* __restrict__ G,
-                                            double* __restrict__ GM, double* __restrict__ PO,
-                                            double* __restrict__ PPc, double* __restrict__ W2c,
-                                            const double* __restrict__ DP, const double* __restrict__ PT,
-                                            const double* __restrict__ W1, double* __restrict__ PK3,
-                                            double* __restrict__ PE, double* __restrict__ PELN,
-                                            double* __restrict__ PK, double* __restrict__ WOUT,
-                                            double* __restrict__ DELZ) {
+__global__ void __launch_bounds__(BLOCK) riem_col_k(RiemArgs a) {
   const Dims& d = a.d;
-  const int km = a.npz;
+  const int km = a.npz, k1 = km + 1;
+  const int ni = d.nx + 2 * a.ring, nj = d.ny + 2 * a.ring;
+  const int c = blockIdx.x * BLOCK + threadIdx.x;
+  const int s = blockIdx.y;
+  if (c >= ni * nj) return;
+  const int i = c % ni - a.ring, j = c / ni - a.ring;
   const long P = d.plane;
+  const long o = pidx(d, i, j);
+  const long b1 = (long)s * k1 * P + o;  // interface fields
+  const long bk = (long)s * km * P + o;  // layer fields
+  double* G = a.G + b1;
+  double* GM = a.gam + b1;
+  double* PO = a.pout + b1;
+  double* PPc = a.pp + b1;  // pp, later pe
+  double* W2c = a.w2 + b1;
+  const double* DP = a.delp + bk;
+  const double* PT = a.pt + bk;
+  const double* W1 = a.w_in + bk;
 #define LP(k) PPc[(k) * P]
 #define LW(k) W2c[(k) * P]
 
@@ -64,7 +69,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
   // S0: dz_min clamp of the interface heights (bottom-up), written back in place
   {
     double gb = G[km * P];
-    _Pragma("unroll 2") for (int k = km - 1; k >= 0; --k) {
+    for (int k = km - 1; k >= 0; --k) {
       double g = fmax(G[k * P], gb + a.dz_min);
       G[k * P] = g;
       gb = g;
@@ -89,11 +94,11 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
   PO[0] = pem0;  // park pem
   if (!cg) {
     const double ptk = exp(KAPPA * pln0);
-    PK3[0] = ptk;
+    a.pk3[b1] = ptk;
     if (a.last_call) {
-      PE[0] = pem0;
-      PELN[0] = pln0;
-      PK[0] = ptk;
+      a.pe[b1] = pem0;
+      a.peln[b1] = pln0;
+      a.pk[b1] = ptk;
     }
   }
   auto advance = [&](int k, double pem_k, double& pem_n, double& pln_n) {
@@ -103,11 +108,11 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
     if (!cg) {
       pln_n = log(pem_n);
       const double pkk = exp(KAPPA * pln_n);
-      PK3[(k + 1) * P] = pkk;
+      a.pk3[b1 + (k + 1) * P] = pkk;
       if (a.last_call) {
-        PE[(k + 1) * P] = pem_n;
-        PELN[(k + 1) * P] = pln_n;
-        PK[(k + 1) * P] = pkk;
+        a.pe[b1 + (k + 1) * P] = pem_n;
+        a.peln[b1 + (k + 1) * P] = pln_n;
+        a.pk[b1 + (k + 1) * P] = pkk;
       }
     } else {
       pln_n = 0.0;
@@ -122,7 +127,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
   double pem_k1 = pem1, pln_k1 = pln1;  // interface k+1
   double bet = 0.0, pp_k = 0.0, g_prev = 0.0;
   LP(0) = 0.0;
-  _Pragma("unroll 2") for (int k = 0; k < km; ++k) {
+  for (int k = 0; k < km; ++k) {
     double g = 0.0, bbk, ddk, dm_n = 0.0, pl_n = 0.0;
     if (k < km - 1) {
       double pem_k2, pln_k2;
@@ -159,7 +164,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
   // S2: back substitution for pp
   {
     double x = LP(km);
-    _Pragma("unroll 2") for (int k = km - 1; k > 0; --k) {
+    for (int k = km - 1; k > 0; --k) {
       x = LP(k) - GM[k * P] * x;
       LP(k) = x;
     }
@@ -176,7 +181,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
     double w_prev = (dm0 * W1[0] + dt * pp_k) / bet;
     LW(0) = w_prev;
     g1 = g2;
-    _Pragma("unroll 2") for (int k = 1; k < km - 1; ++k) {
+    for (int k = 1; k < km - 1; ++k) {
       // here dz_n = dz[k], pp_k = pp[k], aa_k = aa[k]
       const double g_next = G[(k + 2) * P];
       const double dz_nn = g_next - g1;  // dz[k+1]
@@ -205,7 +210,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
   // S4: back substitution for w
   {
     double x = LW(km - 1);
-    _Pragma("unroll 2") for (int k = km - 2; k >= 0; --k) {
+    for (int k = km - 2; k >= 0; --k) {
       x = LW(k) - GM[(k + 1) * P] * x;
       LW(k) = x;
     }
@@ -214,11 +219,11 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
   {
     double pe_k = 0.0;
     LP(0) = 0.0;
-    _Pragma("unroll 2") for (int k = 0; k < km; ++k) {
+    for (int k = 0; k < km; ++k) {
       const double w2 = LW(k);
       pe_k = pe_k + DP[k * P] * (1.0 / GRAV) * (w2 - W1[k * P]) * rdt;
       LP(k + 1) = pe_k;
-      if (WOUT) WOUT[k * P] = w2;
+      if (a.w_out) a.w_out[bk + k * P] = w2;
     }
   }
   // S6: new layer thicknesses (bottom-up), heights / geopotential, pressures out
@@ -232,7 +237,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
     else PO[km * P] = lp1;
     G[km * P] = g_out;
     double dm_b = 0.0;  // dm of layer k+1
-    _Pragma("unroll 2") for (int k = km - 1; k >= 0; --k) {
+    for (int k = km - 1; k >= 0; --k) {
       const double pem_t = PO[k * P];  // still the parked pem
       const double pln_t = cg ? 0.0 : log(pem_t);
       const double dpk2 = DP[k * P];
@@ -252,7 +257,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
         PO[k * P] = k == 0 ? a.ptop : lp0 + pem_t;
       } else {
         g_out = g_out - dz2;
-        DELZ[k * P] = dz2;
+        a.delz[bk + k * P] = dz2;
         PO[k * P] = lp0;
       }
       G[k * P] = g_out;
@@ -265,24 +270,6 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
   }
 #undef LP
 #undef LW
-}
-
-__global__ void __launch_bounds__(BLOCK) riem_col_k(RiemArgs a) {
-  const Dims& d = a.d;
-  const int km = a.npz, k1 = km + 1;
-  const int ni = d.nx + 2 * a.ring, nj = d.ny + 2 * a.ring;
-  const int c = blockIdx.x * BLOCK + threadIdx.x;
-  const int s = blockIdx.y;
-  if (c >= ni * nj) return;
-  const int i = c % ni - a.ring, j = c / ni - a.ring;
-  const long P = d.plane;
-  const long o = pidx(d, i, j);
-  const long b1 = (long)s * k1 * P + o;  // interface fields
-  const long bk = (long)s * km * P + o;  // layer fields
-  auto at = [](double* p, long off) { return p ? p + off : nullptr; };
-  riem_column(a, s, o, a.G + b1, a.gam + b1, a.pout + b1, a.pp + b1, a.w2 + b1, a.delp + bk, a.pt + bk,
-              a.w_in + bk, at(a.pk3, b1), at(a.pe, b1), at(a.peln, b1), at(a.pk, b1), at(a.w_out, bk),
-              at(a.delz, bk));
 }
 
 void launch_riem(const Ctx& c, const RiemArgs& a) {

@@ -64,7 +64,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
   // S0: dz_min clamp of the interface heights (bottom-up), written back in place
   {
     double gb = G[km * P];
-    _Pragma("unroll 2") for (int k = km - 1; k >= 0; --k) {
+    _Pragma("unroll 8") for (int k = km - 1; k >= 0; --k) {
       double g = fmax(G[k * P], gb + a.dz_min);
       G[k * P] = g;
       gb = g;
@@ -122,7 +122,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
   double pem_k1 = pem1, pln_k1 = pln1;  // interface k+1
   double bet = 0.0, pp_k = 0.0, g_prev = 0.0;
   LP(0) = 0.0;
-  _Pragma("unroll 2") for (int k = 0; k < km; ++k) {
+  _Pragma("unroll 4") for (int k = 0; k < km; ++k) {
     double g = 0.0, bbk, ddk, dm_n = 0.0, pl_n = 0.0;
     if (k < km - 1) {
       double pem_k2, pln_k2;
@@ -159,7 +159,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
   // S2: back substitution for pp
   {
     double x = LP(km);
-    _Pragma("unroll 2") for (int k = km - 1; k > 0; --k) {
+    _Pragma("unroll 8") for (int k = km - 1; k > 0; --k) {
       x = LP(k) - GM[k * P] * x;
       LP(k) = x;
     }
@@ -176,7 +176,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
     double w_prev = (dm0 * W1[0] + dt * pp_k) / bet;
     LW(0) = w_prev;
     g1 = g2;
-    _Pragma("unroll 2") for (int k = 1; k < km - 1; ++k) {
+    _Pragma("unroll 4") for (int k = 1; k < km - 1; ++k) {
       // here dz_n = dz[k], pp_k = pp[k], aa_k = aa[k]
       const double g_next = G[(k + 2) * P];
       const double dz_nn = g_next - g1;  // dz[k+1]
@@ -205,7 +205,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
   // S4: back substitution for w
   {
     double x = LW(km - 1);
-    _Pragma("unroll 2") for (int k = km - 2; k >= 0; --k) {
+    _Pragma("unroll 8") for (int k = km - 2; k >= 0; --k) {
       x = LW(k) - GM[(k + 1) * P] * x;
       LW(k) = x;
     }
@@ -214,7 +214,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
   {
     double pe_k = 0.0;
     LP(0) = 0.0;
-    _Pragma("unroll 2") for (int k = 0; k < km; ++k) {
+    _Pragma("unroll 8") for (int k = 0; k < km; ++k) {
       const double w2 = LW(k);
       pe_k = pe_k + DP[k * P] * (1.0 / GRAV) * (w2 - W1[k * P]) * rdt;
       LP(k + 1) = pe_k;
@@ -232,7 +232,7 @@ __device__ __forceinline__ void riem_column(const RiemArgs& a, int s, long o, do
     else PO[km * P] = lp1;
     G[km * P] = g_out;
     double dm_b = 0.0;  // dm of layer k+1
-    _Pragma("unroll 2") for (int k = km - 1; k >= 0; --k) {
+    _Pragma("unroll 4") for (int k = km - 1; k >= 0; --k) {
       const double pem_t = PO[k * P];  // still the parked pem
       const double pln_t = cg ? 0.0 : log(pem_t);
       const double dpk2 = DP[k * P];

@@ -215,6 +215,7 @@ struct TpM {
   const double *crx, *cry, *xfx, *yfx, *ra_x, *ra_y, *mx, *my;
   double *fx, *fy;
   int nz, nstrip, nseg, seg;
+  int noex;  // timing experiment: interior path everywhere (wrong near tile edges)
 };
 
 // Wavefront-wide lane shifts through DPP (no LDS): dpp_prev(v) in lane L is v of lane
@@ -436,7 +437,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
 }
 
 template <int ORD>
-__global__ void __launch_bounds__(MW * MWAVES) tp_march(TpM a) {
+__global__ void __launch_bounds__(MW * MWAVES, 4) tp_march(TpM a) {
   const int wv = threadIdx.x / MW;
   const long w = (long)blockIdx.x * MWAVES + wv;
   const int strip = (int)(w % a.nstrip);
@@ -449,7 +450,7 @@ __global__ void __launch_bounds__(MW * MWAVES) tp_march(TpM a) {
   const int j0 = seg * a.seg;
   const int j1 = j0 + a.seg < a.d.ny ? j0 + a.seg : a.d.ny;
   const int A = strip * MOUT + sub.ioff;
-  const bool ex = !(A - 1 >= 2 && A + MOUT + 1 <= sub.N - 2);
+  const bool ex = !(A - 1 >= 2 && A + MOUT + 1 <= sub.N - 2) && !a.noex;
   if (ex) tp_march_strip<ORD, true>(a, (int)z, strip, j0, j1);
   else tp_march_strip<ORD, false>(a, (int)z, strip, j0, j1);
 }
@@ -609,10 +610,10 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     dim3 g(cdiv(d.nx + 1, TX), cdiv(d.ny + 1, TY), (unsigned)(nz < ZMAX ? nz : ZMAX));
     GT_LAUNCH(tp_fused, g, dim3(TX, TW), 0, c.st, k);
   } else {
-    // segment length: cfg >= 8 selects it (tuning); default 45 rows (C180: 4 segments)
-    const int seg = a.cfg >= 8 ? a.cfg : 45;
+    // segment length: cfg >= 8 selects it (tuning); default 60 rows
+    const int seg = a.cfg >= 8 ? a.cfg : (a.cfg == 1 ? 45 : 60);
     TpM m{d, c.subs, c.met, a.q, a.nt, a.nk, a.crx, a.cry, a.xfx, a.yfx, a.ra_x, a.ra_y,
-          a.mfx ? a.mfx : a.xfx, a.mfy ? a.mfy : a.yfx, a.fx, a.fy, (int)nz, 0, 0, seg};
+          a.mfx ? a.mfx : a.xfx, a.mfy ? a.mfy : a.yfx, a.fx, a.fy, (int)nz, 0, 0, seg, a.cfg == 1};
     m.nstrip = (d.nx + 1 + MOUT - 1) / MOUT;
     m.nseg = (d.ny + seg - 1) / seg;
     const long waves = nz * m.nstrip * m.nseg;
