@@ -105,52 +105,31 @@ __global__ void __launch_bounds__(256) pgradc_k(Dims d, const SubInfo* __restric
 
 // edge_profile of (crx, xfx) on x-face columns and (cry, yfx) on y-face columns.
 // The tridiagonal coefficients depend only on the reference thicknesses dp0, so the
-// elimination factors gam are computed once per workgroup into LDS (same expressions
-// as the per-column form) and each column only carries its edge values.
-__device__ void edge_profile_col(const Col& q, const Col& qe, const double* gam, const double* dp0, int km) {
-  double g0 = dp0[1] / dp0[0];
-  double xt1 = 2.0 * g0 * (g0 + 1.0);
-  double bet = g0 * (g0 + 0.5);
-  double qp = (xt1 * q[0] + q[1]) / bet;
-  qe[0] = qp;
-  double gk = g0;
-  double qprev = q[0];
-  for (int k = 1; k < km; ++k) {
-    gk = dp0[k - 1] / dp0[k];
-    bet = 2.0 + 2.0 * gk - gam[k - 1];
-    const double qk = q[k];
-    qp = (3.0 * (qprev + gk * qk) - qp) / bet;
-    qe[k] = qp;
-    qprev = qk;
-  }
-  double a_bot = 1.0 + gk * (gk + 1.5);
-  xt1 = 2.0 * gk * (gk + 1.0);
-  double xt2 = gk * (gk + 0.5) - a_bot * gam[km - 1];
-  double x = (xt1 * qprev + q[km - 2] - a_bot * qp) / xt2;
-  qe[km] = x;
-  for (int k = km - 1; k >= 0; --k) {
-    x = qe[k] - gam[k] * x;
-    qe[k] = x;
-  }
-}
-
-constexpr int EP_KMAX = 256;
+// ratios gk, the pivots bet and the elimination factors gam are computed once per
+// workgroup into LDS (same expressions as the per-column form).  Each lane then runs
+// its four columns together (four independent recurrences in flight) and reads the
+// levels in blocks of EP_B, all loads of a block issued before the first use, so a
+// sweep waits for one memory latency per block instead of one per level.
+constexpr int EP_KMAX = 256, EP_B = 8;
 
 __global__ void __launch_bounds__(256) edge_prof_k(Dims d, int npz, const double* __restrict__ dp0,
                                                    const double* __restrict__ crx, const double* __restrict__ xfx,
                                                    const double* __restrict__ cry, const double* __restrict__ yfx,
                                                    double* __restrict__ crx_e, double* __restrict__ xfx_e,
                                                    double* __restrict__ cry_e, double* __restrict__ yfx_e) {
-  __shared__ double gam[EP_KMAX];
+  __shared__ double gam[EP_KMAX], gks[EP_KMAX], bets[EP_KMAX];
   const int km = npz, k1 = npz + 1;
-  if (threadIdx.x == 0 && threadIdx.y == 0) {
-    double g0 = dp0[1] / dp0[0];
-    double bet = g0 * (g0 + 0.5);
-    gam[0] = (1.0 + g0 * (g0 + 1.5)) / bet;
+  const int tid = threadIdx.y * blockDim.x + threadIdx.x;
+  for (int k = 1 + tid; k < km; k += blockDim.x * blockDim.y) gks[k] = dp0[k - 1] / dp0[k];
+  __syncthreads();
+  const double g0 = dp0[1] / dp0[0];
+  const double bet0 = g0 * (g0 + 0.5);
+  if (tid == 0) {
+    gam[0] = (1.0 + g0 * (g0 + 1.5)) / bet0;
     for (int k = 1; k < km; ++k) {
-      double gk = dp0[k - 1] / dp0[k];
-      bet = 2.0 + 2.0 * gk - gam[k - 1];
-      gam[k] = gk / bet;
+      const double bet = 2.0 + 2.0 * gks[k] - gam[k - 1];
+      bets[k] = bet;
+      gam[k] = gks[k] / bet;
     }
   }
   __syncthreads();
@@ -158,14 +137,76 @@ __global__ void __launch_bounds__(256) edge_prof_k(Dims d, int npz, const double
   int i, j;
   if (!thread_point(L, i, j)) return;
   const int s = blockIdx.z;
+  const long P = d.plane;
   const long o = pidx(d, i, j);
-  if (i >= 0 && i <= d.nx && j <= d.ny + NG - 1) {
-    edge_profile_col(ccol(crx, d, s, km, o), col(crx_e, d, s, k1, o), gam, dp0, km);
-    edge_profile_col(ccol(xfx, d, s, km, o), col(xfx_e, d, s, k1, o), gam, dp0, km);
+  const bool xface = i >= 0 && i <= d.nx && j <= d.ny + NG - 1;
+  const bool yface = j >= 0 && j <= d.ny && i <= d.nx + NG - 1;
+  if (!xface && !yface) return;
+  const long bq = (long)s * km * P + o, be = (long)s * k1 * P + o;
+  const double* __restrict__ Q[4] = {crx + bq, xfx + bq, cry + bq, yfx + bq};
+  double* __restrict__ E[4] = {crx_e + be, xfx_e + be, cry_e + be, yfx_e + be};
+  const bool ok[4] = {xface, xface, yface, yface};
+  // forward elimination
+  const double xt1_0 = 2.0 * g0 * (g0 + 1.0);
+  double qp[4], qprev[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    const double q0 = Q[c][0], q1 = Q[c][P];
+    qp[c] = (xt1_0 * q0 + q1) / bet0;
+    if (ok[c]) E[c][0] = qp[c];
+    qprev[c] = q0;
   }
-  if (j >= 0 && j <= d.ny && i <= d.nx + NG - 1) {
-    edge_profile_col(ccol(cry, d, s, km, o), col(cry_e, d, s, k1, o), gam, dp0, km);
-    edge_profile_col(ccol(yfx, d, s, km, o), col(yfx_e, d, s, k1, o), gam, dp0, km);
+  for (int kb = 1; kb < km; kb += EP_B) {
+    double qv[EP_B][4];
+#pragma unroll
+    for (int u = 0; u < EP_B; ++u) {
+      const int k = kb + u < km ? kb + u : km - 1;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) qv[u][c] = Q[c][k * P];
+    }
+#pragma unroll
+    for (int u = 0; u < EP_B; ++u) {
+      const int k = kb + u;
+      if (k >= km) break;
+      const double gk = gks[k], bet = bets[k];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        qp[c] = (3.0 * (qprev[c] + gk * qv[u][c]) - qp[c]) / bet;
+        if (ok[c]) E[c][k * P] = qp[c];
+        qprev[c] = qv[u][c];
+      }
+    }
+  }
+  // bottom edge and back substitution
+  const double gk = km > 1 ? gks[km - 1] : g0;
+  const double a_bot = 1.0 + gk * (gk + 1.5);
+  const double xt1 = 2.0 * gk * (gk + 1.0);
+  const double xt2 = gk * (gk + 0.5) - a_bot * gam[km - 1];
+  double x[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    x[c] = (xt1 * qprev[c] + Q[c][(km - 2) * P] - a_bot * qp[c]) / xt2;
+    if (ok[c]) E[c][km * P] = x[c];
+  }
+  for (int kb = km - 1; kb >= 0; kb -= EP_B) {
+    double ev[EP_B][4];
+#pragma unroll
+    for (int u = 0; u < EP_B; ++u) {
+      const int k = kb - u >= 0 ? kb - u : 0;
+#pragma unroll
+      for (int c = 0; c < 4; ++c) ev[u][c] = E[c][k * P];
+    }
+#pragma unroll
+    for (int u = 0; u < EP_B; ++u) {
+      const int k = kb - u;
+      if (k < 0) break;
+      const double gm = gam[k];
+#pragma unroll
+      for (int c = 0; c < 4; ++c) {
+        x[c] = ev[u][c] - gm * x[c];
+        if (ok[c]) E[c][k * P] = x[c];
+      }
+    }
   }
 }
 
