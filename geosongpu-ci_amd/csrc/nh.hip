@@ -406,55 +406,218 @@ __global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restr
   if (set) AT(qout, 0, 0) = val;
 }
 
-// interior qout = 0.5 * (qxx + qyy).  One 64 x 4 tile of corner points per workgroup:
-// the x-interpolants qx (rows j0-2..j0+5) and y-interpolants qy (cols i0-2..i0+65) the
-// tile needs are evaluated once into LDS, so the former qx / qy planes never touch HBM.
-constexpr int A2_TX = 64, A2_TY = 4;
-__global__ void __launch_bounds__(A2_TX * A2_TY) a2b_inner_k(Dims d, const SubInfo* __restrict__ subs,
-                                                             const double* __restrict__ M, int nk,
-                                                             const double* __restrict__ q, double* __restrict__ qout) {
-  __shared__ double QXs[A2_TY + 4][A2_TX];
-  __shared__ double QYs[A2_TY][A2_TX + 4];
-  const int tid = threadIdx.y * A2_TX + threadIdx.x;
-  const int i0 = blockIdx.x * A2_TX, j0 = blockIdx.y * A2_TY;
-  const int z = blockIdx.z, s = z / nk;
-  const SubInfo sub = subs[s];
+// ---- a2b_ord4 interior, column-marching form (default) ----
+// One wavefront owns 64 columns c = a-2 .. a+61 of one (sub-domain, level) and marches up
+// a segment of corner rows; corners a .. a+60 are its outputs.  Per cell row r it loads
+// q once, forms the x-interpolant qx at the lane's corner column (x neighbours by DPP)
+// and keeps q and qx of rows r-5..r in registers; the corner row j = r-2 then needs the
+// y-interpolant qy of its own column (from the q window) and of the neighbour columns
+// (DPP again).  Same expressions as A2bPoint and oracle/nh_core.py a2b_ord4.  (It
+// replaced an LDS-tiled kernel whose 8-row qx tile missed the row j-3 that the
+// J = N-1 form reads, wrong whenever N-1 was the first row of a tile.)
+constexpr int AM_W = 64, AM_OUT = 61, AM_WAVES = 4, AM_B = 2;
+
+__device__ __forceinline__ double dpp_prev_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x138, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x138, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double dpp_next_d(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), 0x130, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), 0x130, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+
+struct A2bM {
+  Dims d;
+  const SubInfo* subs;
+  const double *M, *q;
+  double* qout;
+  int nk, nz, nstrip, nseg, seg;
+};
+
+template <bool EX>
+__device__ void a2b_march_strip(const A2bM& a, int z, int a0, int a1, int j0, int j1) {
+  const Dims& d = a.d;
+  const int lane = threadIdx.x & (AM_W - 1);
+  const int s = z / a.nk;
+  const SubInfo sub = a.subs[s];
   const int N = sub.N, io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+  const int c = a0 - 2 + lane;  // this lane's column (cell column for qy, corner column for qx)
+  const int I = c + io;
+  const long pitch = d.pitch;
   const long zo = (long)z * d.plane;
-  const A2bPoint P{d, sub, q + zo, met(M, d, M_DXA, s), met(M, d, M_DYA, s)};
-  // the interpolants are only evaluated where the 3-pass form defined them
-  auto cell_ok = [&](int i, int j) { return i >= -NG && i <= nx + NG && j >= -NG && j <= ny + NG; };
-  for (int p = tid; p < (A2_TY + 4) * A2_TX; p += A2_TX * A2_TY) {
-    const int r = p / A2_TX, c = p % A2_TX;
-    const int i = i0 + c, j = j0 - 2 + r;
-    QXs[r][c] = (i <= nx && cell_ok(i, j)) ? P.qx(i, j) : 0.0;
+  const double* qq = a.q + zo;
+  const double* dxa = met(a.M, d, M_DXA, s);
+  const double* dya = met(a.M, d, M_DYA, s);
+  const int cc = c > nx + NG ? nx + NG : c;  // addressable
+  const long xo = cc + NG;
+  const bool out_lane = lane >= 2 && lane < 2 + AM_OUT && c < a1;  // corners [a0, a1)
+  const bool icols = I >= max(1, io) && I <= min(N - 1, io + nx) && c <= nx;
+  const bool qy_col = I >= max(0, io - 2) && I <= min(N - 1, io + nx + 1);
+  const bool qx_gen = I >= max(2, io) && I <= min(N - 2, io + nx);
+
+  double Qw[6], QXw[6];  // q and qx of rows r-5 .. r
+#pragma unroll
+  for (int m = 0; m < 6; ++m) Qw[m] = QXw[m] = 0.0;
+  // rows are loaded in blocks of AM_B, one block ahead (double buffered, addresses
+  // clamped to the plane, no conditional loads): a wave then waits for memory once per
+  // block instead of once per row
+  const int rlast = j1 + 1;
+  auto row_of = [&](int r) { return (long)((r < rlast ? r : rlast) + NG) * pitch + xo; };
+  // The tile-edge forms at I = 1, N-1 / J = 1, N-1 read qout on the neighbouring edge
+  // line (written by a2b_edge_k); those loads ride in the same prefetch (a load waited
+  // for in the row it is used in would drain every prefetched block: vmcnt is in order).
+  const long dxs = I == 1 ? -1 : (I == N - 1 ? 1 : 0);
+  const bool xs = dxs != 0;
+  const double* qo = a.qout + zo;
+  double qb[AM_B], db[AM_B], xb[AM_B], yb[AM_B], qn[AM_B], dn[AM_B], xn[AM_B], yn[AM_B];
+  auto fetch = [&](int r, double& q_, double& d_, double& x_, double& y_) {
+    const long o = row_of(r);
+    q_ = qq[o];
+    d_ = EX ? dxa[o] : 0.0;
+    const int j = r - 2;  // corner row of this step
+    const long oj = (long)((j > -NG ? (j < rlast ? j : rlast) : -NG) + NG) * pitch + xo;
+    x_ = 0.0;
+    if (xs) x_ = qo[oj + dxs];
+    const int J = j + jo;
+    y_ = 0.0;
+    if (J == 1) y_ = qo[oj - pitch];
+    else if (J == N - 1) y_ = qo[oj + pitch];
+  };
+#pragma unroll
+  for (int u = 0; u < AM_B; ++u) fetch(j0 - NG + u, qb[u], db[u], xb[u], yb[u]);
+  for (int r0 = j0 - NG; r0 <= rlast; r0 += AM_B) {
+#pragma unroll
+    for (int u = 0; u < AM_B; ++u) fetch(r0 + AM_B + u, qn[u], dn[u], xn[u], yn[u]);
+#pragma unroll
+    for (int u = 0; u < AM_B; ++u) {
+    const int r = r0 + u;
+    if (r > rlast) break;
+    const long o = (long)(r + NG) * pitch + xo;
+    const double qv = qb[u];
+    // ---- qx at (corner column c, cell row r)
+    const double qm1 = dpp_prev_d(qv), qm2 = dpp_prev_d(qm1), qp1 = dpp_next_d(qv);
+    double qx = 0.0;
+    const int Jr = r + jo;
+    if (Jr >= max(0, jo - 2) && Jr <= min(N - 1, jo + ny + 1)) {
+      if (EX) {
+        const double qm3 = dpp_prev_d(qm2), qp2 = dpp_next_d(qp1);
+        const double dx0 = db[u], dxm1 = dpp_prev_d(dx0), dxm2 = dpp_prev_d(dxm1), dxp1 = dpp_next_d(dx0);
+        if (I == 0) {
+          const double gr = dxp1 / dx0;
+          qx = 0.5 * ((2.0 + gr) * (qm1 + qv) - (qm2 + qp1)) / (1.0 + gr);
+        } else if (I == N) {
+          const double gr = dxm2 / dxm1;
+          qx = 0.5 * ((2.0 + gr) * (qm1 + qv) - (qm2 + qp1)) / (1.0 + gr);
+        } else if (I == 1) {
+          const double g1 = dx0 / dxm1;
+          const double gw = dx0 / dxm1;
+          const double qx0 = 0.5 * ((2.0 + gw) * (qm2 + qm1) - (qm3 + qv)) / (1.0 + gw);
+          const double gen1 = B2 * (qm1 + qp2) + B1 * (qv + qp1);
+          qx = (3.0 * (g1 * qm1 + qv) - (g1 * qx0 + gen1)) / (2.0 + 2.0 * g1);
+        } else if (I == N - 1) {
+          const double g1 = dxm1 / dx0;
+          const double ge = dxm1 / dx0;
+          const double qxN = 0.5 * ((2.0 + ge) * (qv + qp1) - (qm1 + qp2)) / (1.0 + ge);
+          const double genm = B2 * (qm3 + qv) + B1 * (qm2 + qm1);
+          qx = (3.0 * (qm1 + g1 * qv) - (g1 * qxN + genm)) / (2.0 + 2.0 * g1);
+        } else if (qx_gen) {
+          qx = B2 * (qm2 + qp1) + B1 * (qm1 + qv);
+        }
+      } else if (qx_gen) {
+        qx = B2 * (qm2 + qp1) + B1 * (qm1 + qv);
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < 5; ++m) {
+      Qw[m] = Qw[m + 1];
+      QXw[m] = QXw[m + 1];
+    }
+    Qw[5] = qv;
+    QXw[5] = qx;
+    // ---- corner row j = r-2: qy of this column, qyy / qxx, output
+    const int j = r - 2;
+    if (j < j0) continue;
+    const int J = j + jo;
+    // Qw[m] = q(c, j-3+m)
+    double qy = 0.0;
+    if (qy_col) {
+      auto gen = [&](int dj) { return B2 * (Qw[dj + 1] + Qw[dj + 4]) + B1 * (Qw[dj + 2] + Qw[dj + 3]); };
+      const long oj = o - 2 * pitch;
+      auto DY = [&](int dj) { return dya[oj + dj * pitch]; };
+      if (J == 0) {
+        const double gr = DY(1) / DY(0);
+        qy = 0.5 * ((2.0 + gr) * (Qw[2] + Qw[3]) - (Qw[1] + Qw[4])) / (1.0 + gr);
+      } else if (J == N) {
+        const double gr = DY(-2) / DY(-1);
+        qy = 0.5 * ((2.0 + gr) * (Qw[2] + Qw[3]) - (Qw[1] + Qw[4])) / (1.0 + gr);
+      } else if (J == 1) {
+        const double g1 = DY(0) / DY(-1);
+        const double gs = DY(0) / DY(-1);
+        const double qy0 = 0.5 * ((2.0 + gs) * (Qw[1] + Qw[2]) - (Qw[0] + Qw[3])) / (1.0 + gs);
+        qy = (3.0 * (g1 * Qw[2] + Qw[3]) - (g1 * qy0 + gen(1))) / (2.0 + 2.0 * g1);
+      } else if (J == N - 1) {
+        const double g1 = DY(-1) / DY(0);
+        const double gn = DY(-1) / DY(0);
+        const double qyN = 0.5 * ((2.0 + gn) * (Qw[3] + Qw[4]) - (Qw[2] + Qw[5])) / (1.0 + gn);
+        qy = (3.0 * (Qw[2] + g1 * Qw[3]) - (g1 * qyN + gen(-1))) / (2.0 + 2.0 * g1);
+      } else if (J >= max(2, jo) && J <= min(N - 2, jo + ny)) {
+        qy = gen(0);
+      }
+    }
+    // neighbour columns' qy (DPP outside any lane-divergent branch)
+    const double qy_m1 = dpp_prev_d(qy), qy_m2 = dpp_prev_d(qy_m1), qy_m3 = dpp_prev_d(qy_m2);
+    const double qy_p1 = dpp_next_d(qy), qy_p2 = dpp_next_d(qy_p1);
+    const bool jrows = J >= max(1, jo) && J <= min(N - 1, jo + ny) && j <= ny;
+    if (!(out_lane && icols && jrows && j < j1)) continue;
+    const long oj = o - 2 * pitch;
+    // QX(dj) = qx(c, j+dj) = QXw[dj + 3]
+    auto qxx_gen = [&](int dj) { return AA2 * (QXw[dj + 1] + QXw[dj + 4]) + AA1 * (QXw[dj + 2] + QXw[dj + 3]); };
+    const double QY[6] = {qy_m3, qy_m2, qy_m1, qy, qy_p1, qy_p2};  // QY(di) = QY[di + 3]
+    auto qyy_gen = [&](int di) { return AA2 * (QY[di + 1] + QY[di + 4]) + AA1 * (QY[di + 2] + QY[di + 3]); };
+    double qxx, qyy;
+    if (J == 1) qxx = AC1 * (QXw[2] + QXw[3]) + AC2 * (yb[u] + qxx_gen(1));
+    else if (J == N - 1) qxx = AC1 * (QXw[2] + QXw[3]) + AC2 * (yb[u] + qxx_gen(-1));
+    else qxx = qxx_gen(0);
+    if (I == 1) qyy = AC1 * (QY[2] + QY[3]) + AC2 * (xb[u] + qyy_gen(1));
+    else if (I == N - 1) qyy = AC1 * (QY[2] + QY[3]) + AC2 * (xb[u] + qyy_gen(-1));
+    else qyy = qyy_gen(0);
+    a.qout[zo + oj] = 0.5 * (qxx + qyy);
+    }
+#pragma unroll
+    for (int u = 0; u < AM_B; ++u) {
+      qb[u] = qn[u];
+      db[u] = dn[u];
+      xb[u] = xn[u];
+      yb[u] = yn[u];
+    }
   }
-  for (int p = tid; p < A2_TY * (A2_TX + 4); p += A2_TX * A2_TY) {
-    const int r = p / (A2_TX + 4), c = p % (A2_TX + 4);
-    const int i = i0 - 2 + c, j = j0 + r;
-    QYs[r][c] = (j <= ny && cell_ok(i, j)) ? P.qy(i, j) : 0.0;
-  }
-  __syncthreads();
-  const int c = threadIdx.x, r = threadIdx.y;
-  const int i = i0 + c, j = j0 + r;
-  if (i > nx || j > ny) return;
-  const int I = i + io, J = j + jo;
-  const bool icols = I >= max(1, io) && I <= min(N - 1, io + nx);
-  const bool jrows = J >= max(1, jo) && J <= min(N - 1, jo + ny);
-  if (!(icols && jrows)) return;
-  const long o = pidx(d, i, j);
-  auto QX = [&](int dj) { return QXs[r + 2 + dj][c]; };
-  auto QY = [&](int di) { return QYs[r][c + 2 + di]; };
-  auto qxx_gen = [&](int dj) { return AA2 * (QX(dj - 2) + QX(dj + 1)) + AA1 * (QX(dj - 1) + QX(dj)); };
-  auto qyy_gen = [&](int di) { return AA2 * (QY(di - 2) + QY(di + 1)) + AA1 * (QY(di - 1) + QY(di)); };
-  double qxx, qyy;
-  if (J == 1) qxx = AC1 * (QX(-1) + QX(0)) + AC2 * (AT(qout, 0, -1) + qxx_gen(1));
-  else if (J == N - 1) qxx = AC1 * (QX(-1) + QX(0)) + AC2 * (AT(qout, 0, 1) + qxx_gen(-1));
-  else qxx = qxx_gen(0);
-  if (I == 1) qyy = AC1 * (QY(-1) + QY(0)) + AC2 * (AT(qout, -1, 0) + qyy_gen(1));
-  else if (I == N - 1) qyy = AC1 * (QY(-1) + QY(0)) + AC2 * (AT(qout, 1, 0) + qyy_gen(-1));
-  else qyy = qyy_gen(0);
-  AT(qout, 0, 0) = 0.5 * (qxx + qyy);
+}
+
+__global__ void __launch_bounds__(AM_W * AM_WAVES) a2b_march_k(A2bM a) {
+  const long w = (long)blockIdx.x * AM_WAVES + threadIdx.x / AM_W;
+  const int strip = (int)(w % a.nstrip);
+  const long t = w / a.nstrip;
+  const int seg = (int)(t % a.nseg);
+  const long z = t / a.nseg;
+  if (z >= a.nz) return;  // whole wavefront leaves; no workgroup barrier follows
+  const int s = (int)(z / a.nk);
+  const SubInfo& sub = a.subs[s];
+  const int nx = a.d.nx;
+  // strips of 61 corners; the last one is shifted left to end at corner nx (so a corner
+  // next to the east tile edge is never a strip's last output: its stencil reaches c+2),
+  // and each strip writes only the corners before the next strip's first one
+  const int last0 = nx + 1 - AM_OUT > 0 ? nx + 1 - AM_OUT : 0;
+  const int a0 = strip * AM_OUT < last0 ? strip * AM_OUT : last0;
+  const int a1 = strip + 1 < a.nstrip ? ((strip + 1) * AM_OUT < last0 ? (strip + 1) * AM_OUT : last0) : nx + 1;
+  const int j0 = seg * a.seg;
+  const int j1 = j0 + a.seg < a.d.ny + 1 ? j0 + a.seg : a.d.ny + 1;
+  const int A = a0 + sub.ioff;
+  // x-interpolant edge forms are needed only where a lane's column reaches I <= 1 or I >= N-1
+  const bool ex = !(A - 2 >= 2 && A + AM_OUT + 1 <= sub.N - 2);
+  if (ex) a2b_march_strip<true>(a, (int)z, a0, a1, j0, j1);
+  else a2b_march_strip<false>(a, (int)z, a0, a1, j0, j1);
 }
 
 // non-hydrostatic pressure gradient on the D-grid winds (u, v arrive x dx, dy)
@@ -565,8 +728,11 @@ void a2b_ord4(const Ctx& c, int nk, const double* q, double* qout, double* qx, d
   GT_LAUNCH(a2b_edge_k, dim3(cdiv(edge_line_count(0, d.nx, 0, d.ny), 256), 1, d.nsub * nk), dim3(256), 0, c.st, d,
             c.subs, c.met, nk, c.cornerw, q, qout);
   HIP_LAUNCH_CHECK();
-  GT_LAUNCH(a2b_inner_k, dim3(cdiv(d.nx + 1, A2_TX), cdiv(d.ny + 1, A2_TY), d.nsub * nk), dim3(A2_TX, A2_TY), 0,
-            c.st, d, c.subs, c.met, nk, q, qout);
+  // interior corners: column-marching kernel (segments of 45 corner rows)
+  A2bM m{d, c.subs, c.met, q, qout, nk, d.nsub * nk, (int)cdiv(d.nx + 1, AM_OUT), 0, 45};
+  m.nseg = (int)cdiv(d.ny + 1, m.seg);
+  const long waves = (long)m.nz * m.nstrip * m.nseg;
+  GT_LAUNCH(a2b_march_k, dim3(cdiv(waves, AM_WAVES)), dim3(AM_W * AM_WAVES), 0, c.st, m);
   HIP_LAUNCH_CHECK();
   ktimer_bytes(8.0 * d.nx * d.ny * d.nsub * nk * 2.0);  // q read, qout written
 }

@@ -9,6 +9,7 @@
 #include "kernels.hpp"
 #include "kernels_column.hpp"
 #include "kernels_misc.hpp"
+#include "kernels_nh.hpp"
 #include "kernels_sw.hpp"
 
 namespace gtfv3 {
@@ -111,6 +112,13 @@ std::map<std::string, Fn>& reg() {
          Field& kidx = F(dy, f[2]);
          if (km.nk != data.nk || kidx.nk != 1) throw std::runtime_error("column_gather_k: field shapes");
          column_gather_k(dy.ctx(), data.nk, data.p, km.p, kidx.p, dy.field(f[3], 1).p);
+       }},
+      // a2b_ord4(q | qout): cell means -> cell corners (4th order, cubed-sphere edge forms)
+      {"a2b_ord4",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
+         need(f, 2, "a2b_ord4");
+         Field& q = F(dy, f[0]);
+         a2b_ord4(dy.ctx(), q.nk, q.p, dy.field(f[1], q.nk).p, nullptr, nullptr);
        }},
       // Held-Suarez forcing: held_suarez(pe, pt, u, v) in place, params: dt
       {"held_suarez",
