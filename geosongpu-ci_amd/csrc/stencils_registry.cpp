@@ -9,6 +9,7 @@
 #include "kernels.hpp"
 #include "kernels_column.hpp"
 #include "kernels_misc.hpp"
+#include "kernels_moist.hpp"
 #include "kernels_nh.hpp"
 #include "kernels_sw.hpp"
 
@@ -119,6 +120,49 @@ std::map<std::string, Fn>& reg() {
          need(f, 2, "a2b_ord4");
          Field& q = F(dy, f[0]);
          a2b_ord4(dy.ctx(), q.nk, q.p, dy.field(f[1], q.nk).p, nullptr, nullptr);
+       }},
+      // moist column physics
+      // moist_qsat(T, pm | qsw, qsi, dqsw)
+      {"moist_qsat",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
+         need(f, 5, "moist_qsat");
+         Field& t = F(dy, f[0]);
+         moist_qsat(dy.ctx(), t.nk, t.p, F(dy, f[1]).p, dy.field(f[2], t.nk).p, dy.field(f[3], t.nk).p,
+                    dy.field(f[4], t.nk).p);
+       }},
+      // fillq2zero(q, delp | fill2d): q in place
+      {"fillq2zero",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
+         need(f, 3, "fillq2zero");
+         Field& q = F(dy, f[0]);
+         fillq2zero(dy.ctx(), q.nk, q.p, F(dy, f[1]).p, dy.field(f[2], 1).p);
+       }},
+      // gfdl_1m(T, qv, ql, qr, qi, qs, qg, delp, delz, pm | prec_r, prec_s, prec_g, prec_i) params: dt;
+      // the first seven fields are updated in place
+      {"gfdl_1m",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 14, "gfdl_1m");
+         Field& t = F(dy, f[0]);
+         Gfdl1mArgs a{};
+         a.nk = t.nk;
+         a.dt = p.at(0);
+         a.T = t.p;
+         a.qv = F(dy, f[1]).p; a.ql = F(dy, f[2]).p; a.qr = F(dy, f[3]).p; a.qi = F(dy, f[4]).p;
+         a.qs = F(dy, f[5]).p; a.qg = F(dy, f[6]).p;
+         a.dp = F(dy, f[7]).p; a.dz = F(dy, f[8]).p; a.pm = F(dy, f[9]).p;
+         for (int n = 1; n <= 9; ++n)
+           if (F(dy, f[n]).nk != t.nk) throw std::runtime_error("gfdl_1m: fields must share the level count");
+         a.pr = dy.field(f[10], 1).p; a.ps = dy.field(f[11], 1).p; a.pg = dy.field(f[12], 1).p;
+         a.pi = dy.field(f[13], 1).p;
+         gfdl_1m(dy.ctx(), a);
+       }},
+      // buoyancy(T, qv, pm, zm | buoy, cape, cin, klcl)
+      {"buoyancy",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
+         need(f, 8, "buoyancy");
+         Field& t = F(dy, f[0]);
+         buoyancy(dy.ctx(), t.nk, t.p, F(dy, f[1]).p, F(dy, f[2]).p, F(dy, f[3]).p, dy.field(f[4], t.nk).p,
+                  dy.field(f[5], 1).p, dy.field(f[6], 1).p, dy.field(f[7], 1).p);
        }},
       // Held-Suarez forcing: held_suarez(pe, pt, u, v) in place, params: dt
       {"held_suarez",
