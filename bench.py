@@ -68,13 +68,17 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--kernel-report", default="", help="write per-kernel stats JSON here")
+    p.add_argument("--moist", action="store_true",
+                   help="Aquaplanet configuration: nq=6 moist tracers and the moist column step "
+                        "(gfdl_1m) after every fv_dynamics call, inside the timed region")
     p.add_argument("--geos-log", default="", help="also write a GEOS-style log (geoslog.py) of K individually "
                    "synchronised steps run after the timed region, for tcn.benchmark's parse_geos_log")
     return p.parse_args()
 
 
-def cpu_baseline(pkg, npx, npz, nq, dt):
-    """One oracle fv_dynamics step of a bounded sample, single host core."""
+def cpu_baseline(pkg, npx, npz, nq, dt, moist=False):
+    """One oracle fv_dynamics step (+ the oracle moist column step with --moist) of a
+    bounded sample, single host core."""
     import importlib
 
     from oracle import fv_dynamics as fvd
@@ -82,6 +86,8 @@ def cpu_baseline(pkg, npx, npz, nq, dt):
     d = pkg.Domain(npx=npx, npz=npz, nq=nq, host_only=1, dt=dt)
     ak, bk, ks = state.hybrid_levels(npz)
     st = state.jablonowski_williamson(d, ak, bk)
+    if moist:
+        state.aquaplanet_tracers(d, st, ak, bk)
     names = ["area", "rarea", "area_c", "rarea_c", "dx", "dy", "dxa", "dya", "dxc", "dyc", "rdx", "rdy",
              "rdxa", "rdya", "rdxc", "rdyc"] + [f"sin_sg{i}" for i in range(1, 10)] + \
         [f"cos_sg{i}" for i in range(1, 10)] + ["cosa_u", "sina_u", "rsin_u", "cosa_v", "sina_v", "rsin_v",
@@ -94,12 +100,20 @@ def cpu_baseline(pkg, npx, npz, nq, dt):
     nl = dict(n_split=6, dt_atmos=dt, hord_mt=6, hord_vt=6, hord_tm=6, hord_dp=6, hord_tr=6, dddmp=0.2, d2_bg=0.0,
               p_fac=0.05, dz_min=2.0, fill=1, nq=nq)
     t0 = time.perf_counter()
-    fvd.fv_dynamics(st, ak, bk, g, nl)
+    out = fvd.fv_dynamics(st, ak, bk, g, nl)
+    if moist:
+        from oracle import moist as om
+        for s in range(d.nsub):
+            pe = out["pe"][s]
+            q = out["q"][s]
+            sp = [q[n * npz:(n + 1) * npz] for n in range(6)]
+            om.gfdl_1m(out["pt"][s], out["delp"][s], out["delz"][s], 0.5 * (pe[1:] + pe[:-1]), *sp, dt)
     el = time.perf_counter() - t0
     cells = 6 * d.N * d.N * npz
     d.close()
     return dict(value=cells / el, unit="grid-cell-updates/s", cores=1, kind="port",
-                sample=f"one fv_dynamics step, C{d.N} L{npz} nq={nq}, 6 tiles, numpy fp64 oracle "
+                sample=f"one fv_dynamics step{' + moist column step' if moist else ''}, C{d.N} L{npz} nq={nq}, "
+                       f"6 tiles, numpy fp64 oracle "
                        f"(oracle/fv_dynamics.py), {el:.1f} s on 1 host core")
 
 
@@ -128,9 +142,12 @@ def main():
         nccl_id = obj[0]
     lx, ly = layout_for(world)
     t_init = time.perf_counter()
-    d = pkg.Domain(rank, world, nccl_id, npx=a.npx, npz=a.npz, nq=a.nq, layout_x=lx, layout_y=ly, dt=a.dt)
+    nq = max(a.nq, 6) if a.moist else a.nq
+    d = pkg.Domain(rank, world, nccl_id, npx=a.npx, npz=a.npz, nq=nq, layout_x=lx, layout_y=ly, dt=a.dt)
     ak, bk, ks = state.hybrid_levels(a.npz)
     st = state.jablonowski_williamson(d, ak, bk)
+    if a.moist:
+        state.aquaplanet_tracers(d, st, ak, bk)
     d.set_vertical(ak, bk, ks)
     for k, v in st.items():
         d.upload(k, v)
@@ -143,14 +160,19 @@ def main():
         if world > 1:
             dist.barrier()
 
-    for _ in range(a.warmup):
+    def one_step():
         d.step(1)
+        if a.moist:
+            d.stencil("aquaplanet_physics", [], [a.dt])
+
+    for _ in range(a.warmup):
+        one_step()
     if not a.no_kernel_timing:
         d.kernel_timing(True)
     barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        d.step(1)
+        one_step()
     d.sync()
     barrier()
     el = time.perf_counter() - t0
@@ -187,7 +209,7 @@ def main():
         for _ in range(a.steps):
             barrier()
             t1 = time.perf_counter()
-            d.step(1)
+            one_step()
             d.sync()
             barrier()
             per_step.append(time.perf_counter() - t1)
@@ -200,7 +222,7 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(pkg, a.cpu_npx, a.npz, a.nq, a.dt)
+        cpu = cpu_baseline(pkg, a.cpu_npx, a.npz, nq, a.dt, a.moist)
 
     if rank == 0:
         out = {
@@ -216,8 +238,10 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (Jablonowski-Williamson baroclinic state on an analytic hybrid L%d grid)" % npz,
-            "config": {"workload": f"Held-Suarez C{N} L{npz} dycore step (fv_dynamics), 6 tiles on "
-                                   f"{world} MI355X", "npx": N + 1, "npz": npz, "nq": a.nq, "layout": f"{lx}x{ly}",
+            "config": {"workload": (f"Aquaplanet C{N} L{npz} dycore step + moist column step (gfdl_1m)"
+                                    if a.moist else f"Held-Suarez C{N} L{npz} dycore step (fv_dynamics)") +
+                                   f", 6 tiles on {world} MI355X", "npx": N + 1, "npz": npz, "nq": nq,
+                       "layout": f"{lx}x{ly}",
                        "dt_atmos": a.dt, "n_split": 6, "k_split": 1, "cells_per_step": cells},
             "roofline": roof,
             "cpu_baseline": cpu,

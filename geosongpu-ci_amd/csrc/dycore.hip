@@ -8,6 +8,7 @@
 
 #include "hip_util.hpp"
 #include "kernels_misc.hpp"
+#include "kernels_moist.hpp"
 #include "kernels_nh.hpp"
 #include "kernels_sw.hpp"
 
@@ -232,6 +233,28 @@ const double* Dycore::vertical_dev() {
 // One fv_dynamics call (FV3 fv_dynamics.F90 / dyn_core.F90 sequence, non-hydrostatic,
 // k_split remap cycles of n_split acoustic sub-steps, tracer_2d_1l, Lagrangian-to-
 // Eulerian remap, then T/omega/A-grid winds for the caller).
+// Aquaplanet moist column step on the device-resident state after
+// fv_dynamics: T = pt, species = tracers 0..5 (qv ql qr qi qs qg), layer pressure from
+// the interfaces pe; surface precipitation accumulates into prec_{rain,snow,graupel,ice}.
+void Dycore::moist_physics(double dt) {
+  const int npz = nl.npz, nq = nl.nq;
+  if (nq < 6) throw std::runtime_error("moist_physics: needs nq >= 6 (qv ql qr qi qs qg)");
+  Field& q = need("q", nq * npz);
+  const long sp = (long)npz * d.plane;  // one species of sub-domain 0
+  Gfdl1mArgs g{};
+  g.nk = npz;
+  g.qsub = nq * npz;
+  g.dt = dt;
+  g.T = need("pt", npz).p;
+  g.qv = q.p; g.ql = q.p + sp; g.qr = q.p + 2 * sp; g.qi = q.p + 3 * sp; g.qs = q.p + 4 * sp; g.qg = q.p + 5 * sp;
+  g.dp = need("delp", npz).p;
+  g.dz = need("delz", npz).p;
+  g.pe = need("pe", npz + 1).p;
+  g.pr = field("prec_rain", 1).p; g.ps = field("prec_snow", 1).p; g.pg = field("prec_graupel", 1).p;
+  g.pi = field("prec_ice", 1).p;
+  gfdl_1m(ctx(), g);
+}
+
 void Dycore::step() {
   if (nl.host_only) throw std::runtime_error("host-only dycore cannot step");
   if (nl.k_split != 1) throw std::runtime_error("step: only k_split = 1 is supported");

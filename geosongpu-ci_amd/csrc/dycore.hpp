@@ -67,6 +67,8 @@ class Dycore {
   void tracer_2d(int nq, double dt);
   void set_vertical(const double* ak_, const double* bk_, int ks_);
   void step();  // one fv_dynamics call on device-resident state
+  // Aquaplanet moist column step on the state (tracers 0..5 = qv ql qr qi qs qg, nq >= 6)
+  void moist_physics(double dt);
 };
 
 }  // namespace gtfv3

@@ -12,9 +12,11 @@ void fillq2zero(const Ctx& c, int nk, double* q, const double* dp, double* fill)
 
 struct Gfdl1mArgs {
   int nk;
+  int qsub = 0;  // levels per sub-domain of the species arrays (0: nk; nq*nk for slices of the tracer array q)
   double dt;
   double *T, *qv, *ql, *qr, *qi, *qs, *qg;  // updated in place
-  const double *dp, *dz, *pm;              // delp (Pa), delz (m, < 0), layer pressure (Pa)
+  const double *dp, *dz;                   // delp (Pa), delz (m, < 0)
+  const double *pm = nullptr, *pe = nullptr;  // layer pressure (Pa), or interface pressure (L+1)
   double *pr, *ps, *pg, *pi;               // surface rain / snow / graupel / ice (kg m-2 per step)
 };
 void gfdl_1m(const Ctx& c, const Gfdl1mArgs& a);

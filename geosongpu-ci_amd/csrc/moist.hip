@@ -146,11 +146,11 @@ struct Fall {  // implicit_fall carry: dd(k-1) * qm(k-1)
 
 struct M1Args {
   Dims d;
-  int nk;
+  int nk, qsub;  // levels; levels per sub-domain of the species arrays (nk, or nq*nk in q)
   double dt;
   Tables tb;
   double *T, *qv, *ql, *qr, *qi, *qs, *qg;
-  const double *dp, *dz, *pm;
+  const double *dp, *dz, *pm, *pe;  // pm null: layer pressure from the interfaces pe (L+1)
   double *pr, *ps, *pg, *pi;
 };
 
@@ -165,8 +165,16 @@ __global__ void __launch_bounds__(256) gfdl_1m_k(M1Args a) {
   Fall fi, fs, fg, fr;
   for (int k = 0; k < a.nk; ++k) {
     const long x = c.at(k);
-    double T = a.T[x], qv = a.qv[x], ql = a.ql[x], qr = a.qr[x], qi = a.qi[x], qs = a.qs[x], qg = a.qg[x];
-    const double dp = a.dp[x], thick = -a.dz[x], pm = a.pm[x];
+    const long y = ((long)s * a.qsub + k) * a.d.plane + o;  // species
+    double T = a.T[x], qv = a.qv[y], ql = a.ql[y], qr = a.qr[y], qi = a.qi[y], qs = a.qs[y], qg = a.qg[y];
+    double pm;
+    if (a.pm) {
+      pm = a.pm[x];
+    } else {
+      const long e = ((long)s * (a.nk + 1) + k) * a.d.plane + o;
+      pm = 0.5 * (a.pe[e] + a.pe[e + a.d.plane]);
+    }
+    const double dp = a.dp[x], thick = -a.dz[x];
     // 1. neg_adj
     {
       double n;
@@ -249,7 +257,7 @@ __global__ void __launch_bounds__(256) gfdl_1m_k(M1Args a) {
       mlt = T > T_ICE ? fmin(fmlt * qg, cap) : 0.0;
       qg -= mlt; qr = qr + mlt; T = T - mlt * icp;
     }
-    a.T[x] = T; a.qv[x] = qv; a.ql[x] = ql; a.qr[x] = qr; a.qi[x] = qi; a.qs[x] = qs; a.qg[x] = qg;
+    a.T[x] = T; a.qv[y] = qv; a.ql[y] = ql; a.qr[y] = qr; a.qi[y] = qi; a.qs[y] = qs; a.qg[y] = qg;
   }
   const long p2 = (long)s * a.d.plane + o;
   a.pr[p2] = fr.carry;
@@ -355,8 +363,9 @@ void fillq2zero(const Ctx& c, int nk, double* q, const double* dp, double* fill)
 }
 
 void gfdl_1m(const Ctx& c, const Gfdl1mArgs& g) {
-  moist::M1Args a{c.d, g.nk, g.dt, moist::device_tables(), g.T, g.qv, g.ql, g.qr, g.qi, g.qs, g.qg,
-                  g.dp, g.dz, g.pm, g.pr, g.ps, g.pg, g.pi};
+  if (!g.pm && !g.pe) throw std::runtime_error("gfdl_1m: layer pressure (pm) or interfaces (pe) required");
+  moist::M1Args a{c.d, g.nk, g.qsub > 0 ? g.qsub : g.nk, g.dt, moist::device_tables(), g.T, g.qv, g.ql, g.qr,
+                  g.qi, g.qs, g.qg, g.dp, g.dz, g.pm, g.pe, g.pr, g.ps, g.pg, g.pi};
   GT_LAUNCH(moist::gfdl_1m_k, moist::colgrid(c.d), dim3(BX, BY), 0, c.st, a);
   HIP_LAUNCH_CHECK();
   // algorithmic bytes: T + 6 species read and written, dp dz pm read (L each), 4 surface fields

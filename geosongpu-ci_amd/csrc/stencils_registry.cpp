@@ -164,6 +164,12 @@ std::map<std::string, Fn>& reg() {
          buoyancy(dy.ctx(), t.nk, t.p, F(dy, f[1]).p, F(dy, f[2]).p, F(dy, f[3]).p, dy.field(f[4], t.nk).p,
                   dy.field(f[5], 1).p, dy.field(f[6], 1).p, dy.field(f[7], 1).p);
        }},
+      // aquaplanet_physics: the moist column step on the dycore state (pt, q tracers 0..5, delp,
+      // delz, pe); params: dt
+      {"aquaplanet_physics",
+       [](Dycore& dy, const std::vector<std::string>&, const std::vector<double>& p) {
+         dy.moist_physics(p.at(0));
+       }},
       // Held-Suarez forcing: held_suarez(pe, pt, u, v) in place, params: dt
       {"held_suarez",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {

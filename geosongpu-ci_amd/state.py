@@ -127,3 +127,33 @@ def jablonowski_williamson(dom, ak, bk, ps=1.0e5):
     for a in out.values():
         np.nan_to_num(a, copy=False)
     return out
+
+
+def aquaplanet_tracers(dom, st, ak, bk, ps=1.0e5, rh_sfc=0.8, seed=20250117):
+    """Moist tracers for the Aquaplanet configuration (BASELINE.json configs[3]) on a JW06
+    state `st` in place: q tracers 0..5 = qv, ql, qr, qi, qs, qg (needs nq >= 6).
+    qv from a relative-humidity profile (rh_sfc at the surface decreasing as (p/ps)^2)
+    with a Tetens saturation curve (initial-state synthesis only; the physics kernels
+    use the GFDL tables), a thin cloud layer where the profile nears saturation, and no
+    precipitating species; the remaining tracers keep their passive bells."""
+    nq = max(dom.nq, 1)
+    if nq < 6:
+        raise ValueError("aquaplanet_tracers: nq >= 6 required")
+    npz = dom.npz
+    pe = ak[:, None, None] + bk[:, None, None] * ps
+    pm = 0.5 * (pe[1:] + pe[:-1])
+    r = np.random.default_rng(seed)
+    for s in range(dom.nsub):
+        t = st["pt"][s]
+        tc = t - 273.15
+        es = 610.78 * np.exp(np.where(tc >= 0.0, 17.27 * tc / (tc + 237.3), 21.875 * tc / (tc + 265.5)))
+        qsat = 0.622 * es / np.maximum(pm - 0.378 * es, 1.0)
+        rh = rh_sfc * (pm / ps) ** 2 * (1.0 + 0.05 * r.standard_normal(t.shape))
+        qv = np.clip(rh, 0.0, 1.02) * qsat
+        cloud = np.clip(rh - 0.75, 0.0, None) * 2e-3
+        st["q"][s, 0:npz] = qv
+        st["q"][s, npz:2 * npz] = np.where(t > 253.0, cloud, 0.0)
+        st["q"][s, 2 * npz:3 * npz] = 0.0
+        st["q"][s, 3 * npz:4 * npz] = np.where(t <= 253.0, cloud, 0.0)
+        st["q"][s, 4 * npz:6 * npz] = 0.0
+    return st
