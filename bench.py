@@ -226,7 +226,8 @@ def main():
 
     if rank == 0:
         out = {
-            "metric": "grid-cell-updates/sec per dycore step, Held-Suarez C180 L72",
+            "metric": "grid-cell-updates/sec per dycore step, " +
+                      ("Aquaplanet C180 L72 + moist physics" if a.moist else "Held-Suarez C180 L72"),
             "value": value,
             "unit": "grid-cell-updates/s",
             "n_gpus": world,
