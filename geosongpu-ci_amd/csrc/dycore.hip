@@ -16,6 +16,10 @@ namespace gtfv3 {
 
 long Field::elems() const { return 0; }
 
+namespace {
+constexpr size_t kGuardElems = 2048;  // 16 KiB guard zones in GTFV3_SYNC_LAUNCH=1 mode
+}  // namespace
+
 Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) : nl(nl_) {
   if (nl.ntiles != 6) throw std::runtime_error("only the 6-tile cubed sphere is supported");
   if (nl.npx != nl.npy) throw std::runtime_error("npx must equal npy");
@@ -45,6 +49,9 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
   HIP_CHECK(hipMemcpy(dmet, hm.m.data(), sizeof(double) * hm.m.size(), hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&dcornerw, sizeof(double) * hm.corner_w.size()));
   HIP_CHECK(hipMemcpy(dcornerw, hm.corner_w.data(), sizeof(double) * hm.corner_w.size(), hipMemcpyHostToDevice));
+  debug_canary("subs", dsubs, hsubs.data(), sizeof(SubInfo) * d.nsub);
+  debug_canary("metrics", dmet, hm.m.data(), sizeof(double) * hm.m.size());
+  debug_canary("corner_w", dcornerw, hm.corner_w.data(), sizeof(double) * hm.corner_w.size());
 
   if (nranks > 1) {
     comm = nl.loopback ? make_loopback_transport(nl.loopback, nranks, rank) : make_nccl_transport(nranks, rank, nccl_id);
@@ -54,7 +61,19 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
 }
 
 Dycore::~Dycore() {
-  for (auto& kv : fields) (void)hipFree(kv.second.p);
+  for (auto& kv : fields) {
+    if (debug_sync_launch()) {
+      double* base = kv.second.p - kGuardElems;
+      debug_canary_drop(base);
+      debug_canary_drop(kv.second.p + field_elems(kv.second.nk));
+      (void)hipFree(base);
+    } else {
+      (void)hipFree(kv.second.p);
+    }
+  }
+  debug_canary_drop(dsubs);
+  debug_canary_drop(dmet);
+  debug_canary_drop(dcornerw);
   if (dsubs) (void)hipFree(dsubs);
   if (dmet) (void)hipFree(dmet);
   if (dcornerw) (void)hipFree(dcornerw);
@@ -71,6 +90,19 @@ Field& Dycore::field(const std::string& name, int nk) {
   Field f;
   f.nk = nk;
   size_t bytes = sizeof(double) * (size_t)field_elems(nk);
+  if (debug_sync_launch()) {
+    // debug mode: guard zones either side of the field, checked after every launch
+    const size_t gb = sizeof(double) * kGuardElems;
+    double* base = nullptr;
+    HIP_CHECK(hipMalloc(&base, bytes + 2 * gb));
+    HIP_CHECK(hipMemset(base, 0xA5, bytes + 2 * gb));
+    f.p = base + kGuardElems;
+    HIP_CHECK(hipMemset(f.p, 0, bytes));
+    const std::vector<unsigned char> pat(gb, 0xA5);
+    debug_canary(("guard-lo " + name).c_str(), base, pat.data(), gb);
+    debug_canary(("guard-hi " + name).c_str(), f.p + field_elems(nk), pat.data(), gb);
+    return fields[name] = f;
+  }
   HIP_CHECK(hipMalloc(&f.p, bytes));
   HIP_CHECK(hipMemsetAsync(f.p, 0, bytes, st));
   return fields[name] = f;

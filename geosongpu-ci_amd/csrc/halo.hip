@@ -39,6 +39,9 @@ struct Src {
 
 HaloExchanger::~HaloExchanger() {
   for (int k = 0; k < H_NKIND; ++k) {
+    debug_canary_drop(d_local_[k]);
+    debug_canary_drop(d_send_[k]);
+    debug_canary_drop(d_recv_[k]);
     if (d_local_[k]) (void)hipFree(d_local_[k]);
     if (d_send_[k]) (void)hipFree(d_send_[k]);
     if (d_recv_[k]) (void)hipFree(d_recv_[k]);
@@ -144,14 +147,17 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
     if (n_local_[kind]) {
       HIP_CHECK(hipMalloc(&d_local_[kind], sizeof(HaloEntry) * n_local_[kind]));
       HIP_CHECK(hipMemcpy(d_local_[kind], h_local_[kind].data(), sizeof(HaloEntry) * n_local_[kind], hipMemcpyHostToDevice));
+      debug_canary("halo d_local_", d_local_[kind], h_local_[kind].data(), sizeof(HaloEntry) * n_local_[kind]);
     }
     if (n_send_[kind]) {
       HIP_CHECK(hipMalloc(&d_send_[kind], sizeof(PackEntry) * n_send_[kind]));
       HIP_CHECK(hipMemcpy(d_send_[kind], hs.data(), sizeof(PackEntry) * n_send_[kind], hipMemcpyHostToDevice));
+      debug_canary("halo d_send_", d_send_[kind], hs.data(), sizeof(PackEntry) * n_send_[kind]);
     }
     if (n_recv_[kind]) {
       HIP_CHECK(hipMalloc(&d_recv_[kind], sizeof(PackEntry) * n_recv_[kind]));
       HIP_CHECK(hipMemcpy(d_recv_[kind], hr.data(), sizeof(PackEntry) * n_recv_[kind], hipMemcpyHostToDevice));
+      debug_canary("halo d_recv_", d_recv_[kind], hr.data(), sizeof(PackEntry) * n_recv_[kind]);
     }
   }
   if (!device) return;
@@ -225,6 +231,10 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
   size_t off = 0;
   std::vector<size_t> foff(nf);
   if (remote) {
+    size_t need = 0;
+    for (int f = 0; f < nf; ++f)
+      need += (size_t)std::max(n_send_[fields[f].kind], n_recv_[fields[f].kind]) * fields[f].nk;
+    if (need > buf_elems_) throw std::runtime_error("halo: exchange buffer too small");
     for (int f = 0; f < nf; ++f) {
       const HaloField& F = fields[f];
       foff[f] = off;
@@ -237,7 +247,6 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
       }
       off += (size_t)std::max(n_send_[F.kind], n_recv_[F.kind]) * F.nk;
     }
-    if (off > buf_elems_) throw std::runtime_error("halo: exchange buffer too small");
     if (!tr_) throw std::runtime_error("halo: multi-rank exchange without a transport");
     tr_->group_start();
     for (int f = 0; f < nf; ++f) {

@@ -21,9 +21,24 @@
 namespace gtfv3 {
 
 // plane offset of local (i,j); i,j may be negative down to -NG
+#ifdef GTFV3_BOUNDS
+// debugging build (make BOUNDS=1): report and clamp plane indices outside the padded plane
+__host__ __device__ inline long pidx(const Dims& d, int i, int j) {
+  if (i < -NG || i > d.pitch - NG - 1 || j < -NG || j > d.nj - NG - 1) {
+#ifdef __HIP_DEVICE_COMPILE__
+    printf("GTFV3_BOUNDS pidx(%d, %d) outside plane pitch %d nj %d (block %d %d %d thread %d %d)\n", i, j, d.pitch,
+           d.nj, blockIdx.x, blockIdx.y, blockIdx.z, threadIdx.x, threadIdx.y);
+#endif
+    i = i < -NG ? -NG : (i > d.pitch - NG - 1 ? d.pitch - NG - 1 : i);
+    j = j < -NG ? -NG : (j > d.nj - NG - 1 ? d.nj - NG - 1 : j);
+  }
+  return (long)(j + NG) * d.pitch + (i + NG);
+}
+#else
 __host__ __device__ inline long pidx(const Dims& d, int i, int j) {
   return (long)(j + NG) * d.pitch + (i + NG);
 }
+#endif
 
 inline unsigned cdiv(long a, long b) { return (unsigned)((a + b - 1) / b); }
 
@@ -56,10 +71,21 @@ struct KScope {
   }
 };
 
-#define GT_LAUNCH(kern, grid, block, shm, st, ...)        \
-  do {                                                    \
-    ::gtfv3::KScope kscope_(#kern, st);                   \
-    hipLaunchKernelGGL(kern, grid, block, shm, st, __VA_ARGS__); \
+// GTFV3_SYNC_LAUNCH=1 (debugging): synchronise after every launch and name the kernel
+// in the error, so an asynchronous fault is attributed to the launch that caused it.
+bool debug_sync_launch();
+void debug_sync_check(const char* kern, hipStream_t st);
+// Debug mode only: register device bytes that must not change (checked after every launch).
+void debug_canary(const char* what, const void* d, const void* h, size_t bytes);
+void debug_canary_drop(const void* d);
+
+#define GT_LAUNCH(kern, grid, block, shm, st, ...)                       \
+  do {                                                                   \
+    {                                                                    \
+      ::gtfv3::KScope kscope_(#kern, st);                                \
+      hipLaunchKernelGGL(kern, grid, block, shm, st, __VA_ARGS__);       \
+    }                                                                    \
+    if (::gtfv3::debug_sync_launch()) ::gtfv3::debug_sync_check(#kern, st); \
   } while (0)
 
 }  // namespace gtfv3

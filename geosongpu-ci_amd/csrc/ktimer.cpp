@@ -1,4 +1,8 @@
 // ktimer.cpp — per-kernel HIP event timing behind GT_LAUNCH (hip_util.hpp).
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
 #include <vector>
 
 #include "hip_util.hpp"
@@ -80,5 +84,55 @@ void ktimer_reset() {
 }
 
 const std::map<std::string, KernelStat>& ktimer_stats() { return kt().stats; }
+
+bool debug_sync_launch() {
+  static const bool on = [] {
+    const char* e = std::getenv("GTFV3_SYNC_LAUNCH");
+    return e && e[0] == '1';
+  }();
+  return on;
+}
+
+namespace {
+struct Canary {
+  std::string what;
+  const void* d;
+  std::vector<unsigned char> h;
+};
+std::mutex g_canary_m;
+std::vector<Canary> g_canaries;
+}  // namespace
+
+void debug_canary(const char* what, const void* d, const void* h, size_t bytes) {
+  if (!debug_sync_launch() || !d || !bytes) return;
+  std::lock_guard<std::mutex> lk(g_canary_m);
+  const unsigned char* hb = static_cast<const unsigned char*>(h);
+  g_canaries.push_back({what, d, std::vector<unsigned char>(hb, hb + bytes)});
+}
+
+void debug_canary_drop(const void* d) {
+  std::lock_guard<std::mutex> lk(g_canary_m);
+  for (size_t i = 0; i < g_canaries.size();)
+    if (g_canaries[i].d == d) g_canaries.erase(g_canaries.begin() + i);
+    else ++i;
+}
+
+void debug_sync_check(const char* kern, hipStream_t st) {
+  const hipError_t e = hipStreamSynchronize(st);
+  if (e != hipSuccess) throw std::runtime_error(std::string("kernel ") + kern + ": " + hipGetErrorString(e));
+  // every registered read-only table / guard zone must still hold its bytes
+  std::lock_guard<std::mutex> lk(g_canary_m);
+  std::vector<unsigned char> tmp;
+  for (const Canary& c : g_canaries) {
+    tmp.resize(c.h.size());
+    HIP_CHECK(hipMemcpy(tmp.data(), c.d, tmp.size(), hipMemcpyDeviceToHost));
+    if (std::memcmp(tmp.data(), c.h.data(), tmp.size()) != 0) {
+      size_t i = 0;
+      while (tmp[i] == c.h[i]) ++i;
+      throw std::runtime_error(std::string("after kernel ") + kern + ": canary '" + c.what + "' overwritten at byte " +
+                               std::to_string(i) + " of " + std::to_string(tmp.size()));
+    }
+  }
+}
 
 }  // namespace gtfv3

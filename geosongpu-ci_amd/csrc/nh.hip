@@ -277,13 +277,15 @@ constexpr double AC1 = 2.0 / 3.0, AC2 = -1.0 / 6.0;
 // evaluated on the fly by the corner-value kernels so those planes never touch HBM.
 // Zero where the 3-pass form left them unset.
 struct A2bPoint {
-  const Dims& d;
-  const SubInfo& sub;
+  // held by value: a reference to the kernel's Dims argument would need its address and
+  // put the struct in scratch memory
+  Dims d;
+  SubInfo sub;
   const double* q;   // plane of the level
   const double* dxa;
   const double* dya;
   __device__ __forceinline__ double Q(int i, int j) const { return q[pidx(d, i, j)]; }
-  __device__ double qx(int i, int j) const {
+  __device__ __forceinline__ double qx(int i, int j) const {
     const int N = sub.N, io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
     const int I = i + io, J = j + jo;
     if (!(J >= max(0, jo - 2) && J <= min(N - 1, jo + ny + 1))) return 0.0;
@@ -310,7 +312,7 @@ struct A2bPoint {
     }
     return 0.0;
   }
-  __device__ double qy(int i, int j) const {
+  __device__ __forceinline__ double qy(int i, int j) const {
     const int N = sub.N, io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
     const int I = i + io, J = j + jo;
     if (!(I >= max(0, io - 2) && I <= min(N - 1, io + nx + 1))) return 0.0;
@@ -339,6 +341,60 @@ struct A2bPoint {
   }
 };
 
+// Cube-corner extrapolation points of a2b_edge (FV3 a2b_ord4 corner treatment): for
+// corner c = 0 (0,0), 1 (N,0), 2 (N,N), 3 (0,N) and face r, the pair of cells
+// (i1, j1, i2, j2), each coordinate A * N + B (tile-global).
+__constant__ int kCornerA[4][3][4] = {{{0, 0, 0, 0}, {0, 0, 0, 0}, {0, 0, 0, 0}},
+                                      {{1, 0, 1, 0}, {1, 0, 1, 0}, {1, 0, 1, 0}},
+                                      {{1, 1, 1, 1}, {1, 1, 1, 1}, {1, 1, 1, 1}},
+                                      {{0, 1, 0, 1}, {0, 1, 0, 1}, {0, 1, 0, 1}}};
+__constant__ int kCornerB[4][3][4] = {{{0, 0, 1, 1}, {-1, 0, -2, 1}, {0, -1, 1, -2}},
+                                      {{-1, 0, -2, 1}, {-1, -1, -2, -2}, {0, 0, 1, 1}},
+                                      {{-1, -1, -2, -2}, {0, -1, 1, -2}, {-1, 0, -2, 1}},
+                                      {{0, -1, 1, -2}, {-1, -1, -2, -2}, {0, 0, 1, 1}}};
+
+// The tile-edge / cube-corner forms of a2b_ord4 as force-inlined members (no lambdas
+// and no references to kernel arguments: either left a stack object in scratch memory,
+// and scratch-using kernels launched from several host threads on concurrent streams
+// faulted in the multi-rank loopback runs).
+struct A2bEdge {
+  A2bPoint P;
+  const double* q;   // plane of the level
+  const double* cw;  // corner weights of the sub-domain [4][3]
+  int N, io, jo;
+  __device__ __forceinline__ double gqx(int Ig, int Jg) const { return P.qx(Ig - io, Jg - jo); }
+  __device__ __forceinline__ double gqy(int Ig, int Jg) const { return P.qy(Ig - io, Jg - jo); }
+  __device__ __forceinline__ double colv(int Ig, int Jg) const {  // W/E edge generic
+    return AA2 * (gqx(Ig, Jg - 2) + gqx(Ig, Jg + 1)) + AA1 * (gqx(Ig, Jg - 1) + gqx(Ig, Jg));
+  }
+  __device__ __forceinline__ double rowv(int Ig, int Jg) const {
+    return AA2 * (gqy(Ig - 2, Jg) + gqy(Ig + 1, Jg)) + AA1 * (gqy(Ig - 1, Jg) + gqy(Ig, Jg));
+  }
+  // cube corner value (extrapolation from the three faces), points from constant memory
+  __device__ __forceinline__ double corner_val(int c) const {
+    double acc = 0.0;
+#pragma unroll
+    for (int r = 0; r < 3; ++r) {
+      const double q1 = q[pidx(P.d, kCornerA[c][r][0] * N + kCornerB[c][r][0] - io,
+                               kCornerA[c][r][1] * N + kCornerB[c][r][1] - jo)];
+      const double q2 = q[pidx(P.d, kCornerA[c][r][2] * N + kCornerB[c][r][2] - io,
+                               kCornerA[c][r][3] * N + kCornerB[c][r][3] - jo)];
+      const double e = q1 + cw[c * 3 + r] * (q1 - q2);
+      acc = r == 0 ? e : acc + e;
+    }
+    return acc * R3;
+  }
+  // value of qout at a tile-edge point (recursion-free)
+  __device__ __forceinline__ double edge_or_corner(int Ig, int Jg) const {
+    if (Ig == 0 && Jg == 0) return corner_val(0);
+    if (Ig == N && Jg == 0) return corner_val(1);
+    if (Ig == N && Jg == N) return corner_val(2);
+    if (Ig == 0 && Jg == N) return corner_val(3);
+    if (Ig == 0 || Ig == N) return colv(Ig, Jg);
+    return rowv(Ig, Jg);
+  }
+};
+
 // qout on cube corners and tile-edge lines
 __global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restrict__ subs,
                                                   const double* __restrict__ M, int nk, const double* __restrict__ cw,
@@ -353,52 +409,23 @@ __global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restr
   const long zo = (long)z * d.plane;
   const long o = pidx(d, i, j);
   const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
-  // cube corner value (extrapolation from the three faces)
-  auto corner_val = [&](int c) {
-    const int pr[4][3][4] = {{{0, 0, 1, 1}, {-1, 0, -2, 1}, {0, -1, 1, -2}},
-                             {{N - 1, 0, N - 2, 1}, {N - 1, -1, N - 2, -2}, {N, 0, N + 1, 1}},
-                             {{N - 1, N - 1, N - 2, N - 2}, {N, N - 1, N + 1, N - 2}, {N - 1, N, N - 2, N + 1}},
-                             {{0, N - 1, 1, N - 2}, {-1, N - 1, -2, N - 2}, {0, N, 1, N + 1}}};
-    double acc = 0.0;
-    for (int r = 0; r < 3; ++r) {
-      double q1 = q[zo + pidx(d, pr[c][r][0] - io, pr[c][r][1] - jo)];
-      double q2 = q[zo + pidx(d, pr[c][r][2] - io, pr[c][r][3] - jo)];
-      double e = q1 + cw[(long)s * 12 + c * 3 + r] * (q1 - q2);
-      acc = r == 0 ? e : acc + e;
-    }
-    return acc * R3;
-  };
-  const A2bPoint P{d, sub, q + zo, met(M, d, M_DXA, s), met(M, d, M_DYA, s)};
-  auto gqx = [&](int Ig, int Jg) { return P.qx(Ig - io, Jg - jo); };
-  auto gqy = [&](int Ig, int Jg) { return P.qy(Ig - io, Jg - jo); };
-  auto colv = [&](int Ig, int Jg) {  // W/E edge generic
-    return AA2 * (gqx(Ig, Jg - 2) + gqx(Ig, Jg + 1)) + AA1 * (gqx(Ig, Jg - 1) + gqx(Ig, Jg));
-  };
-  auto rowv = [&](int Ig, int Jg) {
-    return AA2 * (gqy(Ig - 2, Jg) + gqy(Ig + 1, Jg)) + AA1 * (gqy(Ig - 1, Jg) + gqy(Ig, Jg));
-  };
-  auto edge_or_corner = [&](int Ig, int Jg) -> double {  // value of qout at a tile-edge point (recursive-free)
-    if (Ig == 0 && Jg == 0) return corner_val(0);
-    if (Ig == N && Jg == 0) return corner_val(1);
-    if (Ig == N && Jg == N) return corner_val(2);
-    if (Ig == 0 && Jg == N) return corner_val(3);
-    if (Ig == 0 || Ig == N) return colv(Ig, Jg);
-    return rowv(Ig, Jg);
-  };
+  (void)cw;
   double val;
   bool set = true;
-  if ((I == 0 || I == N) && (J == 0 || J == N)) val = edge_or_corner(I, J);
+  const A2bEdge E{A2bPoint{d, sub, q + zo, met(M, d, M_DXA, s), met(M, d, M_DYA, s)}, q + zo, cw + (long)s * 12, N, io,
+                  jo};
+  if ((I == 0 || I == N) && (J == 0 || J == N)) val = E.edge_or_corner(I, J);
   else if ((I == 0 && io == 0) || (I == N && io + nx == N)) {
-    if (J == 1 && jo == 0) val = AC1 * (gqx(I, 0) + gqx(I, 1)) + AC2 * (edge_or_corner(I, 0) + colv(I, 2));
+    if (J == 1 && jo == 0) val = AC1 * (E.gqx(I, 0) + E.gqx(I, 1)) + AC2 * (E.edge_or_corner(I, 0) + E.colv(I, 2));
     else if (J == N - 1 && jo + ny == N)
-      val = AC1 * (gqx(I, N - 2) + gqx(I, N - 1)) + AC2 * (colv(I, N - 2) + edge_or_corner(I, N));
-    else if (J >= max(2, jo) && J <= min(N - 2, jo + ny)) val = colv(I, J);
+      val = AC1 * (E.gqx(I, N - 2) + E.gqx(I, N - 1)) + AC2 * (E.colv(I, N - 2) + E.edge_or_corner(I, N));
+    else if (J >= max(2, jo) && J <= min(N - 2, jo + ny)) val = E.colv(I, J);
     else set = false;
   } else if ((J == 0 && jo == 0) || (J == N && jo + ny == N)) {
-    if (I == 1 && io == 0) val = AC1 * (gqy(0, J) + gqy(1, J)) + AC2 * (edge_or_corner(0, J) + rowv(2, J));
+    if (I == 1 && io == 0) val = AC1 * (E.gqy(0, J) + E.gqy(1, J)) + AC2 * (E.edge_or_corner(0, J) + E.rowv(2, J));
     else if (I == N - 1 && io + nx == N)
-      val = AC1 * (gqy(N - 2, J) + gqy(N - 1, J)) + AC2 * (rowv(N - 2, J) + edge_or_corner(N, J));
-    else if (I >= max(2, io) && I <= min(N - 2, io + nx)) val = rowv(I, J);
+      val = AC1 * (E.gqy(N - 2, J) + E.gqy(N - 1, J)) + AC2 * (E.rowv(N - 2, J) + E.edge_or_corner(N, J));
+    else if (I >= max(2, io) && I <= min(N - 2, io + nx)) val = E.rowv(I, J);
     else set = false;
   } else {
     set = false;
@@ -482,8 +509,12 @@ __device__ void a2b_march_strip(const A2bM& a, int z, int a0, int a1, int j0, in
     if (xs) x_ = qo[oj + dxs];
     const int J = j + jo;
     y_ = 0.0;
-    if (J == 1) y_ = qo[oj - pitch];
-    else if (J == N - 1) y_ = qo[oj + pitch];
+    // only rows that produce output: a prefetch row below j0 with J == 1 would read
+    // the row before the plane (before the allocation for the first plane)
+    if (j >= j0 && j < j1) {
+      if (J == 1) y_ = qo[oj - pitch];
+      else if (J == N - 1) y_ = qo[oj + pitch];
+    }
   };
 #pragma unroll
   for (int u = 0; u < AM_B; ++u) fetch(j0 - NG + u, qb[u], db[u], xb[u], yb[u]);

@@ -70,7 +70,7 @@ __device__ __forceinline__ long cc_off(const Dims& d, const SubInfo& s, int i, i
 __host__ __device__ inline int edge_line_count(int ilo, int ihi, int jlo, int jhi) {
   return 4 * (jhi - jlo + 1) + 4 * (ihi - ilo + 1);
 }
-__device__ inline bool edge_line_point(int t, const SubInfo& sub, int ilo, int ihi, int jlo, int jhi, int& i,
+__device__ __forceinline__ bool edge_line_point(int t, const SubInfo& sub, int ilo, int ihi, int jlo, int jhi, int& i,
                                        int& j) {
   const int N = sub.N, nj = jhi - jlo + 1, ni = ihi - ilo + 1;
   auto line = [&](int l) { return l == 0 ? -1 : (l == 1 ? 0 : (l == 2 ? N - 1 : N)); };

@@ -493,25 +493,32 @@ __global__ void __launch_bounds__(256) ds_ke(Dims d, const SubInfo* __restrict__
   if (inner) ub = dt5 * (AT(uc, 0, -1) + AT(uc, 0, 0) - (AT(vc, -1, 0) + AT(vc, 0, 0)) * cosa) * rsina;
   if (J == 0 || J == N) ub = dt4 * (-AT(ut, 0, -2) + 3.0 * (AT(ut, 0, -1) + AT(ut, 0, 0)) - AT(ut, 0, 1));
   else if ((I == 0 || I == N) && J >= Jlo && J <= Jhi) ub = dt5 * (AT(ut, 0, -1) + AT(ut, 0, 0));
-  // ytp_v: flux of v through corner (i,j) along j
+  // ytp_v: flux of v through corner (i,j) along j.  Away from the tile edges (interfaces
+  // g-1..g+1 off the edge forms) the interior PPM applies and the metric stencil is not
+  // read: the edge form (six metric loads, divided-difference al) runs only near edges.
   double qv[6], sp[6];
   const double* dy = MT(M_DY);
   const double* dxm = MT(M_DX);
+  auto flux = [&](int g, double c) {
+    const bool edge = !(g - 1 >= 2 && g + 1 <= N - 2);
+    if (edge) return ppm_flux_ord(hord_mt, g, N, qv, sp, c);
+    return hord_mt == 5 ? ppm_flux<5, false>(g, N, qv, sp, c) : ppm_flux<6, false>(g, N, qv, sp, c);
+  };
 #pragma unroll
   for (int m = 0; m < 6; ++m) {
     qv[m] = AT(v, 0, m - 3);
-    sp[m] = MA(dy, 0, m - 3);
+    sp[m] = (J - 1 >= 2 && J + 1 <= N - 2) ? 0.0 : MA(dy, 0, m - 3);
   }
   double cfl = vb > 0.0 ? vb * MA(MT(M_RDY), 0, -1) : vb * MA(MT(M_RDY), 0, 0);
-  double ubf = ppm_flux_ord(hord_mt, J, N, qv, sp, cfl);
+  double ubf = flux(J, cfl);
   double kk = vb * ubf;
 #pragma unroll
   for (int m = 0; m < 6; ++m) {
     qv[m] = AT(u, m - 3, 0);
-    sp[m] = MA(dxm, m - 3, 0);
+    sp[m] = (I - 1 >= 2 && I + 1 <= N - 2) ? 0.0 : MA(dxm, m - 3, 0);
   }
   cfl = ub > 0.0 ? ub * MA(MT(M_RDX), -1, 0) : ub * MA(MT(M_RDX), 0, 0);
-  double vbf = ppm_flux_ord(hord_mt, I, N, qv, sp, cfl);
+  double vbf = flux(I, cfl);
   kk = 0.5 * (kk + ub * vbf);
   const double dt6 = dt / 6.0;
   if (I == 0 && J == 0)

@@ -5,6 +5,8 @@ import numpy as np
 import os
 import re
 
+import pytest
+
 from conftest import ROOT
 
 
@@ -61,3 +63,36 @@ def test_layout_rule_matches_reference():
     assert view.shape == tuple(dim) and view.flags.f_contiguous
     assert view[1, 0, 0] == 1.0 and view[0, 1, 0] == dim[0] and view[0, 0, 1] == dim[0] * dim[1]
     np.testing.assert_array_equal(view.flatten(order="F"), flat)
+
+
+def test_no_kernel_uses_scratch(pkg, tmp_path):
+    """Every gfx950 kernel of the library runs without private (scratch) memory: the
+    multi-rank loopback runs (several host threads launching on concurrent streams)
+    faulted in a kernel that had a stack object in scratch, and scratch traffic is
+    slow anyway.  Reads .private_segment_fixed_size from the code-object metadata."""
+    import shutil
+    import subprocess
+    llvm = "/opt/rocm/lib/llvm/bin"
+    if not os.path.exists(os.path.join(llvm, "llvm-readelf")):
+        pytest.skip("ROCm LLVM tools not installed")
+    lib = tmp_path / "lib.so"
+    shutil.copy(pkg.LIB_PATH, lib)
+    subprocess.run([os.path.join(llvm, "llvm-objdump"), "--offloading", str(lib)], check=True, cwd=tmp_path,
+                   capture_output=True)
+    objs = [p for p in tmp_path.iterdir() if "amdgcn" in p.name and "gfx950" in p.name]
+    assert objs, "no gfx950 code object in the library"
+    bad, nkern = [], 0
+    for obj in objs:
+        notes = subprocess.run([os.path.join(llvm, "llvm-readelf"), "--notes", str(obj)], check=True,
+                               capture_output=True, text=True).stdout
+        name = None
+        for line in notes.splitlines():
+            line = line.strip()
+            if line.startswith(".name:"):
+                name = line.split(":", 1)[1].strip()
+            elif line.startswith(".private_segment_fixed_size:"):
+                nkern += 1
+                if int(line.split(":")[1]) != 0:
+                    bad.append(name)
+    assert nkern > 20
+    assert not bad, f"kernels using scratch memory: {bad}"
