@@ -21,7 +21,7 @@ def load(d, counter):
         for r in csv.DictReader(open(f)):
             if r["Counter_Name"] != counter:
                 continue
-            m = re.search(r"::(\w+)\(", r["Kernel_Name"])
+            m = re.search(r"::(\w+(?:<[^>]*>)?)\(", r["Kernel_Name"])
             out[m.group(1) if m else r["Kernel_Name"]].append(float(r["Counter_Value"]))
     return out
 
