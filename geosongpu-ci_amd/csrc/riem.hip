@@ -24,9 +24,11 @@ constexpr double KAPPA = Constants::kappa;
 constexpr double R3 = 1.0 / 3.0;
 constexpr int BLOCK = 256;
 
+int g_riem_variant = 0;
+
 struct RiemArgs {
   Dims d;
-  int npz, ring, last_call, cgrid;
+  int npz, ring, last_call, cgrid, dump;
   double dt, ptop, p_fac, dz_min;
   const double *delp, *pt, *w_in, *phis;
   double* G;       // zh (heights, D-grid) or gz (heights in -> geopotential out, C-grid); L+1
@@ -285,19 +287,505 @@ __global__ void __launch_bounds__(BLOCK) riem_col_k(RiemArgs a) {
               at(a.delz, bk));
 }
 
+// ---------------- register-resident form (default) ----------------
+//
+// One wavefront owns 16 columns; its 64 lanes are 4 level blocks x 16 columns
+// (lane = 16 b + column), block b holding layers [b M, b M + M) and interfaces
+// b M .. b M + M of its column in registers (M = 18 at L72).  Every input is read from
+// HBM once (PT, W1 a second time, from cache) and every output written once: the
+// sweeps of the column form above never touch memory.
+//
+//   * pointwise work (the transcendentals of pm, pl, pk3, dz2; aa, the numerators) runs
+//     on all 64 lanes at once;
+//   * each recurrence (pem and pe prefixes, both Thomas eliminations and back
+//     substitutions, the p1 recurrence, the height sums) runs block after block with its
+//     carry handed to the next block by a lane shuffle (lane +- 16), so every value is
+//     formed by the same operations in the same order as in riem_column: the results
+//     are bit-identical to the column form (tests/test_gpu_riem.py compares them);
+//   * the dz_min clamp (bottom-up max recurrence) runs on all blocks at once from the
+//     unclamped interface below each block, then repeats only if a block's lower
+//     neighbour changed that interface (exact; the clamp is rarely active).
+// Two per-layer arrays that live from the first sweep to the last (pm, g_rat) are
+// kept in LDS, the rest in VGPRs.
+constexpr int RB_NB = 4, RB_NC = 16, RB_WAVES = 4;
+typedef unsigned int RbU2 __attribute__((ext_vector_type(2)));
+// The pointwise loops are long straight-line runs of independent transcendentals; left
+// alone the scheduler interleaves all M of them and runs out of registers.  A fence per
+// level keeps one or two in flight (two waves per SIMD hide the latency instead).
+#define RB_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
+// Values parked in HBM and read back later by the same lane: the stores must have
+// completed before the loads are issued (a vector-memory load does not wait for an
+// earlier store of the same wave), and neither side may be moved across by the compiler.
+#define RB_PARK_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
+
+__device__ __forceinline__ double from_below(double v, int lane) { return __shfl(v, (lane + RB_NC) & 63); }
+__device__ __forceinline__ double from_above(double v, int lane) { return __shfl(v, (lane - RB_NC) & 63); }
+
+template <int M, bool CG>
+__global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
+  __shared__ double lds_pm[RB_WAVES][M][64];
+  __shared__ double lds_g[RB_WAVES][M][64];
+  constexpr bool cg = CG;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = lane / RB_NC;
+  const Dims& d = a.d;
+  const int km = a.npz;
+  const int nblk = km / M;  // launch_riem guarantees km = nblk * M, nblk <= 4
+  const int ni = d.nx + 2 * a.ring, nj = d.ny + 2 * a.ring;
+  const int ncol = ni * nj;
+  const int s = blockIdx.y;
+  const int c0 = (blockIdx.x * RB_WAVES + wv) * RB_NC;
+  if (c0 >= ncol) return;  // whole wavefront; no workgroup barrier in this kernel
+  int c = c0 + (lane & (RB_NC - 1));
+  const bool act = b < nblk;                // lanes of blocks past the column idle
+  const bool valid = c < ncol && act;       // writes
+  if (c >= ncol) c = ncol - 1;
+  const int i = c % ni - a.ring, j = c / ni - a.ring;
+  const long P = d.plane;
+  const long o = pidx(d, i, j);
+  const int kb0 = act ? b * M : 0;
+  const bool lastblk = b == nblk - 1;
+  double(&spm)[M][64] = lds_pm[wv];
+  double(&sg)[M][64] = lds_g[wv];
+  const double dt = a.dt;
+  const double gama = 1.0 / (1.0 - KAPPA);
+  const double t1g = gama * 2.0 * dt * dt;
+  const double rdt = 1.0 / dt;
+  const double capa1 = KAPPA - 1.0;
+
+  // Memory: one buffer descriptor per array and sub-domain (wave-uniform SGPRs), a 32-bit
+  // per-lane byte offset (the block's first level) and the level as the scalar offset.
+  const uint32_t PB = (uint32_t)P * 8u;
+  const uint32_t lo = (uint32_t)((o + (long)kb0 * P) * 8);
+  const int li = (km + 1) * (int)PB, ll = km * (int)PB;  // bytes of a sub-domain's field
+  auto rs = [&](const double* p, bool itf) {
+    const long so = (long)s * (itf ? km + 1 : km) * P;
+    return __builtin_amdgcn_make_buffer_rsrc((void*)(p + so), 0, itf ? li : ll, 0x00020000);
+  };
+  auto ld = [&](__amdgpu_buffer_rsrc_t r, int m) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lo, (uint32_t)m * PB, 0));
+  };
+  auto st = [&](__amdgpu_buffer_rsrc_t r, int m, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), r, lo, (uint32_t)m * PB, 0);
+  };
+  const auto rG = rs(a.G, true), rPO = rs(a.pout, true);
+  const auto rDP = rs(a.delp, false), rPT = rs(a.pt, false), rW1 = rs(a.w_in, false);
+
+  // ---- loads
+  double gr[M + 1], DP[M];
+#pragma unroll
+  for (int m = 0; m <= M; ++m) gr[m] = ld(rG, m);
+#pragma unroll
+  for (int m = 0; m < M; ++m) DP[m] = ld(rDP, m);
+  // surface values (re-read where used instead of held in registers)
+  const uint32_t o8 = (uint32_t)o * 8u;
+  const auto rPH = __builtin_amdgcn_make_buffer_rsrc((void*)(a.phis + (long)s * P), 0, (int)PB, 0x00020000);
+  auto surf = [&](double& hs, double& zs, double& ws) {
+    hs = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rPH, o8, 0, 0));
+    zs = hs * (1.0 / GRAV);
+    const double gbot = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rG, o8, (uint32_t)km * PB, 0));
+    ws = (zs - gbot) * (1.0 / dt);
+  };
+  if (a.ws_out && valid && b == 0) {
+    double hs, zs, ws;
+    surf(hs, zs, ws);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, ws),
+        __builtin_amdgcn_make_buffer_rsrc((void*)(a.ws_out + (long)s * P), 0, (int)PB, 0x00020000), o8, 0, 0);
+  }
+
+  RB_SCHED_FENCE();
+  // ---- S0: dz_min clamp (bottom-up), speculative per block
+  double gl[M + 1];
+  {
+    double gin = gr[M];  // unclamped interface kb1
+    for (int it = 0; it <= RB_NB; ++it) {
+      gl[M] = gin;
+#pragma unroll
+      for (int m = M - 1; m >= 0; --m) gl[m] = fmax(gr[m], gl[m + 1] + a.dz_min);
+      const double gn = from_below(gl[0], lane);
+      const double want = lastblk || !act ? gin : gn;
+      if (!__any(want != gin)) break;
+      gin = want;
+    }
+  }
+  // park the clamped heights in G until S3 (own slots: same-lane ordering)
+  if (act) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) st(rG, m, gl[m]);
+  }
+  RB_PARK_DRAIN();
+
+  RB_SCHED_FENCE();
+  // ---- S1a: pem prefix (top-down, block after block)
+  double pem[M + 1];
+#pragma unroll
+  for (int m = 0; m <= M; ++m) pem[m] = 0.0;
+  {
+    double carry = a.ptop;
+#pragma unroll 1
+    for (int r = 0; r < nblk; ++r) {
+      if (b == r) {
+        pem[0] = carry;
+#pragma unroll
+        for (int m = 0; m < M; ++m) pem[m + 1] = pem[m] + DP[m];
+      }
+      carry = from_above(pem[M], lane);
+    }
+  }
+  // park pem in the output array until S3 / S6
+  if (act) {
+#pragma unroll
+    for (int m = 0; m < M; ++m) st(rPO, m, pem[m]);
+    if (lastblk) st(rPO, M, pem[M]);
+  }
+  RB_PARK_DRAIN();
+
+  RB_SCHED_FENCE();
+  // ---- S1b: pointwise layer quantities
+  double pl[M], dm[M];
+  {
+    double pln[M + 1];
+    if (!cg) {
+      const auto rK3 = rs(a.pk3, true);
+#pragma unroll
+      for (int m = 0; m <= M; ++m) {
+        pln[m] = log(pem[m]);  // slot 0 of block 0: log(ptop)
+        if (valid && (m < M || lastblk)) {
+          RB_SCHED_FENCE();
+          const double pkk = exp(KAPPA * pln[m]);
+          st(rK3, m, pkk);
+          if (a.last_call) {
+            st(rs(a.pe, true), m, pem[m]);
+            st(rs(a.peln, true), m, pln[m]);
+            st(rs(a.pk, true), m, pkk);
+          }
+        }
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      dm[m] = DP[m] * (1.0 / GRAV);
+      const double dz = gl[m + 1] - gl[m];
+      const double pm = cg ? DP[m] / log(pem[m + 1] / pem[m]) : DP[m] / (pln[m + 1] - pln[m]);
+      spm[m][lane] = pm;
+      pl[m] = exp(gama * log(-dm[m] / dz * RDGAS * ld(rPT, m))) - pm;
+      RB_SCHED_FENCE();
+    }
+  }
+  // g_rat and the right-hand side of the pp system
+  double dd[M], gprev;
+  {
+    const double dm_nb = from_below(dm[0], lane), pl_nb = from_below(pl[0], lane);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const bool bot = m == M - 1 && lastblk;
+      const double dmn = m + 1 < M ? dm[m + 1 < M ? m + 1 : 0] : dm_nb;
+      const double pln_ = m + 1 < M ? pl[m + 1 < M ? m + 1 : 0] : pl_nb;
+      const double g = bot ? 0.0 : dm[m] / dmn;
+      sg[m][lane] = g;
+      dd[m] = bot ? 3.0 * pl[m] : 3.0 * (pl[m] + g * pln_);
+    }
+    gprev = from_above(sg[M - 1][lane], lane);  // g_rat of layer kb0-1
+  }
+
+  RB_SCHED_FENCE();
+  // ---- S1c: forward elimination for pp (top-down, block after block)
+  double pp[M + 1], gam[M];
+#pragma unroll
+  for (int m = 0; m <= M; ++m) pp[m] = 0.0;
+#pragma unroll
+  for (int m = 0; m < M; ++m) gam[m] = 0.0;
+  {
+    double cbet = 0.0, cpp = 0.0;
+#pragma unroll 1
+    for (int r = 0; r < nblk; ++r) {
+      double bet_o = 0.0;
+      if (b == r) {
+        double bet = cbet, ppk = cpp;
+        pp[0] = cpp;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const bool bot = m == M - 1 && lastblk;
+          const double g = sg[m][lane];
+          const double bbk = bot ? 2.0 : 2.0 * (1.0 + g);
+          double ppn;
+          if (m == 0 && b == 0) {
+            bet = bbk;
+            ppn = dd[m] / bet;
+          } else {
+            const double gm = (m == 0 ? gprev : sg[m > 0 ? m - 1 : 0][lane]) / bet;
+            gam[m] = gm;
+            bet = bbk - gm;
+            ppn = (dd[m] - ppk) / bet;
+          }
+          pp[m + 1] = ppn;
+          ppk = ppn;
+        }
+        bet_o = bet;
+      }
+      cbet = from_above(bet_o, lane);
+      cpp = from_above(pp[M], lane);
+    }
+  }
+  RB_SCHED_FENCE();
+  // ---- S2: back substitution for pp (bottom-up)
+  {
+    double cx = 0.0;
+#pragma unroll 1
+    for (int r = nblk - 1; r >= 0; --r) {
+      if (b == r) {
+        if (!lastblk) pp[M] = cx;
+        double x = pp[M];
+#pragma unroll
+        for (int m = M - 1; m >= 0; --m) {
+          if (m > 0 || b > 0) {
+            x = pp[m] - gam[m] * x;
+            pp[m] = x;
+          }
+        }
+      }
+      cx = from_below(pp[0], lane);
+    }
+  }
+
+  RB_SCHED_FENCE();
+  // ---- S3: forward elimination for w (top-down)
+  double aat[M], num[M], aab_last;
+  {
+    double pemr[M + 1], glr[M + 1], dz[M];
+#pragma unroll
+    for (int m = 0; m <= M; ++m) {
+      pemr[m] = ld(rPO, m);
+      glr[m] = ld(rG, m);  // parked clamped heights; interface km is never clamped
+    }
+    {  // interface kb1 belongs to the block below (shuffle outside any divergent branch)
+      const double pb = from_below(pemr[0], lane), gb = from_below(glr[0], lane);
+      if (!lastblk) {
+        pemr[M] = pb;
+        glr[M] = gb;
+      }
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      dz[m] = glr[m + 1] - glr[m];
+      dm[m] = ld(rDP, m) * (1.0 / GRAV);
+    }
+    const double dz_ab = from_above(dz[M - 1], lane);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const double dzu = m == 0 ? dz_ab : dz[m > 0 ? m - 1 : 0];
+      aat[m] = t1g / (dzu + dz[m]) * (pemr[m] + pp[m]);  // aa at interface kb0+m (unused at 0)
+      num[m] = dm[m] * ld(rW1, m) + dt * (pp[m + 1] - pp[m]);
+    }
+    // aa below the block's last layer: the next block's first aa, or p1 for the bottom
+    const double aab_nb = from_below(aat[0], lane);
+    double hs, zs, ws;
+    surf(hs, zs, ws);
+    const double p1 = t1g / dz[M - 1] * (pemr[M] + pp[M]);
+    if (lastblk) num[M - 1] = num[M - 1] - p1 * ws;
+    aab_last = lastblk ? p1 : aab_nb;
+  }
+  double w2[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) w2[m] = 0.0;
+  {
+    double cbet = 0.0, cw = 0.0;
+#pragma unroll 1
+    for (int r = 0; r < nblk; ++r) {
+      double bet_o = 0.0, w_o = 0.0;
+      if (b == r) {
+        double bet = cbet, wp = cw;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const double aab = m + 1 < M ? aat[m + 1 < M ? m + 1 : 0] : aab_last;
+          if (m == 0 && b == 0) {
+            bet = dm[m] - aab;
+            wp = num[m] / bet;
+          } else {
+            const double gm = aat[m] / bet;
+            gam[m] = gm;
+            bet = dm[m] - (aat[m] + aab + aat[m] * gm);
+            wp = (num[m] - aat[m] * wp) / bet;
+          }
+          w2[m] = wp;
+        }
+        bet_o = bet;
+        w_o = wp;
+      }
+      cbet = from_above(bet_o, lane);
+      cw = from_above(w_o, lane);
+    }
+  }
+  RB_SCHED_FENCE();
+  // ---- S4: back substitution for w (bottom-up)
+  {
+    const double gam_nb = from_below(gam[0], lane);
+    double cx = 0.0;
+#pragma unroll 1
+    for (int r = nblk - 1; r >= 0; --r) {
+      if (b == r) {
+        double x = cx;
+#pragma unroll
+        for (int m = M - 1; m >= 0; --m) {
+          if (m == M - 1 && lastblk) {
+            x = w2[m];
+          } else {
+            x = w2[m] - (m + 1 < M ? gam[m + 1 < M ? m + 1 : 0] : gam_nb) * x;
+            w2[m] = x;
+          }
+        }
+      }
+      cx = from_below(w2[0], lane);
+    }
+  }
+
+  RB_SCHED_FENCE();
+  // ---- S5: pe prefix (top-down); w out
+#pragma unroll
+  for (int m = 0; m < M; ++m) num[m] = ld(rDP, m) * (1.0 / GRAV) * (w2[m] - ld(rW1, m)) * rdt;
+  if (a.w_out && valid) {
+    const auto rW = rs(a.w_out, false);
+#pragma unroll
+    for (int m = 0; m < M; ++m) st(rW, m, w2[m]);
+  }
+  if (a.dump && valid) {  // debug: w2 and the final pp into the column kernel's scratch planes
+    const auto rw = rs(a.w2, true), rg = rs(a.gam, true);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      st(rw, m, w2[m]);
+      st(rg, m, gam[m]);
+    }
+  }
+  auto& pe = pp;  // pe replaces pp
+  {
+    double carry = 0.0;
+#pragma unroll 1
+    for (int r = 0; r < nblk; ++r) {
+      if (b == r) {
+        pe[0] = carry;
+#pragma unroll
+        for (int m = 0; m < M; ++m) pe[m + 1] = pe[m] + num[m];
+      }
+      carry = from_above(pe[M], lane);
+    }
+  }
+
+  if (a.dump && valid) {
+    const auto rp = rs(a.pp, true);
+#pragma unroll
+    for (int m = 0; m < M; ++m) st(rp, m, pe[m]);
+  }
+  RB_SCHED_FENCE();
+  // ---- S6: p1 recurrence, dz2, heights (bottom-up)
+  {
+    const double pe2_nb = from_below(pe[1], lane);  // pe at interface kb1+1
+    double t[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const double g = sg[m][lane];
+      const double pe2 = m + 2 <= M ? pe[m + 2 <= M ? m + 2 : 0] : pe2_nb;
+      if (m == M - 1 && lastblk) t[m] = (pe[m] + 2.0 * pe[m + 1]) * R3;
+      else t[m] = (pe[m] + 2.0 * (1.0 + g) * pe[m + 1] + g * pe2) * R3;
+    }
+    double cp = 0.0;
+#pragma unroll 1
+    for (int r = nblk - 1; r >= 0; --r) {
+      if (b == r) {
+        double p1 = cp;
+#pragma unroll
+        for (int m = M - 1; m >= 0; --m) {
+          if (m == M - 1 && lastblk) p1 = t[m];
+          else p1 = t[m] - sg[m][lane] * p1;
+          t[m] = p1;
+        }
+      }
+      cp = from_below(t[0], lane);
+    }
+    // dz2 (pointwise), then the height sums
+    double dz2[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const double pmk = spm[m][lane];
+      dz2[m] = -(ld(rDP, m) * (1.0 / GRAV)) * RDGAS * ld(rPT, m) *
+               exp(capa1 * log(fmax(a.p_fac * pmk, t[m] + pmk)));
+      RB_SCHED_FENCE();
+    }
+    double gz[M + 1];
+#pragma unroll
+    for (int m = 0; m <= M; ++m) gz[m] = 0.0;
+    double hs, zs, ws;
+    surf(hs, zs, ws);
+    double cg_in = cg ? hs : zs;
+#pragma unroll 1
+    for (int r = nblk - 1; r >= 0; --r) {
+      if (b == r) {
+        double go = cg_in;
+        gz[M] = go;
+#pragma unroll
+        for (int m = M - 1; m >= 0; --m) {
+          go = cg ? go - dz2[m] * GRAV : go - dz2[m];
+          gz[m] = go;
+        }
+      }
+      cg_in = from_below(gz[0], lane);
+    }
+    if (valid) {
+      double pemr[M + 1];
+#pragma unroll
+      for (int m = 0; m <= M; ++m) pemr[m] = cg ? ld(rPO, m) : 0.0;
+      const auto rDZ = rs(a.delz, false);
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        st(rG, m, gz[m]);
+        if (cg) {
+          st(rPO, m, m == 0 && b == 0 ? a.ptop : pe[m] + pemr[m]);
+        } else {
+          st(rDZ, m, dz2[m]);
+          st(rPO, m, pe[m]);
+        }
+      }
+      if (lastblk) {
+        st(rG, M, cg ? hs : zs);
+        st(rPO, M, cg ? pe[M] + pemr[M] : pe[M]);
+      }
+    }
+  }
+}
+
+
 void launch_riem(const Ctx& c, const RiemArgs& a) {
   if (a.npz < 2) throw std::runtime_error("riem: npz >= 2 required");
+  const int km = a.npz;
   const int ncol = (c.d.nx + 2 * a.ring) * (c.d.ny + 2 * a.ring);
-  GT_LAUNCH(riem_col_k, dim3(cdiv(ncol, BLOCK), c.d.nsub), dim3(BLOCK), 0, c.st, a);
+  const dim3 gb(cdiv(cdiv(ncol, RB_NC), RB_WAVES), c.d.nsub);
+  const dim3 tb(64 * RB_WAVES);
+  // blocked form when the column splits into at most four blocks of an instantiated size
+  auto fits = [&](int m) { return km % m == 0 && km / m <= RB_NB; };
+  const bool blk = riem_variant() != 1;
+  if (blk && fits(3)) {
+    if (a.cgrid) GT_LAUNCH((riem_blk_k<3, true>), gb, tb, 0, c.st, a);
+    else GT_LAUNCH((riem_blk_k<3, false>), gb, tb, 0, c.st, a);
+  } else if (blk && fits(5)) {
+    if (a.cgrid) GT_LAUNCH((riem_blk_k<5, true>), gb, tb, 0, c.st, a);
+    else GT_LAUNCH((riem_blk_k<5, false>), gb, tb, 0, c.st, a);
+  } else if (blk && fits(18)) {
+    if (a.cgrid) GT_LAUNCH((riem_blk_k<18, true>), gb, tb, 0, c.st, a);
+    else GT_LAUNCH((riem_blk_k<18, false>), gb, tb, 0, c.st, a);
+  } else {
+    GT_LAUNCH(riem_col_k, dim3(cdiv(ncol, BLOCK), c.d.nsub), dim3(BLOCK), 0, c.st, a);
+  }
   HIP_LAUNCH_CHECK();
   // algorithmic bytes per column: C grid reads delpc ptc wc (L) gz (L+1) phis, writes gz pef (L+1);
   // D grid reads zh (L+1) delp pt w (L) phis, writes w delz (L) zh ppe pk3 (L+1) ws (+ pe peln pk)
-  const double km = a.npz, k1 = a.npz + 1;
-  const double per = a.cgrid ? 3 * km + 3 * k1 + 1 : 5 * km + (4 + (a.last_call ? 3 : 0)) * k1 + 2;
+  const double L = km, L1 = km + 1;
+  const double per = a.cgrid ? 3 * L + 3 * L1 + 1 : 5 * L + (4 + (a.last_call ? 3 : 0)) * L1 + 2;
   ktimer_bytes(8.0 * ncol * c.d.nsub * per);
 }
 
 }  // namespace
+
+void set_riem_variant(int v) { g_riem_variant = v; }
+int riem_variant() { return g_riem_variant; }
 
 void riem_solver_c(const Ctx& c, int npz, double dt2, double ptop, double p_fac, double dz_min, const double* delpc,
                    const double* ptc, const double* wc, const double* phis, double* gz, double* pef,
@@ -320,6 +808,7 @@ void riem_solver_c(const Ctx& c, int npz, double dt2, double ptop, double p_fac,
   a.gam = sc.s[5];
   a.pp = sc.s[6];
   a.w2 = sc.s[13];
+  a.dump = riem_variant() == 2;
   launch_riem(c, a);
 }
 

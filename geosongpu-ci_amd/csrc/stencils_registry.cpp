@@ -90,6 +90,47 @@ std::map<std::string, Fn>& reg() {
          a.tp_fx2 = scr("_tp1_fx2"); a.tp_fy2 = scr("_tp1_fy2"); a.tp_qi = scr("_tp1_qi"); a.tp_qj = scr("_tp1_qj");
          d_sw(dy.ctx(), a);
        }},
+      // riem_solver_c(delpc, ptc, wc, phis, gz | pef): gz heights in (clamped to dz_min),
+      // geopotential out.  params: dt2, ptop, p_fac, dz_min[, variant (0 blocked, 1 column)]
+      {"riem_solver_c",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 6, "riem_solver_c");
+         const int npz = F(dy, f[0]).nk;
+         if (F(dy, f[4]).nk != npz + 1 || F(dy, f[3]).nk != 1) throw std::runtime_error("riem_solver_c: field shapes");
+         NhScratch sc{};
+         sc.s[5] = dy.field("_riem_gam", npz + 1).p;
+         sc.s[6] = dy.field("_riem_pp", npz + 1).p;
+         sc.s[13] = dy.field("_riem_w2", npz + 1).p;
+         const int v0 = riem_variant();
+         set_riem_variant(p.size() > 4 ? (int)p[4] : v0);
+         riem_solver_c(dy.ctx(), npz, p.at(0), p.at(1), p.at(2), p.at(3), F(dy, f[0]).p, F(dy, f[1]).p,
+                       F(dy, f[2]).p, F(dy, f[3]).p, F(dy, f[4]).p, dy.field(f[5], npz + 1).p, sc);
+         set_riem_variant(v0);
+       }},
+      // riem_solver3(delp, pt, w, phis, zh | delz, ppe, pk3, pe, peln, pk, ws): w and zh in place.
+      // params: dt, ptop, p_fac, dz_min, last_call[, variant]
+      {"riem_solver3",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 12, "riem_solver3");
+         const int npz = F(dy, f[0]).nk;
+         if (F(dy, f[4]).nk != npz + 1 || F(dy, f[3]).nk != 1) throw std::runtime_error("riem_solver3: field shapes");
+         NhScratch sc{};
+         sc.s[5] = dy.field("_riem_gam", npz + 1).p;
+         sc.s[6] = dy.field("_riem_pp", npz + 1).p;
+         sc.s[13] = dy.field("_riem_w2", npz + 1).p;
+         Riem3Args r{};
+         r.npz = npz;
+         r.dt = p.at(0); r.ptop = p.at(1); r.p_fac = p.at(2); r.dz_min = p.at(3); r.last_call = (int)p.at(4);
+         r.delp = F(dy, f[0]).p; r.pt = F(dy, f[1]).p; r.w = F(dy, f[2]).p; r.phis = F(dy, f[3]).p;
+         r.zh = F(dy, f[4]).p;
+         r.delz = dy.field(f[5], npz).p; r.ppe = dy.field(f[6], npz + 1).p; r.pk3 = dy.field(f[7], npz + 1).p;
+         r.pe = dy.field(f[8], npz + 1).p; r.peln = dy.field(f[9], npz + 1).p; r.pk = dy.field(f[10], npz + 1).p;
+         r.ws = dy.field(f[11], 1).p;
+         const int v0 = riem_variant();
+         set_riem_variant(p.size() > 5 ? (int)p[5] : v0);
+         riem_solver3(dy.ctx(), r, sc);
+         set_riem_variant(v0);
+       }},
       // K-column primitives (dsl_patterns KATs): column_top(in | out)
       {"column_top",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
