@@ -7,6 +7,9 @@
 //   fx = 0.5*(xppm(q_i) + fx2)*mfx     fy = 0.5*(yppm(q_j) + fy2)*mfy
 // Operation order inside each expression follows the Fortran so the fp64
 // numpy oracle (oracle/fv3.py) matches to the last bits.
+#include <cstdlib>
+#include <type_traits>
+
 #include "kernels.hpp"
 #include "stencil_common.hpp"
 
@@ -206,6 +209,7 @@ __global__ void __launch_bounds__(TX * TW) tp_fused(TpK a) {
 // region is that of the tile kernel above (bit-identical results); q, the Courant
 // numbers, the fluxes and the area terms stream through HBM once per strip and segment.
 constexpr int MW = 64, MOUT = MW - 6, MWAVES = 4;
+typedef unsigned int TpU2 __attribute__((ext_vector_type(2)));
 
 struct TpM {
   Dims d;
@@ -288,7 +292,7 @@ __device__ __forceinline__ double ppm_x_dpp(double q, double dx, int g, int N, d
 struct MarchIn {
   double qx, qy, crx, xfx, area_r, rax, dxr;  // row r
   double cry, yfx, my;                        // edge r-2
-  double area_m, ray, mx, dxm;                // row r-3
+  double ray, mx, dxm;                        // row r-3
 };
 
 // y-direction PPM state rolled along the march: al at the last interface computed and
@@ -318,6 +322,23 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   const bool cin = x >= -NG && x < nx + NG;              // q exists (cell halo)
   const bool out_lane = lane >= NG && lane < NG + MOUT;  // owns an output edge / column
   const long xo = xc + NG;
+  // Buffer descriptors (wave-uniform) for every plane the march reads or writes; a lane
+  // addresses column xo of row r with the constant voffset vx and the row offset as the
+  // scalar offset, so the loads of a row step cost no vector address arithmetic.
+  const int PBy = (int)(d.plane * 8);
+  auto rsrc = [&](const double* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, PBy, 0x00020000); };
+  const auto rQ = rsrc(qq), rCRX = rsrc(a.crx + fo), rCRY = rsrc(a.cry + fo), rXFX = rsrc(a.xfx + fo);
+  const auto rYFX = rsrc(a.yfx + fo), rRAX = rsrc(a.ra_x + fo), rRAY = rsrc(a.ra_y + fo);
+  const auto rMX = rsrc(a.mx + fo), rMY = rsrc(a.my + fo), rAR = rsrc(area), rDXA = rsrc(dxa);
+  const uint32_t vx = (uint32_t)xo * 8u;
+  // dxa only enters the tile-edge interface values (ppm_al at g = 0, N reads the four
+  // cells g-2 .. g+1): the other lanes read one shared word instead of their own column
+  const bool dx_lane = (I >= -2 && I <= 1) || (I >= N - 2 && I <= N + 1);
+  const uint32_t vxd = dx_lane ? vx : 0u;
+  const uint32_t rowb = (uint32_t)pitch * 8u;
+  auto bl = [&](__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
+  };
 
   // Every load below is issued unconditionally (addresses clamped into the plane,
   // values masked afterwards): with a fixed count of loads per step the compiler's
@@ -325,33 +346,36 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   auto load = [&](int r) {
     MarchIn v;
     const int rr = r < ny + NG ? r : ny + NG;  // last plane row
-    const long o = (long)(rr + NG) * pitch + xo;
+    const uint32_t so = (uint32_t)(rr + NG) * rowb;
     const int J = r + sub.joff;
     const bool qin = cin && r >= -NG && r < ny + NG;
-    long ox = o, oy = o;
-    if (qin && (J < 0 || J >= N) && (I < 0 || I >= N)) {
-      ox = cc_off(d, sub, x, r, 1);
-      oy = cc_off(d, sub, x, r, 2);
+    if (EX && (J < 0 || J >= N)) {  // cube-corner halo cells read the copy_corners source
+      const bool cc = qin && (I < 0 || I >= N);
+      const uint32_t ox = cc ? (uint32_t)cc_off(d, sub, x, r, 1) * 8u : vx + so;
+      const uint32_t oy = cc ? (uint32_t)cc_off(d, sub, x, r, 2) * 8u : vx + so;
+      const double q1 = bl(rQ, ox, 0), q2 = bl(rQ, oy, 0);
+      v.qx = qin ? q1 : 0.0;
+      v.qy = qin ? q2 : 0.0;
+    } else {
+      const double q1 = bl(rQ, vx, so);
+      v.qx = qin ? q1 : 0.0;
+      v.qy = v.qx;
     }
-    const double q1 = qq[ox], q2 = qq[oy];
-    v.qx = qin ? q1 : 0.0;
-    v.qy = qin ? q2 : 0.0;
-    v.crx = a.crx[fo + o];
-    v.xfx = a.xfx[fo + o];
-    v.area_r = area[o];
-    v.rax = a.ra_x[fo + o];
-    v.dxr = EX ? dxa[o] : 0.0;
+    v.crx = bl(rCRX, vx, so);
+    v.xfx = bl(rXFX, vx, so);
+    v.area_r = bl(rAR, vx, so);
+    v.rax = bl(rRAX, vx, so);
+    v.dxr = EX ? bl(rDXA, vxd, so) : 0.0;
     const int re = r - 2 < -NG ? -NG : r - 2;
-    const long oe = (long)(re + NG) * pitch + xo;
-    v.cry = a.cry[fo + oe];
-    v.yfx = a.yfx[fo + oe];
-    v.my = a.my[fo + oe];
+    const uint32_t se = (uint32_t)(re + NG) * rowb;
+    v.cry = bl(rCRY, vx, se);
+    v.yfx = bl(rYFX, vx, se);
+    v.my = bl(rMY, vx, se);
     const int rm = r - 3 < -NG ? -NG : r - 3;
-    const long om = (long)(rm + NG) * pitch + xo;
-    v.area_m = area[om];
-    v.ray = a.ra_y[fo + om];
-    v.mx = a.mx[fo + om];
-    v.dxm = EX ? dxa[om] : 0.0;
+    const uint32_t sm = (uint32_t)(rm + NG) * rowb;
+    v.ray = bl(rRAY, vx, sm);
+    v.mx = bl(rMX, vx, sm);
+    v.dxm = EX ? bl(rDXA, vxd, sm) : 0.0;
     return v;
   };
 
@@ -369,41 +393,90 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
 
   double qyw[4], qjw[4];  // rows r-3 .. r
   double hf2[4], hcx[4];  // fx2 and crx of rows r-3 .. r
+  double arw[4];          // cell area of rows r-3 .. r (read once per row)
 #pragma unroll
-  for (int m = 0; m < 4; ++m) qyw[m] = qjw[m] = hf2[m] = hcx[m] = 0.0;
+  for (int m = 0; m < 4; ++m) qyw[m] = qjw[m] = hf2[m] = hcx[m] = arw[m] = 0.0;
   YRoll ry{}, rj{};  // q (y fill) and q_j
   double fyy_prev = 0.0;
 
-  MarchIn cur = load(j0 - NG);
-  for (int r = j0 - NG; r <= j1 + 2; ++r) {
-    const MarchIn nxt = load(r + 1);
+  // lane predicates (constant along the march)
+  const bool l_fx2 = x >= 0 && x <= nx, l_qj = x >= 0 && x < nx;
+  const bool l_fy2 = x >= -NG && x <= nx + NG - 1;
+  const bool s_fy = out_lane && x < nx, s_fx = out_lane && x <= nx;
+  const auto rFX = rsrc(a.fx + zo), rFY = rsrc(a.fy + zo);
+  auto bst = [&](__amdgpu_buffer_rsrc_t r, uint32_t soff, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(TpU2, v), r, vx, soff, 0);
+  };
+
+  // One row step.  GEN: the generic step (row clamps, segment ends, tile-edge rows of the
+  // y interpolant, cube-corner fills); steady rows (most of a segment) need none of those
+  // checks, so their step is branch-free apart from the two output stores.
+  // steady load of the step for row rl (rows rl, rl-2, rl-3 inside the plane, away
+  // from the cube corners)
+  auto load_steady = [&](int rl, MarchIn& nxt) {
+      const uint32_t so = (uint32_t)(rl + NG) * rowb;
+      nxt.qx = bl(rQ, vx, so);
+      if (!cin) nxt.qx = 0.0;
+      nxt.qy = nxt.qx;
+      nxt.crx = bl(rCRX, vx, so);
+      nxt.xfx = bl(rXFX, vx, so);
+      nxt.area_r = bl(rAR, vx, so);
+      nxt.rax = bl(rRAX, vx, so);
+      nxt.dxr = EX ? bl(rDXA, vxd, so) : 0.0;
+      const uint32_t se = so - 2 * rowb, sm = so - 3 * rowb;
+      nxt.cry = bl(rCRY, vx, se);
+      nxt.yfx = bl(rYFX, vx, se);
+      nxt.my = bl(rMY, vx, se);
+      nxt.ray = bl(rRAY, vx, sm);
+      nxt.mx = bl(rMX, vx, sm);
+      nxt.dxm = EX ? bl(rDXA, vxd, sm) : 0.0;
+  };
+  // ahead: how many rows ahead the steady step prefetches (1, or 2 in the three-buffer loop)
+  auto step = [&](auto gen, int r, const MarchIn& cur, MarchIn& nxt, int ahead) {
+    constexpr bool GEN = decltype(gen)::value;
+    if (GEN) nxt = load(r + 1);
+    else load_steady(r + ahead, nxt);
     const long o = (long)(r + NG) * pitch + xo;
     // ---- row r: inner x flux fx2, q_j
-    double fx2 = 0.0;
+    double fx2;
     {
       const double f = ppm_x_dpp<ORD, EX>(cur.qx, cur.dxr, I, N, cur.crx);
-      if (x >= 0 && x <= nx && r >= -NG && r <= ny + NG - 1) fx2 = f;
+      const bool ok = GEN ? l_fx2 && r >= -NG && r <= ny + NG - 1 : l_fx2;
+      fx2 = ok ? f : 0.0;
     }
     const double fxx = cur.xfx * fx2;
     const double fxx_e = dpp_next(fxx);
-    double qj = 0.0;
-    if (x >= 0 && x < nx && r >= -NG && r < ny + NG) qj = (cur.qx * cur.area_r + fxx - fxx_e) / cur.rax;
+    double qj;
+    {
+      const double v = (cur.qx * cur.area_r + fxx - fxx_e) / cur.rax;
+      const bool ok = GEN ? l_qj && r >= -NG && r < ny + NG : l_qj;
+      qj = ok ? v : 0.0;
+    }
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
       qyw[m] = qyw[m + 1];
       qjw[m] = qjw[m + 1];
       hf2[m] = hf2[m + 1];
       hcx[m] = hcx[m + 1];
+      arw[m] = arw[m + 1];
     }
     qyw[3] = cur.qy;
     qjw[3] = qj;
     hf2[3] = fx2;
     hcx[3] = cur.crx;
+    arw[3] = cur.area_r;
 
     // ---- y PPM pieces: interface r-1, cell r-2 (both windows)
     const int e = r - 2;
-    const int E = e + sub.joff;
-    const double aly = y_al(qyw, E + 1, o), alj = y_al(qjw, E + 1, o);
+    double aly, alj;
+    if (GEN) {
+      const int E = e + sub.joff;
+      aly = y_al(qyw, E + 1, o);
+      alj = y_al(qjw, E + 1, o);
+    } else {
+      aly = P1 * (qyw[1] + qyw[2]) + P2 * (qyw[0] + qyw[3]);
+      alj = P1 * (qjw[1] + qjw[2]) + P2 * (qjw[0] + qjw[3]);
+    }
     const PpmCell cy = ppm_cell<ORD>(qyw[1], ry.al, aly);
     const PpmCell cj = ppm_cell<ORD>(qjw[1], rj.al, alj);
     const PpmCell cym = ry.cell, cjm = rj.cell;
@@ -412,39 +485,81 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     rj.al = alj;
     rj.cell = cj;
 
-    if (e >= j0) {
+    if (!GEN || e >= j0) {
       // ---- edge e: inner y flux fy2, outer y flux fy
-      const long oe = o - 2 * pitch;
+      const uint32_t se = (uint32_t)(e + NG) * rowb;
       double fy2 = ppm_edge_flux(cym, cy, cur.cry);
-      if (!(e <= ny && x >= -NG && x <= nx + NG - 1)) fy2 = 0.0;
-      const double fyy = e <= ny ? cur.yfx * fy2 : 0.0;
-      if (out_lane && x < nx && e <= ny && (e < j1 || last))
-        a.fy[zo + oe] = 0.5 * (ppm_edge_flux(cjm, cj, cur.cry) + fy2) * cur.my;
+      if (!(GEN ? e <= ny && l_fy2 : l_fy2)) fy2 = 0.0;
+      const double fyy = !GEN || e <= ny ? cur.yfx * fy2 : 0.0;
+      if (GEN ? s_fy && e <= ny && (e < j1 || last) : s_fy)
+        bst(rFY, se, 0.5 * (ppm_edge_flux(cjm, cj, cur.cry) + fy2) * cur.my);
       // ---- row m = r-3: q_i, outer x flux fx
       const int mrow = r - 3;
-      if (mrow >= j0 && mrow < ny) {
-        const long om = o - 3 * pitch;
-        double qi = 0.0;
-        if (x >= -NG && x < nx + NG) qi = (qyw[0] * cur.area_m + fyy_prev - fyy) / cur.ray;
+      if (!GEN || (mrow >= j0 && mrow < ny)) {
+        const double v = (qyw[0] * arw[0] + fyy_prev - fyy) / cur.ray;
+        const double qi = cin ? v : 0.0;
         const double f = ppm_x_dpp<ORD, EX>(qi, cur.dxm, I, N, hcx[0]);
-        if (out_lane && x <= nx && mrow < j1) a.fx[zo + om] = 0.5 * (f + hf2[0]) * cur.mx;
+        if (GEN ? s_fx && mrow < j1 : s_fx) bst(rFX, se - rowb, 0.5 * (f + hf2[0]) * cur.mx);
       }
       fyy_prev = fyy;
     }
+  };
+
+  // steady rows: 2 <= G <= N-2 for the y interpolant's interface G = r-1, rows r+1 (the
+  // prefetch), r-2, r-3 inside the plane and the tile (no corner fills), edge e = r-2 and
+  // row r-3 inside the segment's outputs
+  const int r_lo = j0 - NG, r_hi = j1 + 2;
+  int rs0 = j0 + 3, rs1 = j1 + 1;  // [rs0, rs1] candidate steady rows
+  rs0 = rs0 > 3 - sub.joff ? rs0 : 3 - sub.joff;
+  rs1 = rs1 < N - 2 - sub.joff ? rs1 : N - 2 - sub.joff;
+  rs1 = rs1 < ny + NG - 2 ? rs1 : ny + NG - 2;
+  if (rs1 < rs0) rs1 = rs0 - 1;
+  const std::integral_constant<bool, true> G1{};
+  const std::integral_constant<bool, false> G0{};
+  MarchIn cur = load(r_lo), nxt;
+  int r = r_lo;
+  for (; r < rs0; ++r) {
+    step(G1, r, cur, nxt, 1);
+    cur = nxt;
+  }
+  // steady rows whose two-ahead loads stay in the steady range: three rotating buffers,
+  // each step prefetching two rows ahead (one more step of HBM latency covered)
+  {
+    const int lmax = ny + NG - 1 < N - 1 - sub.joff ? ny + NG - 1 : N - 1 - sub.joff;
+    const int rs1b = rs1 < lmax - 2 ? rs1 : lmax - 2;
+    if (r + 2 <= rs1b) {
+      MarchIn b0 = cur, b1, b2;
+      load_steady(r + 1, b1);
+      for (; r + 2 <= rs1b; r += 3) {
+        step(G0, r, b0, b2, 2);
+        step(G0, r + 1, b1, b0, 2);
+        step(G0, r + 2, b2, b1, 2);
+      }
+      cur = b0;
+    }
+  }
+  for (; r <= rs1; ++r) {
+    step(G0, r, cur, nxt, 1);
+    cur = nxt;
+  }
+  for (; r <= r_hi; ++r) {
+    step(G1, r, cur, nxt, 1);
     cur = nxt;
   }
 }
 
 template <int ORD>
 __global__ void __launch_bounds__(MW * MWAVES) tp_march(TpM a) {
-  const int wv = threadIdx.x / MW;
-  const long w = (long)blockIdx.x * MWAVES + wv;
-  const int strip = (int)(w % a.nstrip);
-  const long t = w / a.nstrip;
-  const int seg = (int)(t % a.nseg);
-  const long z = t / a.nseg;
+  // wave index through readfirstlane: everything derived from it (plane, strip, segment,
+  // buffer descriptors, row offsets) is then provably wave-uniform (SGPRs, no waterfalls)
+  const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / MW);
+  const unsigned w = blockIdx.x * MWAVES + wv;  // < 2^31 (launch_tp checks)
+  const int strip = (int)(w % (unsigned)a.nstrip);
+  const unsigned t = w / (unsigned)a.nstrip;
+  const int seg = (int)(t % (unsigned)a.nseg);
+  const int z = (int)(t / (unsigned)a.nseg);
   if (z >= a.nz) return;  // whole wavefront leaves; no workgroup barrier follows
-  const int s = (int)(z / a.nk / a.nt);
+  const int s = z / a.nk / a.nt;
   const SubInfo& sub = a.subs[s];
   const int j0 = seg * a.seg;
   const int j1 = j0 + a.seg < a.d.ny ? j0 + a.seg : a.d.ny;
@@ -610,12 +725,17 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     GT_LAUNCH(tp_fused, g, dim3(TX, TW), 0, c.st, k);
   } else {
     // segment length: cfg >= 8 selects it (tuning); default 45 rows (C180: 4 segments)
-    const int seg = a.cfg >= 8 ? a.cfg : 45;
+    static const int seg_env = [] {
+      const char* e = getenv("GTFV3_TP_SEG");  // tuning override of the default segment
+      return e ? atoi(e) : 0;
+    }();
+    const int seg = a.cfg >= 8 ? a.cfg : (seg_env >= 8 ? seg_env : 45);
     TpM m{d, c.subs, c.met, a.q, a.nt, a.nk, a.crx, a.cry, a.xfx, a.yfx, a.ra_x, a.ra_y,
           a.mfx ? a.mfx : a.xfx, a.mfy ? a.mfy : a.yfx, a.fx, a.fy, (int)nz, 0, 0, seg};
     m.nstrip = (d.nx + 1 + MOUT - 1) / MOUT;
     m.nseg = (d.ny + seg - 1) / seg;
     const long waves = nz * m.nstrip * m.nseg;
+    if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
     if (a.ord == 5) GT_LAUNCH(tp_march<5>, dim3(cdiv(waves, MWAVES)), dim3(MW * MWAVES), 0, c.st, m);
     else GT_LAUNCH(tp_march<6>, dim3(cdiv(waves, MWAVES)), dim3(MW * MWAVES), 0, c.st, m);
   }

@@ -29,6 +29,6 @@ for s, l in enumerate(lines):
             return sum(1 for y in seg if re.match(r'\s+' + p, y))
         f64 = sum(1 for y in seg if re.search(r'v_\w+_f64', y))
         dpp = sum(1 for y in seg if re.search(r'(row_|wave_|dpp)', y))
-        print('  loop %s span %d: v_=%d f64=%d dpp=%d gload=%d gstore=%d s_=%d waitcnt=%d' % (
-            b.group(1), i - labels[b.group(1)], cnt('v_'), f64, dpp, cnt('global_load'),
-            cnt('global_store'), cnt('s_'), cnt('s_waitcnt')))
+        print('  loop %s span %d: v_=%d f64=%d dpp=%d vmem_ld=%d vmem_st=%d s_=%d waitcnt=%d' % (
+            b.group(1), i - labels[b.group(1)], cnt('v_'), f64, dpp, cnt('(?:global|buffer)_load'),
+            cnt('(?:global|buffer)_store'), cnt('s_'), cnt('s_waitcnt')))
