@@ -165,9 +165,22 @@ def main():
         if a.moist:
             d.stencil("aquaplanet_physics", [], [a.dt])
 
-    for _ in range(a.warmup):
+    # The last warm-up step runs with every kernel bracketed by HIP events to find the
+    # dominant kernel; the timed steps then bracket only that kernel (all kernels when a
+    # per-kernel report is asked for), so the events cost the timed region ~nothing.
+    dominant = None
+    for i in range(a.warmup):
+        probe = not a.no_kernel_timing and not a.kernel_report and i == a.warmup - 1
+        if probe:
+            d.kernel_timing(True)
         one_step()
+        if probe:
+            ks = d.kernel_stats()
+            d.kernel_timing(False)
+            if ks:
+                dominant = max(ks.items(), key=lambda kv: kv[1][0])[0]
     if not a.no_kernel_timing:
+        d.kernel_timing_filter(dominant)
         d.kernel_timing(True)
     barrier()
     t0 = time.perf_counter()
@@ -177,6 +190,8 @@ def main():
     barrier()
     el = time.perf_counter() - t0
     kstats = d.kernel_stats() if not a.no_kernel_timing else {}
+    d.kernel_timing(False)
+    d.kernel_timing_filter(None)
     if world > 1:
         t = torch.tensor([el], dtype=torch.float64, device="cuda")
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

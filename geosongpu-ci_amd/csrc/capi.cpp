@@ -306,6 +306,13 @@ int gtfv3_kernel_timing(void* h, int on) {
   API_CATCH
 }
 
+int gtfv3_kernel_timing_filter(void* h, const char* kernel) {
+  API_TRY
+  (void)D(h);
+  gtfv3::ktimer_filter(kernel);
+  API_CATCH
+}
+
 int gtfv3_kernel_stats(void* h, char* buf, int len) {
   API_TRY
   HIP_CHECK(hipStreamSynchronize(D(h)->st));

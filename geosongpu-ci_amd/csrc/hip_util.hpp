@@ -52,6 +52,10 @@ struct KernelStat {
 };
 bool ktimer_enabled();
 void ktimer_enable(bool on);
+// Restrict timing to the kernel named exactly `name` (GT_LAUNCH spelling, e.g.
+// "tp_march<6>"); empty or null: every kernel.  Untimed launches cost nothing.
+void ktimer_filter(const char* name);
+bool ktimer_wants(const char* name);
 void ktimer_begin(const char* name, hipStream_t s);
 void ktimer_end(hipStream_t s);
 // algorithmic bytes of the launch just issued (DESIGN.md §4 formulas); no-op when off
@@ -63,7 +67,7 @@ const std::map<std::string, KernelStat>& ktimer_stats();
 struct KScope {
   bool on;
   hipStream_t s;
-  KScope(const char* n, hipStream_t st) : on(ktimer_enabled()), s(st) {
+  KScope(const char* n, hipStream_t st) : on(ktimer_enabled() && ktimer_wants(n)), s(st) {
     if (on) ktimer_begin(n, s);
   }
   ~KScope() {

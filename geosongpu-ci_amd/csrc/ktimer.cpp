@@ -18,6 +18,8 @@ struct Pending {
 
 struct KTimer {
   bool on = false;
+  std::string only;       // timed kernel (empty: all)
+  bool last_timed = false;  // the launch just issued was bracketed
   std::vector<hipEvent_t> pool;
   size_t used = 0;
   std::vector<Pending> pending;
@@ -42,6 +44,12 @@ KTimer& kt() {
 
 bool ktimer_enabled() { return kt().on; }
 void ktimer_enable(bool on) { kt().on = on; }
+void ktimer_filter(const char* name) { kt().only = name ? name : ""; }
+bool ktimer_wants(const char* name) {
+  KTimer& t = kt();
+  t.last_timed = t.only.empty() || t.only == name;
+  return t.last_timed;
+}
 
 void ktimer_begin(const char* name, hipStream_t s) {
   KTimer& t = kt();
@@ -59,7 +67,7 @@ void ktimer_end(hipStream_t s) {
 
 void ktimer_bytes(double bytes) {
   KTimer& t = kt();
-  if (t.on && !t.pending.empty()) t.pending.back().bytes = bytes;
+  if (t.on && t.last_timed && !t.pending.empty()) t.pending.back().bytes = bytes;
 }
 
 void ktimer_flush() {

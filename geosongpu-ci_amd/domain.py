@@ -134,6 +134,10 @@ class Domain:
     def kernel_timing(self, on=True):
         check(lib().gtfv3_kernel_timing(self.h, 1 if on else 0))
 
+    def kernel_timing_filter(self, kernel=None):
+        """time only `kernel` (its launch name) while timing is on; None: every kernel"""
+        check(lib().gtfv3_kernel_timing_filter(self.h, kernel.encode() if kernel else None))
+
     def kernel_stats(self):
         """{kernel: (total_ms, launches, algorithmic_bytes)} since kernel_timing(True)"""
         buf = ctypes.create_string_buffer(1 << 16)
