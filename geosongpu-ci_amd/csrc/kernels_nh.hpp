@@ -43,6 +43,8 @@ void set_riem_variant(int v);
 int riem_variant();
 void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* delp, double* pk3, double* pe);
 void a2b_ord4(const Ctx& c, int nk, const double* q, double* qout, double* qx, double* qy);
+// up to four fields in one launch (same result as one a2b_ord4 call per field)
+void a2b_ord4_multi(const Ctx& c, int nf, const int* nk, const double* const* q, double* const* qout);
 
 struct NhPgArgs {
   int npz;

@@ -4,6 +4,8 @@
 // Column kernels put one (i,j) column per lane: a wavefront covers 64 consecutive
 // i, so every k-plane access is coalesced; per-column work arrays are planes of
 // scratch fields (same [sub][k][plane] layout).
+#include <climits>
+
 #include "kernels_nh.hpp"
 #include "stencil_common.hpp"
 
@@ -395,12 +397,42 @@ struct A2bEdge {
   }
 };
 
+// Up to four independent a2b_ord4 fields in one launch (nh_p_grad interpolates pp, pk3,
+// gz and delp): plane index z runs over the fields' planes back to back, zb[f] is the
+// first plane of field f (unused entries: INT_MAX).  More waves per launch overlap the
+// march kernels' row-latency chains of the four fields.
+constexpr int A2B_MAXF = 4;
+struct A2bF {
+  const double* q[A2B_MAXF];
+  double* qo[A2B_MAXF];
+  int nk[A2B_MAXF];
+  int zb[A2B_MAXF + 1];
+};
+struct A2bSel {
+  const double* q;
+  double* qo;
+  int nk, z;  // z: plane within the field
+};
+__device__ __forceinline__ A2bSel a2b_select(const A2bF& F, int z) {
+  const int f = (z >= F.zb[1]) + (z >= F.zb[2]) + (z >= F.zb[3]);
+  A2bSel r;
+  r.q = f == 0 ? F.q[0] : (f == 1 ? F.q[1] : (f == 2 ? F.q[2] : F.q[3]));
+  r.qo = f == 0 ? F.qo[0] : (f == 1 ? F.qo[1] : (f == 2 ? F.qo[2] : F.qo[3]));
+  r.nk = f == 0 ? F.nk[0] : (f == 1 ? F.nk[1] : (f == 2 ? F.nk[2] : F.nk[3]));
+  r.z = z - (f == 0 ? F.zb[0] : (f == 1 ? F.zb[1] : (f == 2 ? F.zb[2] : F.zb[3])));
+  return r;
+}
+
 // qout on cube corners and tile-edge lines
 __global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restrict__ subs,
-                                                  const double* __restrict__ M, int nk, const double* __restrict__ cw,
-                                                  const double* __restrict__ q, double* __restrict__ qout) {
+                                                  const double* __restrict__ M, A2bF F, const double* __restrict__ cw) {
   // all targets lie on the tile-edge lines: one lane per line point
-  const int z = blockIdx.z, s = z / nk;
+  const int zg = blockIdx.z;
+  const int f = (zg >= F.zb[1]) + (zg >= F.zb[2]) + (zg >= F.zb[3]);
+  const int nk = f == 0 ? F.nk[0] : (f == 1 ? F.nk[1] : (f == 2 ? F.nk[2] : F.nk[3]));
+  const int z = zg - (f == 0 ? F.zb[0] : (f == 1 ? F.zb[1] : (f == 2 ? F.zb[2] : F.zb[3]))), s = z / nk;
+  const double* __restrict__ q = f == 0 ? F.q[0] : (f == 1 ? F.q[1] : (f == 2 ? F.q[2] : F.q[3]));
+  double* __restrict__ qout = f == 0 ? F.qo[0] : (f == 1 ? F.qo[1] : (f == 2 ? F.qo[2] : F.qo[3]));
   const SubInfo sub = subs[s];
   int i, j;
   if (!edge_line_point(blockIdx.x * blockDim.x + threadIdx.x, sub, 0, d.nx, 0, d.ny, i, j)) return;
@@ -458,23 +490,24 @@ __device__ __forceinline__ double dpp_next_d(double v) {
 struct A2bM {
   Dims d;
   const SubInfo* subs;
-  const double *M, *q;
-  double* qout;
-  int nk, nz, nstrip, nseg, seg;
+  const double* M;
+  A2bF F;
+  int nz, nstrip, nseg, seg;  // nz: planes of all fields
 };
 
 template <bool EX>
-__device__ void a2b_march_strip(const A2bM& a, int z, int a0, int a1, int j0, int j1) {
+__device__ void a2b_march_strip(const A2bM& a, const double* qf, double* qof, int nk, int z, int a0, int a1, int j0,
+                                int j1) {
   const Dims& d = a.d;
   const int lane = threadIdx.x & (AM_W - 1);
-  const int s = z / a.nk;
+  const int s = z / nk;
   const SubInfo sub = a.subs[s];
   const int N = sub.N, io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
   const int c = a0 - 2 + lane;  // this lane's column (cell column for qy, corner column for qx)
   const int I = c + io;
   const long pitch = d.pitch;
   const long zo = (long)z * d.plane;
-  const double* qq = a.q + zo;
+  const double* qq = qf + zo;
   const double* dxa = met(a.M, d, M_DXA, s);
   const double* dya = met(a.M, d, M_DYA, s);
   const int cc = c > nx + NG ? nx + NG : c;  // addressable
@@ -497,7 +530,7 @@ __device__ void a2b_march_strip(const A2bM& a, int z, int a0, int a1, int j0, in
   // for in the row it is used in would drain every prefetched block: vmcnt is in order).
   const long dxs = I == 1 ? -1 : (I == N - 1 ? 1 : 0);
   const bool xs = dxs != 0;
-  const double* qo = a.qout + zo;
+  const double* qo = qof + zo;
   double qb[AM_B], db[AM_B], xb[AM_B], yb[AM_B], qn[AM_B], dn[AM_B], xn[AM_B], yn[AM_B];
   auto fetch = [&](int r, double& q_, double& d_, double& x_, double& y_) {
     const long o = row_of(r);
@@ -614,7 +647,7 @@ __device__ void a2b_march_strip(const A2bM& a, int z, int a0, int a1, int j0, in
     if (I == 1) qyy = AC1 * (QY[2] + QY[3]) + AC2 * (xb[u] + qyy_gen(1));
     else if (I == N - 1) qyy = AC1 * (QY[2] + QY[3]) + AC2 * (xb[u] + qyy_gen(-1));
     else qyy = qyy_gen(0);
-    a.qout[zo + oj] = 0.5 * (qxx + qyy);
+    qof[zo + oj] = 0.5 * (qxx + qyy);
     }
 #pragma unroll
     for (int u = 0; u < AM_B; ++u) {
@@ -633,7 +666,8 @@ __global__ void __launch_bounds__(AM_W * AM_WAVES) a2b_march_k(A2bM a) {
   const int seg = (int)(t % a.nseg);
   const long z = t / a.nseg;
   if (z >= a.nz) return;  // whole wavefront leaves; no workgroup barrier follows
-  const int s = (int)(z / a.nk);
+  const A2bSel fs = a2b_select(a.F, (int)z);
+  const int s = fs.z / fs.nk;
   const SubInfo& sub = a.subs[s];
   const int nx = a.d.nx;
   // strips of 61 corners; the last one is shifted left to end at corner nx (so a corner
@@ -647,8 +681,8 @@ __global__ void __launch_bounds__(AM_W * AM_WAVES) a2b_march_k(A2bM a) {
   const int A = a0 + sub.ioff;
   // x-interpolant edge forms are needed only where a lane's column reaches I <= 1 or I >= N-1
   const bool ex = !(A - 2 >= 2 && A + AM_OUT + 1 <= sub.N - 2);
-  if (ex) a2b_march_strip<true>(a, (int)z, a0, a1, j0, j1);
-  else a2b_march_strip<false>(a, (int)z, a0, a1, j0, j1);
+  if (ex) a2b_march_strip<true>(a, fs.q, fs.qo, fs.nk, fs.z, a0, a1, j0, j1);
+  else a2b_march_strip<false>(a, fs.q, fs.qo, fs.nk, fs.z, a0, a1, j0, j1);
 }
 
 // non-hydrostatic pressure gradient on the D-grid winds (u, v arrive x dx, dy)
@@ -751,30 +785,58 @@ void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* d
   HIP_LAUNCH_CHECK();
 }
 
-void a2b_ord4(const Ctx& c, int nk, const double* q, double* qout, double* qx, double* qy) {
-  (void)qx;
-  (void)qy;
+void a2b_ord4_multi(const Ctx& c, int nf, const int* nk, const double* const* q, double* const* qout) {
   const Dims& d = c.d;
+  if (nf < 1 || nf > A2B_MAXF) throw std::runtime_error("a2b_ord4: 1..4 fields per launch");
+  A2bF F{};
+  long nz = 0, lev = 0;
+  for (int f = 0; f < A2B_MAXF; ++f) {
+    F.zb[f] = f < nf ? (int)nz : INT_MAX;
+    if (f < nf) {
+      if (nk[f] < 1 || !q[f] || !qout[f]) throw std::runtime_error("a2b_ord4: bad field");
+      F.q[f] = q[f];
+      F.qo[f] = qout[f];
+      F.nk[f] = nk[f];
+      nz += (long)d.nsub * nk[f];
+      lev += nk[f];
+    } else {
+      F.q[f] = q[0];
+      F.qo[f] = qout[0];
+      F.nk[f] = 1;
+    }
+  }
+  F.zb[A2B_MAXF] = INT_MAX;
+  if (nz >= 65536) throw std::runtime_error("a2b_ord4: too many planes for one launch");
   // corner / tile-edge values first: the interior points next to the tile edges use them
-  GT_LAUNCH(a2b_edge_k, dim3(cdiv(edge_line_count(0, d.nx, 0, d.ny), 256), 1, d.nsub * nk), dim3(256), 0, c.st, d,
-            c.subs, c.met, nk, c.cornerw, q, qout);
+  GT_LAUNCH(a2b_edge_k, dim3(cdiv(edge_line_count(0, d.nx, 0, d.ny), 256), 1, (unsigned)nz), dim3(256), 0, c.st, d,
+            c.subs, c.met, F, c.cornerw);
   HIP_LAUNCH_CHECK();
-  // interior corners: column-marching kernel (segments of 45 corner rows)
-  A2bM m{d, c.subs, c.met, q, qout, nk, d.nsub * nk, (int)cdiv(d.nx + 1, AM_OUT), 0, 45};
-  m.nseg = (int)cdiv(d.ny + 1, m.seg);
+  // interior corners: column-marching kernel (balanced segments of at most 46 corner
+  // rows: C180 has 181 corner rows -> 4 x 46, not 4 x 45 + 1)
+  A2bM m{d, c.subs, c.met, F, (int)nz, (int)cdiv(d.nx + 1, AM_OUT), 0, 0};
+  m.nseg = (int)cdiv(d.ny + 1, 46);
+  m.seg = (int)cdiv(d.ny + 1, m.nseg);
   const long waves = (long)m.nz * m.nstrip * m.nseg;
   GT_LAUNCH(a2b_march_k, dim3(cdiv(waves, AM_WAVES)), dim3(AM_W * AM_WAVES), 0, c.st, m);
   HIP_LAUNCH_CHECK();
-  ktimer_bytes(8.0 * d.nx * d.ny * d.nsub * nk * 2.0);  // q read, qout written
+  ktimer_bytes(8.0 * d.nx * d.ny * d.nsub * lev * 2.0);  // q read, qout written
+}
+
+void a2b_ord4(const Ctx& c, int nk, const double* q, double* qout, double* qx, double* qy) {
+  (void)qx;
+  (void)qy;
+  a2b_ord4_multi(c, 1, &nk, &q, &qout);
 }
 
 void nh_p_grad(const Ctx& c, const NhPgArgs& a) {
   const Dims& d = c.d;
   const int k1 = a.npz + 1;
-  a2b_ord4(c, k1, a.pp, a.ppb, a.qx, a.qy);
-  a2b_ord4(c, k1, a.pk3, a.pkb, a.qx, a.qy);
-  a2b_ord4(c, k1, a.gz, a.gzb, a.qx, a.qy);
-  a2b_ord4(c, a.npz, a.delp, a.wk1, a.qx, a.qy);
+  {
+    const int nk[4] = {k1, k1, k1, a.npz};
+    const double* q[4] = {a.pp, a.pk3, a.gz, a.delp};
+    double* qo[4] = {a.ppb, a.pkb, a.gzb, a.wk1};
+    a2b_ord4_multi(c, 4, nk, q, qo);
+  }
   const double ptk = exp(Constants::kappa * log(a.ptop));
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
   GT_LAUNCH(nhpgrad_k, g2(d, L, d.nsub * a.npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, ptk,
