@@ -155,6 +155,22 @@ std::map<std::string, Fn>& reg() {
          if (km.nk != data.nk || kidx.nk != 1) throw std::runtime_error("column_gather_k: field shapes");
          column_gather_k(dy.ctx(), data.nk, data.p, km.p, kidx.p, dy.field(f[3], 1).p);
        }},
+      // Lagrangian_to_Eulerian on the dycore's own state fields (pe, peln, pk, pkz, delp, delz,
+      // pt, w, q, u, v, ps, ws; pt enters as virtual potential temperature) with the vertical
+      // grid of set_vertical(); no field arguments.  params: fill
+      {"lagrangian_to_eulerian",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 0, "lagrangian_to_eulerian");
+         const int npz = dy.nl.npz, k1 = npz + 1, nq = dy.nl.nq;
+         const double* vert = dy.vertical_dev();
+         RemapState rs{dy.need("pe", k1).p, dy.need("peln", k1).p, dy.field("pk", k1).p, dy.field("pkz", npz).p,
+                       dy.need("delp", npz).p, dy.need("delz", npz).p, dy.need("pt", npz).p, dy.need("w", npz).p,
+                       dy.need("q", nq * npz).p, dy.need("u", npz).p, dy.need("v", npz).p, dy.field("ps", 1).p,
+                       dy.field("ws", 1).p};
+         RemapScratch rsc;
+         for (int n = 0; n < 3; ++n) rsc.s[n] = dy.field("_rmj" + std::to_string(n), remap_jobs(nq) * k1).p;
+         lagrangian_to_eulerian(dy.ctx(), npz, nq, dy.ak.at(0), p.empty() || p[0] != 0.0, vert, vert + k1, rs, rsc);
+       }},
       // a2b_ord4(q | qout): cell means -> cell corners (4th order, cubed-sphere edge forms)
       {"a2b_ord4",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
