@@ -251,14 +251,16 @@ __device__ __forceinline__ PpmCell ppm_cell(double q, double al_l, double al_r) 
   c.s = ORD == 5 ? c.bl * c.br < 0.0 : 3.0 * fabs(c.b0) < fabs(c.bl - c.br);
   return c;
 }
+// Both upwind candidates are evaluated and one is selected (no lane-divergent branch:
+// neighbouring lanes see Courant numbers of both signs); each candidate is the
+// expression of the branch it replaces, so results are unchanged.
 __device__ __forceinline__ double ppm_edge_flux(const PpmCell& m, const PpmCell& z, double c) {
   const bool smooth = m.s || z.s;
-  if (c > 0.0) {
-    const double fx1 = (1.0 - c) * (m.br - c * m.b0);
-    return m.q + (smooth ? fx1 : 0.0);
-  }
-  const double fx1 = (1.0 + c) * (z.bl + c * z.b0);
-  return z.q + (smooth ? fx1 : 0.0);
+  const double fm = (1.0 - c) * (m.br - c * m.b0);
+  const double fz = (1.0 + c) * (z.bl + c * z.b0);
+  const double vm = m.q + (smooth ? fm : 0.0);
+  const double vz = z.q + (smooth ? fz : 0.0);
+  return c > 0.0 ? vm : vz;
 }
 
 // x-PPM flux at the lane's edge (interface g = I, between cells x-1 and x), cells held
@@ -302,7 +304,7 @@ struct YRoll {
   PpmCell cell;
 };
 
-template <int ORD, bool EX>
+template <int ORD, bool EX, bool AHEAD2>
 __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   const Dims& d = a.d;
   const int lane = threadIdx.x & (MW - 1);
@@ -527,7 +529,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   {
     const int lmax = ny + NG - 1 < N - 1 - sub.joff ? ny + NG - 1 : N - 1 - sub.joff;
     const int rs1b = rs1 < lmax - 2 ? rs1 : lmax - 2;
-    if (r + 2 <= rs1b) {
+    if (AHEAD2 && r + 2 <= rs1b) {
       MarchIn b0 = cur, b1, b2;
       load_steady(r + 1, b1);
       for (; r + 2 <= rs1b; r += 3) {
@@ -548,8 +550,10 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   }
 }
 
-template <int ORD>
-__global__ void __launch_bounds__(MW * MWAVES) tp_march(TpM a) {
+// AHEAD2: steady rows prefetch two rows ahead (three row buffers, 149 VGPRs, three
+// waves per SIMD); otherwise one row ahead (two buffers, <= 128 VGPRs, four waves)
+template <int ORD, bool AHEAD2>
+__global__ void __launch_bounds__(MW * MWAVES, AHEAD2 ? 1 : 4) tp_march(TpM a) {
   // wave index through readfirstlane: everything derived from it (plane, strip, segment,
   // buffer descriptors, row offsets) is then provably wave-uniform (SGPRs, no waterfalls)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / MW);
@@ -565,8 +569,8 @@ __global__ void __launch_bounds__(MW * MWAVES) tp_march(TpM a) {
   const int j1 = j0 + a.seg < a.d.ny ? j0 + a.seg : a.d.ny;
   const int A = strip * MOUT + sub.ioff;
   const bool ex = !(A - 1 >= 2 && A + MOUT + 1 <= sub.N - 2);
-  if (ex) tp_march_strip<ORD, true>(a, (int)z, strip, j0, j1);
-  else tp_march_strip<ORD, false>(a, (int)z, strip, j0, j1);
+  if (ex) tp_march_strip<ORD, true, AHEAD2>(a, (int)z, strip, j0, j1);
+  else tp_march_strip<ORD, false, AHEAD2>(a, (int)z, strip, j0, j1);
 }
 
 // ---------------- tracer_2d_1l ----------------
@@ -736,8 +740,14 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     m.nseg = (d.ny + seg - 1) / seg;
     const long waves = nz * m.nstrip * m.nseg;
     if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
-    if (a.ord == 5) GT_LAUNCH(tp_march<5>, dim3(cdiv(waves, MWAVES)), dim3(MW * MWAVES), 0, c.st, m);
-    else GT_LAUNCH(tp_march<6>, dim3(cdiv(waves, MWAVES)), dim3(MW * MWAVES), 0, c.st, m);
+    const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
+    if (a.cfg == -2) {  // tuning: one-row-ahead variant
+      if (a.ord == 5) GT_LAUNCH((tp_march<5, false>), g, b, 0, c.st, m);
+      else GT_LAUNCH((tp_march<6, false>), g, b, 0, c.st, m);
+    } else {
+      if (a.ord == 5) GT_LAUNCH((tp_march<5, true>), g, b, 0, c.st, m);
+      else GT_LAUNCH((tp_march<6, true>), g, b, 0, c.st, m);
+    }
   }
   HIP_LAUNCH_CHECK();
   // algorithmic bytes: q read + fx, fy written per plane; crx cry xfx yfx ra_x ra_y (+ mfx mfy)
