@@ -36,8 +36,24 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E, /opt/skills/guides/MI355X_MICROARCH.md
 # domain; formulas in DESIGN.md §4) with the event timer.
 
 
-def pmc_traffic(kernel):
-    """HBM bytes per launch of `kernel` from the newest committed PMC summary
+def family(kernel):
+    """kernel family: the launch name without template arguments ("(tp_march<6, true,
+    false>)" -> "tp_march"); the roofline reports the family with the most device time"""
+    return kernel.strip("()").split("<")[0]
+
+
+def families(kstats):
+    """{family: (total_ms, launches, algorithmic_bytes)} summed over instantiations"""
+    out = {}
+    for k, (ms, n, b) in kstats.items():
+        t = out.get(family(k), (0.0, 0, 0.0))
+        out[family(k)] = (t[0] + ms, t[1] + n, t[2] + b)
+    return out
+
+
+def pmc_traffic(fam, launches):
+    """HBM bytes per launch of kernel family `fam` (launch-weighted over the instantiations
+    timed, `launches` = {launch name: count}) from the newest committed PMC summary
     (profiles/rNN_pmc_traffic.json, made by tools/pmc_summary.py from separate
     FETCH_SIZE / WRITE_SIZE rocprofv3 passes of this same command); None if absent."""
     import glob
@@ -45,8 +61,11 @@ def pmc_traffic(kernel):
     for f in reversed(files):
         with open(f) as fh:
             t = json.load(fh)
-        if kernel in t:
-            return t[kernel]["traffic_bytes"], os.path.basename(f)
+        keys = {k: k.strip("()").replace(" ", "") for k in launches}
+        tk = {k.replace(" ", ""): v for k, v in t.items()}
+        if keys and all(v in tk for v in keys.values()):
+            tot = sum(tk[keys[k]]["traffic_bytes"] * n for k, n in launches.items())
+            return tot / sum(launches.values()), os.path.basename(f)
     return None, None
 
 
@@ -175,10 +194,10 @@ def main():
             d.kernel_timing(True)
         one_step()
         if probe:
-            ks = d.kernel_stats()
+            fam = families(d.kernel_stats())
             d.kernel_timing(False)
-            if ks:
-                dominant = max(ks.items(), key=lambda kv: kv[1][0])[0]
+            if fam:
+                dominant = max(fam.items(), key=lambda kv: kv[1][0])[0]
     if not a.no_kernel_timing:
         d.kernel_timing_filter(dominant)
         d.kernel_timing(True)
@@ -204,9 +223,10 @@ def main():
 
     roof = None
     if kstats:
-        name, (tot, n, byt) = max(kstats.items(), key=lambda kv: kv[1][0])
+        fam = families(kstats)
+        name, (tot, n, byt) = max(fam.items(), key=lambda kv: kv[1][0])
         avg_ms = tot / n
-        traffic, src = pmc_traffic(name)
+        traffic, src = pmc_traffic(name, {k: v[1] for k, v in kstats.items() if family(k) == name})
         ach = byt / (tot * 1e-3) / 1e9 if byt > 0 else None
         roof = dict(bound="hbm", kernel=name, achieved=ach, peak=HBM_PEAK_GBS, unit="GB/s",
                     frac=ach / HBM_PEAK_GBS if ach else None, traffic=traffic, traffic_source=src,

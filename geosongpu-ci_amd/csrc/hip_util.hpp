@@ -52,8 +52,9 @@ struct KernelStat {
 };
 bool ktimer_enabled();
 void ktimer_enable(bool on);
-// Restrict timing to the kernel named exactly `name` (GT_LAUNCH spelling, e.g.
-// "tp_march<6>"); empty or null: every kernel.  Untimed launches cost nothing.
+// Restrict timing to one kernel family: `name` is the kernel's name without template
+// arguments (e.g. "tp_march" times every tp_march<...> instantiation); empty or null:
+// every kernel.  Untimed launches cost nothing.
 void ktimer_filter(const char* name);
 bool ktimer_wants(const char* name);
 void ktimer_begin(const char* name, hipStream_t s);

@@ -45,9 +45,16 @@ KTimer& kt() {
 bool ktimer_enabled() { return kt().on; }
 void ktimer_enable(bool on) { kt().on = on; }
 void ktimer_filter(const char* name) { kt().only = name ? name : ""; }
+// the filter names a kernel family: "tp_march" matches "(tp_march<6, true, false>)"
 bool ktimer_wants(const char* name) {
   KTimer& t = kt();
-  t.last_timed = t.only.empty() || t.only == name;
+  if (t.only.empty()) {
+    t.last_timed = true;
+    return true;
+  }
+  const char* n = name[0] == '(' ? name + 1 : name;
+  const size_t L = t.only.size();
+  t.last_timed = std::strncmp(n, t.only.c_str(), L) == 0 && (n[L] == '\0' || n[L] == '<' || n[L] == ')');
   return t.last_timed;
 }
 

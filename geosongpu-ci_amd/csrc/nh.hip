@@ -213,26 +213,20 @@ __global__ void __launch_bounds__(256) edge_prof_k(Dims d, int npz, const double
 }
 
 // ra_x, ra_y for the interface-level transport of zh
-__global__ void __launch_bounds__(256) ra_k(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
-                                            int nk, const double* __restrict__ xfx, const double* __restrict__ yfx,
-                                            double* __restrict__ ra_x, double* __restrict__ ra_y) {
-  Launch2D L{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  KSETUP2(nk)
-  const double area = MA(MT(M_AREA), 0, 0);
-  AT(ra_y, 0, 0) = (j >= 0 && j < d.ny) ? area + AT(yfx, 0, 0) - AT(yfx, 0, 1) : 0.0;
-  AT(ra_x, 0, 0) = (i >= 0 && i < d.nx) ? area + AT(xfx, 0, 0) - AT(xfx, 1, 0) : 0.0;
-}
-
 // zh update from the transported fluxes (compute cells, all interfaces)
+// (ra_x = area + xfx|i - xfx|i+1 and ra_y = area + yfx|j - yfx|j+1 formed here, as in
+// fv_tp_2d, instead of being stored as planes)
 __global__ void __launch_bounds__(256) zh_update_k(Dims d, const SubInfo* __restrict__ subs,
                                                    const double* __restrict__ M, int nk, const double* __restrict__ fx,
-                                                   const double* __restrict__ fy, const double* __restrict__ ra_x,
-                                                   const double* __restrict__ ra_y, double* __restrict__ zh) {
+                                                   const double* __restrict__ fy, const double* __restrict__ xfx,
+                                                   const double* __restrict__ yfx, double* __restrict__ zh) {
   Launch2D L{0, 0, d.nx, d.ny};
   KSETUP2(nk)
   const double area = MA(MT(M_AREA), 0, 0);
+  const double ra_x = area + AT(xfx, 0, 0) - AT(xfx, 1, 0);
+  const double ra_y = area + AT(yfx, 0, 0) - AT(yfx, 0, 1);
   AT(zh, 0, 0) = (AT(zh, 0, 0) * area + AT(fx, 0, 0) - AT(fx, 1, 0) + AT(fy, 0, 0) - AT(fy, 0, 1)) /
-                 (AT(ra_x, 0, 0) + AT(ra_y, 0, 0) - area);
+                 (ra_x + ra_y - area);
 }
 
 // pk3 on the 2-wide halo ring and pe on the 1-wide ring (from the halo-updated delp):
@@ -761,10 +755,6 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
   GT_LAUNCH(edge_prof_k, g2(d, Lf, d.nsub), dim3(BX, BY), 0, c.st, d, a.npz, a.dp0, a.crx, a.xfx, a.cry,
             a.yfx, a.crx_e, a.xfx_e, a.cry_e, a.yfx_e);
   HIP_LAUNCH_CHECK();
-  Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  GT_LAUNCH(ra_k, g2(d, Lr, d.nsub * k1), dim3(BX, BY), 0, c.st, d, c.subs, c.met, k1, a.xfx_e, a.yfx_e,
-                     a.ra_x, a.ra_y);
-  HIP_LAUNCH_CHECK();
   TpArgs t{};
   t.q = a.zh; t.nt = 1; t.nk = k1;
   t.crx = a.crx_e; t.cry = a.cry_e; t.xfx = a.xfx_e; t.yfx = a.yfx_e; t.ra_x = a.ra_x; t.ra_y = a.ra_y;
@@ -773,7 +763,7 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
   fv_tp_2d(c, t);
   Launch2D Li{0, 0, d.nx, d.ny};
   GT_LAUNCH(zh_update_k, g2(d, Li, d.nsub * k1), dim3(BX, BY), 0, c.st, d, c.subs, c.met, k1, a.fx, a.fy,
-                     a.ra_x, a.ra_y, a.zh);
+                     a.xfx_e, a.yfx_e, a.zh);
   HIP_LAUNCH_CHECK();
 }
 

@@ -31,7 +31,8 @@ void need(const std::vector<std::string>& f, size_t n, const char* who) {
 
 std::map<std::string, Fn>& reg() {
   static std::map<std::string, Fn> r = {
-      // fv_tp_2d(q, crx, cry, xfx, yfx, ra_x, ra_y, mfx|-, mfy|-, fx, fy) params: ord, nt
+      // fv_tp_2d(q, crx, cry, xfx, yfx, ra_x, ra_y, mfx|-, mfy|-, fx, fy) params: ord, nt, cfg
+      // (FV3 argument list; ra_x / ra_y are formed in the kernel from area, xfx, yfx and not read)
       {"fv_tp_2d",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
          need(f, 11, "fv_tp_2d");

@@ -426,16 +426,6 @@ __global__ void __launch_bounds__(256) ds_courant(Dims d, const SubInfo* __restr
   AT(yfx, 0, 0) = e;
 }
 
-__global__ void __launch_bounds__(256) ds_ra(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
-                                             int npz, const double* __restrict__ xfx, const double* __restrict__ yfx,
-                                             double* __restrict__ ra_x, double* __restrict__ ra_y) {
-  Launch2D L{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  KSETUP(npz)
-  const double area = MA(MT(M_AREA), 0, 0);
-  AT(ra_y, 0, 0) = (j >= 0 && j < d.ny) ? area + AT(yfx, 0, 0) - AT(yfx, 0, 1) : 0.0;
-  AT(ra_x, 0, 0) = (i >= 0 && i < d.nx) ? area + AT(xfx, 0, 0) - AT(xfx, 1, 0) : 0.0;
-}
-
 // Courant / mass-flux accumulation for tracer transport ("flux capacitor")
 __global__ void __launch_bounds__(256) ds_accum(Dims d, const SubInfo* __restrict__ subs, int npz,
                                                 const double* __restrict__ crx, const double* __restrict__ cry,
@@ -630,10 +620,6 @@ void d_sw(const Ctx& c, const DswArgs& a) {
   GT_LAUNCH(ds_courant, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.ut, a.vt,
                      a.crx, a.cry, a.xfx, a.yfx);
   HIP_LAUNCH_CHECK();
-  Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  GT_LAUNCH(ds_ra, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.xfx, a.yfx, a.ra_x,
-                     a.ra_y);
-  HIP_LAUNCH_CHECK();
   TpArgs t{};
   t.nt = 1;
   t.nk = a.npz;
@@ -661,6 +647,7 @@ void d_sw(const Ctx& c, const DswArgs& a) {
                      a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke);
   HIP_LAUNCH_CHECK();
   // vorticity transport
+  Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
   GT_LAUNCH(ds_vort, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.vort);
   HIP_LAUNCH_CHECK();
   t.mfx = nullptr; t.mfy = nullptr;

@@ -1,7 +1,7 @@
 // tp.hip — fv_tp_2d (Lin & Rood 1996 two-dimensional flux-form PPM transport,
 // FV3 tp_core) and the tracer_2d_1l pieces (FV3 fv_tracer2d), HIP for gfx950.
 //
-// fv_tp_2d (HBM-bound, no MFMA) is one fused LDS-tiled kernel computing, per tile:
+// fv_tp_2d (HBM-bound, no MFMA) is one column-marching kernel computing:
 //   fx2 = xppm(q, crx) [x-corner-filled q]   fy2 = yppm(q, cry) [y-corner-filled q]
 //   q_i = (q*area + yfx*fy2|j - yfx*fy2|j+1)/ra_y    q_j = (q*area + xfx*fx2|i - ...)/ra_x
 //   fx = 0.5*(xppm(q_i) + fx2)*mfx     fy = 0.5*(yppm(q_j) + fy2)*mfy
@@ -18,180 +18,6 @@ namespace {
 
 constexpr int ZMAX = 65535;
 
-inline dim3 grid_for(const Launch2D& L, long nz) {
-  return dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), (unsigned)(nz < ZMAX ? nz : ZMAX));
-}
-
-// Fused fv_tp_2d: one workgroup = one 64 x 8 tile of one (sub-domain, level), 256
-// threads as 64 x 4 (a wavefront = one 64-wide tile row, so global row reads are
-// coalesced).  The corner-filled q tiles, the inner fluxes fx2 / fy2 and the
-// advective updates q_i / q_j all stay in LDS, so HBM sees q, the Courant numbers
-// and area fluxes once and the two output fluxes once (the unfused form round-
-// tripped four scratch fields).  Tiles away from the tile edges take the interior
-// PPM path (no edge-interface branches, no dxa reads) and tiles away from the cube
-// corners skip the copy_corners remap; regions and expressions are exactly those of
-// the three-pass form (FV3 fv_tp_2d).
-constexpr int TX = 64, TY = 8, TW = 4;
-constexpr int QX_C = TX + 6, QX_R = TY + 5;  // q (x corner fill): cols i0-3..i0+TX+2, rows j0-3..j0+TY+1
-constexpr int QY_C = TX + 5, QY_R = TY + 6;  // q (y corner fill): cols i0-3..i0+TX+1, rows j0-3..j0+TY+2
-constexpr int FX_C = TX + 1, FX_R = TY + 5;  // fx2: edges i0..i0+TX, rows j0-3..j0+TY+1
-constexpr int FY_C = TX + 5, FY_R = TY + 1;  // fy2: cols i0-3..i0+TX+1, edges j0..j0+TY
-constexpr int QI_C = TX + 5, QI_R = TY;      // q_i: cols i0-3..i0+TX+1, rows j0..j0+TY-1
-constexpr int QJ_C = TX, QJ_R = TY + 5;      // q_j: cols i0..i0+TX-1, rows j0-3..j0+TY+1
-
-struct TpTiles {
-  double QX[QX_R][QX_C];
-  double QY[QY_R][QY_C];
-  double FX2[FX_R][FX_C];
-  double FY2[FY_R][FY_C];
-  double QI[QI_R][QI_C];
-  double QJ[QJ_R][QJ_C];
-};
-
-struct TpK {
-  Dims d;
-  const SubInfo* subs;
-  const double *M, *q;
-  int nt, nk;
-  const double *crx, *cry, *xfx, *yfx, *ra_x, *ra_y, *mx, *my;
-  double *fx, *fy;
-  int ord, nz;
-};
-
-template <bool EX, bool EY, bool CORNER>
-__device__ void tp_tile(const TpK& a, TpTiles& T, int z, int i0, int j0) {
-  const Dims& d = a.d;
-  const int tx = threadIdx.x, ty = threadIdx.y, tid = ty * TX + tx;
-  const int nx = d.nx, ny = d.ny;
-  const int k = z % a.nk, s = z / a.nk / a.nt;
-  const SubInfo sub = a.subs[s];
-  const double* qq = a.q + (long)z * d.plane;
-  const long fo = ((long)s * a.nk + k) * d.plane;
-  const long zo = (long)z * d.plane;
-  const double* dxa = met(a.M, d, M_DXA, s);
-  const double* dya = met(a.M, d, M_DYA, s);
-  const double* area = met(a.M, d, M_AREA, s);
-  const int ord = a.ord;
-  // cell halo only (not the +1 staggered row/column): copy_corners sources of points
-  // beyond it would leave the plane
-  auto inplane = [&](int i, int j) { return i >= -NG && i < nx + NG && j >= -NG && j < ny + NG; };
-  for (int p = tid; p < QX_R * QX_C; p += TX * TW) {
-    const int r = p / QX_C, c = p % QX_C;
-    const int i = i0 - 3 + c, j = j0 - 3 + r;
-    T.QX[r][c] = inplane(i, j) ? qq[CORNER ? cc_off(d, sub, i, j, 1) : pidx(d, i, j)] : 0.0;
-  }
-  for (int p = tid; p < QY_R * QY_C; p += TX * TW) {
-    const int r = p / QY_C, c = p % QY_C;
-    const int i = i0 - 3 + c, j = j0 - 3 + r;
-    T.QY[r][c] = inplane(i, j) ? qq[CORNER ? cc_off(d, sub, i, j, 2) : pidx(d, i, j)] : 0.0;
-  }
-  __syncthreads();
-  // inner fluxes: fx2 on x-edges i in [0, nx], rows [-3, ny+2]; fy2 on y-edges j in [0, ny], cols [-3, nx+2]
-  for (int p = tid; p < FX_R * FX_C; p += TX * TW) {
-    const int r = p / FX_C, c = p % FX_C;
-    const int i = i0 + c, j = j0 - 3 + r;
-    double v = 0.0;
-    if (i <= nx && j >= -NG && j <= ny + NG - 1) {
-      double qv[6], dx[6];
-#pragma unroll
-      for (int m = 0; m < 6; ++m) {
-        qv[m] = T.QX[r][c + m];
-        dx[m] = EX ? dxa[pidx(d, i - 3 + m, j)] : 0.0;
-      }
-      v = ppm_flux_o<EX>(ord, i + sub.ioff, sub.N, qv, dx, a.crx[fo + pidx(d, i, j)]);
-    }
-    T.FX2[r][c] = v;
-  }
-  for (int p = tid; p < FY_R * FY_C; p += TX * TW) {
-    const int r = p / FY_C, c = p % FY_C;
-    const int i = i0 - 3 + c, j = j0 + r;
-    double v = 0.0;
-    if (j <= ny && i >= -NG && i <= nx + NG - 1) {
-      double qv[6], dy[6];
-#pragma unroll
-      for (int m = 0; m < 6; ++m) {
-        qv[m] = T.QY[r + m][c];
-        dy[m] = EY ? dya[pidx(d, i, j - 3 + m)] : 0.0;
-      }
-      v = ppm_flux_o<EY>(ord, j + sub.joff, sub.N, qv, dy, a.cry[fo + pidx(d, i, j)]);
-    }
-    T.FY2[r][c] = v;
-  }
-  __syncthreads();
-  // advective updates q_i (rows [0, ny)) and q_j (cols [0, nx))
-  for (int p = tid; p < QI_R * QI_C; p += TX * TW) {
-    const int r = p / QI_C, c = p % QI_C;
-    const int i = i0 - 3 + c, j = j0 + r;
-    double v = 0.0;
-    if (j < ny && i >= -NG && i < nx + NG) {
-      const long o = pidx(d, i, j), on = pidx(d, i, j + 1);
-      const double fyy0 = a.yfx[fo + o] * T.FY2[r][c];
-      const double fyy1 = a.yfx[fo + on] * T.FY2[r + 1][c];
-      v = (T.QY[r + 3][c] * area[o] + fyy0 - fyy1) / a.ra_y[fo + o];
-    }
-    T.QI[r][c] = v;
-  }
-  for (int p = tid; p < QJ_R * QJ_C; p += TX * TW) {
-    const int r = p / QJ_C, c = p % QJ_C;
-    const int i = i0 + c, j = j0 - 3 + r;
-    double v = 0.0;
-    if (i < nx && j >= -NG && j < ny + NG) {
-      const long o = pidx(d, i, j), oe = pidx(d, i + 1, j);
-      const double fxx0 = a.xfx[fo + o] * T.FX2[r][c];
-      const double fxx1 = a.xfx[fo + oe] * T.FX2[r][c + 1];
-      v = (T.QX[r][c + 3] * area[o] + fxx0 - fxx1) / a.ra_x[fo + o];
-    }
-    T.QJ[r][c] = v;
-  }
-  __syncthreads();
-  // outer fluxes
-  for (int r = ty; r < TY; r += TW) {
-    const int c = tx;
-    const int i = i0 + c, j = j0 + r;
-    const long o = pidx(d, i, j);
-    if (j < ny && i <= nx) {
-      double qv[6], dx[6];
-#pragma unroll
-      for (int m = 0; m < 6; ++m) {
-        qv[m] = T.QI[r][c + m];
-        dx[m] = EX ? dxa[pidx(d, i - 3 + m, j)] : 0.0;
-      }
-      const double f = ppm_flux_o<EX>(ord, i + sub.ioff, sub.N, qv, dx, a.crx[fo + o]);
-      a.fx[zo + o] = 0.5 * (f + T.FX2[r + 3][c]) * a.mx[fo + o];
-    }
-    if (i < nx && j <= ny) {
-      double qv[6], dy[6];
-#pragma unroll
-      for (int m = 0; m < 6; ++m) {
-        qv[m] = T.QJ[r + m][c];
-        dy[m] = EY ? dya[pidx(d, i, j - 3 + m)] : 0.0;
-      }
-      const double f = ppm_flux_o<EY>(ord, j + sub.joff, sub.N, qv, dy, a.cry[fo + o]);
-      a.fy[zo + o] = 0.5 * (f + T.FY2[r][c + 3]) * a.my[fo + o];
-    }
-  }
-}
-
-__global__ void __launch_bounds__(TX * TW) tp_fused(TpK a) {
-  __shared__ TpTiles T;
-  const int i0 = blockIdx.x * TX, j0 = blockIdx.y * TY;
-  for (int z = blockIdx.z; z < a.nz; z += gridDim.z) {
-    const int s = z / a.nk / a.nt;
-    const SubInfo& sub = a.subs[s];
-    const int N = sub.N, I0 = i0 + sub.ioff, J0 = j0 + sub.joff;
-    // interfaces g-1..g+1 touched by this tile's fluxes: [I0-1, I0+TX+1] (x), [J0-1, J0+TY+1] (y)
-    const bool ex = !(I0 - 1 >= 2 && I0 + TX + 1 <= N - 2);
-    const bool ey = !(J0 - 1 >= 2 && J0 + TY + 1 <= N - 2);
-    const bool corner = (I0 - 3 < 0 || I0 + TX + 2 >= N) && (J0 - 3 < 0 || J0 + TY + 2 >= N);
-    __syncthreads();  // previous level's readers are done with the tiles
-    if (corner) tp_tile<true, true, true>(a, T, z, i0, j0);
-    else if (ex && ey) tp_tile<true, true, false>(a, T, z, i0, j0);
-    else if (ex) tp_tile<true, false, false>(a, T, z, i0, j0);
-    else if (ey) tp_tile<false, true, false>(a, T, z, i0, j0);
-    else tp_tile<false, false, false>(a, T, z, i0, j0);
-  }
-}
-
 // ---------------- fv_tp_2d, column-marching form (default) ----------------
 //
 // One wavefront owns a strip of 64 columns x = a-3 .. a+60 of one (sub-domain, level)
@@ -205,9 +31,11 @@ __global__ void __launch_bounds__(TX * TW) tp_fused(TpK a) {
 //   * writes fx on row r-3 (x-PPM of q_i through the LDS row) and fy on edge r-2.
 // The outputs are the 58 edges / columns a..a+57 (the outer three lanes on each side
 // are the x halo); the y halo costs six extra rows per segment.  Each step's loads are
-// issued one step ahead (MarchIn) so their latency overlaps the previous row's work.  Every expression and
-// region is that of the tile kernel above (bit-identical results); q, the Courant
+// issued ahead (MarchIn) so their latency overlaps the previous rows' work.  Every
+// expression follows tp_core / the oracle (bit-identical results); q, the Courant
 // numbers, the fluxes and the area terms stream through HBM once per strip and segment.
+// (An LDS-tiled form with 64 x 8 tiles, the first fused version, gave bit-identical
+// results and ran 1.9x slower at C180; removed with the ra_x / ra_y planes it read.)
 constexpr int MW = 64, MOUT = MW - 6, MWAVES = 4;
 typedef unsigned int TpU2 __attribute__((ext_vector_type(2)));
 
@@ -216,7 +44,7 @@ struct TpM {
   const SubInfo* subs;
   const double *M, *q;
   int nt, nk;
-  const double *crx, *cry, *xfx, *yfx, *ra_x, *ra_y, *mx, *my;
+  const double *crx, *cry, *xfx, *yfx, *mx, *my;
   double *fx, *fy;
   int nz, nstrip, nseg, seg;
 };
@@ -291,10 +119,14 @@ __device__ __forceinline__ double ppm_x_dpp(double q, double dx, int g, int N, d
 }
 
 // everything one row step reads from HBM, prefetched one step ahead
+// (ra_x / ra_y are not read: the march forms them from area and the fluxes it already
+// holds, ra_x = area + xfx|i - xfx|i+1 (x neighbour by DPP), ra_y = area + yfx|j - yfx|j+1
+// (previous row step), the expressions of ds_ra / ra_k / tracer_ra_k; without separate
+// mass fluxes (MF = false) mfx, mfy are xfx, yfx and come from registers too)
 struct MarchIn {
-  double qx, qy, crx, xfx, area_r, rax, dxr;  // row r
-  double cry, yfx, my;                        // edge r-2
-  double ray, mx, dxm;                        // row r-3
+  double qx, qy, crx, xfx, area_r, dxr;  // row r
+  double cry, yfx, my;                   // edge r-2
+  double mx, dxm;                        // row r-3
 };
 
 // y-direction PPM state rolled along the march: al at the last interface computed and
@@ -304,7 +136,7 @@ struct YRoll {
   PpmCell cell;
 };
 
-template <int ORD, bool EX, bool AHEAD2>
+template <int ORD, bool EX, bool AHEAD2, bool MF>
 __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   const Dims& d = a.d;
   const int lane = threadIdx.x & (MW - 1);
@@ -330,7 +162,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   const int PBy = (int)(d.plane * 8);
   auto rsrc = [&](const double* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, PBy, 0x00020000); };
   const auto rQ = rsrc(qq), rCRX = rsrc(a.crx + fo), rCRY = rsrc(a.cry + fo), rXFX = rsrc(a.xfx + fo);
-  const auto rYFX = rsrc(a.yfx + fo), rRAX = rsrc(a.ra_x + fo), rRAY = rsrc(a.ra_y + fo);
+  const auto rYFX = rsrc(a.yfx + fo);
   const auto rMX = rsrc(a.mx + fo), rMY = rsrc(a.my + fo), rAR = rsrc(area), rDXA = rsrc(dxa);
   const uint32_t vx = (uint32_t)xo * 8u;
   // dxa only enters the tile-edge interface values (ppm_al at g = 0, N reads the four
@@ -366,17 +198,15 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     v.crx = bl(rCRX, vx, so);
     v.xfx = bl(rXFX, vx, so);
     v.area_r = bl(rAR, vx, so);
-    v.rax = bl(rRAX, vx, so);
     v.dxr = EX ? bl(rDXA, vxd, so) : 0.0;
     const int re = r - 2 < -NG ? -NG : r - 2;
     const uint32_t se = (uint32_t)(re + NG) * rowb;
     v.cry = bl(rCRY, vx, se);
     v.yfx = bl(rYFX, vx, se);
-    v.my = bl(rMY, vx, se);
+    v.my = MF ? bl(rMY, vx, se) : 0.0;
     const int rm = r - 3 < -NG ? -NG : r - 3;
     const uint32_t sm = (uint32_t)(rm + NG) * rowb;
-    v.ray = bl(rRAY, vx, sm);
-    v.mx = bl(rMX, vx, sm);
+    v.mx = MF ? bl(rMX, vx, sm) : 0.0;
     v.dxm = EX ? bl(rDXA, vxd, sm) : 0.0;
     return v;
   };
@@ -396,10 +226,12 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   double qyw[4], qjw[4];  // rows r-3 .. r
   double hf2[4], hcx[4];  // fx2 and crx of rows r-3 .. r
   double arw[4];          // cell area of rows r-3 .. r (read once per row)
+  double hxf[4];          // xfx of rows r-3 .. r (the mass flux mfx when MF = false)
 #pragma unroll
-  for (int m = 0; m < 4; ++m) qyw[m] = qjw[m] = hf2[m] = hcx[m] = arw[m] = 0.0;
+  for (int m = 0; m < 4; ++m) qyw[m] = qjw[m] = hf2[m] = hcx[m] = arw[m] = hxf[m] = 0.0;
   YRoll ry{}, rj{};  // q (y fill) and q_j
   double fyy_prev = 0.0;
+  double yfx_prev = 0.0;  // yfx at edge r-3 (the previous row step's edge r-2)
 
   // lane predicates (constant along the march)
   const bool l_fx2 = x >= 0 && x <= nx, l_qj = x >= 0 && x < nx;
@@ -408,6 +240,14 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   const auto rFX = rsrc(a.fx + zo), rFY = rsrc(a.fy + zo);
   auto bst = [&](__amdgpu_buffer_rsrc_t r, uint32_t soff, double v) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(TpU2, v), r, vx, soff, 0);
+  };
+  // lane-predicated store without a branch: a lane that must not store addresses past the
+  // end of the plane (the descriptor's range check drops the write), so the steady rows
+  // stay one basic block the scheduler can interleave across the three unrolled rows
+  constexpr uint32_t OOB = 0x80000000u;
+  const uint32_t vfy = s_fy ? vx : OOB, vfx = s_fx ? vx : OOB;
+  auto bstv = [&](__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(TpU2, v), r, voff, soff, 0);
   };
 
   // One row step.  GEN: the generic step (row clamps, segment ends, tile-edge rows of the
@@ -423,14 +263,12 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
       nxt.crx = bl(rCRX, vx, so);
       nxt.xfx = bl(rXFX, vx, so);
       nxt.area_r = bl(rAR, vx, so);
-      nxt.rax = bl(rRAX, vx, so);
       nxt.dxr = EX ? bl(rDXA, vxd, so) : 0.0;
       const uint32_t se = so - 2 * rowb, sm = so - 3 * rowb;
       nxt.cry = bl(rCRY, vx, se);
       nxt.yfx = bl(rYFX, vx, se);
-      nxt.my = bl(rMY, vx, se);
-      nxt.ray = bl(rRAY, vx, sm);
-      nxt.mx = bl(rMX, vx, sm);
+      nxt.my = MF ? bl(rMY, vx, se) : 0.0;
+      nxt.mx = MF ? bl(rMX, vx, sm) : 0.0;
       nxt.dxm = EX ? bl(rDXA, vxd, sm) : 0.0;
   };
   // ahead: how many rows ahead the steady step prefetches (1, or 2 in the three-buffer loop)
@@ -448,9 +286,10 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     }
     const double fxx = cur.xfx * fx2;
     const double fxx_e = dpp_next(fxx);
+    const double rax = cur.area_r + cur.xfx - dpp_next(cur.xfx);
     double qj;
     {
-      const double v = (cur.qx * cur.area_r + fxx - fxx_e) / cur.rax;
+      const double v = (cur.qx * cur.area_r + fxx - fxx_e) / rax;
       const bool ok = GEN ? l_qj && r >= -NG && r < ny + NG : l_qj;
       qj = ok ? v : 0.0;
     }
@@ -461,12 +300,15 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
       hf2[m] = hf2[m + 1];
       hcx[m] = hcx[m + 1];
       arw[m] = arw[m + 1];
+      hxf[m] = hxf[m + 1];
     }
     qyw[3] = cur.qy;
     qjw[3] = qj;
     hf2[3] = fx2;
     hcx[3] = cur.crx;
     arw[3] = cur.area_r;
+    hxf[3] = cur.xfx;
+    const double my = MF ? cur.my : cur.yfx, mx = MF ? cur.mx : hxf[0];
 
     // ---- y PPM pieces: interface r-1, cell r-2 (both windows)
     const int e = r - 2;
@@ -493,18 +335,27 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
       double fy2 = ppm_edge_flux(cym, cy, cur.cry);
       if (!(GEN ? e <= ny && l_fy2 : l_fy2)) fy2 = 0.0;
       const double fyy = !GEN || e <= ny ? cur.yfx * fy2 : 0.0;
-      if (GEN ? s_fy && e <= ny && (e < j1 || last) : s_fy)
-        bst(rFY, se, 0.5 * (ppm_edge_flux(cjm, cj, cur.cry) + fy2) * cur.my);
+      if (GEN) {
+        if (s_fy && e <= ny && (e < j1 || last)) bst(rFY, se, 0.5 * (ppm_edge_flux(cjm, cj, cur.cry) + fy2) * my);
+      } else {
+        bstv(rFY, vfy, se, 0.5 * (ppm_edge_flux(cjm, cj, cur.cry) + fy2) * my);
+      }
       // ---- row m = r-3: q_i, outer x flux fx
       const int mrow = r - 3;
       if (!GEN || (mrow >= j0 && mrow < ny)) {
-        const double v = (qyw[0] * arw[0] + fyy_prev - fyy) / cur.ray;
+        const double ray = arw[0] + yfx_prev - cur.yfx;
+        const double v = (qyw[0] * arw[0] + fyy_prev - fyy) / ray;
         const double qi = cin ? v : 0.0;
         const double f = ppm_x_dpp<ORD, EX>(qi, cur.dxm, I, N, hcx[0]);
-        if (GEN ? s_fx && mrow < j1 : s_fx) bst(rFX, se - rowb, 0.5 * (f + hf2[0]) * cur.mx);
+        if (GEN) {
+          if (s_fx && mrow < j1) bst(rFX, se - rowb, 0.5 * (f + hf2[0]) * mx);
+        } else {
+          bstv(rFX, vfx, se - rowb, 0.5 * (f + hf2[0]) * mx);
+        }
       }
       fyy_prev = fyy;
     }
+    yfx_prev = cur.yfx;
   };
 
   // steady rows: 2 <= G <= N-2 for the y interpolant's interface G = r-1, rows r+1 (the
@@ -552,7 +403,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
 
 // AHEAD2: steady rows prefetch two rows ahead (three row buffers, 149 VGPRs, three
 // waves per SIMD); otherwise one row ahead (two buffers, <= 128 VGPRs, four waves)
-template <int ORD, bool AHEAD2>
+template <int ORD, bool AHEAD2, bool MF>
 __global__ void __launch_bounds__(MW * MWAVES, AHEAD2 ? 1 : 4) tp_march(TpM a) {
   // wave index through readfirstlane: everything derived from it (plane, strip, segment,
   // buffer descriptors, row offsets) is then provably wave-uniform (SGPRs, no waterfalls)
@@ -569,8 +420,8 @@ __global__ void __launch_bounds__(MW * MWAVES, AHEAD2 ? 1 : 4) tp_march(TpM a) {
   const int j1 = j0 + a.seg < a.d.ny ? j0 + a.seg : a.d.ny;
   const int A = strip * MOUT + sub.ioff;
   const bool ex = !(A - 1 >= 2 && A + MOUT + 1 <= sub.N - 2);
-  if (ex) tp_march_strip<ORD, true, AHEAD2>(a, (int)z, strip, j0, j1);
-  else tp_march_strip<ORD, false, AHEAD2>(a, (int)z, strip, j0, j1);
+  if (ex) tp_march_strip<ORD, true, AHEAD2, MF>(a, (int)z, strip, j0, j1);
+  else tp_march_strip<ORD, false, AHEAD2, MF>(a, (int)z, strip, j0, j1);
 }
 
 // ---------------- tracer_2d_1l ----------------
@@ -665,20 +516,6 @@ __global__ void __launch_bounds__(256) tracer_split_k(Dims d, const double* __re
   }
 }
 
-__global__ void __launch_bounds__(256) tracer_ra_k(Dims d, const double* __restrict__ M, int npz,
-                                                   const double* __restrict__ xfx, const double* __restrict__ yfx,
-                                                   double* __restrict__ ra_x, double* __restrict__ ra_y) {
-  Launch2D L{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  int i, j;
-  if (!thread_point(L, i, j)) return;
-  const int z = blockIdx.z, s = z / npz;
-  const long fo = (long)z * d.plane;
-  const long o = pidx(d, i, j);
-  const double area = met(M, d, M_AREA, s)[o];
-  if (i >= 0 && i < d.nx) ra_x[fo + o] = area + xfx[fo + o] - xfx[fo + pidx(d, i + 1, j)];
-  if (j >= 0 && j < d.ny) ra_y[fo + o] = area + yfx[fo + o] - yfx[fo + pidx(d, i, j + 1)];
-}
-
 __global__ void __launch_bounds__(256) tracer_dp2_k(Dims d, const double* __restrict__ M, int npz,
                                                     const double* __restrict__ dp1, const double* __restrict__ mfx,
                                                     const double* __restrict__ mfy, double* __restrict__ dp2) {
@@ -722,38 +559,36 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
   const Dims& d = c.d;
   long nz = (long)d.nsub * a.nt * a.nk;
   if (a.ord != 5 && a.ord != 6) throw std::runtime_error("fv_tp_2d: hord must be 5 or 6");
-  if (a.cfg == 0) {  // LDS-tiled form (kept for comparison: tools/tp_bench.py)
-    TpK k{d, c.subs, c.met, a.q, a.nt, a.nk, a.crx, a.cry, a.xfx, a.yfx, a.ra_x, a.ra_y,
-          a.mfx ? a.mfx : a.xfx, a.mfy ? a.mfy : a.yfx, a.fx, a.fy, a.ord, (int)nz};
-    dim3 g(cdiv(d.nx + 1, TX), cdiv(d.ny + 1, TY), (unsigned)(nz < ZMAX ? nz : ZMAX));
-    GT_LAUNCH(tp_fused, g, dim3(TX, TW), 0, c.st, k);
-  } else {
+  {
     // segment length: cfg >= 8 selects it (tuning); default 45 rows (C180: 4 segments)
     static const int seg_env = [] {
       const char* e = getenv("GTFV3_TP_SEG");  // tuning override of the default segment
       return e ? atoi(e) : 0;
     }();
     const int seg = a.cfg >= 8 ? a.cfg : (seg_env >= 8 ? seg_env : 45);
-    TpM m{d, c.subs, c.met, a.q, a.nt, a.nk, a.crx, a.cry, a.xfx, a.yfx, a.ra_x, a.ra_y,
+    TpM m{d, c.subs, c.met, a.q, a.nt, a.nk, a.crx, a.cry, a.xfx, a.yfx,
           a.mfx ? a.mfx : a.xfx, a.mfy ? a.mfy : a.yfx, a.fx, a.fy, (int)nz, 0, 0, seg};
     m.nstrip = (d.nx + 1 + MOUT - 1) / MOUT;
     m.nseg = (d.ny + seg - 1) / seg;
     const long waves = nz * m.nstrip * m.nseg;
     if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
     const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
-    if (a.cfg == -2) {  // tuning: one-row-ahead variant
-      if (a.ord == 5) GT_LAUNCH((tp_march<5, false>), g, b, 0, c.st, m);
-      else GT_LAUNCH((tp_march<6, false>), g, b, 0, c.st, m);
+    // (the one-row-ahead form, tp_march<ORD, false>, measured 3 % slower at C180)
+    // MF: separate mass fluxes (w, pt and the tracers) or xfx / yfx themselves
+    if (a.mfx) {
+      if (a.ord == 5) GT_LAUNCH((tp_march<5, true, true>), g, b, 0, c.st, m);
+      else GT_LAUNCH((tp_march<6, true, true>), g, b, 0, c.st, m);
     } else {
-      if (a.ord == 5) GT_LAUNCH((tp_march<5, true>), g, b, 0, c.st, m);
-      else GT_LAUNCH((tp_march<6, true>), g, b, 0, c.st, m);
+      if (a.ord == 5) GT_LAUNCH((tp_march<5, true, false>), g, b, 0, c.st, m);
+      else GT_LAUNCH((tp_march<6, true, false>), g, b, 0, c.st, m);
     }
   }
   HIP_LAUNCH_CHECK();
-  // algorithmic bytes: q read + fx, fy written per plane; crx cry xfx yfx ra_x ra_y (+ mfx mfy)
-  // read once per (sub-domain, level) however many tracers share them
+  // algorithmic bytes: q read + fx, fy written per plane; crx cry xfx yfx (+ mfx mfy) read
+  // once per (sub-domain, level) however many tracers share them (ra_x, ra_y are formed
+  // in the kernel, the 2-D area plane is not counted)
   const double cells = (double)d.nx * d.ny;
-  ktimer_bytes(8.0 * cells * (3.0 * nz + (double)d.nsub * a.nk * (6 + (a.mfx ? 2 : 0))));
+  ktimer_bytes(8.0 * cells * (3.0 * nz + (double)d.nsub * a.nk * (4 + (a.mfx ? 2 : 0))));
 }
 
 void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, double* xfx, double* yfx, double* ra_x,
@@ -774,10 +609,7 @@ void tracer_split(const Ctx& c, int npz, const int* nsplt_dev, double* cx, doubl
   GT_LAUNCH(tracer_split_k, dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
                      c.met, npz, nsplt_dev, cx, cy, xfx, yfx, mfx, mfy, ra_x, ra_y);
   HIP_LAUNCH_CHECK();
-  Launch2D L2{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  GT_LAUNCH(tracer_ra_k, dim3(cdiv(L2.ni, BX), cdiv(L2.nj, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
-                     c.met, npz, xfx, yfx, ra_x, ra_y);
-  HIP_LAUNCH_CHECK();
+  // (no ra_x / ra_y planes: fv_tp_2d forms them from area and the split fluxes)
 }
 
 void tracer_dp2(const Ctx& c, int npz, const double* dp1, const double* mfx, const double* mfy, double* dp2) {

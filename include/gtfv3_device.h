@@ -66,7 +66,7 @@ void* gtfv3_stream(void* h);
 int gtfv3_timers(void* h, char* buf, int len);
 /* per-kernel HIP-event timing (off by default); enabling resets the statistics */
 int gtfv3_kernel_timing(void* h, int on);
-/* time only the kernel with this launch name (e.g. "tp_march<6>"); NULL or "": all */
+/* time only this kernel family (name without template arguments, e.g. "tp_march"); NULL or "": all */
 int gtfv3_kernel_timing_filter(void* h, const char* kernel);
 /* per-kernel totals since enabling, "kernel=ms,launches;..." into buf */
 int gtfv3_kernel_stats(void* h, char* buf, int len);

@@ -19,7 +19,7 @@ def main():
     ap.add_argument("--npx", type=int, default=181)
     ap.add_argument("--npz", type=int, default=72)
     ap.add_argument("--reps", type=int, default=10)
-    ap.add_argument("--cfgs", default="0,-1,30,45,60,90")
+    ap.add_argument("--cfgs", default="-1,30,45,60,90")
     a = ap.parse_args()
     import torch
     import gtfv3_pkg
