@@ -48,6 +48,9 @@ HaloExchanger::~HaloExchanger() {
   }
   if (sendbuf_) (void)hipFree(sendbuf_);
   if (recvbuf_) (void)hipFree(recvbuf_);
+  if (ev_packed_) (void)hipEventDestroy(ev_packed_);
+  if (ev_recvd_) (void)hipEventDestroy(ev_recvd_);
+  if (comm_st_) (void)hipStreamDestroy(comm_st_);
 }
 
 void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d, int max_nk,
@@ -168,6 +171,11 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
     HIP_CHECK(hipMalloc(&sendbuf_, sizeof(double) * buf_elems_));
     HIP_CHECK(hipMalloc(&recvbuf_, sizeof(double) * buf_elems_));
   }
+  if (nranks_ > 1) {
+    HIP_CHECK(hipStreamCreateWithFlags(&comm_st_, hipStreamNonBlocking));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_packed_, hipEventDisableTiming));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_recvd_, hipEventDisableTiming));
+  }
 }
 
 std::vector<int> HaloExchanger::remote_table(int kind, int dir) const {
@@ -185,97 +193,133 @@ std::vector<int> HaloExchanger::remote_table(int kind, int dir) const {
 
 namespace {
 
-__global__ void halo_local_kernel(const HaloEntry* __restrict__ tab, int n, int nk, long plane,
-                                  double* __restrict__ p0, double* __restrict__ p1) {
-  int e = blockIdx.x * blockDim.x + threadIdx.x;
-  int k = blockIdx.y;
-  if (e >= n) return;
-  HaloEntry h = tab[e];
+// All fields of one exchange in one launch per stage (grid z = field, y = level):
+// up to HB fields; the per-field table, extent and pointers are picked by a uniform
+// compare chain (no dynamically indexed kernel-argument array, no scratch).
+constexpr int HB = 8;
+struct HaloBatch {
+  const void* tab[HB];
+  int n[HB], nk[HB];
+  double* p0[HB];
+  double* p1[HB];
+  long boff[HB];  // field offset in the pack buffers
+};
+struct HaloSel {
+  const void* tab;
+  int n, nk;
+  double *p0, *p1;
+  long boff;
+};
+__device__ __forceinline__ HaloSel halo_sel(const HaloBatch b, int f) {  // by value: no reference to the kernel argument
+  HaloSel r{b.tab[0], b.n[0], b.nk[0], b.p0[0], b.p1[0], b.boff[0]};
+#pragma unroll
+  for (int q = 1; q < HB; ++q)
+    if (f == q) r = HaloSel{b.tab[q], b.n[q], b.nk[q], b.p0[q], b.p1[q], b.boff[q]};
+  return r;
+}
+
+__global__ void halo_local_kernel(HaloBatch b, long plane) {
+  const HaloSel F = halo_sel(b, blockIdx.z);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (e >= F.n || k >= F.nk) return;
+  const HaloEntry h = static_cast<const HaloEntry*>(F.tab)[e];
   double v = 0.0;
   if (h.src_sub >= 0) {
-    const double* src = (h.comp & 2) ? p1 : p0;
-    v = h.sign * src[((long)h.src_sub * nk + k) * plane + h.src_off];
+    const double* src = (h.comp & 2) ? F.p1 : F.p0;
+    v = h.sign * src[((long)h.src_sub * F.nk + k) * plane + h.src_off];
   }
-  double* dst = (h.comp & 1) ? p1 : p0;
-  dst[((long)h.dst_sub * nk + k) * plane + h.dst_off] = v;
+  double* dst = (h.comp & 1) ? F.p1 : F.p0;
+  dst[((long)h.dst_sub * F.nk + k) * plane + h.dst_off] = v;
 }
 
-__global__ void halo_pack_kernel(const PackEntry* __restrict__ tab, int n, int nk, long plane,
-                                 const double* __restrict__ p0, const double* __restrict__ p1,
-                                 double* __restrict__ buf) {
-  int e = blockIdx.x * blockDim.x + threadIdx.x;
-  int k = blockIdx.y;
-  if (e >= n) return;
-  PackEntry h = tab[e];
-  const double* src = h.comp ? p1 : p0;
-  buf[(long)h.pstart * nk + (long)k * h.pcount + (e - h.pstart)] =
-      h.sign * src[((long)h.sub * nk + k) * plane + h.off];
+__global__ void halo_pack_kernel(HaloBatch b, long plane, double* __restrict__ buf) {
+  const HaloSel F = halo_sel(b, blockIdx.z);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (e >= F.n || k >= F.nk) return;
+  const PackEntry h = static_cast<const PackEntry*>(F.tab)[e];
+  const double* src = h.comp ? F.p1 : F.p0;
+  buf[F.boff + (long)h.pstart * F.nk + (long)k * h.pcount + (e - h.pstart)] =
+      h.sign * src[((long)h.sub * F.nk + k) * plane + h.off];
 }
 
-__global__ void halo_unpack_kernel(const PackEntry* __restrict__ tab, int n, int nk, long plane,
-                                   double* __restrict__ p0, double* __restrict__ p1,
-                                   const double* __restrict__ buf) {
-  int e = blockIdx.x * blockDim.x + threadIdx.x;
-  int k = blockIdx.y;
-  if (e >= n) return;
-  PackEntry h = tab[e];
-  double* dst = h.comp ? p1 : p0;
-  dst[((long)h.sub * nk + k) * plane + h.off] = buf[(long)h.pstart * nk + (long)k * h.pcount + (e - h.pstart)];
+__global__ void halo_unpack_kernel(HaloBatch b, long plane, const double* __restrict__ buf) {
+  const HaloSel F = halo_sel(b, blockIdx.z);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int k = blockIdx.y;
+  if (e >= F.n || k >= F.nk) return;
+  const PackEntry h = static_cast<const PackEntry*>(F.tab)[e];
+  double* dst = h.comp ? F.p1 : F.p0;
+  dst[((long)h.sub * F.nk + k) * plane + h.off] = buf[F.boff + (long)h.pstart * F.nk + (long)k * h.pcount + (e - h.pstart)];
 }
 
 }  // namespace
 
 void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream) {
-  // remote part first (pack + post), then local gather while messages fly
-  bool remote = nranks_ > 1;
-  size_t off = 0;
+  const bool remote = nranks_ > 1;
   std::vector<size_t> foff(nf);
   if (remote) {
-    size_t need = 0;
-    for (int f = 0; f < nf; ++f)
-      need += (size_t)std::max(n_send_[fields[f].kind], n_recv_[fields[f].kind]) * fields[f].nk;
-    if (need > buf_elems_) throw std::runtime_error("halo: exchange buffer too small");
+    size_t off = 0;
     for (int f = 0; f < nf; ++f) {
-      const HaloField& F = fields[f];
       foff[f] = off;
-      int n = n_send_[F.kind];
-      if (n) {
-        GT_LAUNCH(halo_pack_kernel, dim3(cdiv(n, 256), F.nk), dim3(256), 0, stream,
-                           d_send_[F.kind], n, F.nk, d_.plane, F.p[0], F.p[1] ? F.p[1] : F.p[0],
-                           sendbuf_ + off);
-        HIP_LAUNCH_CHECK();
-      }
-      off += (size_t)std::max(n_send_[F.kind], n_recv_[F.kind]) * F.nk;
+      off += (size_t)std::max(n_send_[fields[f].kind], n_recv_[fields[f].kind]) * fields[f].nk;
     }
+    if (off > buf_elems_) throw std::runtime_error("halo: exchange buffer too small");
     if (!tr_) throw std::runtime_error("halo: multi-rank exchange without a transport");
+  }
+  // one launch per stage for (up to HB) fields; stage 0 local gather, 1 pack, 2 unpack
+  auto launch = [&](int stage) {
+    for (int f0 = 0; f0 < nf; f0 += HB) {
+      HaloBatch b{};
+      int nb = 0, maxn = 0, maxk = 0;
+      for (int f = f0; f < nf && f < f0 + HB; ++f) {
+        const HaloField& F = fields[f];
+        const int n = stage == 0 ? n_local_[F.kind] : (stage == 1 ? n_send_[F.kind] : n_recv_[F.kind]);
+        if (!n) continue;
+        b.tab[nb] = stage == 0 ? (const void*)d_local_[F.kind]
+                               : (stage == 1 ? (const void*)d_send_[F.kind] : (const void*)d_recv_[F.kind]);
+        b.n[nb] = n;
+        b.nk[nb] = F.nk;
+        b.p0[nb] = F.p[0];
+        b.p1[nb] = F.p[1] ? F.p[1] : F.p[0];
+        b.boff[nb] = stage ? (long)foff[f] : 0;
+        maxn = std::max(maxn, n);
+        maxk = std::max(maxk, F.nk);
+        ++nb;
+      }
+      if (!nb) continue;
+      const dim3 g(cdiv(maxn, 256), maxk, nb);
+      if (stage == 0) GT_LAUNCH(halo_local_kernel, g, dim3(256), 0, stream, b, d_.plane);
+      else if (stage == 1) GT_LAUNCH(halo_pack_kernel, g, dim3(256), 0, stream, b, d_.plane, sendbuf_);
+      else GT_LAUNCH(halo_unpack_kernel, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
+      HIP_LAUNCH_CHECK();
+    }
+  };
+  if (remote) {
+    // pack on the compute stream, messages on the comm stream (after the pack), the
+    // same-rank gather on the compute stream meanwhile, then the unpack after the
+    // messages.  The next exchange's pack follows this unpack in stream order, so the
+    // pack buffers are never rewritten while a send may still read them.
+    launch(1);
+    HIP_CHECK(hipEventRecord(ev_packed_, stream));
+    HIP_CHECK(hipStreamWaitEvent(comm_st_, ev_packed_, 0));
     tr_->group_start();
     for (int f = 0; f < nf; ++f) {
       const HaloField& F = fields[f];
       for (int p = 0; p < nranks_; ++p) {
         int ns = send_peer_count_[F.kind][p], nr = recv_peer_count_[F.kind][p];
-        if (ns) tr_->send(sendbuf_ + foff[f] + (size_t)send_peer_start_[F.kind][p] * F.nk, (size_t)ns * F.nk, p, stream);
-        if (nr) tr_->recv(recvbuf_ + foff[f] + (size_t)recv_peer_start_[F.kind][p] * F.nk, (size_t)nr * F.nk, p, stream);
+        if (ns) tr_->send(sendbuf_ + foff[f] + (size_t)send_peer_start_[F.kind][p] * F.nk, (size_t)ns * F.nk, p, comm_st_);
+        if (nr) tr_->recv(recvbuf_ + foff[f] + (size_t)recv_peer_start_[F.kind][p] * F.nk, (size_t)nr * F.nk, p, comm_st_);
       }
     }
-    tr_->group_end(stream);
+    tr_->group_end(comm_st_);
+    HIP_CHECK(hipEventRecord(ev_recvd_, comm_st_));
   }
-  for (int f = 0; f < nf; ++f) {
-    const HaloField& F = fields[f];
-    int n = n_local_[F.kind];
-    if (!n) continue;
-    GT_LAUNCH(halo_local_kernel, dim3(cdiv(n, 256), F.nk), dim3(256), 0, stream, d_local_[F.kind], n,
-                       F.nk, d_.plane, F.p[0], F.p[1] ? F.p[1] : F.p[0]);
-    HIP_LAUNCH_CHECK();
-  }
+  launch(0);
   if (remote) {
-    for (int f = 0; f < nf; ++f) {
-      const HaloField& F = fields[f];
-      int n = n_recv_[F.kind];
-      if (!n) continue;
-      GT_LAUNCH(halo_unpack_kernel, dim3(cdiv(n, 256), F.nk), dim3(256), 0, stream, d_recv_[F.kind], n,
-                         F.nk, d_.plane, F.p[0], F.p[1] ? F.p[1] : F.p[0], recvbuf_ + foff[f]);
-      HIP_LAUNCH_CHECK();
-    }
+    HIP_CHECK(hipStreamWaitEvent(stream, ev_recvd_, 0));
+    launch(2);
   }
 }
 

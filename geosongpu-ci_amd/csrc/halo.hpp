@@ -68,6 +68,10 @@ class HaloExchanger {
   double* sendbuf_ = nullptr;
   double* recvbuf_ = nullptr;
   size_t buf_elems_ = 0;
+  // multi-rank: the point-to-point messages run on their own stream, so the same-rank
+  // gather (and whatever precedes the unpack) overlaps them
+  hipStream_t comm_st_ = nullptr;
+  hipEvent_t ev_packed_ = nullptr, ev_recvd_ = nullptr;
 };
 
 }  // namespace gtfv3
