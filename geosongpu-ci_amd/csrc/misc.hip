@@ -138,7 +138,10 @@ __global__ void fill_k(long n, double a, double* __restrict__ x) {
   for (; t < n; t += stride) x[t] = a;
 }
 
-inline dim3 g2(const Dims& d, const Launch2D& L, int nz) { return dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), nz); }
+inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
+  (void)d;
+  return plane_grid(L, nz);
+}
 
 }  // namespace
 

@@ -725,7 +725,10 @@ __global__ void scale_k(long n, double a, const double* __restrict__ x, double* 
   for (; t < n; t += stride) y[t] = a * x[t];
 }
 
-inline dim3 g2(const Dims& d, const Launch2D& L, int nz) { return dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), nz); }
+inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
+  (void)d;
+  return plane_grid(L, nz);
+}
 
 }  // namespace
 

@@ -19,7 +19,10 @@ __device__ __forceinline__ const double* met(const double* __restrict__ M, const
   return M + ((long)metric * d.nsub + s) * d.plane;
 }
 
-// Block shape for plane-parallel stencils: one wavefront row of 64 columns x 4 rows.
+// Block shape for plane-parallel stencils: 256 threads (64 x 4).  thread_point maps the
+// block's threads onto the launch region flattened row-major (i fastest), so the waves are
+// full whatever the region's width (a 91-wide sub-domain row in 64-wide blocks left 29 %
+// of the lanes idle) and consecutive lanes still read consecutive i.
 constexpr int BX = 64, BY = 4;
 
 struct Launch2D {
@@ -28,9 +31,16 @@ struct Launch2D {
 };
 
 __device__ __forceinline__ bool thread_point(const Launch2D& L, int& i, int& j) {
-  i = L.i0 + (int)(blockIdx.x * BX + threadIdx.x);
-  j = L.j0 + (int)(blockIdx.y * BY + threadIdx.y);
-  return i < L.i0 + L.ni && j < L.j0 + L.nj;
+  const int t = (int)(blockIdx.x * (BX * BY) + threadIdx.y * BX + threadIdx.x);
+  if (t >= L.ni * L.nj) return false;
+  j = t / L.ni;
+  i = L.i0 + (t - j * L.ni);
+  j += L.j0;
+  return true;
+}
+// grid for thread_point over region L and nz planes (blockIdx.z)
+inline dim3 plane_grid(const Launch2D& L, long nz) {
+  return dim3((unsigned)(((long)L.ni * L.nj + BX * BY - 1) / (BX * BY)), 1, (unsigned)nz);
 }
 
 // FV3 copy_corners source cell (global indices) for a cube-corner halo cell,

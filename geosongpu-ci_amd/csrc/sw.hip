@@ -579,7 +579,10 @@ __global__ void __launch_bounds__(256) ds_uv(Dims d, const SubInfo* __restrict__
   if (j < d.ny) AT(v, 0, 0) = AT(v, 0, 0) * MA(MT(M_DY), 0, 0) + AT(ke, 0, 0) - AT(ke, 0, 1) - AT(fxv, 0, 0);
 }
 
-inline dim3 g2(const Dims& d, const Launch2D& L, int nz) { return dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), nz); }
+inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
+  (void)d;
+  return plane_grid(L, nz);
+}
 
 }  // namespace
 

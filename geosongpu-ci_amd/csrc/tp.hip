@@ -606,7 +606,7 @@ void tracer_split(const Ctx& c, int npz, const int* nsplt_dev, double* cx, doubl
                   double* mfx, double* mfy, double* ra_x, double* ra_y) {
   const Dims& d = c.d;
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  GT_LAUNCH(tracer_split_k, dim3(cdiv(L.ni, BX), cdiv(L.nj, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
+  GT_LAUNCH(tracer_split_k, plane_grid(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d,
                      c.met, npz, nsplt_dev, cx, cy, xfx, yfx, mfx, mfy, ra_x, ra_y);
   HIP_LAUNCH_CHECK();
   // (no ra_x / ra_y planes: fv_tp_2d forms them from area and the split fluxes)
@@ -614,7 +614,7 @@ void tracer_split(const Ctx& c, int npz, const int* nsplt_dev, double* cx, doubl
 
 void tracer_dp2(const Ctx& c, int npz, const double* dp1, const double* mfx, const double* mfy, double* dp2) {
   const Dims& d = c.d;
-  GT_LAUNCH(tracer_dp2_k, dim3(cdiv(d.nx, BX), cdiv(d.ny, BY), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
+  GT_LAUNCH(tracer_dp2_k, plane_grid(Launch2D{0, 0, d.nx, d.ny}, d.nsub * npz), dim3(BX, BY), 0, c.st, d,
                      c.met, npz, dp1, mfx, mfy, dp2);
   HIP_LAUNCH_CHECK();
 }
@@ -624,7 +624,7 @@ void tracer_update(const Ctx& c, int npz, int nq, double* q, const double* qn, c
   (void)qn;
   const Dims& d = c.d;
   long nz = (long)d.nsub * nq * npz;
-  GT_LAUNCH(tracer_update_k, dim3(cdiv(d.nx, BX), cdiv(d.ny, BY), (unsigned)(nz < ZMAX ? nz : ZMAX)),
+  GT_LAUNCH(tracer_update_k, plane_grid(Launch2D{0, 0, d.nx, d.ny}, nz < ZMAX ? nz : ZMAX),
                      dim3(BX, BY), 0, c.st, d, c.met, npz, nq, q, dp1, dp2, fx, fy, nsplt_dev, it, (int)nz);
   HIP_LAUNCH_CHECK();
 }
