@@ -4,6 +4,7 @@
 // Column kernels put one (i,j) column per lane: a wavefront covers 64 consecutive
 // i, so every k-plane access is coalesced; per-column work arrays are planes of
 // scratch fields (same [sub][k][plane] layout).
+#include <algorithm>
 #include <climits>
 
 #include "kernels_nh.hpp"
@@ -806,8 +807,13 @@ void a2b_ord4_multi(const Ctx& c, int nf, const int* nk, const double* const* q,
   HIP_LAUNCH_CHECK();
   // interior corners: column-marching kernel (balanced segments of at most 46 corner
   // rows: C180 has 181 corner rows -> 4 x 46, not 4 x 45 + 1)
+  // (more, shorter segments, down to 15 rows, when the launch would have fewer than ~6900
+  // waves: small sub-domains on 4-8 GPUs)
   A2bM m{d, c.subs, c.met, F, (int)nz, (int)cdiv(d.nx + 1, AM_OUT), 0, 0};
-  m.nseg = (int)cdiv(d.ny + 1, 46);
+  {
+    const long want = cdiv(6912, nz * m.nstrip);
+    m.nseg = (int)std::max<long>(cdiv(d.ny + 1, 46), std::min<long>(cdiv(d.ny + 1, 15), want));
+  }
   m.seg = (int)cdiv(d.ny + 1, m.nseg);
   const long waves = (long)m.nz * m.nstrip * m.nseg;
   GT_LAUNCH(a2b_march_k, dim3(cdiv(waves, AM_WAVES)), dim3(AM_W * AM_WAVES), 0, c.st, m);

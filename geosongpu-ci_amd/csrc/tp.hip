@@ -7,6 +7,7 @@
 //   fx = 0.5*(xppm(q_i) + fx2)*mfx     fy = 0.5*(yppm(q_j) + fy2)*mfy
 // Operation order inside each expression follows the Fortran so the fp64
 // numpy oracle (oracle/fv3.py) matches to the last bits.
+#include <algorithm>
 #include <cstdlib>
 #include <type_traits>
 
@@ -565,10 +566,19 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
       const char* e = getenv("GTFV3_TP_SEG");  // tuning override of the default segment
       return e ? atoi(e) : 0;
     }();
-    const int seg = a.cfg >= 8 ? a.cfg : (seg_env >= 8 ? seg_env : 45);
+    // Default: segments of <= 45 rows, more (down to 15 rows) when the launch would
+    // otherwise have fewer than ~6900 waves (the C180 wave count on one GPU; small
+    // sub-domains, as on 4-8 GPUs, need the shorter segments to fill the chip).
+    const int nstrip = (d.nx + 1 + MOUT - 1) / MOUT;
+    int seg = a.cfg >= 8 ? a.cfg : seg_env;
+    if (seg < 8) {
+      const long want = (6912 + nz * nstrip - 1) / (nz * nstrip);
+      const long nseg = std::max<long>((d.ny + 44) / 45, std::min<long>((d.ny + 14) / 15, want));
+      seg = (int)((d.ny + nseg - 1) / nseg);
+    }
     TpM m{d, c.subs, c.met, a.q, a.nt, a.nk, a.crx, a.cry, a.xfx, a.yfx,
           a.mfx ? a.mfx : a.xfx, a.mfy ? a.mfy : a.yfx, a.fx, a.fy, (int)nz, 0, 0, seg};
-    m.nstrip = (d.nx + 1 + MOUT - 1) / MOUT;
+    m.nstrip = nstrip;
     m.nseg = (d.ny + seg - 1) / seg;
     const long waves = nz * m.nstrip * m.nseg;
     if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
