@@ -71,7 +71,9 @@ def pmc_traffic(fam, launches):
 
 def layout_for(n):
     """(layout_x, layout_y) for n ranks: 6*lx*ly sub-domains divisible by n"""
-    return {1: (1, 1), 2: (1, 1), 3: (1, 1), 6: (1, 1), 4: (1, 2), 8: (2, 2), 12: (1, 2), 24: (2, 2)}.get(n, (2, 2))
+    # bands of full tile width (1 x ly): the x-marching kernels keep C180's strip
+    # efficiency; with all 24 sub-domains on one GPU 1x4 ran 52.4 ms/step, 2x2 54.7
+    return {1: (1, 1), 2: (1, 1), 3: (1, 1), 6: (1, 1), 4: (1, 2), 8: (1, 4), 12: (1, 2), 24: (1, 4)}.get(n, (2, 2))
 
 
 def parse():
@@ -82,6 +84,7 @@ def parse():
     p.add_argument("--npx", type=int, default=181)
     p.add_argument("--npz", type=int, default=72)
     p.add_argument("--nq", type=int, default=4)
+    p.add_argument("--layout", default="", help="sub-domain layout per tile, e.g. 2x2 (default: by rank count)")
     p.add_argument("--dt", type=float, default=450.0)
     p.add_argument("--cpu-npx", type=int, default=25, help="cpu_baseline sample grid (C24)")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -159,7 +162,7 @@ def main():
         obj = [pkg.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         nccl_id = obj[0]
-    lx, ly = layout_for(world)
+    lx, ly = (tuple(int(v) for v in a.layout.split("x")) if a.layout else layout_for(world))
     t_init = time.perf_counter()
     nq = max(a.nq, 6) if a.moist else a.nq
     d = pkg.Domain(rank, world, nccl_id, npx=a.npx, npz=a.npz, nq=nq, layout_x=lx, layout_y=ly, dt=a.dt)

@@ -49,19 +49,19 @@ def _run_ranks(pkg, nranks, layout, npx=13, npz=10, nq=2):
     return doms, out
 
 
-@pytest.mark.parametrize("nranks,layout", [(2, (1, 1)), (4, (1, 2)), (8, (2, 2))])
-def test_multirank_step_matches_single_rank(pkg, require_gpu, nranks, layout):
+@pytest.mark.parametrize("nranks,layout,npx", [(2, (1, 1), 13), (4, (1, 2), 13), (8, (2, 2), 13), (8, (1, 4), 25)])
+def test_multirank_step_matches_single_rank(pkg, require_gpu, nranks, layout, npx):
     state = importlib.import_module(pkg.__name__ + ".state")
     npz = 10
     ak, bk, ks = state.hybrid_levels(npz)
-    ref = pkg.Domain(npx=13, npz=npz, nq=2, layout_x=layout[0], layout_y=layout[1])
+    ref = pkg.Domain(npx=npx, npz=npz, nq=2, layout_x=layout[0], layout_y=layout[1])
     st = state.jablonowski_williamson(ref, ak, bk)
     ref.set_vertical(ak, bk, ks)
     for k, v in st.items():
         ref.upload(k, v)
     ref.step(1)
     want = {k: ref.download(k) for k in FIELDS}
-    doms, got = _run_ranks(pkg, nranks, layout, npz=npz)
+    doms, got = _run_ranks(pkg, nranks, layout, npx=npx, npz=npz)
     nper = doms[0].nsub
     nx, ny = ref.nx, ref.ny
     for r, d in enumerate(doms):

@@ -34,7 +34,7 @@ def _table(lib, fn, *args):
     return np.frombuffer(buf, dtype=np.int32)[:6 * n].reshape(n, 6).copy()
 
 
-def _worker(rank, world, port, layout, q):
+def _worker(rank, world, port, layout, q, npx=13):
     try:
         sys.path.insert(0, ROOT)
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -49,7 +49,7 @@ def _worker(rank, world, port, layout, q):
         lib = pkg.lib()
         dist.init_process_group("gloo", rank=rank, world_size=world)
         lx, ly = layout
-        d = pkg.Domain(rank, world, None, npx=13, npz=2, nq=1, layout_x=lx, layout_y=ly, host_only=1)
+        d = pkg.Domain(rank, world, None, npx=npx, npz=2, nq=1, layout_x=lx, layout_y=ly, host_only=1)
         nper = d.nsub
         ntot = 6 * lx * ly
         lay = ohalo.Layout(d.N, lx, ly)
@@ -107,12 +107,12 @@ def _worker(rank, world, port, layout, q):
         q.put((rank, [repr(e)]))
 
 
-@pytest.mark.parametrize("world,layout", [(2, (1, 1)), (2, (2, 2)), (4, (1, 2))])
-def test_gloo_halo_exchange_matches_oracle(world, layout):
+@pytest.mark.parametrize("world,layout,npx", [(2, (1, 1), 13), (2, (2, 2), 13), (4, (1, 2), 13), (4, (1, 4), 25)])
+def test_gloo_halo_exchange_matches_oracle(world, layout, npx):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, layout, q)) for r in range(world)]
+    procs = [ctx.Process(target=_worker, args=(r, world, port, layout, q, npx)) for r in range(world)]
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in procs)
