@@ -43,6 +43,9 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
     return;
   }
   HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  HIP_CHECK(hipStreamCreateWithFlags(&st_b, hipStreamNonBlocking));
+  HIP_CHECK(hipStreamCreateWithFlags(&st_c, hipStreamNonBlocking));
+  for (hipEvent_t* e : {&ev_fork, &ev_b, &ev_c}) HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   HIP_CHECK(hipMalloc(&dsubs, sizeof(SubInfo) * d.nsub));
   HIP_CHECK(hipMemcpy(dsubs, hsubs.data(), sizeof(SubInfo) * d.nsub, hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&dmet, sizeof(double) * hm.m.size()));
@@ -77,6 +80,10 @@ Dycore::~Dycore() {
   if (dsubs) (void)hipFree(dsubs);
   if (dmet) (void)hipFree(dmet);
   if (dcornerw) (void)hipFree(dcornerw);
+  for (hipEvent_t e : {ev_fork, ev_b, ev_c})
+    if (e) (void)hipEventDestroy(e);
+  if (st_b) (void)hipStreamDestroy(st_b);
+  if (st_c) (void)hipStreamDestroy(st_c);
   if (st) (void)hipStreamDestroy(st);
 }
 
@@ -366,6 +373,7 @@ void Dycore::step() {
   da.ut = S("_ds_ut", npz); da.vt = S("_ds_vt", npz); da.ra_x = S("_ds_ra_x", npz); da.ra_y = S("_ds_ra_y", npz);
   da.fx = S("_ds_fx", npz); da.fy = S("_ds_fy", npz); da.gwx = S("_ds_gwx", npz); da.gwy = S("_ds_gwy", npz);
   da.gtx = S("_ds_gtx", npz); da.gty = S("_ds_gty", npz); da.ke = S("_ds_ke", npz); da.vort = S("_ds_vort", npz);
+  da.gvx = S("_ds_gvx", npz); da.gvy = S("_ds_gvy", npz);
   da.tp_fx2 = S("_tp1_fx2", npz); da.tp_fy2 = S("_tp1_fy2", npz); da.tp_qi = S("_tp1_qi", npz);
   da.tp_qj = S("_tp1_qj", npz);
 
@@ -406,9 +414,25 @@ void Dycore::step() {
     riem_solver_c(c, npz, dt2, ptop, nl.p_fac, nl.dz_min, ca.delpc, ca.ptc, ca.wc, phis.p, gzc, pef, nsc);
     p_grad_c(c, npz, dt2, ca.delpc, pef, gzc, uc, vc);
     halo_update({{"uc", 'C'}, {"vc", 'C'}});
-    d_sw(c, da);
+    // fork: after the Courant numbers, the wind stage of d_sw (stream b) and update_dz_d
+    // (stream c) run beside the mass / thermodynamic transport and its halo update
+    d_sw_courant(c, da);
+    HIP_CHECK(hipEventRecord(ev_fork, st));
+    HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
+    HIP_CHECK(hipStreamWaitEvent(st_c, ev_fork, 0));
+    {
+      Ctx cb = c, cc = c;
+      cb.st = st_b;
+      cc.st = st_c;
+      d_sw_winds(cb, da);
+      update_dz_d(cc, za);
+    }
+    d_sw_thermo(c, da);
     halo_update({{"delp", 'c'}, {"pt", 'c'}});
-    update_dz_d(c, za);
+    HIP_CHECK(hipEventRecord(ev_b, st_b));
+    HIP_CHECK(hipEventRecord(ev_c, st_c));
+    HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
+    HIP_CHECK(hipStreamWaitEvent(st, ev_c, 0));
     ra.last_call = last ? 1 : 0;
     riem_solver3(c, ra, nsc);
     halo_update({{"zh", 'c'}, {"ppe", 'c'}, {"w", 'c'}});

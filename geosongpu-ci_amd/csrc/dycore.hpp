@@ -41,6 +41,10 @@ class Dycore {
   double* dcornerw = nullptr;
   HaloExchanger halo;
   hipStream_t st = nullptr;
+  // side streams of the acoustic sub-step: d_sw's wind stage and update_dz_d run beside
+  // its thermodynamic transport (fork after the Courant numbers, join before riem_solver3)
+  hipStream_t st_b = nullptr, st_c = nullptr;
+  hipEvent_t ev_fork = nullptr, ev_b = nullptr, ev_c = nullptr;
   std::unique_ptr<Transport> comm;  // null for one rank
   std::map<std::string, Field> fields;
   std::vector<double> ak, bk;  // npz+1

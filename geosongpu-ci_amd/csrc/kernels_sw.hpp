@@ -24,8 +24,12 @@ struct DswArgs {
   double *crx, *cry, *xfx, *yfx;      // per level, saved for update_dz_d
   double *cx, *cy, *mfx, *mfy;        // accumulated
   double *ut, *vt, *ra_x, *ra_y, *fx, *fy, *gwx, *gwy, *gtx, *gty, *ke, *vort;  // scratch
+  double *gvx, *gvy;  // vorticity fluxes (own planes: the wind stage may run beside the thermo stage)
   double *tp_fx2, *tp_fy2, *tp_qi, *tp_qj;
 };
-void d_sw(const Ctx& c, const DswArgs& a);
+void d_sw(const Ctx& c, const DswArgs& a);  // the three stages in order
+void d_sw_courant(const Ctx& c, const DswArgs& a);  // ut, vt, Courant numbers and area fluxes
+void d_sw_thermo(const Ctx& c, const DswArgs& a);   // delp / w / pt transport, flux accumulation
+void d_sw_winds(const Ctx& c, const DswArgs& a);    // kinetic energy, vorticity transport, u, v
 
 }  // namespace gtfv3

@@ -88,6 +88,7 @@ std::map<std::string, Fn>& reg() {
          a.ut = scr("_ds_ut"); a.vt = scr("_ds_vt"); a.ra_x = scr("_ds_ra_x"); a.ra_y = scr("_ds_ra_y");
          a.fx = scr("_ds_fx"); a.fy = scr("_ds_fy"); a.gwx = scr("_ds_gwx"); a.gwy = scr("_ds_gwy");
          a.gtx = scr("_ds_gtx"); a.gty = scr("_ds_gty"); a.vort = scr("_ds_vort");
+         a.gvx = scr("_ds_gvx"); a.gvy = scr("_ds_gvy");
          a.tp_fx2 = scr("_tp1_fx2"); a.tp_fy2 = scr("_tp1_fy2"); a.tp_qi = scr("_tp1_qi"); a.tp_qj = scr("_tp1_qj");
          d_sw(dy.ctx(), a);
        }},

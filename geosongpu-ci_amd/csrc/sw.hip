@@ -610,7 +610,11 @@ void c_sw(const Ctx& c, const CswArgs& a) {
   HIP_LAUNCH_CHECK();
 }
 
-void d_sw(const Ctx& c, const DswArgs& a) {
+// d_sw in three stages: the contravariant winds and Courant numbers; the mass-flux and
+// thermodynamic transport (delp, w, pt); the kinetic energy and vorticity transport that
+// update u, v.  After the first stage the other two touch disjoint fields (the vorticity
+// transport writes its own flux planes gvx, gvy), so the dycore runs them on two streams.
+void d_sw_courant(const Ctx& c, const DswArgs& a) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
@@ -623,11 +627,22 @@ void d_sw(const Ctx& c, const DswArgs& a) {
   GT_LAUNCH(ds_courant, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.ut, a.vt,
                      a.crx, a.cry, a.xfx, a.yfx);
   HIP_LAUNCH_CHECK();
+}
+
+static TpArgs d_sw_tp(const DswArgs& a) {
   TpArgs t{};
   t.nt = 1;
   t.nk = a.npz;
   t.crx = a.crx; t.cry = a.cry; t.xfx = a.xfx; t.yfx = a.yfx; t.ra_x = a.ra_x; t.ra_y = a.ra_y;
   t.fx2 = a.tp_fx2; t.fy2 = a.tp_fy2; t.qi = a.tp_qi; t.qj = a.tp_qj;
+  return t;
+}
+
+void d_sw_thermo(const Ctx& c, const DswArgs& a) {
+  const Dims& d = c.d;
+  const int nz = d.nsub * a.npz;
+  Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  TpArgs t = d_sw_tp(a);
   // mass fluxes
   t.q = a.delp; t.mfx = nullptr; t.mfy = nullptr; t.fx = a.fx; t.fy = a.fy; t.ord = a.hord_dp;
   fv_tp_2d(c, t);
@@ -644,6 +659,11 @@ void d_sw(const Ctx& c, const DswArgs& a) {
   GT_LAUNCH(ds_thermo, g2(d, Li, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.fx, a.fy, a.gwx,
                      a.gwy, a.gtx, a.gty, a.delp, a.pt, a.w);
   HIP_LAUNCH_CHECK();
+}
+
+void d_sw_winds(const Ctx& c, const DswArgs& a) {
+  const Dims& d = c.d;
+  const int nz = d.nsub * a.npz;
   // kinetic energy (+ divergence damping) at corners
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
   GT_LAUNCH(ds_ke, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.hord_mt, a.dddmp,
@@ -653,12 +673,19 @@ void d_sw(const Ctx& c, const DswArgs& a) {
   Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
   GT_LAUNCH(ds_vort, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.vort);
   HIP_LAUNCH_CHECK();
+  TpArgs t = d_sw_tp(a);
   t.mfx = nullptr; t.mfy = nullptr;
-  t.q = a.vort; t.fx = a.gwx; t.fy = a.gwy; t.ord = a.hord_vt;
+  t.q = a.vort; t.fx = a.gvx; t.fy = a.gvy; t.ord = a.hord_vt;
   fv_tp_2d(c, t);
-  GT_LAUNCH(ds_uv, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.ke, a.gwx, a.gwy, a.u,
+  GT_LAUNCH(ds_uv, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.ke, a.gvx, a.gvy, a.u,
                      a.v);
   HIP_LAUNCH_CHECK();
+}
+
+void d_sw(const Ctx& c, const DswArgs& a) {
+  d_sw_courant(c, a);
+  d_sw_thermo(c, a);
+  d_sw_winds(c, a);
 }
 
 }  // namespace gtfv3
