@@ -3,6 +3,7 @@
 #include "dycore.hpp"
 
 #include <algorithm>
+#include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
@@ -46,6 +47,10 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
   HIP_CHECK(hipStreamCreateWithFlags(&st_b, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&st_c, hipStreamNonBlocking));
   for (hipEvent_t* e : {&ev_fork, &ev_b, &ev_c}) HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  {
+    const char* e = std::getenv("GTFV3_STREAMS");
+    fork_substep = e ? e[0] == '1' : nranks > 1;
+  }
   HIP_CHECK(hipMalloc(&dsubs, sizeof(SubInfo) * d.nsub));
   HIP_CHECK(hipMemcpy(dsubs, hsubs.data(), sizeof(SubInfo) * d.nsub, hipMemcpyHostToDevice));
   HIP_CHECK(hipMalloc(&dmet, sizeof(double) * hm.m.size()));
@@ -200,20 +205,14 @@ void Dycore::tracer_2d(int nq, double /*dt*/) {
   Field& mfy = field("mfy", npz);
   Field& xfx = field("tr_xfx", npz);
   Field& yfx = field("tr_yfx", npz);
-  Field& ra_x = field("tr_ra_x", npz);
-  Field& ra_y = field("tr_ra_y", npz);
   Field& dp2 = field("tr_dp2", npz);
   Field& cmax = field("tr_cmax", 1);  // first npz doubles used
   Field& nspl = field("tr_nsplt", 1);
   Field& fx = field("tr_fx", nq * npz);
   Field& fy = field("tr_fy", nq * npz);
-  Field& fx2 = field("tr_fx2", nq * npz);
-  Field& fy2 = field("tr_fy2", nq * npz);
-  Field& qi = field("tr_qi", nq * npz);
-  Field& qj = field("tr_qj", nq * npz);
   if ((long)npz > d.plane) throw std::runtime_error("tracer cmax scratch too small");
 
-  tracer_prep(c, npz, cx.p, cy.p, xfx.p, yfx.p, ra_x.p, ra_y.p, cmax.p);
+  tracer_prep(c, npz, cx.p, cy.p, xfx.p, yfx.p, cmax.p);
   allreduce_max(cmax.p, npz);
   std::vector<double> hcm(npz);
   HIP_CHECK(hipMemcpyAsync(hcm.data(), cmax.p, sizeof(double) * npz, hipMemcpyDeviceToHost, st));
@@ -226,15 +225,15 @@ void Dycore::tracer_2d(int nq, double /*dt*/) {
   }
   int* dns = reinterpret_cast<int*>(nspl.p);
   HIP_CHECK(hipMemcpyAsync(dns, ns.data(), sizeof(int) * npz, hipMemcpyHostToDevice, st));
-  tracer_split(c, npz, dns, cx.p, cy.p, xfx.p, yfx.p, mfx.p, mfy.p, ra_x.p, ra_y.p);
+  tracer_split(c, npz, dns, cx.p, cy.p, xfx.p, yfx.p, mfx.p, mfy.p);
   halo_update({{"q", 'c'}});
   for (int it = 0; it < nmax; ++it) {
     tracer_dp2(c, npz, dp1.p, mfx.p, mfy.p, dp2.p);
     TpArgs a{};
     a.q = q.p; a.nt = nq; a.nk = npz;
-    a.crx = cx.p; a.cry = cy.p; a.xfx = xfx.p; a.yfx = yfx.p; a.ra_x = ra_x.p; a.ra_y = ra_y.p;
+    a.crx = cx.p; a.cry = cy.p; a.xfx = xfx.p; a.yfx = yfx.p;
     a.mfx = mfx.p; a.mfy = mfy.p;
-    a.fx = fx.p; a.fy = fy.p; a.fx2 = fx2.p; a.fy2 = fy2.p; a.qi = qi.p; a.qj = qj.p;
+    a.fx = fx.p; a.fy = fy.p;
     a.ord = nl.hord_tr;
     fv_tp_2d(c, a);
     tracer_update(c, npz, nq, q.p, nullptr, dp1.p, dp2.p, fx.p, fy.p, dns, it);
@@ -370,12 +369,10 @@ void Dycore::step() {
   da.uc = uc; da.vc = vc; da.ua = ua; da.va = va;
   da.crx = S("crx", npz); da.cry = S("cry", npz); da.xfx = S("xfx", npz); da.yfx = S("yfx", npz);
   da.cx = cx; da.cy = cy; da.mfx = mfx; da.mfy = mfy;
-  da.ut = S("_ds_ut", npz); da.vt = S("_ds_vt", npz); da.ra_x = S("_ds_ra_x", npz); da.ra_y = S("_ds_ra_y", npz);
+  da.ut = S("_ds_ut", npz); da.vt = S("_ds_vt", npz);
   da.fx = S("_ds_fx", npz); da.fy = S("_ds_fy", npz); da.gwx = S("_ds_gwx", npz); da.gwy = S("_ds_gwy", npz);
   da.gtx = S("_ds_gtx", npz); da.gty = S("_ds_gty", npz); da.ke = S("_ds_ke", npz); da.vort = S("_ds_vort", npz);
   da.gvx = S("_ds_gvx", npz); da.gvy = S("_ds_gvy", npz);
-  da.tp_fx2 = S("_tp1_fx2", npz); da.tp_fy2 = S("_tp1_fy2", npz); da.tp_qi = S("_tp1_qi", npz);
-  da.tp_qj = S("_tp1_qj", npz);
 
   UdzdArgs za{};
   za.npz = npz;
@@ -383,11 +380,9 @@ void Dycore::step() {
   za.dp0 = dp_ref;
   za.crx = da.crx; za.cry = da.cry; za.xfx = da.xfx; za.yfx = da.yfx;
   za.crx_e = S("_ud_crx", k1); za.cry_e = S("_ud_cry", k1); za.xfx_e = S("_ud_xfx", k1); za.yfx_e = S("_ud_yfx", k1);
-  za.ra_x = S("_ud_ra_x", k1); za.ra_y = S("_ud_ra_y", k1); za.fx = S("_ud_fx", k1); za.fy = S("_ud_fy", k1);
+  za.fx = S("_ud_fx", k1); za.fy = S("_ud_fy", k1);
   za.gam = S("_ud_gam", k1);
   za.zh = zh;
-  za.tp_fx2 = S("_tp2_fx2", k1); za.tp_fy2 = S("_tp2_fy2", k1); za.tp_qi = S("_tp2_qi", k1);
-  za.tp_qj = S("_tp2_qj", k1);
 
   Riem3Args ra{};
   ra.npz = npz;
@@ -415,8 +410,18 @@ void Dycore::step() {
     p_grad_c(c, npz, dt2, ca.delpc, pef, gzc, uc, vc);
     halo_update({{"uc", 'C'}, {"vc", 'C'}});
     // fork: after the Courant numbers, the wind stage of d_sw (stream b) and update_dz_d
-    // (stream c) run beside the mass / thermodynamic transport and its halo update
+    // (stream c) run beside the mass / thermodynamic transport and its halo update (the
+    // RCCL exchange of delp / pt then overlaps compute).  Multi-rank runs only (or
+    // GTFV3_STREAMS=1): on one GPU the C180 kernels fill the chip by themselves (the fork
+    // gained 0.6 %) and concurrent kernels would stretch the per-kernel event times the
+    // roofline line is built from.
     d_sw_courant(c, da);
+    if (!fork_substep) {
+      d_sw_thermo(c, da);
+      halo_update({{"delp", 'c'}, {"pt", 'c'}});
+      d_sw_winds(c, da);
+      update_dz_d(c, za);
+    } else {
     HIP_CHECK(hipEventRecord(ev_fork, st));
     HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
     HIP_CHECK(hipStreamWaitEvent(st_c, ev_fork, 0));
@@ -433,6 +438,7 @@ void Dycore::step() {
     HIP_CHECK(hipEventRecord(ev_c, st_c));
     HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
     HIP_CHECK(hipStreamWaitEvent(st, ev_c, 0));
+    }
     ra.last_call = last ? 1 : 0;
     riem_solver3(c, ra, nsc);
     halo_update({{"zh", 'c'}, {"ppe", 'c'}, {"w", 'c'}});

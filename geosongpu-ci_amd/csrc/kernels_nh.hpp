@@ -22,9 +22,8 @@ struct UdzdArgs {
   int npz, hord;
   const double* dp0;
   const double *crx, *cry, *xfx, *yfx;
-  double *crx_e, *cry_e, *xfx_e, *yfx_e, *ra_x, *ra_y, *fx, *fy, *gam;
+  double *crx_e, *cry_e, *xfx_e, *yfx_e, *fx, *fy, *gam;
   double* zh;
-  double *tp_fx2, *tp_fy2, *tp_qi, *tp_qj;
 };
 void update_dz_d(const Ctx& c, const UdzdArgs& a);
 

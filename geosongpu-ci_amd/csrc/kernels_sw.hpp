@@ -23,9 +23,8 @@ struct DswArgs {
   const double *uc, *vc, *ua, *va;
   double *crx, *cry, *xfx, *yfx;      // per level, saved for update_dz_d
   double *cx, *cy, *mfx, *mfy;        // accumulated
-  double *ut, *vt, *ra_x, *ra_y, *fx, *fy, *gwx, *gwy, *gtx, *gty, *ke, *vort;  // scratch
+  double *ut, *vt, *fx, *fy, *gwx, *gwy, *gtx, *gty, *ke, *vort;  // scratch
   double *gvx, *gvy;  // vorticity fluxes (own planes: the wind stage may run beside the thermo stage)
-  double *tp_fx2, *tp_fy2, *tp_qi, *tp_qj;
 };
 void d_sw(const Ctx& c, const DswArgs& a);  // the three stages in order
 void d_sw_courant(const Ctx& c, const DswArgs& a);  // ut, vt, Courant numbers and area fluxes

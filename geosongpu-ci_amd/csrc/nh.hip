@@ -761,9 +761,8 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
   HIP_LAUNCH_CHECK();
   TpArgs t{};
   t.q = a.zh; t.nt = 1; t.nk = k1;
-  t.crx = a.crx_e; t.cry = a.cry_e; t.xfx = a.xfx_e; t.yfx = a.yfx_e; t.ra_x = a.ra_x; t.ra_y = a.ra_y;
-  t.mfx = nullptr; t.mfy = nullptr; t.fx = a.fx; t.fy = a.fy;
-  t.fx2 = a.tp_fx2; t.fy2 = a.tp_fy2; t.qi = a.tp_qi; t.qj = a.tp_qj; t.ord = a.hord;
+  t.crx = a.crx_e; t.cry = a.cry_e; t.xfx = a.xfx_e; t.yfx = a.yfx_e;
+  t.mfx = nullptr; t.mfy = nullptr; t.fx = a.fx; t.fy = a.fy; t.ord = a.hord;
   fv_tp_2d(c, t);
   Launch2D Li{0, 0, d.nx, d.ny};
   GT_LAUNCH(zh_update_k, g2(d, Li, d.nsub * k1), dim3(BX, BY), 0, c.st, d, c.subs, c.met, k1, a.fx, a.fy,

@@ -43,14 +43,30 @@ std::map<std::string, Fn>& reg() {
          TpArgs a{};
          a.q = q.p; a.nt = nt; a.nk = nk;
          a.crx = F(dy, f[1]).p; a.cry = F(dy, f[2]).p; a.xfx = F(dy, f[3]).p; a.yfx = F(dy, f[4]).p;
-         a.ra_x = F(dy, f[5]).p; a.ra_y = F(dy, f[6]).p;
+         (void)F(dy, f[5]); (void)F(dy, f[6]);  // ra_x, ra_y: checked to exist, not read
          a.mfx = f[7] == "-" ? nullptr : F(dy, f[7]).p;
          a.mfy = f[8] == "-" ? nullptr : F(dy, f[8]).p;
          a.fx = dy.field(f[9], q.nk).p; a.fy = dy.field(f[10], q.nk).p;
-         a.fx2 = dy.field("_tp_fx2", q.nk).p; a.fy2 = dy.field("_tp_fy2", q.nk).p;
-         a.qi = dy.field("_tp_qi", q.nk).p; a.qj = dy.field("_tp_qj", q.nk).p;
          a.ord = ord;
          a.cfg = p.size() > 2 ? (int)p[2] : -1;
+         fv_tp_2d(dy.ctx(), a);
+       }},
+      // fv_tp_2d_pair(q, q2, crx, cry, xfx, yfx, mfx|-, mfy|-, fx, fy, fx_2, fy_2) params: ord
+      // two fields with shared Courant numbers and fluxes in one launch (d_sw's w and pt)
+      {"fv_tp_2d_pair",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 12, "fv_tp_2d_pair");
+         Field& q = F(dy, f[0]);
+         Field& q2 = F(dy, f[1]);
+         if (q2.nk != q.nk) throw std::runtime_error("fv_tp_2d_pair: fields must share the level count");
+         TpArgs a{};
+         a.q = q.p; a.q2 = q2.p; a.nt = 1; a.nk = q.nk;
+         a.crx = F(dy, f[2]).p; a.cry = F(dy, f[3]).p; a.xfx = F(dy, f[4]).p; a.yfx = F(dy, f[5]).p;
+         a.mfx = f[6] == "-" ? nullptr : F(dy, f[6]).p;
+         a.mfy = f[7] == "-" ? nullptr : F(dy, f[7]).p;
+         a.fx = dy.field(f[8], q.nk).p; a.fy = dy.field(f[9], q.nk).p;
+         a.fx_2 = dy.field(f[10], q.nk).p; a.fy_2 = dy.field(f[11], q.nk).p;
+         a.ord = p.size() > 0 ? (int)p[0] : 6;
          fv_tp_2d(dy.ctx(), a);
        }},
       // c_sw(delp, pt, w, u, v | uc, vc, ua, va, ut, vt, delpc, ptc, wc) params: dt2
@@ -85,11 +101,10 @@ std::map<std::string, Fn>& reg() {
          a.uc = F(dy, f[5]).p; a.vc = F(dy, f[6]).p; a.ua = F(dy, f[7]).p; a.va = F(dy, f[8]).p;
          a.crx = out(9); a.cry = out(10); a.xfx = out(11); a.yfx = out(12);
          a.cx = out(13); a.cy = out(14); a.mfx = out(15); a.mfy = out(16); a.ke = out(17);
-         a.ut = scr("_ds_ut"); a.vt = scr("_ds_vt"); a.ra_x = scr("_ds_ra_x"); a.ra_y = scr("_ds_ra_y");
+         a.ut = scr("_ds_ut"); a.vt = scr("_ds_vt");
          a.fx = scr("_ds_fx"); a.fy = scr("_ds_fy"); a.gwx = scr("_ds_gwx"); a.gwy = scr("_ds_gwy");
          a.gtx = scr("_ds_gtx"); a.gty = scr("_ds_gty"); a.vort = scr("_ds_vort");
          a.gvx = scr("_ds_gvx"); a.gvy = scr("_ds_gvy");
-         a.tp_fx2 = scr("_tp1_fx2"); a.tp_fy2 = scr("_tp1_fy2"); a.tp_qi = scr("_tp1_qi"); a.tp_qj = scr("_tp1_qj");
          d_sw(dy.ctx(), a);
        }},
       // riem_solver_c(delpc, ptc, wc, phis, gz | pef): gz heights in (clamped to dz_min),

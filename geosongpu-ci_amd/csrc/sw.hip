@@ -633,8 +633,7 @@ static TpArgs d_sw_tp(const DswArgs& a) {
   TpArgs t{};
   t.nt = 1;
   t.nk = a.npz;
-  t.crx = a.crx; t.cry = a.cry; t.xfx = a.xfx; t.yfx = a.yfx; t.ra_x = a.ra_x; t.ra_y = a.ra_y;
-  t.fx2 = a.tp_fx2; t.fy2 = a.tp_fy2; t.qi = a.tp_qi; t.qj = a.tp_qj;
+  t.crx = a.crx; t.cry = a.cry; t.xfx = a.xfx; t.yfx = a.yfx;
   return t;
 }
 
@@ -649,12 +648,19 @@ void d_sw_thermo(const Ctx& c, const DswArgs& a) {
   GT_LAUNCH(ds_accum, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, a.npz, a.crx, a.cry, a.fx, a.fy,
                      a.cx, a.cy, a.mfx, a.mfy);
   HIP_LAUNCH_CHECK();
-  // w and pt with the mass fluxes
+  // w and pt with the mass fluxes: one launch for the pair when their PPM orders agree
+  // (each wave carries both fields and loads the shared Courant numbers and fluxes once)
   t.mfx = a.fx; t.mfy = a.fy;
-  t.q = a.w; t.fx = a.gwx; t.fy = a.gwy; t.ord = a.hord_vt;
-  fv_tp_2d(c, t);
-  t.q = a.pt; t.fx = a.gtx; t.fy = a.gty; t.ord = a.hord_tm;
-  fv_tp_2d(c, t);
+  if (a.hord_vt == a.hord_tm) {
+    t.q = a.w; t.fx = a.gwx; t.fy = a.gwy;
+    t.q2 = a.pt; t.fx_2 = a.gtx; t.fy_2 = a.gty; t.ord = a.hord_vt;
+    fv_tp_2d(c, t);
+  } else {
+    t.q = a.w; t.fx = a.gwx; t.fy = a.gwy; t.ord = a.hord_vt;
+    fv_tp_2d(c, t);
+    t.q = a.pt; t.fx = a.gtx; t.fy = a.gty; t.ord = a.hord_tm;
+    fv_tp_2d(c, t);
+  }
   Launch2D Li{0, 0, d.nx, d.ny};
   GT_LAUNCH(ds_thermo, g2(d, Li, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.fx, a.fy, a.gwx,
                      a.gwy, a.gtx, a.gty, a.delp, a.pt, a.w);

@@ -40,13 +40,17 @@ constexpr int ZMAX = 65535;
 constexpr int MW = 64, MOUT = MW - 6, MWAVES = 4;
 typedef unsigned int TpU2 __attribute__((ext_vector_type(2)));
 
+// NF fields per wave (field group g of a sub-domain = fields g*NF .. g*NF+NF-1, field f
+// of the group at qf[f] / fxf[f] / fyf[f] + the group's plane offset); ntg groups
 struct TpM {
   Dims d;
   const SubInfo* subs;
-  const double *M, *q;
-  int nt, nk;
+  const double* M;
+  const double* qf[2];
+  int nt, nk, ntg;
   const double *crx, *cry, *xfx, *yfx, *mx, *my;
-  double *fx, *fy;
+  double* fxf[2];
+  double* fyf[2];
   int nz, nstrip, nseg, seg;
 };
 
@@ -124,10 +128,12 @@ __device__ __forceinline__ double ppm_x_dpp(double q, double dx, int g, int N, d
 // holds, ra_x = area + xfx|i - xfx|i+1 (x neighbour by DPP), ra_y = area + yfx|j - yfx|j+1
 // (previous row step), the expressions of ds_ra / ra_k / tracer_ra_k; without separate
 // mass fluxes (MF = false) mfx, mfy are xfx, yfx and come from registers too)
+template <int NF>
 struct MarchIn {
-  double qx, qy, crx, xfx, area_r, dxr;  // row r
-  double cry, yfx, my;                   // edge r-2
-  double mx, dxm;                        // row r-3
+  double qx[NF], qy[NF];            // row r, per field (x- / y-corner fill)
+  double crx, xfx, area_r, dxr;     // row r
+  double cry, yfx, my;              // edge r-2
+  double mx, dxm;                   // row r-3
 };
 
 // y-direction PPM state rolled along the march: al at the last interface computed and
@@ -137,11 +143,13 @@ struct YRoll {
   PpmCell cell;
 };
 
-template <int ORD, bool EX, bool AHEAD2, bool MF>
+template <int ORD, bool EX, bool AHEAD2, bool MF, int NF>
 __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   const Dims& d = a.d;
   const int lane = threadIdx.x & (MW - 1);
-  const int k = z % a.nk, s = z / a.nk / a.nt;
+  // z: (sub-domain, field group, level); the NF fields of a group share the Courant
+  // numbers and fluxes, so those planes are loaded once for all of them
+  const int k = z % a.nk, s = z / a.nk / a.ntg, tg = (z / a.nk) % a.ntg;
   const SubInfo sub = a.subs[s];
   const int nx = d.nx, ny = d.ny, N = sub.N;
   const bool last = j1 >= ny;
@@ -149,8 +157,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   const int I = x + sub.ioff;
   const int xc = x < -NG ? -NG : (x > nx + NG ? nx + NG : x);  // addressable column
   const long pitch = d.pitch;
-  const double* qq = a.q + (long)z * d.plane;
-  const long zo = (long)z * d.plane, fo = ((long)s * a.nk + k) * d.plane;
+  const long zo = ((long)(s * a.nt + tg * NF) * a.nk + k) * d.plane, fo = ((long)s * a.nk + k) * d.plane;
   const double* area = met(a.M, d, M_AREA, s);
   const double* dxa = met(a.M, d, M_DXA, s);
   const double* dya = met(a.M, d, M_DYA, s);
@@ -162,7 +169,10 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   // scalar offset, so the loads of a row step cost no vector address arithmetic.
   const int PBy = (int)(d.plane * 8);
   auto rsrc = [&](const double* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, PBy, 0x00020000); };
-  const auto rQ = rsrc(qq), rCRX = rsrc(a.crx + fo), rCRY = rsrc(a.cry + fo), rXFX = rsrc(a.xfx + fo);
+  __amdgpu_buffer_rsrc_t rQ[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) rQ[f] = rsrc(a.qf[f] + zo);
+  const auto rCRX = rsrc(a.crx + fo), rCRY = rsrc(a.cry + fo), rXFX = rsrc(a.xfx + fo);
   const auto rYFX = rsrc(a.yfx + fo);
   const auto rMX = rsrc(a.mx + fo), rMY = rsrc(a.my + fo), rAR = rsrc(area), rDXA = rsrc(dxa);
   const uint32_t vx = (uint32_t)xo * 8u;
@@ -179,7 +189,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   // values masked afterwards): with a fixed count of loads per step the compiler's
   // vmcnt bookkeeping lets the next step's prefetch stay in flight across this step.
   auto load = [&](int r) {
-    MarchIn v;
+    MarchIn<NF> v;
     const int rr = r < ny + NG ? r : ny + NG;  // last plane row
     const uint32_t so = (uint32_t)(rr + NG) * rowb;
     const int J = r + sub.joff;
@@ -188,13 +198,19 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
       const bool cc = qin && (I < 0 || I >= N);
       const uint32_t ox = cc ? (uint32_t)cc_off(d, sub, x, r, 1) * 8u : vx + so;
       const uint32_t oy = cc ? (uint32_t)cc_off(d, sub, x, r, 2) * 8u : vx + so;
-      const double q1 = bl(rQ, ox, 0), q2 = bl(rQ, oy, 0);
-      v.qx = qin ? q1 : 0.0;
-      v.qy = qin ? q2 : 0.0;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const double q1 = bl(rQ[f], ox, 0), q2 = bl(rQ[f], oy, 0);
+        v.qx[f] = qin ? q1 : 0.0;
+        v.qy[f] = qin ? q2 : 0.0;
+      }
     } else {
-      const double q1 = bl(rQ, vx, so);
-      v.qx = qin ? q1 : 0.0;
-      v.qy = v.qx;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        const double q1 = bl(rQ[f], vx, so);
+        v.qx[f] = qin ? q1 : 0.0;
+        v.qy[f] = v.qx[f];
+      }
     }
     v.crx = bl(rCRX, vx, so);
     v.xfx = bl(rXFX, vx, so);
@@ -224,21 +240,34 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     return P1 * (w[1] + w[2]) + P2 * (w[0] + w[3]);
   };
 
-  double qyw[4], qjw[4];  // rows r-3 .. r
-  double hf2[4], hcx[4];  // fx2 and crx of rows r-3 .. r
-  double arw[4];          // cell area of rows r-3 .. r (read once per row)
-  double hxf[4];          // xfx of rows r-3 .. r (the mass flux mfx when MF = false)
+  double qyw[NF][4], qjw[NF][4];  // rows r-3 .. r
+  double hf2[NF][4], hcx[4];      // fx2 and crx of rows r-3 .. r
+  double arw[4];                  // cell area of rows r-3 .. r (read once per row)
+  double hxf[4];                  // xfx of rows r-3 .. r (the mass flux mfx when MF = false)
+  YRoll ry[NF], rj[NF];           // q (y fill) and q_j
+  double fyy_prev[NF];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) qyw[m] = qjw[m] = hf2[m] = hcx[m] = arw[m] = hxf[m] = 0.0;
-  YRoll ry{}, rj{};  // q (y fill) and q_j
-  double fyy_prev = 0.0;
+  for (int m = 0; m < 4; ++m) hcx[m] = arw[m] = hxf[m] = 0.0;
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+#pragma unroll
+    for (int m = 0; m < 4; ++m) qyw[f][m] = qjw[f][m] = hf2[f][m] = 0.0;
+    ry[f] = YRoll{};
+    rj[f] = YRoll{};
+    fyy_prev[f] = 0.0;
+  }
   double yfx_prev = 0.0;  // yfx at edge r-3 (the previous row step's edge r-2)
 
   // lane predicates (constant along the march)
   const bool l_fx2 = x >= 0 && x <= nx, l_qj = x >= 0 && x < nx;
   const bool l_fy2 = x >= -NG && x <= nx + NG - 1;
   const bool s_fy = out_lane && x < nx, s_fx = out_lane && x <= nx;
-  const auto rFX = rsrc(a.fx + zo), rFY = rsrc(a.fy + zo);
+  __amdgpu_buffer_rsrc_t rFX[NF], rFY[NF];
+#pragma unroll
+  for (int f = 0; f < NF; ++f) {
+    rFX[f] = rsrc(a.fxf[f] + zo);
+    rFY[f] = rsrc(a.fyf[f] + zo);
+  }
   auto bst = [&](__amdgpu_buffer_rsrc_t r, uint32_t soff, double v) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(TpU2, v), r, vx, soff, 0);
   };
@@ -256,11 +285,14 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   // checks, so their step is branch-free apart from the two output stores.
   // steady load of the step for row rl (rows rl, rl-2, rl-3 inside the plane, away
   // from the cube corners)
-  auto load_steady = [&](int rl, MarchIn& nxt) {
+  auto load_steady = [&](int rl, MarchIn<NF>& nxt) {
       const uint32_t so = (uint32_t)(rl + NG) * rowb;
-      nxt.qx = bl(rQ, vx, so);
-      if (!cin) nxt.qx = 0.0;
-      nxt.qy = nxt.qx;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        nxt.qx[f] = bl(rQ[f], vx, so);
+        if (!cin) nxt.qx[f] = 0.0;
+        nxt.qy[f] = nxt.qx[f];
+      }
       nxt.crx = bl(rCRX, vx, so);
       nxt.xfx = bl(rXFX, vx, so);
       nxt.area_r = bl(rAR, vx, so);
@@ -273,88 +305,103 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
       nxt.dxm = EX ? bl(rDXA, vxd, sm) : 0.0;
   };
   // ahead: how many rows ahead the steady step prefetches (1, or 2 in the three-buffer loop)
-  auto step = [&](auto gen, int r, const MarchIn& cur, MarchIn& nxt, int ahead) {
+  auto step = [&](auto gen, int r, const MarchIn<NF>& cur, MarchIn<NF>& nxt, int ahead) {
     constexpr bool GEN = decltype(gen)::value;
     if (GEN) nxt = load(r + 1);
     else load_steady(r + ahead, nxt);
     const long o = (long)(r + NG) * pitch + xo;
-    // ---- row r: inner x flux fx2, q_j
-    double fx2;
-    {
-      const double f = ppm_x_dpp<ORD, EX>(cur.qx, cur.dxr, I, N, cur.crx);
-      const bool ok = GEN ? l_fx2 && r >= -NG && r <= ny + NG - 1 : l_fx2;
-      fx2 = ok ? f : 0.0;
-    }
-    const double fxx = cur.xfx * fx2;
-    const double fxx_e = dpp_next(fxx);
     const double rax = cur.area_r + cur.xfx - dpp_next(cur.xfx);
-    double qj;
-    {
-      const double v = (cur.qx * cur.area_r + fxx - fxx_e) / rax;
+    // ---- row r: inner x flux fx2, q_j (per field)
+    double fx2[NF], qj[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      {
+        const double v = ppm_x_dpp<ORD, EX>(cur.qx[f], cur.dxr, I, N, cur.crx);
+        const bool ok = GEN ? l_fx2 && r >= -NG && r <= ny + NG - 1 : l_fx2;
+        fx2[f] = ok ? v : 0.0;
+      }
+      const double fxx = cur.xfx * fx2[f];
+      const double fxx_e = dpp_next(fxx);
+      const double v = (cur.qx[f] * cur.area_r + fxx - fxx_e) / rax;
       const bool ok = GEN ? l_qj && r >= -NG && r < ny + NG : l_qj;
-      qj = ok ? v : 0.0;
+      qj[f] = ok ? v : 0.0;
     }
 #pragma unroll
     for (int m = 0; m < 3; ++m) {
-      qyw[m] = qyw[m + 1];
-      qjw[m] = qjw[m + 1];
-      hf2[m] = hf2[m + 1];
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        qyw[f][m] = qyw[f][m + 1];
+        qjw[f][m] = qjw[f][m + 1];
+        hf2[f][m] = hf2[f][m + 1];
+      }
       hcx[m] = hcx[m + 1];
       arw[m] = arw[m + 1];
       hxf[m] = hxf[m + 1];
     }
-    qyw[3] = cur.qy;
-    qjw[3] = qj;
-    hf2[3] = fx2;
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      qyw[f][3] = cur.qy[f];
+      qjw[f][3] = qj[f];
+      hf2[f][3] = fx2[f];
+    }
     hcx[3] = cur.crx;
     arw[3] = cur.area_r;
     hxf[3] = cur.xfx;
     const double my = MF ? cur.my : cur.yfx, mx = MF ? cur.mx : hxf[0];
 
-    // ---- y PPM pieces: interface r-1, cell r-2 (both windows)
+    // ---- y PPM pieces: interface r-1, cell r-2 (both windows, per field)
     const int e = r - 2;
-    double aly, alj;
-    if (GEN) {
-      const int E = e + sub.joff;
-      aly = y_al(qyw, E + 1, o);
-      alj = y_al(qjw, E + 1, o);
-    } else {
-      aly = P1 * (qyw[1] + qyw[2]) + P2 * (qyw[0] + qyw[3]);
-      alj = P1 * (qjw[1] + qjw[2]) + P2 * (qjw[0] + qjw[3]);
+    PpmCell cy[NF], cj[NF], cym[NF], cjm[NF];
+#pragma unroll
+    for (int f = 0; f < NF; ++f) {
+      double aly, alj;
+      if (GEN) {
+        const int E = e + sub.joff;
+        aly = y_al(qyw[f], E + 1, o);
+        alj = y_al(qjw[f], E + 1, o);
+      } else {
+        aly = P1 * (qyw[f][1] + qyw[f][2]) + P2 * (qyw[f][0] + qyw[f][3]);
+        alj = P1 * (qjw[f][1] + qjw[f][2]) + P2 * (qjw[f][0] + qjw[f][3]);
+      }
+      cy[f] = ppm_cell<ORD>(qyw[f][1], ry[f].al, aly);
+      cj[f] = ppm_cell<ORD>(qjw[f][1], rj[f].al, alj);
+      cym[f] = ry[f].cell;
+      cjm[f] = rj[f].cell;
+      ry[f].al = aly;
+      ry[f].cell = cy[f];
+      rj[f].al = alj;
+      rj[f].cell = cj[f];
     }
-    const PpmCell cy = ppm_cell<ORD>(qyw[1], ry.al, aly);
-    const PpmCell cj = ppm_cell<ORD>(qjw[1], rj.al, alj);
-    const PpmCell cym = ry.cell, cjm = rj.cell;
-    ry.al = aly;
-    ry.cell = cy;
-    rj.al = alj;
-    rj.cell = cj;
 
     if (!GEN || e >= j0) {
-      // ---- edge e: inner y flux fy2, outer y flux fy
       const uint32_t se = (uint32_t)(e + NG) * rowb;
-      double fy2 = ppm_edge_flux(cym, cy, cur.cry);
-      if (!(GEN ? e <= ny && l_fy2 : l_fy2)) fy2 = 0.0;
-      const double fyy = !GEN || e <= ny ? cur.yfx * fy2 : 0.0;
-      if (GEN) {
-        if (s_fy && e <= ny && (e < j1 || last)) bst(rFY, se, 0.5 * (ppm_edge_flux(cjm, cj, cur.cry) + fy2) * my);
-      } else {
-        bstv(rFY, vfy, se, 0.5 * (ppm_edge_flux(cjm, cj, cur.cry) + fy2) * my);
-      }
-      // ---- row m = r-3: q_i, outer x flux fx
       const int mrow = r - 3;
-      if (!GEN || (mrow >= j0 && mrow < ny)) {
-        const double ray = arw[0] + yfx_prev - cur.yfx;
-        const double v = (qyw[0] * arw[0] + fyy_prev - fyy) / ray;
-        const double qi = cin ? v : 0.0;
-        const double f = ppm_x_dpp<ORD, EX>(qi, cur.dxm, I, N, hcx[0]);
+      const double ray = arw[0] + yfx_prev - cur.yfx;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) {
+        // ---- edge e: inner y flux fy2, outer y flux fy
+        double fy2 = ppm_edge_flux(cym[f], cy[f], cur.cry);
+        if (!(GEN ? e <= ny && l_fy2 : l_fy2)) fy2 = 0.0;
+        const double fyy = !GEN || e <= ny ? cur.yfx * fy2 : 0.0;
         if (GEN) {
-          if (s_fx && mrow < j1) bst(rFX, se - rowb, 0.5 * (f + hf2[0]) * mx);
+          if (s_fy && e <= ny && (e < j1 || last))
+            bst(rFY[f], se, 0.5 * (ppm_edge_flux(cjm[f], cj[f], cur.cry) + fy2) * my);
         } else {
-          bstv(rFX, vfx, se - rowb, 0.5 * (f + hf2[0]) * mx);
+          bstv(rFY[f], vfy, se, 0.5 * (ppm_edge_flux(cjm[f], cj[f], cur.cry) + fy2) * my);
         }
+        // ---- row m = r-3: q_i, outer x flux fx
+        if (!GEN || (mrow >= j0 && mrow < ny)) {
+          const double v = (qyw[f][0] * arw[0] + fyy_prev[f] - fyy) / ray;
+          const double qi = cin ? v : 0.0;
+          const double fo_ = ppm_x_dpp<ORD, EX>(qi, cur.dxm, I, N, hcx[0]);
+          if (GEN) {
+            if (s_fx && mrow < j1) bst(rFX[f], se - rowb, 0.5 * (fo_ + hf2[f][0]) * mx);
+          } else {
+            bstv(rFX[f], vfx, se - rowb, 0.5 * (fo_ + hf2[f][0]) * mx);
+          }
+        }
+        fyy_prev[f] = fyy;
       }
-      fyy_prev = fyy;
     }
     yfx_prev = cur.yfx;
   };
@@ -370,7 +417,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   if (rs1 < rs0) rs1 = rs0 - 1;
   const std::integral_constant<bool, true> G1{};
   const std::integral_constant<bool, false> G0{};
-  MarchIn cur = load(r_lo), nxt;
+  MarchIn<NF> cur = load(r_lo), nxt;
   int r = r_lo;
   for (; r < rs0; ++r) {
     step(G1, r, cur, nxt, 1);
@@ -382,7 +429,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     const int lmax = ny + NG - 1 < N - 1 - sub.joff ? ny + NG - 1 : N - 1 - sub.joff;
     const int rs1b = rs1 < lmax - 2 ? rs1 : lmax - 2;
     if (AHEAD2 && r + 2 <= rs1b) {
-      MarchIn b0 = cur, b1, b2;
+      MarchIn<NF> b0 = cur, b1, b2;
       load_steady(r + 1, b1);
       for (; r + 2 <= rs1b; r += 3) {
         step(G0, r, b0, b2, 2);
@@ -404,7 +451,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
 
 // AHEAD2: steady rows prefetch two rows ahead (three row buffers, 149 VGPRs, three
 // waves per SIMD); otherwise one row ahead (two buffers, <= 128 VGPRs, four waves)
-template <int ORD, bool AHEAD2, bool MF>
+template <int ORD, bool AHEAD2, bool MF, int NF>
 __global__ void __launch_bounds__(MW * MWAVES, AHEAD2 ? 1 : 4) tp_march(TpM a) {
   // wave index through readfirstlane: everything derived from it (plane, strip, segment,
   // buffer descriptors, row offsets) is then provably wave-uniform (SGPRs, no waterfalls)
@@ -415,14 +462,14 @@ __global__ void __launch_bounds__(MW * MWAVES, AHEAD2 ? 1 : 4) tp_march(TpM a) {
   const int seg = (int)(t % (unsigned)a.nseg);
   const int z = (int)(t / (unsigned)a.nseg);
   if (z >= a.nz) return;  // whole wavefront leaves; no workgroup barrier follows
-  const int s = z / a.nk / a.nt;
+  const int s = z / a.nk / a.ntg;
   const SubInfo& sub = a.subs[s];
   const int j0 = seg * a.seg;
   const int j1 = j0 + a.seg < a.d.ny ? j0 + a.seg : a.d.ny;
   const int A = strip * MOUT + sub.ioff;
   const bool ex = !(A - 1 >= 2 && A + MOUT + 1 <= sub.N - 2);
-  if (ex) tp_march_strip<ORD, true, AHEAD2, MF>(a, (int)z, strip, j0, j1);
-  else tp_march_strip<ORD, false, AHEAD2, MF>(a, (int)z, strip, j0, j1);
+  if (ex) tp_march_strip<ORD, true, AHEAD2, MF, NF>(a, (int)z, strip, j0, j1);
+  else tp_march_strip<ORD, false, AHEAD2, MF, NF>(a, (int)z, strip, j0, j1);
 }
 
 // ---------------- tracer_2d_1l ----------------
@@ -493,8 +540,7 @@ __global__ void __launch_bounds__(256) tracer_split_k(Dims d, const double* __re
                                                       const int* __restrict__ nsplt, double* __restrict__ cx,
                                                       double* __restrict__ cy, double* __restrict__ xfx,
                                                       double* __restrict__ yfx, double* __restrict__ mfx,
-                                                      double* __restrict__ mfy, double* __restrict__ ra_x,
-                                                      double* __restrict__ ra_y) {
+                                                      double* __restrict__ mfy) {
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   int i, j;
   if (!thread_point(L, i, j)) return;
@@ -558,53 +604,77 @@ __global__ void copy_k(long n, const double* __restrict__ a, double* __restrict_
 
 void fv_tp_2d(const Ctx& c, const TpArgs& a) {
   const Dims& d = c.d;
-  long nz = (long)d.nsub * a.nt * a.nk;
   if (a.ord != 5 && a.ord != 6) throw std::runtime_error("fv_tp_2d: hord must be 5 or 6");
+  // field pairs share a wave (and the Courant / flux loads): a second field array (q2), or
+  // consecutive tracers when their count is even
+  const bool pair2 = a.q2 != nullptr;
+  if (pair2 && a.nt != 1) throw std::runtime_error("fv_tp_2d: a second field array needs nt = 1");
+  const int NFw = pair2 || (a.nt % 2 == 0) ? 2 : 1;
+  const int nfields = pair2 ? 2 : a.nt;
   {
-    // segment length: cfg >= 8 selects it (tuning); default 45 rows (C180: 4 segments)
     static const int seg_env = [] {
       const char* e = getenv("GTFV3_TP_SEG");  // tuning override of the default segment
       return e ? atoi(e) : 0;
     }();
+    TpM m{};
+    m.d = d;
+    m.subs = c.subs;
+    m.M = c.met;
+    const long tstride = (long)a.nk * d.plane;  // next tracer of the same sub-domain
+    m.qf[0] = a.q;
+    m.qf[1] = pair2 ? a.q2 : a.q + tstride;
+    m.fxf[0] = a.fx;
+    m.fyf[0] = a.fy;
+    m.fxf[1] = pair2 ? a.fx_2 : a.fx + tstride;
+    m.fyf[1] = pair2 ? a.fy_2 : a.fy + tstride;
+    m.nt = a.nt;
+    m.nk = a.nk;
+    m.ntg = pair2 ? 1 : a.nt / NFw;
+    m.crx = a.crx; m.cry = a.cry; m.xfx = a.xfx; m.yfx = a.yfx;
+    m.mx = a.mfx ? a.mfx : a.xfx;
+    m.my = a.mfy ? a.mfy : a.yfx;
+    const long nz = (long)d.nsub * m.ntg * a.nk;
+    m.nz = (int)nz;
     // Default: segments of <= 45 rows, more (down to 15 rows) when the launch would
-    // otherwise have fewer than ~6900 waves (the C180 wave count on one GPU; small
+    // otherwise have fewer than ~6900 field-waves (the C180 count on one GPU; small
     // sub-domains, as on 4-8 GPUs, need the shorter segments to fill the chip).
     const int nstrip = (d.nx + 1 + MOUT - 1) / MOUT;
     int seg = a.cfg >= 8 ? a.cfg : seg_env;
     if (seg < 8) {
-      const long want = (6912 + nz * nstrip - 1) / (nz * nstrip);
+      const long fw = nz * NFw * nstrip;
+      const long want = (6912 + fw - 1) / fw;
       const long nseg = std::max<long>((d.ny + 44) / 45, std::min<long>((d.ny + 14) / 15, want));
       seg = (int)((d.ny + nseg - 1) / nseg);
     }
-    TpM m{d, c.subs, c.met, a.q, a.nt, a.nk, a.crx, a.cry, a.xfx, a.yfx,
-          a.mfx ? a.mfx : a.xfx, a.mfy ? a.mfy : a.yfx, a.fx, a.fy, (int)nz, 0, 0, seg};
+    m.seg = seg;
     m.nstrip = nstrip;
     m.nseg = (d.ny + seg - 1) / seg;
     const long waves = nz * m.nstrip * m.nseg;
     if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
     const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
-    // (the one-row-ahead form, tp_march<ORD, false>, measured 3 % slower at C180)
+    // (the one-row-ahead form, tp_march<ORD, false, ...>, measured 3 % slower at C180)
     // MF: separate mass fluxes (w, pt and the tracers) or xfx / yfx themselves
+#define TP_GO(O, M_, F_) GT_LAUNCH((tp_march<O, true, M_, F_>), g, b, 0, c.st, m)
     if (a.mfx) {
-      if (a.ord == 5) GT_LAUNCH((tp_march<5, true, true>), g, b, 0, c.st, m);
-      else GT_LAUNCH((tp_march<6, true, true>), g, b, 0, c.st, m);
+      if (NFw == 2) { if (a.ord == 5) TP_GO(5, true, 2); else TP_GO(6, true, 2); }
+      else { if (a.ord == 5) TP_GO(5, true, 1); else TP_GO(6, true, 1); }
     } else {
-      if (a.ord == 5) GT_LAUNCH((tp_march<5, true, false>), g, b, 0, c.st, m);
-      else GT_LAUNCH((tp_march<6, true, false>), g, b, 0, c.st, m);
+      if (NFw == 2) { if (a.ord == 5) TP_GO(5, false, 2); else TP_GO(6, false, 2); }
+      else { if (a.ord == 5) TP_GO(5, false, 1); else TP_GO(6, false, 1); }
     }
+#undef TP_GO
   }
   HIP_LAUNCH_CHECK();
-  // algorithmic bytes: q read + fx, fy written per plane; crx cry xfx yfx (+ mfx mfy) read
-  // once per (sub-domain, level) however many tracers share them (ra_x, ra_y are formed
-  // in the kernel, the 2-D area plane is not counted)
+  // algorithmic bytes: q read + fx, fy written per field plane; crx cry xfx yfx (+ mfx mfy)
+  // read once per (sub-domain, level) however many fields share them (ra_x, ra_y are
+  // formed in the kernel, the 2-D area plane is not counted)
   const double cells = (double)d.nx * d.ny;
-  ktimer_bytes(8.0 * cells * (3.0 * nz + (double)d.nsub * a.nk * (4 + (a.mfx ? 2 : 0))));
+  ktimer_bytes(8.0 * cells * (double)d.nsub * a.nk * (3.0 * nfields + 4 + (a.mfx ? 2 : 0)));
 }
 
-void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, double* xfx, double* yfx, double* ra_x,
-                 double* ra_y, double* cmax_dev) {
+void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, double* xfx, double* yfx,
+                 double* cmax_dev) {
   const Dims& d = c.d;
-  (void)ra_x; (void)ra_y;
   HIP_CHECK(hipMemsetAsync(cmax_dev, 0, sizeof(double) * npz, c.st));
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   GT_LAUNCH(tracer_prep_k, dim3(cdiv(L.ni, BX), cdiv(L.nj, BY * TP_RPT), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
@@ -613,11 +683,11 @@ void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, doub
 }
 
 void tracer_split(const Ctx& c, int npz, const int* nsplt_dev, double* cx, double* cy, double* xfx, double* yfx,
-                  double* mfx, double* mfy, double* ra_x, double* ra_y) {
+                  double* mfx, double* mfy) {
   const Dims& d = c.d;
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   GT_LAUNCH(tracer_split_k, plane_grid(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d,
-                     c.met, npz, nsplt_dev, cx, cy, xfx, yfx, mfx, mfy, ra_x, ra_y);
+                     c.met, npz, nsplt_dev, cx, cy, xfx, yfx, mfx, mfy);
   HIP_LAUNCH_CHECK();
   // (no ra_x / ra_y planes: fv_tp_2d forms them from area and the split fluxes)
 }

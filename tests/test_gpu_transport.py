@@ -115,3 +115,38 @@ def test_tracer_2d_1l_parity(pkg, require_gpu, cmax_amp):
     a = got[:, :, NG:NG + d.ny, NG:NG + d.nx]
     b = ref[:, :, NG:NG + d.ny, NG:NG + d.nx]
     assert relerr(a, b) <= RTOL, relerr(a, b)
+
+
+@pytest.mark.parametrize("ord_,mf,layout", [(6, True, (1, 1)), (6, False, (2, 2)), (5, True, (2, 2))])
+def test_fv_tp_2d_field_pairs_bitwise(pkg, require_gpu, ord_, mf, layout):
+    """Field pairs in one wave (shared Courant / flux loads): nt = 4 tracers (two pairs) and a
+    pair of separate arrays (d_sw's w, pt) give bit for bit the fluxes of one launch per field."""
+    npz = 3
+    d = make_dom(pkg, 13, npz, 1, *layout)
+    r = rng(17)
+    inp = tp_inputs(d, npz, r)
+    for k, v in inp.items():
+        if k != "q":
+            d.upload("p_" + k, v)
+    qs = [1.0 + 0.3 * r.standard_normal(d.shape(npz)) for _ in range(4)]
+    mfx, mfy = ("p_mfx", "p_mfy") if mf else ("-", "-")
+    args = ["p_crx", "p_cry", "p_xfx", "p_yfx", "p_ra_x", "p_ra_y", mfx, mfy]
+    single = []
+    for n, q in enumerate(qs):
+        d.upload(f"p_q{n}", q)
+        d.stencil("fv_tp_2d", [f"p_q{n}"] + args + [f"p_fx{n}", f"p_fy{n}"], [ord_, 1])
+        single.append((d.download(f"p_fx{n}"), d.download(f"p_fy{n}")))
+    # four tracers in one array [sub][t][k]: two pairs
+    d.upload("p_q4", np.concatenate(qs, axis=1))
+    d.stencil("fv_tp_2d", ["p_q4"] + args + ["p_fx4", "p_fy4"], [ord_, 4])
+    gx, gy = d.download("p_fx4"), d.download("p_fy4")
+    for n in range(4):
+        assert np.array_equal(gx[:, n * npz:(n + 1) * npz], single[n][0]), f"tracer {n} fx"
+        assert np.array_equal(gy[:, n * npz:(n + 1) * npz], single[n][1]), f"tracer {n} fy"
+    # two separate arrays
+    d.stencil("fv_tp_2d_pair", ["p_q0", "p_q1", "p_crx", "p_cry", "p_xfx", "p_yfx", mfx, mfy, "p_ax", "p_ay",
+                                "p_bx", "p_by"], [ord_])
+    assert np.array_equal(d.download("p_ax"), single[0][0])
+    assert np.array_equal(d.download("p_ay"), single[0][1])
+    assert np.array_equal(d.download("p_bx"), single[1][0])
+    assert np.array_equal(d.download("p_by"), single[1][1])
