@@ -104,11 +104,22 @@ __device__ __forceinline__ double ppm_x_dpp(double q, double dx, int g, int N, d
   const double qm1 = dpp_prev(q), qm2 = dpp_prev(qm1), qp1 = dpp_next(q);
   double al;
   if (EX) {
-    // DPP outside any lane-divergent branch: every source lane must be active
-    const double dxm1 = dpp_prev(dx);
-    const double qv[4] = {qm2, qm1, q, qp1};
-    const double dv[4] = {dpp_prev(dxm1), dxm1, dx, dpp_next(dx)};
-    al = ppm_al(g, N, qv, dv);
+    // ppm_al with the tile-edge form at g = 0, N, 0.5 * (Q1 + Q2), evaluated with ONE
+    // division per lane instead of two: the edge lane divides for Q1 (its cells g-2, g-1)
+    // and its right neighbour (g = 1, N+1) divides for the edge lane's Q2 (cells g, g+1,
+    // held by that neighbour as its own g-1, g); Q2 then comes back by DPP.  Same operands
+    // and operation order as ppm_al, so the same values.  (All DPP outside any
+    // lane-divergent branch: every source lane must be active.)
+    const double dxm1 = dpp_prev(dx), dxm2 = dpp_prev(dxm1);
+    const bool e0 = g == 0 || g == N, e1 = g == 1 || g == N + 1;
+    const double num = e0 ? (2.0 * dxm1 + dxm2) * qm1 - dxm1 * qm2 : (2.0 * dxm1 + dx) * qm1 - dxm1 * q;
+    const double den = e0 ? dxm2 + dxm1 : dxm1 + dx;
+    const double qd = (e0 || e1) ? num / den : 0.0;
+    const double q2 = dpp_next(qd);
+    if (g == -1 || g == N - 1) al = C1 * qm2 + C2 * qm1 + C3 * q;
+    else if (e1) al = C3 * qm1 + C2 * q + C1 * qp1;
+    else if (e0) al = 0.5 * (qd + q2);
+    else al = P1 * (qm1 + q) + P2 * (qm2 + qp1);
   } else {
     al = P1 * (qm1 + q) + P2 * (qm2 + qp1);
   }
