@@ -213,6 +213,81 @@ __global__ void __launch_bounds__(256) edge_prof_k(Dims d, int npz, const double
   }
 }
 
+// Register-resident edge_profile: one lane per (face column, field), the column's KMAX
+// levels held in VGPRs.  The forward pivots overwrite the inputs in place and the back
+// substitution reads them from registers, so each field is read once and its result
+// written once (8 field passes instead of the 16 of edge_prof_k, whose forward values
+// round-trip through the output).  Same expressions in the same order as edge_prof_k:
+// bit-identical results.  Loops are unrolled over KMAX with uniform guards k < km.
+template <int KMAX>
+__global__ void __launch_bounds__(256) edge_prof_reg_k(Dims d, int npz, const double* __restrict__ dp0,
+                                                       const double* __restrict__ crx, const double* __restrict__ xfx,
+                                                       const double* __restrict__ cry, const double* __restrict__ yfx,
+                                                       double* __restrict__ crx_e, double* __restrict__ xfx_e,
+                                                       double* __restrict__ cry_e, double* __restrict__ yfx_e) {
+  __shared__ double gam[KMAX], gks[KMAX], bets[KMAX];
+  const int km = npz, k1 = npz + 1;
+  const int tid = threadIdx.y * blockDim.x + threadIdx.x;
+  for (int k = 1 + tid; k < km; k += blockDim.x * blockDim.y) gks[k] = dp0[k - 1] / dp0[k];
+  __syncthreads();
+  const double g0 = dp0[1] / dp0[0];
+  const double bet0 = g0 * (g0 + 0.5);
+  if (tid == 0) {
+    gam[0] = (1.0 + g0 * (g0 + 1.5)) / bet0;
+    for (int k = 1; k < km; ++k) {
+      const double bet = 2.0 + 2.0 * gks[k] - gam[k - 1];
+      bets[k] = bet;
+      gam[k] = gks[k] / bet;
+    }
+  }
+  __syncthreads();
+  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  int i, j;
+  if (!thread_point(L, i, j)) return;
+  const int s = blockIdx.z >> 2, c = blockIdx.z & 3;
+  const long P = d.plane;
+  const long o = pidx(d, i, j);
+  const bool ok = c < 2 ? (i >= 0 && i <= d.nx && j <= d.ny + NG - 1) : (j >= 0 && j <= d.ny && i <= d.nx + NG - 1);
+  if (!ok) return;
+  const double* __restrict__ Q = (c == 0 ? crx : c == 1 ? xfx : c == 2 ? cry : yfx) + (long)s * km * P + o;
+  double* __restrict__ E = (c == 0 ? crx_e : c == 1 ? xfx_e : c == 2 ? cry_e : yfx_e) + (long)s * k1 * P + o;
+  double q[KMAX];
+#pragma unroll
+  for (int k = 0; k < KMAX; ++k)
+    if (k < km) q[k] = Q[k * P];
+  // forward elimination, pivots in place of the inputs
+  const double xt1_0 = 2.0 * g0 * (g0 + 1.0);
+  double qprev = q[0], qkm2 = q[0];
+  q[0] = (xt1_0 * q[0] + q[1]) / bet0;
+#pragma unroll
+  for (int k = 1; k < KMAX; ++k) {
+    if (k < km) {
+      const double qk = q[k];
+      if (k == km - 2) qkm2 = qk;
+      q[k] = (3.0 * (qprev + gks[k] * qk) - q[k - 1]) / bets[k];
+      qprev = qk;
+    }
+  }
+  double qlast = q[0];
+#pragma unroll
+  for (int k = 1; k < KMAX; ++k)
+    if (k == km - 1) qlast = q[k];
+  // bottom edge and back substitution
+  const double gk = gks[km - 1];
+  const double a_bot = 1.0 + gk * (gk + 1.5);
+  const double xt1 = 2.0 * gk * (gk + 1.0);
+  const double xt2 = gk * (gk + 0.5) - a_bot * gam[km - 1];
+  double x = (xt1 * qprev + qkm2 - a_bot * qlast) / xt2;
+  E[km * P] = x;
+#pragma unroll
+  for (int k = KMAX - 1; k >= 0; --k) {
+    if (k < km) {
+      x = q[k] - gam[k] * x;
+      E[k * P] = x;
+    }
+  }
+}
+
 // ra_x, ra_y for the interface-level transport of zh
 // zh update from the transported fluxes (compute cells, all interfaces)
 // (ra_x = area + xfx|i - xfx|i+1 and ra_y = area + yfx|j - yfx|j+1 formed here, as in
@@ -756,8 +831,15 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
   const int k1 = a.npz + 1;
   Launch2D Lf{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   if (a.npz > EP_KMAX) throw std::runtime_error("update_dz_d: npz too large");
-  GT_LAUNCH(edge_prof_k, g2(d, Lf, d.nsub), dim3(BX, BY), 0, c.st, d, a.npz, a.dp0, a.crx, a.xfx, a.cry,
-            a.yfx, a.crx_e, a.xfx_e, a.cry_e, a.yfx_e);
+  if (a.npz >= 3 && a.npz <= 32)
+    GT_LAUNCH(edge_prof_reg_k<32>, g2(d, Lf, 4 * d.nsub), dim3(BX, BY), 0, c.st, d, a.npz, a.dp0, a.crx, a.xfx,
+              a.cry, a.yfx, a.crx_e, a.xfx_e, a.cry_e, a.yfx_e);
+  else if (a.npz >= 3 && a.npz <= 80)
+    GT_LAUNCH(edge_prof_reg_k<80>, g2(d, Lf, 4 * d.nsub), dim3(BX, BY), 0, c.st, d, a.npz, a.dp0, a.crx, a.xfx,
+              a.cry, a.yfx, a.crx_e, a.xfx_e, a.cry_e, a.yfx_e);
+  else
+    GT_LAUNCH(edge_prof_k, g2(d, Lf, d.nsub), dim3(BX, BY), 0, c.st, d, a.npz, a.dp0, a.crx, a.xfx, a.cry,
+              a.yfx, a.crx_e, a.xfx_e, a.cry_e, a.yfx_e);
   HIP_LAUNCH_CHECK();
   TpArgs t{};
   t.q = a.zh; t.nt = 1; t.nk = k1;
