@@ -26,6 +26,11 @@ struct UdzdArgs {
   double* zh;
 };
 void update_dz_d(const Ctx& c, const UdzdArgs& a);
+// update_dz_d's edge_profile of (crx, xfx) on x-face and (cry, yfx) on y-face columns.
+// variant: 0 = by level count (register column for 3 <= npz <= 80, blocked above),
+// 1 = force the blocked form edge_prof_k (the bitwise reference of the register form)
+void edge_profile(const Ctx& c, int npz, const double* dp0, const double* crx, const double* xfx, const double* cry,
+                  const double* yfx, double* crx_e, double* xfx_e, double* cry_e, double* yfx_e, int variant = 0);
 
 struct Riem3Args {
   int npz;
@@ -62,7 +67,9 @@ struct RemapScratch {
   double* s[3];  // q edges, gam, source copy: remap_jobs(nq) * (npz+1) levels each
 };
 int remap_jobs(int nq);
+// variant: 0 = register-resident columns where instantiated (L10/12/20/72), else the
+// scratch-column jobs; 1 = force the scratch-column jobs (remap_job_k, the bitwise reference)
 void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fill, const double* ak_dev,
-                            const double* bk_dev, const RemapState& S, const RemapScratch& R);
+                            const double* bk_dev, const RemapState& S, const RemapScratch& R, int variant = 0);
 
 }  // namespace gtfv3

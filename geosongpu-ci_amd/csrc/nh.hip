@@ -826,21 +826,27 @@ void p_grad_c(const Ctx& c, int npz, double dt2, const double* delpc, const doub
   HIP_LAUNCH_CHECK();
 }
 
+void edge_profile(const Ctx& c, int npz, const double* dp0, const double* crx, const double* xfx, const double* cry,
+                  const double* yfx, double* crx_e, double* xfx_e, double* cry_e, double* yfx_e, int variant) {
+  const Dims& d = c.d;
+  Launch2D Lf{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  if (npz > EP_KMAX || npz < 2) throw std::runtime_error("edge_profile: 2 <= npz <= 256 required");
+  if (variant != 1 && npz >= 3 && npz <= 32)
+    GT_LAUNCH(edge_prof_reg_k<32>, g2(d, Lf, 4 * d.nsub), dim3(BX, BY), 0, c.st, d, npz, dp0, crx, xfx, cry, yfx,
+              crx_e, xfx_e, cry_e, yfx_e);
+  else if (variant != 1 && npz >= 3 && npz <= 80)
+    GT_LAUNCH(edge_prof_reg_k<80>, g2(d, Lf, 4 * d.nsub), dim3(BX, BY), 0, c.st, d, npz, dp0, crx, xfx, cry, yfx,
+              crx_e, xfx_e, cry_e, yfx_e);
+  else
+    GT_LAUNCH(edge_prof_k, g2(d, Lf, d.nsub), dim3(BX, BY), 0, c.st, d, npz, dp0, crx, xfx, cry, yfx, crx_e,
+              xfx_e, cry_e, yfx_e);
+  HIP_LAUNCH_CHECK();
+}
+
 void update_dz_d(const Ctx& c, const UdzdArgs& a) {
   const Dims& d = c.d;
   const int k1 = a.npz + 1;
-  Launch2D Lf{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  if (a.npz > EP_KMAX) throw std::runtime_error("update_dz_d: npz too large");
-  if (a.npz >= 3 && a.npz <= 32)
-    GT_LAUNCH(edge_prof_reg_k<32>, g2(d, Lf, 4 * d.nsub), dim3(BX, BY), 0, c.st, d, a.npz, a.dp0, a.crx, a.xfx,
-              a.cry, a.yfx, a.crx_e, a.xfx_e, a.cry_e, a.yfx_e);
-  else if (a.npz >= 3 && a.npz <= 80)
-    GT_LAUNCH(edge_prof_reg_k<80>, g2(d, Lf, 4 * d.nsub), dim3(BX, BY), 0, c.st, d, a.npz, a.dp0, a.crx, a.xfx,
-              a.cry, a.yfx, a.crx_e, a.xfx_e, a.cry_e, a.yfx_e);
-  else
-    GT_LAUNCH(edge_prof_k, g2(d, Lf, d.nsub), dim3(BX, BY), 0, c.st, d, a.npz, a.dp0, a.crx, a.xfx, a.cry,
-              a.yfx, a.crx_e, a.xfx_e, a.cry_e, a.yfx_e);
-  HIP_LAUNCH_CHECK();
+  edge_profile(c, a.npz, a.dp0, a.crx, a.xfx, a.cry, a.yfx, a.crx_e, a.xfx_e, a.cry_e, a.yfx_e, 0);
   TpArgs t{};
   t.q = a.zh; t.nt = 1; t.nk = k1;
   t.crx = a.crx_e; t.cry = a.cry_e; t.xfx = a.xfx_e; t.yfx = a.yfx_e;

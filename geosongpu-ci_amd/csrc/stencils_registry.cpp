@@ -186,7 +186,43 @@ std::map<std::string, Fn>& reg() {
                        dy.field("ws", 1).p};
          RemapScratch rsc;
          for (int n = 0; n < 3; ++n) rsc.s[n] = dy.field("_rmj" + std::to_string(n), remap_jobs(nq) * k1).p;
-         lagrangian_to_eulerian(dy.ctx(), npz, nq, dy.ak.at(0), p.empty() || p[0] != 0.0, vert, vert + k1, rs, rsc);
+         lagrangian_to_eulerian(dy.ctx(), npz, nq, dy.ak.at(0), p.empty() || p[0] != 0.0, vert, vert + k1, rs, rsc,
+                                p.size() > 1 ? (int)p[1] : 0);
+       }},
+      // edge_profile(crx, xfx, cry, yfx | crx_e, xfx_e, cry_e, yfx_e): update_dz_d's interface values
+      // (npz+1 levels) with the reference thicknesses of set_vertical().  params: variant (0 by level
+      // count, 1 the blocked edge_prof_k)
+      {"edge_profile",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 8, "edge_profile");
+         Field& cx = F(dy, f[0]);
+         const int npz = cx.nk, k1 = npz + 1;
+         if (npz != dy.nl.npz) throw std::runtime_error("edge_profile: fields must have npz levels");
+         const double* vert = dy.vertical_dev();
+         edge_profile(dy.ctx(), npz, vert + 2 * k1, cx.p, F(dy, f[1]).p, F(dy, f[2]).p, F(dy, f[3]).p,
+                      dy.field(f[4], k1).p, dy.field(f[5], k1).p, dy.field(f[6], k1).p, dy.field(f[7], k1).p,
+                      p.empty() ? 0 : (int)p[0]);
+       }},
+      // update_dz_d(zh, crx, cry, xfx, yfx): the interface heights zh (npz+1 levels) transported in
+      // place with the interface-level Courant numbers and area fluxes (edge_profile + fv_tp_2d +
+      // the flux-form update; FV3 update_dz_d before its dz_min clamp).  params: hord
+      {"update_dz_d",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 5, "update_dz_d");
+         Field& zh = F(dy, f[0]);
+         const int npz = dy.nl.npz, k1 = npz + 1;
+         if (zh.nk != k1 || F(dy, f[1]).nk != npz) throw std::runtime_error("update_dz_d: field shapes");
+         const double* vert = dy.vertical_dev();
+         UdzdArgs za{};
+         za.npz = npz;
+         za.hord = p.empty() ? 6 : (int)p[0];
+         za.dp0 = vert + 2 * k1;
+         za.crx = F(dy, f[1]).p; za.cry = F(dy, f[2]).p; za.xfx = F(dy, f[3]).p; za.yfx = F(dy, f[4]).p;
+         za.crx_e = dy.field("_ud_crx", k1).p; za.cry_e = dy.field("_ud_cry", k1).p;
+         za.xfx_e = dy.field("_ud_xfx", k1).p; za.yfx_e = dy.field("_ud_yfx", k1).p;
+         za.fx = dy.field("_ud_fx", k1).p; za.fy = dy.field("_ud_fy", k1).p; za.gam = dy.field("_ud_gam", k1).p;
+         za.zh = zh.p;
+         update_dz_d(dy.ctx(), za);
        }},
       // a2b_ord4(q | qout): cell means -> cell corners (4th order, cubed-sphere edge forms)
       {"a2b_ord4",

@@ -217,8 +217,10 @@ def edge_profile(q, dp0):
     return qe
 
 
-def update_dz_d(zh, crx, cry, xfx, yfx, zs, sub, m, nx, ny, dp0, dt, hord, dz_min):
-    km = crx.shape[0]
+def update_dz_d_transport(zh, crx, cry, xfx, yfx, sub, m, nx, ny, dp0, hord):
+    """the interface heights zh transported with the interface-level Courant numbers and
+    area fluxes (edge_profile, fv_tp_2d, flux-form update); compute cells updated, the
+    rest of the plane unchanged.  FV3 update_dz_d before its dz_min clamp."""
     P = Plane(sub, nx, ny, zh.shape[-2], zh.shape[-1])
     rx = P.reg(0, nx, -NG, ny + NG - 1)
     ry = P.reg(-NG, nx + NG - 1, 0, ny)
@@ -232,7 +234,14 @@ def update_dz_d(zh, crx, cry, xfx, yfx, zs, sub, m, nx, ny, dp0, dt, hord, dz_mi
     fx, fy = fv_tp_2d(zh, crx_e, cry_e, xfx_e, yfx_e, ra_x, ra_y, sub, m, nx, ny, hord)
     comp = P.reg(0, nx - 1, 0, ny - 1)
     new = (zh * area + fx - sh(fx, 1, 0) + fy - sh(fy, 0, 1)) / (ra_x + ra_y - area)
-    out = np.where(comp, new, zh)
+    return np.where(comp, new, zh)
+
+
+def update_dz_d(zh, crx, cry, xfx, yfx, zs, sub, m, nx, ny, dp0, dt, hord, dz_min):
+    km = crx.shape[0]
+    P = Plane(sub, nx, ny, zh.shape[-2], zh.shape[-1])
+    comp = P.reg(0, nx - 1, 0, ny - 1)
+    out = update_dz_d_transport(zh, crx, cry, xfx, yfx, sub, m, nx, ny, dp0, hord)
     ws = np.where(comp, (zs - out[km]) * (1.0 / dt), 0.0)
     for k in range(km - 1, -1, -1):
         out[k] = np.where(comp, np.maximum(out[k], out[k + 1] + dz_min), out[k])
