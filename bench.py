@@ -69,6 +69,30 @@ def pmc_traffic(fam, launches):
     return None, None
 
 
+def state_check(d, ptop, names=("ps", "pt", "delp", "u", "w")):
+    """After the timed steps: the state must be finite and physically bounded, else the run
+    has diverged and its throughput means nothing (raises).  Returns the bounds and a
+    checksum (fp64 sums of the compute-domain fields) for the JSON line."""
+    NG = 3
+    n_x, n_y = d.nx, d.ny
+    out = {}
+    for k in names:
+        a = d.download(k)[..., NG:NG + n_y, NG:NG + n_x]
+        if not np.all(np.isfinite(a)):
+            raise SystemExit(f"bench: state field {k} is not finite after the timed steps")
+        out[k] = a
+    pt, dp, ps = out["pt"], out["delp"], out["ps"]
+    ok = (150.0 < pt.min() and pt.max() < 400.0 and dp.min() > 0.0 and 3.0e4 < ps.min() and ps.max() < 1.2e5
+          and np.abs(out["u"]).max() < 200.0)
+    res = dict(finite=True, bounded=bool(ok), pt_min=float(pt.min()), pt_max=float(pt.max()),
+               ps_min=float(ps.min()), ps_max=float(ps.max()), max_abs_u=float(np.abs(out["u"]).max()),
+               max_abs_w=float(np.abs(out["w"]).max()),
+               checksum={k: float(v.sum(dtype=np.float64)) for k, v in out.items()})
+    if not ok:
+        raise SystemExit(f"bench: state out of physical bounds after the timed steps: {res}")
+    return res
+
+
 def layout_for(n):
     """(layout_x, layout_y) for n ranks: 6*lx*ly sub-domains divisible by n"""
     # bands of full tile width (1 x ly): the x-marching kernels keep C180's strip
@@ -258,6 +282,8 @@ def main():
                                    backend="hip-gfx950-f64", step_seconds=per_step, init_s=t_init,
                                    run_s=sum(per_step), finalize_s=time.perf_counter() - t_fin)
 
+    check = state_check(d, ak[0])  # every rank checks its own sub-domains
+
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         cpu = cpu_baseline(pkg, a.cpu_npx, a.npz, nq, a.dt, a.moist)
@@ -284,6 +310,7 @@ def main():
                        "dt_atmos": a.dt, "n_split": 6, "k_split": 1, "cells_per_step": cells},
             "roofline": roof,
             "cpu_baseline": cpu,
+            "state_check": check,
         }
         print(json.dumps(out))
     d.close()

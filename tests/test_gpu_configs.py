@@ -1,0 +1,111 @@
+"""GPU runs of the BASELINE.json configurations that fit one GPU (VERDICT r01 configs_untested).
+
+* config 2, Held-Suarez C48 L72 with all 6 tiles on one MI355X: one HIP fv_dynamics step
+  against the oracle step committed as a fixture (tools/make_c48_golden.py runs
+  oracle/fv_dynamics.py on the CPU, ~90 s: too slow to repeat on the GPU box).  Compared:
+  the field values at 1500 fixed random compute points per field and the compute-domain
+  mean of every (tile, level) plane.  Bar as tests/test_gpu_step.py: scaled error
+  <= 1e-9 of the field's mean magnitude, w and omega absolute (exp / log of ocml vs glibc).
+* config 3's grid, Held-Suarez C180 L72 (the benchmark workload) on one GPU: property
+  checks of one step — finite and physically bounded, every column's mass equal to
+  ps - ptop on the hybrid levels after the remap, global dry mass within the documented
+  drift — and decomposition invariance: the 1x1 layout and the 8-GPU band layout 1x4
+  (24 sub-domains on one GPU) give the same bits.
+"""
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, metrics_of
+from oracle import NG
+
+pytestmark = pytest.mark.gpu
+FIELDS = ("u", "v", "w", "delz", "pt", "delp", "q", "ua", "va", "omga", "pkz", "ps", "pe", "peln", "pk")
+
+
+def jw_domain(pkg, npx, npz, nq, dt, layout=(1, 1)):
+    state = importlib.import_module(pkg.__name__ + ".state")
+    d = pkg.Domain(npx=npx, npz=npz, nq=nq, layout_x=layout[0], layout_y=layout[1], dt=dt)
+    ak, bk, ks = state.hybrid_levels(npz)
+    st = state.jablonowski_williamson(d, ak, bk)
+    d.set_vertical(ak, bk, ks)
+    for k, v in st.items():
+        d.upload(k, v)
+    return d, st, ak, bk
+
+
+def test_c48_l72_step_vs_oracle_fixture(pkg, require_gpu):
+    g = np.load(os.path.join(ROOT, "tests", "golden", "c48_l72_step.npz"))
+    d, _, _, _ = jw_domain(pkg, int(g["npx"]), int(g["npz"]), int(g["nq"]), float(g["dt"]))
+    try:
+        d.step(1)
+        n = d.N
+        worst = {}
+        for k in FIELDS:
+            a = d.download(k)[..., NG:NG + n, NG:NG + n]
+            assert np.all(np.isfinite(a)), k
+            got = a[tuple(g[f"{k}_idx"].astype(np.int64).T)]
+            want = g[f"{k}_val"]
+            means = a.mean(axis=(2, 3))
+            scale = np.abs(g[f"{k}_mean"]).mean() + 1e-300
+            if k == "w":
+                err = np.abs(got - want).max()
+                assert err <= 1e-9, f"w: abs error {err:.3e} m/s"
+            elif k == "omga":
+                err = np.abs(got - want).max()
+                assert err <= 1e-7, f"omga: abs error {err:.3e} Pa/s"
+            else:
+                err = np.abs(got - want).max() / scale
+                assert err <= 1e-9, f"{k}: scaled point error {err:.3e}"
+                merr = np.abs(means - g[f"{k}_mean"]).max() / scale
+                assert merr <= 1e-9, f"{k}: scaled plane-mean error {merr:.3e}"
+            worst[k] = err
+        print("C48 L72 HIP vs oracle fixture:", {k: f"{v:.1e}" for k, v in worst.items()})
+    finally:
+        d.close()
+
+
+def test_c180_l72_step_properties_and_band_layout(pkg, require_gpu):
+    npx, npz, nq, dt = 181, 72, 4, 450.0
+    d1, st, ak, bk = jw_domain(pkg, npx, npz, nq, dt)
+    n = d1.N
+    area = d1.metric("area")[:, NG:NG + n, NG:NG + n]
+
+    def mass(dp):
+        return float((dp[:, :, NG:NG + n, NG:NG + n] * area[:, None]).sum())
+
+    m0 = mass(st["delp"])
+    del st
+    d1.step(1)
+    names = ("u", "v", "w", "pt", "delp", "delz", "q", "ps", "pe", "omga")
+    o1 = {k: d1.download(k) for k in names}
+    d1.close()
+    c = (Ellipsis, slice(NG, NG + n), slice(NG, NG + n))
+    for k in names:
+        assert np.all(np.isfinite(o1[k][c])), f"{k} not finite"
+    assert 150.0 < o1["pt"][c].min() and o1["pt"][c].max() < 400.0
+    assert np.abs(o1["u"][c]).max() < 150.0 and np.abs(o1["v"][c]).max() < 150.0
+    assert np.abs(o1["w"][c]).max() < 20.0
+    assert o1["delp"][c].min() > 0.0 and o1["delz"][c].max() < 0.0
+    ps = o1["ps"][:, 0, NG:NG + n, NG:NG + n]
+    np.testing.assert_allclose(o1["delp"][c].sum(axis=1), ps - ak[0], rtol=1e-13)
+    np.testing.assert_allclose(o1["pe"][c][:, 1:-1], ak[None, 1:-1, None, None] + bk[None, 1:-1, None, None]
+                               * ps[:, None], rtol=1e-14)
+    # global dry mass: the documented cube-corner drift, not more
+    assert abs(mass(o1["delp"]) - m0) / m0 < 1e-6
+    # the 8-GPU band layout on one GPU: same bits
+    d4, _, _, _ = jw_domain(pkg, npx, npz, nq, dt, layout=(1, 4))
+    try:
+        d4.step(1)
+        ny = d4.ny
+        for k in names:
+            a4 = d4.download(k)
+            for s, sub in enumerate(d4.subs):
+                t, jo = sub["tile"], sub["joff"]
+                a = a4[s][..., NG:NG + ny, NG:NG + n]
+                b = o1[k][t][..., NG + jo:NG + jo + ny, NG:NG + n]
+                assert np.array_equal(a, b), f"{k}: band layout differs on sub-domain {s}"
+    finally:
+        d4.close()
