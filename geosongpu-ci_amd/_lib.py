@@ -23,6 +23,8 @@ DEVICE_SYMBOLS = [
     "gtfv3_create",
     "gtfv3_destroy",
     "gtfv3_get_unique_id",
+    "gtfv3_bootstrap_id",
+    "gtfv3_bootstrap_done",
     "gtfv3_dims",
     "gtfv3_sub_info",
     "gtfv3_field_create",
@@ -73,6 +75,8 @@ def lib():
         "gtfv3_create": (P, [S, I, I, P]),
         "gtfv3_destroy": (None, [P]),
         "gtfv3_get_unique_id": (I, [P]),
+        "gtfv3_bootstrap_id": (I, [P, ctypes.c_char_p, IP, IP]),
+        "gtfv3_bootstrap_done": (I, []),
         "gtfv3_dims": (I, [P, IP]),
         "gtfv3_sub_info": (I, [P, I, IP]),
         "gtfv3_field_create": (I, [P, S, I]),

@@ -1,11 +1,16 @@
 // bridge.hip — process-global geos_gtfv3 context and Fortran <-> HBM conversion.
 #include "bridge.hpp"
 
+#include <dlfcn.h>
+#include <unistd.h>
+
 #include <chrono>
+#include <cstdint>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <fstream>
+#include <iterator>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -117,6 +122,121 @@ void bridge_fatal(const std::string& msg) {
   if (!(nf && std::atoi(nf) == 1)) std::abort();
 }
 
+// ---- ncclUniqueId bootstrap ----
+// Under GEOS the caller hands its Fortran communicator handle by value in `comm`
+// (argument.py:57-58,83-84; the reference's C shim does MPI_Comm_f2c on it, base.py:89-96)
+// and the executable itself links MPI.  The bridge does not link MPI: it resolves
+// MPI_Comm_f2c / MPI_Comm_rank / MPI_Comm_size / MPI_Bcast from the process at run time
+// (dlsym(RTLD_DEFAULT)), so one library serves MPICH-ABI MPIs (MPICH, Cray, Intel: MPI_Comm
+// an int, MPI_BYTE = 0x4c00010d) and Open MPI (handles are pointers, MPI_BYTE is
+// &ompi_mpi_byte).  Without MPI in the process (standalone runs) the rank comes from the
+// launcher's environment and the id travels through GTFV3_NCCL_ID_FILE, stamped with a
+// job token so that a file left by an earlier job is never taken for this job's id.
+namespace {
+struct MpiSyms {
+  intptr_t (*f2c)(intptr_t) = nullptr;
+  int (*rank)(intptr_t, int*) = nullptr;
+  int (*size)(intptr_t, int*) = nullptr;
+  int (*bcast)(void*, int, intptr_t, int, intptr_t) = nullptr;
+  int (*initialized)(int*) = nullptr;
+  intptr_t byte = 0;
+  // MPI present in the process and initialised (any handle value, Open MPI's world is 0)
+  bool ok() const {
+    int flag = 0;
+    return f2c && rank && size && bcast && initialized && initialized(&flag) == 0 && flag;
+  }
+};
+
+MpiSyms mpi_syms() {
+  MpiSyms m;
+  m.f2c = (intptr_t(*)(intptr_t))dlsym(RTLD_DEFAULT, "MPI_Comm_f2c");
+  m.rank = (int (*)(intptr_t, int*))dlsym(RTLD_DEFAULT, "MPI_Comm_rank");
+  m.size = (int (*)(intptr_t, int*))dlsym(RTLD_DEFAULT, "MPI_Comm_size");
+  m.bcast = (int (*)(void*, int, intptr_t, int, intptr_t))dlsym(RTLD_DEFAULT, "MPI_Bcast");
+  m.initialized = (int (*)(int*))dlsym(RTLD_DEFAULT, "MPI_Initialized");
+  void* ompi_byte = dlsym(RTLD_DEFAULT, "ompi_mpi_byte");
+  m.byte = ompi_byte ? (intptr_t)ompi_byte : (intptr_t)0x4c00010d;
+  return m;
+}
+
+// the Fortran handle is an integer passed by value through a void* parameter
+intptr_t fortran_handle(void* comm) { return (intptr_t)(int)(intptr_t)comm; }
+
+std::string job_token() {
+  const char* names[] = {"GTFV3_JOB_TOKEN", "SLURM_JOB_ID", "PBS_JOBID", "TORCHELASTIC_RUN_ID", "MASTER_PORT",
+                         nullptr};
+  std::string t;
+  for (const char* const* n = names; *n; ++n) {
+    const char* v = std::getenv(*n);
+    if (v && *v) { t = std::string(*n) + "=" + v; break; }
+  }
+  const char* step = std::getenv("SLURM_STEP_ID");
+  if (step) t += std::string(".") + step;
+  return t;
+}
+
+std::string g_id_file;  // written by rank 0, removed at finalize
+}  // namespace
+
+void job_rank_size(void* comm, int* rank, int* nranks) {
+  MpiSyms m = mpi_syms();
+  if (m.ok()) {
+    intptr_t c = m.f2c(fortran_handle(comm));
+    if (m.rank(c, rank) != 0 || m.size(c, nranks) != 0) throw std::runtime_error("MPI_Comm_rank/size failed");
+    return;
+  }
+  const char* rk[] = {"GTFV3_RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID", "RANK", nullptr};
+  const char* sz[] = {"GTFV3_WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS", "WORLD_SIZE", nullptr};
+  *rank = env_int(rk, 0);
+  *nranks = env_int(sz, 1);
+}
+
+void share_unique_id(void* comm, int rank, int nranks, unsigned char* id) {
+  if (nranks <= 1) return;
+  MpiSyms m = mpi_syms();
+  if (m.ok()) {
+    intptr_t c = m.f2c(fortran_handle(comm));
+    if (m.bcast(id, 128, m.byte, 0, c) != 0) throw std::runtime_error("MPI_Bcast of the ncclUniqueId failed");
+    return;
+  }
+  const char* fn = std::getenv("GTFV3_NCCL_ID_FILE");
+  if (!fn) throw std::runtime_error("multi-rank bridge without MPI needs GTFV3_NCCL_ID_FILE");
+  const std::string token = job_token();
+  if (token.empty())
+    throw std::runtime_error("GTFV3_NCCL_ID_FILE needs a job token (GTFV3_JOB_TOKEN, SLURM_JOB_ID, ...)");
+  // record: "GTFV3ID1" | token length (4 B) | token | 128-byte id
+  if (rank == 0) {
+    std::string rec = "GTFV3ID1";
+    uint32_t n = (uint32_t)token.size();
+    rec.append((const char*)&n, 4);
+    rec += token;
+    rec.append((const char*)id, 128);
+    std::string tmp = std::string(fn) + ".tmp." + std::to_string((long)getpid());
+    {
+      std::ofstream out(tmp, std::ios::binary | std::ios::trunc);
+      out.write(rec.data(), (std::streamsize)rec.size());
+      if (!out) throw std::runtime_error("cannot write the ncclUniqueId file");
+    }
+    if (std::rename(tmp.c_str(), fn) != 0) throw std::runtime_error("cannot publish the ncclUniqueId file");
+    g_id_file = fn;
+    return;
+  }
+  for (int t = 0;; ++t) {
+    std::ifstream in(fn, std::ios::binary);
+    std::string rec((std::istreambuf_iterator<char>(in)), std::istreambuf_iterator<char>());
+    if (rec.size() >= 12 && rec.compare(0, 8, "GTFV3ID1") == 0) {
+      uint32_t n;
+      std::memcpy(&n, rec.data() + 8, 4);
+      if (rec.size() == 12 + n + 128 && rec.compare(12, n, token) == 0) {
+        std::memcpy(id, rec.data() + 12 + n, 128);
+        return;
+      }
+    }
+    if (t >= 6000) throw std::runtime_error("timed out waiting for this job's ncclUniqueId file");
+    std::this_thread::sleep_for(std::chrono::milliseconds(10));
+  }
+}
+
 void bridge_init(void* comm, int npx, int npy, int npz, int ntiles, int is, int ie, int js, int je, int isd, int ied,
                  int jsd, int jed, float bdt, int nq_tot) {
   (void)comm;
@@ -124,10 +244,9 @@ void bridge_init(void* comm, int npx, int npy, int npz, int ntiles, int is, int 
   if (npx != npy) throw std::runtime_error("geos_gtfv3_init: npx != npy");
   if (isd != is - NG || ied != ie + NG || jsd != js - NG || jed != je + NG)
     throw std::runtime_error("geos_gtfv3_init: data domain must be the compute domain +/- 3 halo points");
-  const char* rk[] = {"GTFV3_RANK", "OMPI_COMM_WORLD_RANK", "PMI_RANK", "SLURM_PROCID", "RANK", nullptr};
-  const char* sz[] = {"GTFV3_WORLD_SIZE", "OMPI_COMM_WORLD_SIZE", "PMI_SIZE", "SLURM_NTASKS", "WORLD_SIZE", nullptr};
   const char* tp[] = {"GTFV3_BRIDGE_TILES_PER_RANK", nullptr};
-  int rank = env_int(rk, 0), nranks = env_int(sz, 1);
+  int rank = 0, nranks = 1;
+  job_rank_size(comm, &rank, &nranks);
   g_tiles_per_rank = env_int(tp, 1);
   int N = npx - 1, nx = ie - is + 1, ny = je - js + 1;
   Namelist nl;
@@ -146,28 +265,19 @@ void bridge_init(void* comm, int npx, int npy, int npz, int ntiles, int is, int 
   }
   std::vector<unsigned char> id(128, 0);
   if (nranks > 1) {
-    // GEOS path: rank 0's ncclUniqueId would be broadcast over the communicator
-    // handed in as `comm` (MPI_Comm_f2c, base.py:89-96).  MPI is not linked
-    // here, so the id goes through a shared file named by GTFV3_NCCL_ID_FILE.
-    const char* fn = std::getenv("GTFV3_NCCL_ID_FILE");
-    if (!fn) throw std::runtime_error("multi-rank bridge needs GTFV3_NCCL_ID_FILE");
-    std::string tmp = std::string(fn) + ".tmp";
     if (rank == 0) {
       ncclUniqueId uid;
       if (ncclGetUniqueId(&uid) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
       std::memcpy(id.data(), &uid, sizeof(uid));
-      std::ofstream(tmp, std::ios::binary).write((const char*)id.data(), 128);
-      std::rename(tmp.c_str(), fn);
-    } else {
-      for (int t = 0; t < 6000; ++t) {
-        std::ifstream in(fn, std::ios::binary);
-        if (in && in.read((char*)id.data(), 128)) break;
-        std::this_thread::sleep_for(std::chrono::milliseconds(10));
-        if (t == 5999) throw std::runtime_error("timed out waiting for the ncclUniqueId file");
-      }
     }
+    share_unique_id(comm, rank, nranks, id.data());
   }
   g_dy = std::make_unique<Dycore>(nl, rank, nranks, nranks > 1 ? id.data() : nullptr);
+  // ncclCommInitRank is collective: every rank has read the id once the Dycore exists
+  if (!g_id_file.empty()) {
+    std::remove(g_id_file.c_str());
+    g_id_file.clear();
+  }
   if (g_tiles_per_rank == 1) {
     const SubInfo& s = g_dy->hsubs[0];
     if (s.ioff != is - 1 || s.joff != js - 1)
@@ -249,6 +359,10 @@ template void bridge_run<double>(const BridgeArgs<double>&);
 
 void bridge_finalize() {
   g_dy.reset();
+  if (!g_id_file.empty()) {
+    std::remove(g_id_file.c_str());
+    g_id_file.clear();
+  }
   if (g_stage) {
     (void)hipFree(g_stage);
     g_stage = nullptr;

@@ -29,6 +29,11 @@ template <typename T>
 void bridge_run(const BridgeArgs<T>& a);
 void bridge_finalize();
 void bridge_fatal(const std::string& msg);
+// rank / size of the job: from the caller's Fortran MPI communicator when MPI is in the
+// process, else from the launcher's environment
+void job_rank_size(void* comm, int* rank, int* nranks);
+// rank 0's 128-byte ncclUniqueId to every rank (MPI_Bcast over `comm`, else a job-stamped file)
+void share_unique_id(void* comm, int rank, int nranks, unsigned char* id);
 class Dycore;
 Dycore* bridge_dycore();  // process-global context (nullptr before init)
 

@@ -129,6 +129,19 @@ int gtfv3_get_unique_id(void* out) {
   API_CATCH
 }
 
+int gtfv3_bootstrap_id(void* comm, unsigned char* id128, int* rank, int* nranks) {
+  API_TRY
+  job_rank_size(comm, rank, nranks);
+  share_unique_id(comm, *rank, *nranks, id128);
+  API_CATCH
+}
+
+int gtfv3_bootstrap_done(void) {
+  API_TRY
+  bridge_finalize();
+  API_CATCH
+}
+
 int gtfv3_dims(void* h, int* out) {
   API_TRY
   Dycore* d = D(h);

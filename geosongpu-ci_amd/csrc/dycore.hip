@@ -303,6 +303,9 @@ void Dycore::step() {
   const double mdt = bdt / nl.k_split;
   const double dt = mdt / nl.n_split, dt2 = 0.5 * dt;
   const double ptop = ak[0];
+  // adiabatic (the bridge's `adiabatic` argument, example_def_dycore.yaml:40): dry
+  // dynamics, no moisture in the virtual temperature (FV3 moist_phys = .false.)
+  const double zvir = nl.adiabatic ? 0.0 : Constants::zvir;
   const double* vert = vertical_dev();
   const double* ak_dev = vert;
   const double* bk_dev = vert + k1;
@@ -337,7 +340,7 @@ void Dycore::step() {
   double* cy = S("cy", npz);
   double* dp1 = S("dp1", npz);
 
-  fv_prep(c, npz, nq, delp.p, delz.p, q.p, pt.p, pkz);
+  fv_prep(c, npz, nq, zvir, delp.p, delz.p, q.p, pt.p, pkz);
   copy_levels(c, field_elems(npz), delp.p, dp1);
   for (double* x : {mfx, mfy, cx, cy}) fill_field(c, field_elems(npz), 0.0, x);
 
@@ -461,7 +464,7 @@ void Dycore::step() {
   HIP_CHECK(hipEventRecord(ev[3], st));
 
   // ---- exit: T, omega, A-grid winds ----
-  fv_wrapup(c, npz, nq, q.p, delp.p, delz.p, w.p, pt.p, omga);
+  fv_wrapup(c, npz, nq, zvir, q.p, delp.p, delz.p, w.p, pt.p, omga);
   halo_update({{"u", 'd'}, {"v", 'd'}});
   c2l_ord4(c, npz, u.p, v.p, ua, va);
   HIP_CHECK(hipEventRecord(ev[4], st));

@@ -4,10 +4,11 @@
 
 namespace gtfv3 {
 
-void fv_prep(const Ctx& c, int npz, int nq, const double* delp, const double* delz, const double* q, double* pt,
+// zvir: Constants::zvir with moist physics, 0 for adiabatic (dry) dynamics
+void fv_prep(const Ctx& c, int npz, int nq, double zvir, const double* delp, const double* delz, const double* q, double* pt,
              double* pkz);
 void zh_init(const Ctx& c, int npz, const double* phis, const double* delz, double* zh);
-void fv_wrapup(const Ctx& c, int npz, int nq, const double* q, const double* delp, const double* delz,
+void fv_wrapup(const Ctx& c, int npz, int nq, double zvir, const double* q, const double* delp, const double* delz,
                const double* w, double* pt, double* omga);
 void c2l_ord4(const Ctx& c, int npz, const double* u, const double* v, double* ua, double* va);
 void held_suarez(const Ctx& c, int npz, double dt, const double* pe, double* pt, double* u, double* v);

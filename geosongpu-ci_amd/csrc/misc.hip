@@ -10,7 +10,6 @@ namespace {
 constexpr double GRAV = Constants::grav;
 constexpr double RDGAS = Constants::rdgas;
 constexpr double KAPPA = Constants::kappa;
-constexpr double ZVIR = Constants::zvir;
 
 #define KSETUP3(nk_)                                                 \
   int i, j;                                                          \
@@ -27,7 +26,7 @@ constexpr double ZVIR = Constants::zvir;
 #define MA(arr, di, dj) arr[o + (long)(dj) * d.pitch + (di)]
 
 // fv_dynamics entry: pkz from the non-hydrostatic state, pt -> virtual potential temperature
-__global__ void __launch_bounds__(256) prep_k(Dims d, const SubInfo* __restrict__ subs, int npz, int nq,
+__global__ void __launch_bounds__(256) prep_k(Dims d, const SubInfo* __restrict__ subs, int npz, int nq, double zvir,
                                               const double* __restrict__ delp, const double* __restrict__ delz,
                                               const double* __restrict__ q, double* __restrict__ pt,
                                               double* __restrict__ pkz) {
@@ -36,7 +35,7 @@ __global__ void __launch_bounds__(256) prep_k(Dims d, const SubInfo* __restrict_
   const int k = z % npz;
   const double rdg = -RDGAS * (1.0 / GRAV);
   const double qv = q[((long)s * nq * npz + k) * d.plane + o];  // tracer 0 = specific humidity
-  const double dp1 = ZVIR * qv;
+  const double dp1 = zvir * qv;
   double pk = exp(KAPPA * log(rdg * AT(delp, 0, 0) * AT(pt, 0, 0) * (1.0 + dp1) / AT(delz, 0, 0)));
   AT(pkz, 0, 0) = pk;
   AT(pt, 0, 0) = AT(pt, 0, 0) * (1.0 + dp1) / pk;
@@ -61,7 +60,7 @@ __global__ void __launch_bounds__(256) zh_init_k(Dims d, int npz, const double* 
 }
 
 // fv_dynamics exit: T_v -> T and omega from w
-__global__ void __launch_bounds__(256) wrapup_k(Dims d, const SubInfo* __restrict__ subs, int npz, int nq,
+__global__ void __launch_bounds__(256) wrapup_k(Dims d, const SubInfo* __restrict__ subs, int npz, int nq, double zvir,
                                                 const double* __restrict__ q, const double* __restrict__ delp,
                                                 const double* __restrict__ delz, const double* __restrict__ w,
                                                 double* __restrict__ pt, double* __restrict__ omga) {
@@ -69,7 +68,7 @@ __global__ void __launch_bounds__(256) wrapup_k(Dims d, const SubInfo* __restric
   KSETUP3(npz)
   const int k = z % npz;
   const double qv = q[((long)s * nq * npz + k) * d.plane + o];
-  AT(pt, 0, 0) = AT(pt, 0, 0) / (1.0 + ZVIR * qv);
+  AT(pt, 0, 0) = AT(pt, 0, 0) / (1.0 + zvir * qv);
   AT(omga, 0, 0) = AT(delp, 0, 0) / AT(delz, 0, 0) * AT(w, 0, 0);
 }
 
@@ -145,12 +144,12 @@ inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
 
 }  // namespace
 
-void fv_prep(const Ctx& c, int npz, int nq, const double* delp, const double* delz, const double* q, double* pt,
+void fv_prep(const Ctx& c, int npz, int nq, double zvir, const double* delp, const double* delz, const double* q, double* pt,
              double* pkz) {
   const Dims& d = c.d;
   Launch2D L{0, 0, d.nx, d.ny};
-  GT_LAUNCH(prep_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nq, delp, delz, q, pt,
-                     pkz);
+  GT_LAUNCH(prep_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nq, zvir, delp, delz, q,
+                     pt, pkz);
   HIP_LAUNCH_CHECK();
 }
 
@@ -161,12 +160,12 @@ void zh_init(const Ctx& c, int npz, const double* phis, const double* delz, doub
   HIP_LAUNCH_CHECK();
 }
 
-void fv_wrapup(const Ctx& c, int npz, int nq, const double* q, const double* delp, const double* delz,
+void fv_wrapup(const Ctx& c, int npz, int nq, double zvir, const double* q, const double* delp, const double* delz,
                const double* w, double* pt, double* omga) {
   const Dims& d = c.d;
   Launch2D L{0, 0, d.nx, d.ny};
-  GT_LAUNCH(wrapup_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nq, q, delp, delz, w,
-                     pt, omga);
+  GT_LAUNCH(wrapup_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nq, zvir, q, delp, delz,
+                     w, pt, omga);
   HIP_LAUNCH_CHECK();
 }
 

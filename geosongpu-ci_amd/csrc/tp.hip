@@ -6,7 +6,7 @@
 //   q_i = (q*area + yfx*fy2|j - yfx*fy2|j+1)/ra_y    q_j = (q*area + xfx*fx2|i - ...)/ra_x
 //   fx = 0.5*(xppm(q_i) + fx2)*mfx     fy = 0.5*(yppm(q_j) + fy2)*mfy
 // Operation order inside each expression follows the Fortran so the fp64
-// numpy oracle (oracle/fv3.py) matches to the last bits.
+// numpy oracle (oracle/tp_core.py) matches to the last bits.
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>

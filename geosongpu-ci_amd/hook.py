@@ -17,6 +17,7 @@ The keyword `is` of the reference argument list is spelled `is_` here (Python
 keyword); `is` is also accepted through **kwargs.
 """
 import ctypes
+import os
 
 import numpy as np
 
@@ -28,6 +29,29 @@ RUN_SCALARS = INIT_ARGS + ("ng", "ptop", "ks", "layout_1", "layout_2", "adiabati
 RUN_ARRAYS = ("ak", "bk", "u", "v", "w", "delz", "pt", "delp", "q", "ps", "pe", "pk", "peln", "pkz", "phis",
               "q_con", "omga", "ua", "va", "uc", "vc", "mfx", "mfy", "cx", "cy", "diss_est")
 FLOATS = ("bdt", "ptop")
+
+
+def expected_sizes(kw):
+    """Element count of every run array implied by the scalar arguments (FV3 declarations,
+    SURVEY.md §8b); the bridge copies exactly this many elements in and out, so a smaller
+    caller buffer would be read and written out of bounds."""
+    i0, i1, j0, j1 = kw["is"], kw["ie"], kw["js"], kw["je"]
+    ni_d, nj_d = kw["ied"] - kw["isd"] + 1, kw["jed"] - kw["jsd"] + 1
+    ni, nj, npz, nq = i1 - i0 + 1, j1 - j0 + 1, kw["npz"], kw["nq_tot"]
+    cell = ni_d * nj_d
+    n = {
+        "ak": npz + 1, "bk": npz + 1,
+        "u": ni_d * (nj_d + 1) * npz, "v": (ni_d + 1) * nj_d * npz,
+        "q": cell * npz * nq, "ps": cell, "phis": cell,
+        "pe": (ni + 2) * (nj + 2) * (npz + 1), "pk": ni * nj * (npz + 1), "peln": ni * nj * (npz + 1),
+        "pkz": ni * nj * npz, "uc": (ni_d + 1) * nj_d * npz, "vc": ni_d * (nj_d + 1) * npz,
+        "mfx": (ni + 1) * nj * npz, "mfy": ni * (nj + 1) * npz,
+        "cx": (ni + 1) * nj_d * npz, "cy": ni_d * (nj + 1) * npz,
+    }
+    for f in ("w", "delz", "pt", "delp", "q_con", "omga", "ua", "va", "diss_est"):
+        n[f] = cell * npz
+    tiles = int(os.environ.get("GTFV3_BRIDGE_TILES_PER_RANK", "1"))
+    return {k: v * (tiles if k not in ("ak", "bk") else 1) for k, v in n.items()}
 
 
 def _norm(kwargs):
@@ -64,11 +88,14 @@ class GEOS_GTFV3:
         if dtype not in (np.float32, np.float64):
             raise TypeError("geos_gtfv3.run: state arrays must be float32 or float64")
         ct = ctypes.c_double if dtype == np.float64 else ctypes.c_float
+        need = expected_sizes(kw)
         for n in RUN_ARRAYS:
             a = kw[n]
             if not (isinstance(a, np.ndarray) and a.dtype == dtype and (a.flags.f_contiguous or a.ndim == 1)):
                 raise TypeError(f"geos_gtfv3.run: {n} must be a Fortran-contiguous {dtype} array "
                                 "(in-place update of the caller's buffer)")
+            if a.size != need[n]:
+                raise ValueError(f"geos_gtfv3.run: {n} has {a.size} elements, the bounds imply {need[n]}")
             arrs.append(a.ctypes.data_as(ctypes.POINTER(ct)))
         fn = lib().geos_gtfv3_run_f64_c if dtype == np.float64 else lib().geos_gtfv3_run_c
         fn(*_scalar_args(kw, RUN_SCALARS), *arrs)

@@ -21,6 +21,12 @@ extern "C" {
 void* gtfv3_create(const char* config, int rank, int nranks, const void* nccl_id);
 void gtfv3_destroy(void* h);
 int gtfv3_get_unique_id(void* out128);
+/* The bridge's id bootstrap on its own (no GPU): rank/size from the Fortran MPI handle
+ * `comm` when MPI is initialised in the process, else from the launcher environment; rank 0's
+ * id128 (filled by the caller) reaches every rank by MPI_Bcast, else through the job-stamped
+ * GTFV3_NCCL_ID_FILE.  gtfv3_bootstrap_done removes rank 0's id file (as finalize does). */
+int gtfv3_bootstrap_id(void* comm, unsigned char* id128, int* rank, int* nranks);
+int gtfv3_bootstrap_done(void);
 
 /* out[0..9] = nx, ny, pitch, nj, nsub, npz, N, layout_x, layout_y, nq */
 int gtfv3_dims(void* h, int* out);

@@ -110,11 +110,13 @@ def fv_dynamics(st, ak, bk, g, nl):
     dp0 = nh_core.dp_ref(ak, bk)
     comp = [P.reg(0, nx - 1, 0, ny - 1) for P in g.P]
     q0 = st["q"][:, :npz]
+    # adiabatic = dry dynamics: no moisture in the virtual temperature (FV3 moist_phys off)
+    zvir = 0.0 if nl.get("adiabatic", 0) else ZVIR
 
     # ---- entry ----
     rdg = -RDGAS * (1.0 / GRAV)
     for s in range(nsub):
-        dp1 = ZVIR * q0[s]
+        dp1 = zvir * q0[s]
         pk = np.exp(KAPPA * np.log(rdg * st["delp"][s] * st["pt"][s] * (1.0 + dp1) / st["delz"][s]))
         st["pkz"][s] = np.where(comp[s], pk, st["pkz"][s])
         st["pt"][s] = np.where(comp[s], st["pt"][s] * (1.0 + dp1) / pk, st["pt"][s])
@@ -209,7 +211,7 @@ def fv_dynamics(st, ak, bk, g, nl):
     # ---- exit ----
     for s in range(nsub):
         q0s = st["q"][s, :npz]
-        st["pt"][s] = np.where(comp[s], st["pt"][s] / (1.0 + ZVIR * q0s), st["pt"][s])
+        st["pt"][s] = np.where(comp[s], st["pt"][s] / (1.0 + zvir * q0s), st["pt"][s])
         st["omga"][s] = np.where(comp[s], st["delp"][s] / st["delz"][s] * st["w"][s], st["omga"][s])
     _halo(g, st, [("u", "d"), ("v", "d")])
     for s in range(nsub):

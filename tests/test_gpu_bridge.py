@@ -33,30 +33,13 @@ def from_fortran(f, nsub, nk, nj, pitch, lo_i, hi_i, lo_j, hi_j, kj=False):
     return out
 
 
-def test_bridge_run_matches_device_api(pkg, require_gpu):
-    os.environ["GTFV3_BRIDGE_TILES_PER_RANK"] = "6"
-    os.environ["GTFV3_NONFATAL"] = "1"
-    hook = importlib.import_module(pkg.__name__ + ".hook").geos_gtfv3
-    state = importlib.import_module(pkg.__name__ + ".state")
-    npx, npz, nq = 13, 10, 2
-    N = npx - 1
-    d = pkg.Domain(npx=npx, npz=npz, nq=nq)
-    ak, bk, ks = state.hybrid_levels(npz)
-    st = state.jablonowski_williamson(d, ak, bk)
-    d.set_vertical(ak, bk, ks)
-    for k, v in st.items():
-        d.upload(k, v)
-    d.step(1)
-    want = {k: d.download(k) for k in ("u", "v", "w", "delz", "pt", "delp", "q", "ps", "pe", "peln", "pk", "pkz",
-                                       "ua", "va", "omga")}
-    nsub, nj, pitch = d.nsub, d.nj, d.pitch
-    d.close()
-
-    # Fortran bounds (1-based FV3 -> local 0-based: subtract is = 1)
+def _shapes(N, npz, nq):
+    """Fortran bounds of the 24 run arrays (example_def_dycore.yaml:21-70) as
+    local 0-based (lo_i, hi_i, lo_j, hi_j, nk, k-in-the-middle)."""
     is_, ie, js, je = 1, N, 1, N
     isd, ied, jsd, jed = is_ - NG, ie + NG, js - NG, je + NG
     L = lambda x: x - 1  # noqa: E731
-    shapes = {  # name: (lo_i, hi_i, lo_j, hi_j, nk, kj)
+    return {
         "u": (L(isd), L(ied), L(jsd), L(jed + 1), npz, False),
         "v": (L(isd), L(ied + 1), L(jsd), L(jed), npz, False),
         "w": (L(isd), L(ied), L(jsd), L(jed), npz, False),
@@ -82,22 +65,107 @@ def test_bridge_run_matches_device_api(pkg, require_gpu):
         "cy": (L(isd), L(ied), L(js), L(je + 1), npz, False),
         "diss_est": (L(isd), L(ied), L(jsd), L(jed), npz, False),
     }
-    zeros = lambda nk: np.zeros((nsub, nk, nj, pitch))  # noqa: E731
+
+
+def _setup(pkg, npx, npz, nq, **cfg):
+    state = importlib.import_module(pkg.__name__ + ".state")
+    d = pkg.Domain(npx=npx, npz=npz, nq=nq, **cfg)
+    ak, bk, ks = state.hybrid_levels(npz)
+    st = state.jablonowski_williamson(d, ak, bk)
+    d.set_vertical(ak, bk, ks)
+    return d, st, ak, bk, ks
+
+
+def _bridge_call(pkg, st, d, ak, bk, ks, npx, npz, nq, dtype=np.float64, adiabatic=0):
+    """One geos_gtfv3 init/run/finalize over Fortran-layout copies of `st`; returns the
+    updated Fortran arrays and the shape table."""
+    os.environ["GTFV3_BRIDGE_TILES_PER_RANK"] = "6"
+    os.environ["GTFV3_NONFATAL"] = "1"
+    hook = importlib.import_module(pkg.__name__ + ".hook").geos_gtfv3
+    N = npx - 1
+    shapes = _shapes(N, npz, nq)
+    zeros = lambda nk: np.zeros((d.nsub, nk, d.nj, d.pitch))  # noqa: E731
     fort = {}
     for name, (li, hi, lj, hj, nk, kj) in shapes.items():
         src = st[name] if name in st else zeros(nk)
-        fort[name] = to_fortran(src, li, hi, lj, hj, kj)
+        fort[name] = np.asfortranarray(to_fortran(src, li, hi, lj, hj, kj).astype(dtype))
     addr = {k: v.ctypes.data for k, v in fort.items()}
-    scal = dict(comm=0, npx=npx, npy=npx, npz=npz, ntiles=6, is_=is_, ie=ie, js=js, je=je, isd=isd, ied=ied,
-                jsd=jsd, jed=jed, bdt=900.0, nq_tot=nq)
+    scal = dict(comm=0, npx=npx, npy=npx, npz=npz, ntiles=6, is_=1, ie=N, js=1, je=N, isd=1 - NG, ied=N + NG,
+                jsd=1 - NG, jed=N + NG, bdt=900.0, nq_tot=nq)
     hook.init(**scal)
-    hook.run(**scal, ng=NG, ptop=float(ak[0]), ks=ks, layout_1=1, layout_2=1, adiabatic=1,
-             ak=np.asfortranarray(ak), bk=np.asfortranarray(bk), **fort)
+    hook.run(**scal, ng=NG, ptop=float(ak[0]), ks=ks, layout_1=1, layout_2=1, adiabatic=adiabatic,
+             ak=np.asfortranarray(ak.astype(dtype)), bk=np.asfortranarray(bk.astype(dtype)), **fort)
     hook.finalize()
+    for k in fort:
+        assert fort[k].ctypes.data == addr[k], "buffers must be updated in place"
+    return fort, shapes
+
+
+OUT = ("u", "v", "w", "delz", "pt", "delp", "q", "ps", "pe", "peln", "pk", "pkz", "ua", "va", "omga")
+
+
+def test_bridge_run_matches_device_api(pkg, require_gpu):
+    npx, npz, nq = 13, 10, 2
+    N = npx - 1
+    d, st, ak, bk, ks = _setup(pkg, npx, npz, nq)
+    for k, v in st.items():
+        d.upload(k, v)
+    d.step(1)
+    want = {k: d.download(k) for k in OUT}
+    nsub, nj, pitch = d.nsub, d.nj, d.pitch
+    fort, shapes = _bridge_call(pkg, st, d, ak, bk, ks, npx, npz, nq)
+    d.close()
     for name in want:
-        assert fort[name].ctypes.data == addr[name], "buffers must be updated in place"
         li, hi, lj, hj, nk, kj = shapes[name]
         got = from_fortran(fort[name], nsub, nk, nj, pitch, li, hi, lj, hj, kj)
         a = got[..., NG:NG + N, NG:NG + N]
         b = want[name][..., NG:NG + N, NG:NG + N]
         assert np.array_equal(a, b), f"{name}: bridge result differs from the device API"
+
+
+def test_bridge_fp32_abi_matches_fp64(pkg, require_gpu):
+    """geos_gtfv3_run_c (the CI's PACE_FLOAT_PRECISION=32 ABI, float* arrays) against the
+    fp64 twin on the same fp32-representable state, with the reference hook's own bar
+    np.isclose(rtol=1e-5, atol=1e-8) (hook.py.jinja2:58,69)."""
+    npx, npz, nq = 13, 10, 2
+    d, st, ak, bk, ks = _setup(pkg, npx, npz, nq)
+    st = {k: v.astype(np.float32).astype(np.float64) for k, v in st.items()}
+    ak = ak.astype(np.float32).astype(np.float64)
+    bk = bk.astype(np.float32).astype(np.float64)
+    f64, shapes = _bridge_call(pkg, st, d, ak, bk, ks, npx, npz, nq, np.float64)
+    f32, _ = _bridge_call(pkg, st, d, ak, bk, ks, npx, npz, nq, np.float32)
+    d.close()
+    for name in OUT:
+        a, b = f32[name].astype(np.float64), f64[name]
+        assert f32[name].dtype == np.float32
+        ok = np.isclose(a, b, rtol=1e-5, atol=1e-8)
+        assert ok.all(), f"{name}: fp32 ABI differs from fp64 at {np.argwhere(~ok)[:3].tolist()}"
+        # the fp32 result is the fp64 result rounded once (same device arithmetic in fp64)
+        assert np.array_equal(f32[name], b.astype(np.float32)), f"{name}: fp32 ABI is not the rounded fp64 result"
+
+
+def test_bridge_adiabatic_is_dry_dynamics(pkg, require_gpu):
+    """adiabatic=1 through the ABI = the oracle step with zvir = 0 (no moisture in the
+    virtual temperature); adiabatic=0 differs from it wherever q != 0."""
+    from conftest import metrics_of
+    from oracle import fv_dynamics as fvd
+    npx, npz, nq = 13, 10, 2
+    N = npx - 1
+    d, st, ak, bk, ks = _setup(pkg, npx, npz, nq)
+    ms = metrics_of(d)
+    sc = d.scalars()
+    g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
+    nsub, nj, pitch = d.nsub, d.nj, d.pitch
+    fort, shapes = _bridge_call(pkg, st, d, ak, bk, ks, npx, npz, nq, adiabatic=1)
+    moist, _ = _bridge_call(pkg, st, d, ak, bk, ks, npx, npz, nq, adiabatic=0)
+    d.close()
+    nl = dict(n_split=6, dt_atmos=900.0, hord_mt=6, hord_vt=6, hord_tm=6, hord_dp=6, hord_tr=6, dddmp=0.2,
+              d2_bg=0.0, p_fac=0.05, dz_min=2.0, fill=1, nq=nq, adiabatic=1)
+    ref = fvd.fv_dynamics(st, ak, bk, g, nl)
+    for name in ("pt", "delp", "u", "v", "ps"):
+        li, hi, lj, hj, nk, kj = shapes[name]
+        got = from_fortran(fort[name], nsub, nk, nj, pitch, li, hi, lj, hj, kj)[..., NG:NG + N, NG:NG + N]
+        b = ref[name][..., NG:NG + N, NG:NG + N]
+        err = np.abs(got - b).max() / np.abs(b).mean()
+        assert err <= 1e-9, f"{name}: adiabatic bridge step vs oracle {err:.2e}"
+    assert not np.array_equal(fort["pt"], moist["pt"]), "adiabatic must change the virtual-temperature step"

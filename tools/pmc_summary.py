@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """Summarise rocprofv3 FETCH_SIZE / WRITE_SIZE passes (separate runs) into per-kernel
 HBM traffic per launch, with the gfx950 correction of MI355X_MICROARCH.md (HBM
-section): FETCH_SIZE reports half the bytes of wide coalesced reads -> x2;
+section): FETCH_SIZE reports half the bytes of coalesced streaming reads -> x2 (calibrated on
+gfx950 for 4-, 8- and 16-B-per-lane loads by tools/pmc_calib.hip, profiles/r02_pmc_calibration.json);
 WRITE_SIZE taken as is; both counters are in KiB.
 
     tools/pmc_summary.py FETCH_DIR WRITE_DIR OUT_JSON
@@ -35,7 +36,7 @@ def main():
         w = sum(write[k]) / len(write[k])
         res[k] = dict(fetch_kib=f, write_kib=w, launches=len(fetch[k]),
                       traffic_bytes=(2.0 * f + w) * 1024.0,
-                      note="FETCH_SIZE x2 (gfx950 wide-read correction; 8-B/lane loads are uncalibrated) + WRITE_SIZE")
+                      note="FETCH_SIZE x2 + WRITE_SIZE (factors calibrated for 4-, 8- and 16-B/lane loads and 8-B/lane stores: profiles/r02_pmc_calibration.json)")
     json.dump(res, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
