@@ -14,7 +14,9 @@ the global grid is fixed).
 Prints ONE JSON line on rank 0 (contract in DESIGN.md §Measurement):
   value            whole-job cells*levels advanced per second (max-over-ranks time)
   roofline         dominant kernel: algorithmic bytes per launch / its mean HIP-event
-                   duration over the timed steps, against 8 TB/s HBM
+                   duration over the timed steps, against 8 TB/s HBM; and the whole step:
+                   step_bytes (every kernel's algorithmic bytes, bytes_manifest.yaml, as
+                   registered by the launchers on the probe step) / ms_per_step -> step_frac
   cpu_baseline     the numpy oracle (oracle/fv_dynamics.py) timed for one step on a
                    bounded sample (C24 L72, 6 tiles) on the host, rank 0 only
 """
@@ -48,6 +50,21 @@ def families(kstats):
     for k, (ms, n, b) in kstats.items():
         t = out.get(family(k), (0.0, 0, 0.0))
         out[family(k)] = (t[0] + ms, t[1] + n, t[2] + b)
+    return out
+
+
+def manifest_step_bytes(nx, ny, nsub, npz, nq, n_split, pitch, nj):
+    """Algorithmic bytes of one step from bytes_manifest.yaml (evaluated independently of
+    the launchers' registration; tests/test_bytes_manifest.py compares the two)."""
+    import yaml
+    with open(os.path.join(ROOT, "bytes_manifest.yaml")) as f:
+        man = yaml.safe_load(f)["families"]
+    env = dict(C=nsub * nx * ny, X=nsub * (nx + 1) * ny, Y=nsub * nx * (ny + 1), K=nsub * (nx + 1) * (ny + 1),
+               L=npz, L1=npz + 1, nq=nq, ns=n_split, nsub=nsub, nx=nx, ny=ny, pitch=pitch, nj=nj)
+    out = {}
+    for fam, spec in man.items():
+        kinds = spec.get("launches") or ([spec] if "doubles" in spec else [])
+        out[fam] = sum(8.0 * eval(k["n"], {}, env) * eval(k["doubles"], {}, env) for k in kinds)
     return out
 
 
@@ -215,13 +232,16 @@ def main():
     # dominant kernel; the timed steps then bracket only that kernel (all kernels when a
     # per-kernel report is asked for), so the events cost the timed region ~nothing.
     dominant = None
+    step_bytes = None
     for i in range(a.warmup):
         probe = not a.no_kernel_timing and not a.kernel_report and i == a.warmup - 1
         if probe:
             d.kernel_timing(True)
         one_step()
         if probe:
-            fam = families(d.kernel_stats())
+            ks = d.kernel_stats()
+            fam = families(ks)
+            step_bytes = sum(v[2] for v in ks.values())
             d.kernel_timing(False)
             if fam:
                 dominant = max(fam.items(), key=lambda kv: kv[1][0])[0]
@@ -248,6 +268,8 @@ def main():
     value = cells * a.steps / el
     ms_step = 1000.0 * el / a.steps
 
+    if a.kernel_report and kstats:
+        step_bytes = sum(v[2] for v in kstats.values()) / a.steps
     roof = None
     if kstats:
         fam = families(kstats)
@@ -259,9 +281,15 @@ def main():
                     frac=ach / HBM_PEAK_GBS if ach else None, traffic=traffic, traffic_source=src,
                     bytes_per_launch=byt / n if byt > 0 else None, avg_ms=avg_ms,
                     share_of_step=tot / (ms_step * a.steps))
+        if step_bytes:
+            man = manifest_step_bytes(d.nx, d.ny, d.nsub, npz, nq, 6, d.pitch, d.nj)
+            roof.update(step_bytes=step_bytes, step_bytes_manifest=sum(man.values()),
+                        step_achieved=step_bytes / (ms_step * 1e-3) / 1e9,
+                        step_frac=step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS)
         if a.kernel_report and rank == 0:
             with open(a.kernel_report, "w") as f:
                 json.dump({k: dict(ms_total=v[0], launches=v[1], ms_per_step=v[0] / a.steps,
+                                   bytes_per_step=v[2] / a.steps, bytes_per_launch=v[2] / v[1],
                                    gbs=(v[2] / (v[0] * 1e-3) / 1e9) if v[2] > 0 else None)
                            for k, v in sorted(kstats.items(), key=lambda kv: -kv[1][0])}, f, indent=1)
 

@@ -294,6 +294,10 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
       else if (stage == 1) GT_LAUNCH(halo_pack_kernel, g, dim3(256), 0, stream, b, d_.plane, sendbuf_);
       else GT_LAUNCH(halo_unpack_kernel, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
       HIP_LAUNCH_CHECK();
+      // every halo point of every level: one value read, one written
+      double pts = 0.0;
+      for (int q = 0; q < nb; ++q) pts += (double)b.n[q] * b.nk[q];
+      ktimer_bytes(16.0 * pts);
     }
   };
   if (remote) {

@@ -4,8 +4,24 @@
 #include <hip/hip_runtime.h>
 
 #include "gtfv3.hpp"
+#include "hip_util.hpp"
 
 namespace gtfv3 {
+
+// Algorithmic bytes of one launch (bytes_manifest.yaml at the repo root):
+// fp64 fields over the compute domain of every local sub-domain, each counted once per
+// level read and once per level written -- cells C = nx*ny, x-edges X = (nx+1)*ny,
+// y-edges Y = nx*(ny+1), corners K = (nx+1)*(ny+1) -- and 2-D metric planes once per
+// launch (counted as C); halo re-reads and kernel-internal temporaries are not counted.
+struct Ext {
+  double C, X, Y, K;
+};
+inline Ext ext(const Dims& d) {
+  const double n = d.nsub;
+  return Ext{n * d.nx * d.ny, n * (d.nx + 1) * d.ny, n * d.nx * (d.ny + 1), n * (d.nx + 1) * (d.ny + 1)};
+}
+// register `doubles` fp64 values moved by the launch just issued
+inline void gt_bytes(double doubles) { ktimer_bytes(8.0 * doubles); }
 
 struct Ctx {
   Dims d;

@@ -151,6 +151,7 @@ void fv_prep(const Ctx& c, int npz, int nq, double zvir, const double* delp, con
   GT_LAUNCH(prep_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nq, zvir, delp, delz, q,
                      pt, pkz);
   HIP_LAUNCH_CHECK();
+  gt_bytes(npz * 6 * ext(d).C);
 }
 
 void zh_init(const Ctx& c, int npz, const double* phis, const double* delz, double* zh) {
@@ -158,6 +159,7 @@ void zh_init(const Ctx& c, int npz, const double* phis, const double* delz, doub
   Launch2D L{0, 0, d.nx, d.ny};
   GT_LAUNCH(zh_init_k, g2(d, L, d.nsub), dim3(BX, BY), 0, c.st, d, npz, phis, delz, zh);
   HIP_LAUNCH_CHECK();
+  gt_bytes((2.0 * npz + 2) * ext(d).C);
 }
 
 void fv_wrapup(const Ctx& c, int npz, int nq, double zvir, const double* q, const double* delp, const double* delz,
@@ -167,6 +169,7 @@ void fv_wrapup(const Ctx& c, int npz, int nq, double zvir, const double* q, cons
   GT_LAUNCH(wrapup_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nq, zvir, q, delp, delz,
                      w, pt, omga);
   HIP_LAUNCH_CHECK();
+  gt_bytes(npz * 7 * ext(d).C);
 }
 
 void c2l_ord4(const Ctx& c, int npz, const double* u, const double* v, double* ua, double* va) {
@@ -174,6 +177,8 @@ void c2l_ord4(const Ctx& c, int npz, const double* u, const double* v, double* u
   Launch2D L{0, 0, d.nx, d.ny};
   GT_LAUNCH(c2l_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, u, v, ua, va);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  gt_bytes(npz * (e.X + e.Y + 2 * e.C) + 8 * e.C);
 }
 
 void held_suarez(const Ctx& c, int npz, double dt, const double* pe, double* pt, double* u, double* v) {
@@ -181,11 +186,14 @@ void held_suarez(const Ctx& c, int npz, double dt, const double* pe, double* pt,
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
   GT_LAUNCH(hs_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt, pe, pt, u, v);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  gt_bytes((npz + 1) * e.C + npz * (2 * e.C + 2 * e.X + 2 * e.Y) + 2 * e.C);
 }
 
 void fill_field(const Ctx& c, long n, double a, double* x) {
   GT_LAUNCH(fill_k, dim3(cdiv(n, 256) < 8192 ? cdiv(n, 256) : 8192), dim3(256), 0, c.st, n, a, x);
   HIP_LAUNCH_CHECK();
+  gt_bytes((double)n);
 }
 
 }  // namespace gtfv3

@@ -815,6 +815,8 @@ void update_dz_c(const Ctx& c, int npz, const double* dp0, const double* ut, con
   GT_LAUNCH(udzc_k, g2(d, L, d.nsub * (npz + 1)), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dp0, ut, vt,
                      gz, gz_out);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  gt_bytes(npz * (e.X + e.Y) + (npz + 1) * 2 * e.C + 3 * e.C);
 }
 
 void p_grad_c(const Ctx& c, int npz, double dt2, const double* delpc, const double* pkc, const double* gz, double* uc,
@@ -824,6 +826,8 @@ void p_grad_c(const Ctx& c, int npz, double dt2, const double* delpc, const doub
   GT_LAUNCH(pgradc_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt2, delpc, pkc,
                      gz, uc, vc);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  gt_bytes(npz * (e.C + 2 * e.X + 2 * e.Y) + (npz + 1) * 2 * e.C + 2 * e.C);
 }
 
 void edge_profile(const Ctx& c, int npz, const double* dp0, const double* crx, const double* xfx, const double* cry,
@@ -841,6 +845,8 @@ void edge_profile(const Ctx& c, int npz, const double* dp0, const double* crx, c
     GT_LAUNCH(edge_prof_k, g2(d, Lf, d.nsub), dim3(BX, BY), 0, c.st, d, npz, dp0, crx, xfx, cry, yfx, crx_e,
               xfx_e, cry_e, yfx_e);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  gt_bytes((2.0 * npz + 1) * (2 * e.X + 2 * e.Y));
 }
 
 void update_dz_d(const Ctx& c, const UdzdArgs& a) {
@@ -856,6 +862,8 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
   GT_LAUNCH(zh_update_k, g2(d, Li, d.nsub * k1), dim3(BX, BY), 0, c.st, d, c.subs, c.met, k1, a.fx, a.fy,
                      a.xfx_e, a.yfx_e, a.zh);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  gt_bytes(k1 * (2 * e.X + 2 * e.Y + 2 * e.C) + e.C);
 }
 
 void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* delp, double* pk3, double* pe) {
@@ -864,6 +872,7 @@ void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* d
   GT_LAUNCH(pk3_pe_halo_k, dim3(cdiv(nring, 256), 1, d.nsub * npz), dim3(256), 0, c.st, d, npz, ptop, do_pe ? 1 : 0, delp, pk3,
                      pe);
   HIP_LAUNCH_CHECK();
+  gt_bytes((double)d.nsub * npz * (4.0 * (d.nx + 2) + 4.0 * d.ny) * (do_pe ? 3 : 2));  // halo ring only
 }
 
 void a2b_ord4_multi(const Ctx& c, int nf, const int* nk, const double* const* q, double* const* qout) {
@@ -905,7 +914,8 @@ void a2b_ord4_multi(const Ctx& c, int nf, const int* nk, const double* const* q,
   const long waves = (long)m.nz * m.nstrip * m.nseg;
   GT_LAUNCH(a2b_march_k, dim3(cdiv(waves, AM_WAVES)), dim3(AM_W * AM_WAVES), 0, c.st, m);
   HIP_LAUNCH_CHECK();
-  ktimer_bytes(8.0 * d.nx * d.ny * d.nsub * lev * 2.0);  // q read, qout written
+  const Ext e = ext(d);
+  gt_bytes(lev * (e.C + e.K));  // q (cells) read, qout (corners) written
 }
 
 void a2b_ord4(const Ctx& c, int nk, const double* q, double* qout, double* qx, double* qy) {
@@ -928,11 +938,14 @@ void nh_p_grad(const Ctx& c, const NhPgArgs& a) {
   GT_LAUNCH(nhpgrad_k, g2(d, L, d.nsub * a.npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, ptk,
                      a.ppb, a.gzb, a.pkb, a.wk1, a.u, a.v);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  gt_bytes(k1 * 3 * e.K + a.npz * (e.K + 2 * e.X + 2 * e.Y) + 2 * e.C);
 }
 
 void scale_field(const Ctx& c, long n, double a, const double* x, double* y) {
   GT_LAUNCH(scale_k, dim3(cdiv(n, 256) < 8192 ? cdiv(n, 256) : 8192), dim3(256), 0, c.st, n, a, x, y);
   HIP_LAUNCH_CHECK();
+  gt_bytes(2.0 * n);
 }
 
 }  // namespace gtfv3

@@ -859,6 +859,9 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
   const int nc = d.nx * d.ny, nce = (d.nx + 1) * (d.ny + 1);
   GT_LAUNCH(remap_prep_k, dim3(cdiv(nc, BLOCK), d.nsub), dim3(BLOCK), 0, c.st, a);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  const double L = npz, L1 = npz + 1;
+  gt_bytes(L * 5 * e.C);  // delp delz pt read, T_v and -delz/delp source columns written
   // register-resident columns for the instantiated level counts (L72 of the benchmark and
   // the L10 / L12 / L20 test configurations), the scratch-column jobs otherwise (L137)
   const bool reg = variant != 1 && (npz == 72 || npz == 10 || npz == 12 || npz == 20);
@@ -866,11 +869,18 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
     const unsigned gx = cdiv(nce, 64);
     auto go = [&](auto KMc, auto CHc) {
       constexpr int KM = decltype(KMc)::value, CH = decltype(CHc)::value;
+      // per launch: each job's source column read and its field written (L levels), the
+      // source pressures (pe, + peln for T_v; winds: pe of both neighbours) read once
       GT_LAUNCH((remap_reg_k<KM, JK_PT, CH>), dim3(gx, 1, d.nsub), dim3(64), 0, c.st, a);
+      gt_bytes(L * 2 * e.C + L1 * 2 * e.C);
       GT_LAUNCH((remap_reg_k<KM, JK_DZ, CH>), dim3(gx, 1, d.nsub), dim3(64), 0, c.st, a);
+      gt_bytes(L * 2 * e.C + L1 * e.C);
       GT_LAUNCH((remap_reg_k<KM, JK_W, CH>), dim3(gx, 1, d.nsub), dim3(64), 0, c.st, a);
+      gt_bytes(L * 2 * e.C + L1 * e.C + e.C);
       GT_LAUNCH((remap_reg_k<KM, JK_UV, CH>), dim3(gx, 2, d.nsub), dim3(64), 0, c.st, a);
+      gt_bytes(L * 2 * (e.X + e.Y) + L1 * e.C);
       if (nq > 0) GT_LAUNCH((remap_reg_k<KM, JK_Q, CH>), dim3(gx, nq, d.nsub), dim3(64), 0, c.st, a);
+      if (nq > 0) gt_bytes(nq * L * 2 * e.C + L1 * e.C);
     };
     if (npz == 72) go(std::integral_constant<int, 72>{}, std::integral_constant<int, 8>{});
     else if (npz == 10) go(std::integral_constant<int, 10>{}, std::integral_constant<int, 8>{});
@@ -878,13 +888,14 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
     else go(std::integral_constant<int, 20>{}, std::integral_constant<int, 8>{});
   } else {
     GT_LAUNCH(remap_job_k, dim3(cdiv(nce, BLOCK), a.njob, d.nsub), dim3(BLOCK), 0, c.st, a);
+    // every job reads its source column and writes its field (L each), pe + peln once, ws
+    gt_bytes(L * 2 * ((a.njob - 2) * e.C + e.X + e.Y) + L1 * 2 * e.C + e.C);
   }
   HIP_LAUNCH_CHECK();
-  // algorithmic bytes per column: every job reads its field and writes it back (L each),
-  // pe (+ peln for T) read once, ws
-  ktimer_bytes(8.0 * nc * d.nsub * (2.0 * npz * a.njob + 2.0 * (npz + 1) + 1));
   GT_LAUNCH(remap_finish_k, dim3(cdiv(nc, BLOCK), d.nsub), dim3(BLOCK), 0, c.st, a);
   HIP_LAUNCH_CHECK();
+  // reads delz pt (L) pe peln (L+1); writes delz delp pkz (L) pk peln pe (L+1) ps
+  gt_bytes(L * 5 * e.C + L1 * 5 * e.C + e.C);
 }
 
 }  // namespace gtfv3

@@ -593,21 +593,28 @@ void c_sw(const Ctx& c, const CswArgs& a) {
   GT_LAUNCH(cs_tmp, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.utmp,
                      a.vtmp, a.ua, a.va);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  const double L = a.npz;
+  gt_bytes(L * (e.Y + e.X + 4 * e.C) + 2 * e.C);
   GT_LAUNCH(cs_corner_fix, dim3(nz), dim3(64), 0, c.st, d, c.subs, a.npz, a.utmp, a.vtmp, a.ua, a.va);
   HIP_LAUNCH_CHECK();
   GT_LAUNCH(cs_cgrid, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
                      a.utmp, a.vtmp, a.ua, a.va, a.uc, a.vc, a.ut, a.vt);
   HIP_LAUNCH_CHECK();
+  gt_bytes(L * (3 * e.X + 3 * e.Y + 4 * e.C) + 12 * e.C);
   Launch2D Lt{-1, -1, d.nx + 2, d.ny + 2};
   GT_LAUNCH(cs_transport_ke, g2(d, Lt, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.delp,
                      a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke);
   HIP_LAUNCH_CHECK();
+  gt_bytes(L * (9 * e.C + 3 * e.X + 3 * e.Y) + 9 * e.C);
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
   GT_LAUNCH(cs_vort, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.vort);
   HIP_LAUNCH_CHECK();
+  gt_bytes(L * (e.X + e.Y + e.K) + 4 * e.C);
   GT_LAUNCH(cs_update, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
                      a.vort, a.ke, a.uc, a.vc);
   HIP_LAUNCH_CHECK();
+  gt_bytes(L * (e.C + e.K + 3 * e.X + 3 * e.Y) + 6 * e.C);
 }
 
 // d_sw in three stages: the contravariant winds and Courant numbers; the mass-flux and
@@ -621,12 +628,16 @@ void d_sw_courant(const Ctx& c, const DswArgs& a) {
   GT_LAUNCH(ds_utvt1, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.uc, a.vc,
                      a.ut, a.vt);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  const double L = a.npz;
+  gt_bytes(L * (2 * e.X + 2 * e.Y) + 8 * e.C);
   GT_LAUNCH(ds_utvt2, dim3(cdiv(edge_line_count(-NG, d.nx + NG, -NG, d.ny + NG), 256), 1, nz), dim3(256), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.ut,
                      a.vt);
   HIP_LAUNCH_CHECK();
   GT_LAUNCH(ds_courant, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.ut, a.vt,
                      a.crx, a.cry, a.xfx, a.yfx);
   HIP_LAUNCH_CHECK();
+  gt_bytes(L * (3 * e.X + 3 * e.Y) + 8 * e.C);
 }
 
 static TpArgs d_sw_tp(const DswArgs& a) {
@@ -648,6 +659,9 @@ void d_sw_thermo(const Ctx& c, const DswArgs& a) {
   GT_LAUNCH(ds_accum, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, a.npz, a.crx, a.cry, a.fx, a.fy,
                      a.cx, a.cy, a.mfx, a.mfy);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  const double L = a.npz;
+  gt_bytes(L * (6 * e.X + 6 * e.Y));
   // w and pt with the mass fluxes: one launch for the pair when their PPM orders agree
   // (each wave carries both fields and loads the shared Courant numbers and fluxes once)
   t.mfx = a.fx; t.mfy = a.fy;
@@ -665,6 +679,7 @@ void d_sw_thermo(const Ctx& c, const DswArgs& a) {
   GT_LAUNCH(ds_thermo, g2(d, Li, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.fx, a.fy, a.gwx,
                      a.gwy, a.gtx, a.gty, a.delp, a.pt, a.w);
   HIP_LAUNCH_CHECK();
+  gt_bytes(L * (6 * e.C + 3 * e.X + 3 * e.Y) + e.C);
 }
 
 void d_sw_winds(const Ctx& c, const DswArgs& a) {
@@ -675,10 +690,14 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
   GT_LAUNCH(ds_ke, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.hord_mt, a.dddmp,
                      a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  const double L = a.npz;
+  gt_bytes(L * (2 * e.C + 3 * e.X + 3 * e.Y + e.K) + 17 * e.C);
   // vorticity transport
   Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
   GT_LAUNCH(ds_vort, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.vort);
   HIP_LAUNCH_CHECK();
+  gt_bytes(L * (e.X + e.Y + e.C) + 4 * e.C);
   TpArgs t = d_sw_tp(a);
   t.mfx = nullptr; t.mfy = nullptr;
   t.q = a.vort; t.fx = a.gvx; t.fy = a.gvy; t.ord = a.hord_vt;
@@ -686,6 +705,7 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
   GT_LAUNCH(ds_uv, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.ke, a.gvx, a.gvy, a.u,
                      a.v);
   HIP_LAUNCH_CHECK();
+  gt_bytes(L * (e.K + 3 * e.X + 3 * e.Y) + 2 * e.C);
 }
 
 void d_sw(const Ctx& c, const DswArgs& a) {

@@ -679,8 +679,8 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
   // algorithmic bytes: q read + fx, fy written per field plane; crx cry xfx yfx (+ mfx mfy)
   // read once per (sub-domain, level) however many fields share them (ra_x, ra_y are
   // formed in the kernel, the 2-D area plane is not counted)
-  const double cells = (double)d.nx * d.ny;
-  ktimer_bytes(8.0 * cells * (double)d.nsub * a.nk * (3.0 * nfields + 4 + (a.mfx ? 2 : 0)));
+  const Ext e = ext(d);
+  gt_bytes((double)a.nk * (nfields * (e.C + e.X + e.Y) + (a.mfx ? 3 : 2) * (e.X + e.Y)));
 }
 
 void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, double* xfx, double* yfx,
@@ -691,6 +691,8 @@ void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, doub
   GT_LAUNCH(tracer_prep_k, dim3(cdiv(L.ni, BX), cdiv(L.nj, BY * TP_RPT), d.nsub * npz), dim3(BX, BY), 0, c.st, d,
                      c.met, npz, cx, cy, xfx, yfx, cmax_dev);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  gt_bytes(npz * (2 * e.X + 2 * e.Y) + 4 * e.C);
 }
 
 void tracer_split(const Ctx& c, int npz, const int* nsplt_dev, double* cx, double* cy, double* xfx, double* yfx,
@@ -708,6 +710,8 @@ void tracer_dp2(const Ctx& c, int npz, const double* dp1, const double* mfx, con
   GT_LAUNCH(tracer_dp2_k, plane_grid(Launch2D{0, 0, d.nx, d.ny}, d.nsub * npz), dim3(BX, BY), 0, c.st, d,
                      c.met, npz, dp1, mfx, mfy, dp2);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  gt_bytes(npz * (2 * e.C + e.X + e.Y) + e.C);
 }
 
 void tracer_update(const Ctx& c, int npz, int nq, double* q, const double* qn, const double* dp1, const double* dp2,
@@ -718,11 +722,14 @@ void tracer_update(const Ctx& c, int npz, int nq, double* q, const double* qn, c
   GT_LAUNCH(tracer_update_k, plane_grid(Launch2D{0, 0, d.nx, d.ny}, nz < ZMAX ? nz : ZMAX),
                      dim3(BX, BY), 0, c.st, d, c.met, npz, nq, q, dp1, dp2, fx, fy, nsplt_dev, it, (int)nz);
   HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  gt_bytes((double)nq * npz * (4 * e.C + e.X + e.Y) + e.C);
 }
 
 void copy_levels(const Ctx& c, long n, const double* src, double* dst) {
   GT_LAUNCH(copy_k, dim3(cdiv(n, 256) < 8192 ? cdiv(n, 256) : 8192), dim3(256), 0, c.st, n, src, dst);
   HIP_LAUNCH_CHECK();
+  gt_bytes(2.0 * n);
 }
 
 }  // namespace gtfv3
