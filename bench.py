@@ -53,14 +53,23 @@ def families(kstats):
     return out
 
 
-def manifest_step_bytes(nx, ny, nsub, npz, nq, n_split, pitch, nj):
+def march_ex_fraction(nx, subs, mout=58):
+    """share of (sub-domain, strip) pairs of the column marches whose 64-column strip reaches
+    a tile edge (tp.hip ex_fraction: the tile-edge kernel's part of each march)"""
+    nstrip = (nx + 1 + mout - 1) // mout
+    nex = sum(1 for s in subs for st in range(nstrip)
+              if not (st * mout + s["ioff"] - 1 >= 2 and st * mout + s["ioff"] + mout + 1 <= s["N"] - 2))
+    return nex / (len(subs) * nstrip)
+
+
+def manifest_step_bytes(nx, ny, nsub, npz, nq, n_split, pitch, nj, fex=0.5):
     """Algorithmic bytes of one step from bytes_manifest.yaml (evaluated independently of
     the launchers' registration; tests/test_bytes_manifest.py compares the two)."""
     import yaml
     with open(os.path.join(ROOT, "bytes_manifest.yaml")) as f:
         man = yaml.safe_load(f)["families"]
     env = dict(C=nsub * nx * ny, X=nsub * (nx + 1) * ny, Y=nsub * nx * (ny + 1), K=nsub * (nx + 1) * (ny + 1),
-               L=npz, L1=npz + 1, nq=nq, ns=n_split, nsub=nsub, nx=nx, ny=ny, pitch=pitch, nj=nj)
+               L=npz, L1=npz + 1, nq=nq, ns=n_split, nsub=nsub, nx=nx, ny=ny, pitch=pitch, nj=nj, fex=fex)
     out = {}
     for fam, spec in man.items():
         kinds = spec.get("launches") or ([spec] if "doubles" in spec else [])
@@ -282,7 +291,8 @@ def main():
                     bytes_per_launch=byt / n if byt > 0 else None, avg_ms=avg_ms,
                     share_of_step=tot / (ms_step * a.steps))
         if step_bytes:
-            man = manifest_step_bytes(d.nx, d.ny, d.nsub, npz, nq, 6, d.pitch, d.nj)
+            man = manifest_step_bytes(d.nx, d.ny, d.nsub, npz, nq, 6, d.pitch, d.nj,
+                                      march_ex_fraction(d.nx, d.subs))
             roof.update(step_bytes=step_bytes, step_bytes_manifest=sum(man.values()),
                         step_achieved=step_bytes / (ms_step * 1e-3) / 1e9,
                         step_frac=step_bytes / (ms_step * 1e-3) / 1e9 / HBM_PEAK_GBS)

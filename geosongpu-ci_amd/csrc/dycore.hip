@@ -402,6 +402,36 @@ void Dycore::step() {
   pa.qx = S("_pg_qx", k1); pa.qy = S("_pg_qy", k1);
   pa.u = u.p; pa.v = v.p;
 
+  // fused d_sw thermo march: delp / w / pt are updated into a second set of planes, which
+  // then become the fields (pointer swap; n_split even ends on the original planes).  The
+  // second set starts as a copy so the halo points no exchange fills match the first.
+  DswArgs probe{};
+  probe.hord_vt = nl.hord_vt; probe.hord_tm = nl.hord_tm; probe.hord_dp = nl.hord_dp;
+  probe.delp_o = probe.w_o = probe.pt_o = delp.p;  // (only their presence is tested)
+  const bool tfused = d_sw_thermo_fused(probe);
+  Field* alt[3] = {nullptr, nullptr, nullptr};
+  Field* cur3[3] = {&delp, &w, &pt};
+  double* orig3[3] = {delp.p, w.p, pt.p};
+  if (tfused) {
+    const char* an[3] = {"_delp_alt", "_w_alt", "_pt_alt"};
+    for (int f = 0; f < 3; ++f) {
+      alt[f] = &field(an[f], npz);
+      copy_levels(c, field_elems(npz), cur3[f]->p, alt[f]->p);
+    }
+  }
+  auto thermo_swap = [&]() {
+    for (int f = 0; f < 3; ++f) std::swap(cur3[f]->p, alt[f]->p);
+    ca.delp = da.delp = delp.p;
+    ra.delp = pa.delp = delp.p;
+    ca.pt = da.pt = pt.p;
+    ra.pt = pt.p;
+    ca.w = da.w = ra.w = w.p;
+    da.delp_o = alt[0]->p; da.w_o = alt[1]->p; da.pt_o = alt[2]->p;
+  };
+  if (tfused) {
+    da.delp_o = alt[0]->p; da.w_o = alt[1]->p; da.pt_o = alt[2]->p;
+  }
+
   halo_update({{"u", 'd'}, {"v", 'd'}, {"delp", 'c'}, {"pt", 'c'}, {"w", 'c'}, {"phis", 'c'}});
   zh_init(c, npz, phis.p, delz.p, zh);
   halo_update({{"zh", 'c'}});
@@ -421,6 +451,7 @@ void Dycore::step() {
     d_sw_courant(c, da);
     if (!fork_substep) {
       d_sw_thermo(c, da);
+      if (tfused) thermo_swap();
       halo_update({{"delp", 'c'}, {"pt", 'c'}});
       d_sw_winds(c, da);
       update_dz_d(c, za);
@@ -436,6 +467,7 @@ void Dycore::step() {
       update_dz_d(cc, za);
     }
     d_sw_thermo(c, da);
+    if (tfused) thermo_swap();
     halo_update({{"delp", 'c'}, {"pt", 'c'}});
     HIP_CHECK(hipEventRecord(ev_b, st_b));
     HIP_CHECK(hipEventRecord(ev_c, st_c));
@@ -449,6 +481,11 @@ void Dycore::step() {
     scale_field(c, field_elems(k1), Constants::grav, zh, gz);
     nh_p_grad(c, pa);
     if (!last) halo_update({{"u", 'd'}, {"v", 'd'}});
+  }
+  // odd n_split: the fields end on the second planes; copy back to the caller's planes
+  if (tfused && delp.p != orig3[0]) {
+    for (int f = 0; f < 3; ++f) copy_levels(c, field_elems(npz), cur3[f]->p, alt[f]->p);
+    thermo_swap();
   }
   HIP_CHECK(hipEventRecord(ev[1], st));
 

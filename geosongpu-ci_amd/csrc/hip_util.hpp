@@ -84,6 +84,17 @@ void debug_sync_check(const char* kern, hipStream_t st);
 void debug_canary(const char* what, const void* d, const void* h, size_t bytes);
 void debug_canary_drop(const void* d);
 
+// GT_LAUNCH_N: the same with an explicit (string literal) timer name, for launch sites
+// whose template arguments are not spelled out at the call
+#define GT_LAUNCH_N(name, kern, grid, block, shm, st, ...)                 \
+  do {                                                                   \
+    {                                                                    \
+      ::gtfv3::KScope kscope_(name, st);                                 \
+      hipLaunchKernelGGL(kern, grid, block, shm, st, __VA_ARGS__);       \
+    }                                                                    \
+    if (::gtfv3::debug_sync_launch()) ::gtfv3::debug_sync_check(name, st); \
+  } while (0)
+
 #define GT_LAUNCH(kern, grid, block, shm, st, ...)                       \
   do {                                                                   \
     {                                                                    \

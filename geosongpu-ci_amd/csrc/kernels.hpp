@@ -47,6 +47,20 @@ struct TpArgs {
 };
 void fv_tp_2d(const Ctx& c, const TpArgs& a);
 
+// d_sw's thermodynamic transport in one march (tp.hip, tp_march<.., 3, TM = 1>): fv_tp_2d
+// of delp (mass fluxes xfx / yfx), of w and pt with delp's fluxes as mass fluxes, the
+// flux-capacitor accumulation mfx += fx, mfy += fy, and the delp / w / pt update, the
+// fluxes never leaving registers.  New values go to *_o (the inputs are the march's halo
+// sources for neighbouring waves, so the update cannot be in place).
+struct ThermoArgs {
+  int npz, ord;
+  const double *delp, *w, *pt;
+  double *delp_o, *w_o, *pt_o;
+  const double *crx, *cry, *xfx, *yfx;
+  double *mfx, *mfy;
+};
+void d_sw_thermo_march(const Ctx& c, const ThermoArgs& a);
+
 // tracer_2d_1l pieces
 void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, double* xfx, double* yfx,
                  double* cmax_dev);

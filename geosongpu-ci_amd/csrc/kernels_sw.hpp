@@ -20,6 +20,9 @@ struct DswArgs {
   double dt, dddmp, d2_bg;
   int hord_mt, hord_vt, hord_tm, hord_dp;
   double *delp, *pt, *w, *u, *v;      // updated in place (u, v left multiplied by dx, dy)
+  // optional: delp, pt, w updated into these (fused thermo march, d_sw_thermo_fused) --
+  // the caller then takes them as the new fields
+  double *delp_o = nullptr, *pt_o = nullptr, *w_o = nullptr;
   const double *uc, *vc, *ua, *va;
   double *crx, *cry, *xfx, *yfx;      // per level, saved for update_dz_d
   double *cx, *cy, *mfx, *mfy;        // accumulated
@@ -30,5 +33,6 @@ void d_sw(const Ctx& c, const DswArgs& a);  // the three stages in order
 void d_sw_courant(const Ctx& c, const DswArgs& a);  // ut, vt, Courant numbers and area fluxes
 void d_sw_thermo(const Ctx& c, const DswArgs& a);   // delp / w / pt transport, flux accumulation
 void d_sw_winds(const Ctx& c, const DswArgs& a);    // kinetic energy, vorticity transport, u, v
+bool d_sw_thermo_fused(const DswArgs& a);           // delp/w/pt go to *_o (one march)
 
 }  // namespace gtfv3

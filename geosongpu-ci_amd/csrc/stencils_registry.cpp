@@ -86,7 +86,7 @@ std::map<std::string, Fn>& reg() {
          c_sw(dy.ctx(), a);
        }},
       // d_sw(delp, pt, w, u, v, uc, vc, ua, va | crx, cry, xfx, yfx, cx, cy, mfx, mfy, ke)
-      // params: dt, dddmp, d2_bg, hord_mt, hord_vt, hord_tm, hord_dp
+      // params: dt, dddmp, d2_bg, hord_mt, hord_vt, hord_tm, hord_dp[, fused thermo march]
       {"d_sw",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
          need(f, 18, "d_sw");
@@ -105,7 +105,23 @@ std::map<std::string, Fn>& reg() {
          a.fx = scr("_ds_fx"); a.fy = scr("_ds_fy"); a.gwx = scr("_ds_gwx"); a.gwy = scr("_ds_gwy");
          a.gtx = scr("_ds_gtx"); a.gty = scr("_ds_gty"); a.vort = scr("_ds_vort");
          a.gvx = scr("_ds_gvx"); a.gvy = scr("_ds_gvy");
+         // params[7] (optional): 0 = the separate transport launches, ds_accum and ds_thermo;
+         // else the fused thermo march (into scratch planes, copied back: in-place semantics)
+         const bool fused = p.size() < 8 || p[7] != 0.0;
+         if (fused) {
+           a.delp_o = scr("_ds_delp_o"); a.w_o = scr("_ds_w_o"); a.pt_o = scr("_ds_pt_o");
+           const long n = dy.field_elems(npz);  // halo points carried over as in place
+           copy_levels(dy.ctx(), n, a.delp, a.delp_o);
+           copy_levels(dy.ctx(), n, a.w, a.w_o);
+           copy_levels(dy.ctx(), n, a.pt, a.pt_o);
+         }
          d_sw(dy.ctx(), a);
+         if (d_sw_thermo_fused(a)) {
+           const long n = dy.field_elems(npz);
+           copy_levels(dy.ctx(), n, a.delp_o, a.delp);
+           copy_levels(dy.ctx(), n, a.w_o, a.w);
+           copy_levels(dy.ctx(), n, a.pt_o, a.pt);
+         }
        }},
       // riem_solver_c(delpc, ptc, wc, phis, gz | pef): gz heights in (clamped to dz_min),
       // geopotential out.  params: dt2, ptop, p_fac, dz_min[, variant (0 blocked, 1 column)]

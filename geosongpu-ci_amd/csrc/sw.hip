@@ -3,6 +3,8 @@
 // short chain of plane-parallel kernels over (i, j) x (sub, level); fv_tp_2d is
 // the shared transport operator (tp.hip).  Index conventions: stencil_common.hpp.
 // Fortran index f (1-based, npx = N+1) appears here as tile-global g = f-1.
+#include <cstdlib>
+
 #include "kernels_sw.hpp"
 #include "stencil_common.hpp"
 
@@ -395,7 +397,8 @@ __global__ void __launch_bounds__(256) ds_courant(Dims d, const SubInfo* __restr
                                                   const double* __restrict__ M, int npz, double dt,
                                                   const double* __restrict__ ut, const double* __restrict__ vt,
                                                   double* __restrict__ crx, double* __restrict__ cry,
-                                                  double* __restrict__ xfx, double* __restrict__ yfx) {
+                                                  double* __restrict__ xfx, double* __restrict__ yfx,
+                                                  double* __restrict__ cx, double* __restrict__ cy) {
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   KSETUP(npz)
   const int nx = d.nx, ny = d.ny;
@@ -424,6 +427,12 @@ __global__ void __launch_bounds__(256) ds_courant(Dims d, const SubInfo* __restr
   AT(xfx, 0, 0) = b;
   AT(cry, 0, 0) = c;
   AT(yfx, 0, 0) = e;
+  // Courant accumulation of the flux capacitor (ds_accum's cx / cy part, same ranges), here
+  // when the thermo march accumulates the mass fluxes itself
+  if (cx) {
+    if (i >= 0 && i <= nx && j <= ny + NG - 1) AT(cx, 0, 0) += a;
+    if (j >= 0 && j <= ny && i <= nx + NG - 1) AT(cy, 0, 0) += c;
+  }
 }
 
 // Courant / mass-flux accumulation for tracer transport ("flux capacitor")
@@ -621,6 +630,17 @@ void c_sw(const Ctx& c, const CswArgs& a) {
 // thermodynamic transport (delp, w, pt); the kinetic energy and vorticity transport that
 // update u, v.  After the first stage the other two touch disjoint fields (the vorticity
 // transport writes its own flux planes gvx, gvy), so the dycore runs them on two streams.
+// d_sw's delp / w / pt transport as one register-resident march (tp.hip) when the three
+// PPM orders agree and the caller provides the output planes (GTFV3_THERMO_FUSED=0: the
+// separate fv_tp_2d launches, ds_accum and ds_thermo)
+bool d_sw_thermo_fused(const DswArgs& a) {
+  static const bool on = [] {
+    const char* e = getenv("GTFV3_THERMO_FUSED");
+    return !(e && e[0] == '0');
+  }();
+  return on && a.delp_o && a.w_o && a.pt_o && a.hord_dp == a.hord_vt && a.hord_vt == a.hord_tm;
+}
+
 void d_sw_courant(const Ctx& c, const DswArgs& a) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
@@ -634,10 +654,11 @@ void d_sw_courant(const Ctx& c, const DswArgs& a) {
   GT_LAUNCH(ds_utvt2, dim3(cdiv(edge_line_count(-NG, d.nx + NG, -NG, d.ny + NG), 256), 1, nz), dim3(256), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.ut,
                      a.vt);
   HIP_LAUNCH_CHECK();
+  const bool acc = d_sw_thermo_fused(a);
   GT_LAUNCH(ds_courant, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.ut, a.vt,
-                     a.crx, a.cry, a.xfx, a.yfx);
+                     a.crx, a.cry, a.xfx, a.yfx, acc ? a.cx : nullptr, acc ? a.cy : nullptr);
   HIP_LAUNCH_CHECK();
-  gt_bytes(L * (3 * e.X + 3 * e.Y) + 8 * e.C);
+  gt_bytes(L * ((acc ? 5 : 3) * e.X + (acc ? 5 : 3) * e.Y) + 8 * e.C);
 }
 
 static TpArgs d_sw_tp(const DswArgs& a) {
@@ -650,6 +671,17 @@ static TpArgs d_sw_tp(const DswArgs& a) {
 
 void d_sw_thermo(const Ctx& c, const DswArgs& a) {
   const Dims& d = c.d;
+  if (d_sw_thermo_fused(a)) {
+    ThermoArgs t{};
+    t.npz = a.npz;
+    t.ord = a.hord_dp;
+    t.delp = a.delp; t.w = a.w; t.pt = a.pt;
+    t.delp_o = a.delp_o; t.w_o = a.w_o; t.pt_o = a.pt_o;
+    t.crx = a.crx; t.cry = a.cry; t.xfx = a.xfx; t.yfx = a.yfx;
+    t.mfx = a.mfx; t.mfy = a.mfy;
+    d_sw_thermo_march(c, t);
+    return;
+  }
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   TpArgs t = d_sw_tp(a);

@@ -10,6 +10,7 @@
 #include <algorithm>
 #include <cstdlib>
 #include <type_traits>
+#include <vector>
 
 #include "kernels.hpp"
 #include "stencil_common.hpp"
@@ -38,6 +39,7 @@ constexpr int ZMAX = 65535;
 // (An LDS-tiled form with 64 x 8 tiles, the first fused version, gave bit-identical
 // results and ran 1.9x slower at C180; removed with the ra_x / ra_y planes it read.)
 constexpr int MW = 64, MOUT = MW - 6, MWAVES = 4;
+constexpr int MAXPAIR = 192;
 typedef unsigned int TpU2 __attribute__((ext_vector_type(2)));
 
 // NF fields per wave (field group g of a sub-domain = fields g*NF .. g*NF+NF-1, field f
@@ -46,12 +48,18 @@ struct TpM {
   Dims d;
   const SubInfo* subs;
   const double* M;
-  const double* qf[2];
+  const double* qf[3];
+  double* qo[3];  // TM = 1: the updated delp, w, pt
   int nt, nk, ntg;
   const double *crx, *cry, *xfx, *yfx, *mx, *my;
   double* fxf[2];
   double* fyf[2];
   int nz, nstrip, nseg, seg;
+  // split launches (EXS != 0): the (sub-domain, strip) pairs of this launch's kind, as
+  // s * 256 + strip; a wave's pair index runs fastest, so the four waves of a workgroup
+  // all have work (a workgroup holds its CU slots until its last wave ends)
+  int npair;
+  int pairs[MAXPAIR];
 };
 
 // Wavefront-wide lane shifts through DPP (no LDS): dpp_prev(v) in lane L is v of lane
@@ -154,8 +162,16 @@ struct YRoll {
   PpmCell cell;
 };
 
-template <int ORD, bool EX, bool AHEAD2, bool MF, int NF>
+// TM = 0: fv_tp_2d proper, the NF fields' fluxes fx, fy are written.
+// TM = 1: d_sw's thermodynamic transport fused (NF = 3: delp, w, pt): delp's fluxes (mass
+//   fluxes xfx / yfx) stay in registers and are the mass fluxes of w and pt at the same
+//   edge in the same row step (fv_tp_2d(w | pt, ..., mfx = fx, mfy = fy)); they are
+//   accumulated into mfx / mfy (MX / MY planes, read-modify-write: the flux capacitor),
+//   and the three fields are updated on row r-3 from the fluxes of its four edges
+//   (ds_thermo's expressions) into qo -- no flux plane is written or re-read.
+template <int ORD, bool EX, bool AHEAD2, bool MF, int NF, int TM>
 __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
+  static_assert(TM == 0 || (NF == 3 && MF), "thermo march: delp, w, pt with the accumulators as MX / MY");
   const Dims& d = a.d;
   const int lane = threadIdx.x & (MW - 1);
   // z: (sub-domain, field group, level); the NF fields of a group share the Courant
@@ -257,6 +273,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   double hxf[4];                  // xfx of rows r-3 .. r (the mass flux mfx when MF = false)
   YRoll ry[NF], rj[NF];           // q (y fill) and q_j
   double fyy_prev[NF];
+  double fyo_prev[NF];            // TM = 1: outer y flux of edge r-3
 #pragma unroll
   for (int m = 0; m < 4; ++m) hcx[m] = arw[m] = hxf[m] = 0.0;
 #pragma unroll
@@ -266,6 +283,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     ry[f] = YRoll{};
     rj[f] = YRoll{};
     fyy_prev[f] = 0.0;
+    fyo_prev[f] = 0.0;
   }
   double yfx_prev = 0.0;  // yfx at edge r-3 (the previous row step's edge r-2)
 
@@ -276,8 +294,12 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   __amdgpu_buffer_rsrc_t rFX[NF], rFY[NF];
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
-    rFX[f] = rsrc(a.fxf[f] + zo);
-    rFY[f] = rsrc(a.fyf[f] + zo);
+    if (TM == 0) {
+      rFX[f] = rsrc(a.fxf[f < 2 ? f : 0] + zo);
+      rFY[f] = rsrc(a.fyf[f < 2 ? f : 0] + zo);
+    } else {
+      rFX[f] = rsrc(a.qo[f] + fo);  // updated field f (TM = 1 groups are one field each)
+    }
   }
   auto bst = [&](__amdgpu_buffer_rsrc_t r, uint32_t soff, double v) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(TpU2, v), r, vx, soff, 0);
@@ -388,30 +410,78 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
       const uint32_t se = (uint32_t)(e + NG) * rowb;
       const int mrow = r - 3;
       const double ray = arw[0] + yfx_prev - cur.yfx;
+      const bool rowm = !GEN || (mrow >= j0 && mrow < ny);  // wave-uniform
+      double fyo[NF], fxo[NF];
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
         // ---- edge e: inner y flux fy2, outer y flux fy
         double fy2 = ppm_edge_flux(cym[f], cy[f], cur.cry);
         if (!(GEN ? e <= ny && l_fy2 : l_fy2)) fy2 = 0.0;
         const double fyy = !GEN || e <= ny ? cur.yfx * fy2 : 0.0;
-        if (GEN) {
-          if (s_fy && e <= ny && (e < j1 || last))
-            bst(rFY[f], se, 0.5 * (ppm_edge_flux(cjm[f], cj[f], cur.cry) + fy2) * my);
-        } else {
-          bstv(rFY[f], vfy, se, 0.5 * (ppm_edge_flux(cjm[f], cj[f], cur.cry) + fy2) * my);
+        // TM = 1: w and pt take delp's flux (field 0, this edge) as their mass flux
+        const double myf = TM == 1 ? (f == 0 ? cur.yfx : fyo[0]) : my;
+        fyo[f] = 0.5 * (ppm_edge_flux(cjm[f], cj[f], cur.cry) + fy2) * myf;
+        if (TM == 0) {
+          if (GEN) {
+            if (s_fy && e <= ny && (e < j1 || last)) bst(rFY[f], se, fyo[f]);
+          } else {
+            bstv(rFY[f], vfy, se, fyo[f]);
+          }
         }
         // ---- row m = r-3: q_i, outer x flux fx
-        if (!GEN || (mrow >= j0 && mrow < ny)) {
+        if (rowm) {
           const double v = (qyw[f][0] * arw[0] + fyy_prev[f] - fyy) / ray;
           const double qi = cin ? v : 0.0;
           const double fo_ = ppm_x_dpp<ORD, EX>(qi, cur.dxm, I, N, hcx[0]);
-          if (GEN) {
-            if (s_fx && mrow < j1) bst(rFX[f], se - rowb, 0.5 * (fo_ + hf2[f][0]) * mx);
-          } else {
-            bstv(rFX[f], vfx, se - rowb, 0.5 * (fo_ + hf2[f][0]) * mx);
+          const double mxf = TM == 1 ? (f == 0 ? hxf[0] : fxo[0]) : mx;
+          fxo[f] = 0.5 * (fo_ + hf2[f][0]) * mxf;
+          if (TM == 0) {
+            if (GEN) {
+              if (s_fx && mrow < j1) bst(rFX[f], se - rowb, fxo[f]);
+            } else {
+              bstv(rFX[f], vfx, se - rowb, fxo[f]);
+            }
           }
         }
         fyy_prev[f] = fyy;
+      }
+      if constexpr (TM == 1) {
+        // flux capacitor (ds_accum): mfy on edge e, mfx on row m (cur.my / cur.mx hold them)
+        if (GEN) {
+          if (s_fy && e <= ny && (e < j1 || last)) bst(rMY, se, cur.my + fyo[0]);
+        } else {
+          bstv(rMY, vfy, se, cur.my + fyo[0]);
+        }
+        if (rowm) {
+          if (GEN) {
+            if (s_fx && mrow < j1) bst(rMX, se - rowb, cur.mx + fxo[0]);
+          } else {
+            bstv(rMX, vfx, se - rowb, cur.mx + fxo[0]);
+          }
+          // ds_thermo on row m: flux differences of the cell's four edges (x neighbour by
+          // DPP, edge m from the previous row step), same expressions and order
+          const double ra = 1.0 / arw[0];  // == rarea (grid.cpp: 1 / area, both IEEE)
+          double num[NF];
+#pragma unroll
+          for (int f = 0; f < NF; ++f) num[f] = fxo[f] - dpp_next(fxo[f]) + fyo_prev[f] - fyo[f];
+          const double dp = qyw[0][0];
+          const double dpn = dp + num[0] * ra;
+          const double wn = dp * qyw[1][0] + num[1] * ra;
+          const double ptn = qyw[2][0] * dp + num[2] * ra;
+          if (GEN) {
+            if (s_fy && mrow < j1) {
+              bst(rFX[0], se - rowb, dpn);
+              bst(rFX[1], se - rowb, wn / dpn);
+              bst(rFX[2], se - rowb, ptn / dpn);
+            }
+          } else {
+            bstv(rFX[0], vfy, se - rowb, dpn);
+            bstv(rFX[1], vfy, se - rowb, wn / dpn);
+            bstv(rFX[2], vfy, se - rowb, ptn / dpn);
+          }
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) fyo_prev[f] = fyo[f];
       }
     }
     yfx_prev = cur.yfx;
@@ -462,25 +532,93 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
 
 // AHEAD2: steady rows prefetch two rows ahead (three row buffers, 149 VGPRs, three
 // waves per SIMD); otherwise one row ahead (two buffers, <= 128 VGPRs, four waves)
-template <int ORD, bool AHEAD2, bool MF, int NF>
-__global__ void __launch_bounds__(MW * MWAVES, AHEAD2 ? 1 : 4) tp_march(TpM a) {
+// OCC: minimum workgroups per CU the register budget must allow (0: 1 with AHEAD2, else 4)
+// EXS: 1 = only the strips reaching a tile edge (tile-edge PPM forms), 2 = only interior
+// strips (fewer registers, so more waves per SIMD), 0 = both; the other waves leave at once
+template <int ORD, bool AHEAD2, bool MF, int NF, int TM = 0, int OCC = 0, int EXS = 0>
+__global__ void __launch_bounds__(MW * MWAVES, OCC ? OCC : (AHEAD2 ? 1 : 4)) tp_march(TpM a) {
   // wave index through readfirstlane: everything derived from it (plane, strip, segment,
   // buffer descriptors, row offsets) is then provably wave-uniform (SGPRs, no waterfalls)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / MW);
   const unsigned w = blockIdx.x * MWAVES + wv;  // < 2^31 (launch_tp checks)
-  const int strip = (int)(w % (unsigned)a.nstrip);
-  const unsigned t = w / (unsigned)a.nstrip;
-  const int seg = (int)(t % (unsigned)a.nseg);
-  const int z = (int)(t / (unsigned)a.nseg);
-  if (z >= a.nz) return;  // whole wavefront leaves; no workgroup barrier follows
+  int strip, seg, z;
+  if constexpr (EXS == 0) {
+    strip = (int)(w % (unsigned)a.nstrip);
+    const unsigned t = w / (unsigned)a.nstrip;
+    seg = (int)(t % (unsigned)a.nseg);
+    z = (int)(t / (unsigned)a.nseg);
+    if (z >= a.nz) return;  // whole wavefront leaves; no workgroup barrier follows
+  } else {
+    // pair p = (sub-domain, strip) of this kind; then segment; then (field group, level)
+    const unsigned p = w % (unsigned)a.npair;
+    const unsigned t = w / (unsigned)a.npair;
+    seg = (int)(t % (unsigned)a.nseg);
+    const int zz = (int)(t / (unsigned)a.nseg);
+    const int pr = a.pairs[p];
+    strip = pr & 255;
+    if (zz >= a.ntg * a.nk) return;
+    z = (pr >> 8) * a.ntg * a.nk + zz;
+  }
   const int s = z / a.nk / a.ntg;
   const SubInfo& sub = a.subs[s];
   const int j0 = seg * a.seg;
   const int j1 = j0 + a.seg < a.d.ny ? j0 + a.seg : a.d.ny;
   const int A = strip * MOUT + sub.ioff;
   const bool ex = !(A - 1 >= 2 && A + MOUT + 1 <= sub.N - 2);
-  if (ex) tp_march_strip<ORD, true, AHEAD2, MF, NF>(a, (int)z, strip, j0, j1);
-  else tp_march_strip<ORD, false, AHEAD2, MF, NF>(a, (int)z, strip, j0, j1);
+  if constexpr (EXS == 1) {
+    if (ex) tp_march_strip<ORD, true, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1);
+  } else if constexpr (EXS == 2) {
+    if (!ex) tp_march_strip<ORD, false, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1);
+  } else {
+    if (ex) tp_march_strip<ORD, true, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1);
+    else tp_march_strip<ORD, false, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1);
+  }
+}
+
+// Fraction of the (sub-domain, strip) pairs of a launch whose strip reaches a tile edge
+// (same test as the kernel): the EX kernel's share of the launch's algorithmic bytes.
+// `pex` / `pin` receive the (sub-domain, strip) pairs of each kind (s * 256 + strip).
+double ex_fraction(const Ctx& c, int nstrip, std::vector<int>* pex = nullptr, std::vector<int>* pin = nullptr) {
+  int nex = 0;
+  for (int s = 0; s < c.d.nsub; ++s)
+    for (int st = 0; st < nstrip; ++st) {
+      const int A = st * MOUT + c.hsubs[s].ioff;
+      const bool ex = !(A - 1 >= 2 && A + MOUT + 1 <= c.hsubs[s].N - 2);
+      nex += ex ? 1 : 0;
+      std::vector<int>* v = ex ? pex : pin;
+      if (v) v->push_back(s * 256 + st);
+    }
+  return (double)nex / ((double)c.d.nsub * nstrip);
+}
+
+// One march as two kernels: the tile-edge strips (EX forms, AHEAD2, their register count)
+// and the interior strips (A2_IN prefetch depth, OCC_IN workgroups per CU).  Each launch
+// registers its share of the algorithmic bytes.
+template <int ORD, bool MF, int NF, int TM, int OCC_IN, bool A2_IN>
+void march2(const Ctx& c, const TpM& m0, double bytes, const char* name_ex, const char* name_in) {
+  std::vector<int> pex, pin;
+  const double fex = ex_fraction(c, m0.nstrip, &pex, &pin);
+  if ((int)pex.size() > MAXPAIR || (int)pin.size() > MAXPAIR || c.d.nsub > 128)
+    throw std::runtime_error("fv_tp_2d: too many (sub-domain, strip) pairs for one launch");
+  auto go = [&](const std::vector<int>& pr, bool ex) {
+    TpM m = m0;
+    m.npair = (int)pr.size();
+    for (int q = 0; q < m.npair; ++q) m.pairs[q] = pr[q];
+    const long waves = (long)m.ntg * m.nk * m.npair * m.nseg;
+    if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
+    const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
+    if (ex) GT_LAUNCH_N(name_ex, (tp_march<ORD, true, MF, NF, TM, 0, 1>), g, b, 0, c.st, m);
+    else GT_LAUNCH_N(name_in, (tp_march<ORD, A2_IN, MF, NF, TM, OCC_IN, 2>), g, b, 0, c.st, m);
+    HIP_LAUNCH_CHECK();
+  };
+  if (!pex.empty()) {
+    go(pex, true);
+    ktimer_bytes(bytes * fex);
+  }
+  if (!pin.empty()) {
+    go(pin, false);
+    ktimer_bytes(bytes * (1.0 - fex));
+  }
 }
 
 // ---------------- tracer_2d_1l ----------------
@@ -660,12 +798,25 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     m.seg = seg;
     m.nstrip = nstrip;
     m.nseg = (d.ny + seg - 1) / seg;
+    // algorithmic bytes: q read + fx, fy written per field plane; crx cry xfx yfx (+ mfx mfy)
+    // read once per (sub-domain, level) however many fields share them (ra_x, ra_y are
+    // formed in the kernel, the 2-D area plane is not counted)
+    const Ext e = ext(d);
+    const double bytes = 8.0 * a.nk * (nfields * (e.C + e.X + e.Y) + (a.mfx ? 3 : 2) * (e.X + e.Y));
+    // (the one-row-ahead form measured 3 % slower at C180; tile-edge and interior strips
+    // as two kernels -- the interior one at four waves per SIMD for single fields --
+    // measured 314 against 245 us per single-field launch at C180: two launch tails, and
+    // the interior strips' rows are not 128-B aligned, so they are no cheaper)
+    // MF: separate mass fluxes (w, pt and the tracers) or xfx / yfx themselves
     const long waves = nz * m.nstrip * m.nseg;
     if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
     const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
-    // (the one-row-ahead form, tp_march<ORD, false, ...>, measured 3 % slower at C180)
-    // MF: separate mass fluxes (w, pt and the tracers) or xfx / yfx themselves
-#define TP_GO(O, M_, F_) GT_LAUNCH((tp_march<O, true, M_, F_>), g, b, 0, c.st, m)
+#define TP_GO(O, M_, F_)                                                                           \
+  do {                                                                                             \
+    GT_LAUNCH_N("tp_march<" #O ", " #M_ ", " #F_ ">", (tp_march<O, true, M_, F_>), g, b, 0, c.st, m); \
+    HIP_LAUNCH_CHECK();                                                                            \
+    gt_bytes(bytes / 8.0);                                                                         \
+  } while (0)
     if (a.mfx) {
       if (NFw == 2) { if (a.ord == 5) TP_GO(5, true, 2); else TP_GO(6, true, 2); }
       else { if (a.ord == 5) TP_GO(5, true, 1); else TP_GO(6, true, 1); }
@@ -675,12 +826,39 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     }
 #undef TP_GO
   }
-  HIP_LAUNCH_CHECK();
-  // algorithmic bytes: q read + fx, fy written per field plane; crx cry xfx yfx (+ mfx mfy)
-  // read once per (sub-domain, level) however many fields share them (ra_x, ra_y are
-  // formed in the kernel, the 2-D area plane is not counted)
+}
+
+void d_sw_thermo_march(const Ctx& c, const ThermoArgs& a) {
+  const Dims& d = c.d;
+  if (a.ord != 5 && a.ord != 6) throw std::runtime_error("d_sw thermo march: hord must be 5 or 6");
+  TpM m{};
+  m.d = d;
+  m.subs = c.subs;
+  m.M = c.met;
+  m.qf[0] = a.delp; m.qf[1] = a.w; m.qf[2] = a.pt;
+  m.qo[0] = a.delp_o; m.qo[1] = a.w_o; m.qo[2] = a.pt_o;
+  m.nt = 1;
+  m.nk = a.npz;
+  m.ntg = 1;
+  m.crx = a.crx; m.cry = a.cry; m.xfx = a.xfx; m.yfx = a.yfx;
+  m.mx = a.mfx;  // accumulators, read-modify-write
+  m.my = a.mfy;
+  const long nz = (long)d.nsub * a.npz;
+  m.nz = (int)nz;
+  const int nstrip = (d.nx + 1 + MOUT - 1) / MOUT;
+  const long fw = nz * 3 * nstrip;
+  const long want = (6912 + fw - 1) / fw;
+  const long nseg = std::max<long>((d.ny + 44) / 45, std::min<long>((d.ny + 14) / 15, want));
+  m.seg = (int)((d.ny + nseg - 1) / nseg);
+  m.nstrip = nstrip;
+  m.nseg = (d.ny + m.seg - 1) / m.seg;
+  // delp w pt read and written, crx cry xfx yfx read, mfx mfy read and written; the
+  // interior strips prefetch one row ahead to fit two waves per SIMD (233 VGPRs; the
+  // tile-edge form takes 292 with the two-ahead prefetch)
   const Ext e = ext(d);
-  gt_bytes((double)a.nk * (nfields * (e.C + e.X + e.Y) + (a.mfx ? 3 : 2) * (e.X + e.Y)));
+  const double bytes = 8.0 * a.npz * (6 * e.C + 4 * (e.X + e.Y));
+  if (a.ord == 5) march2<5, true, 3, 1, 2, false>(c, m, bytes, "tp_march_thermo<5, ex>", "tp_march_thermo<5, in>");
+  else march2<6, true, 3, 1, 2, false>(c, m, bytes, "tp_march_thermo<6, ex>", "tp_march_thermo<6, in>");
 }
 
 void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, double* xfx, double* yfx,

@@ -95,3 +95,65 @@ def test_d_sw_parity(pkg, require_gpu, layout):
                 mfx=(0, nx, 0, ny - 1), mfy=(0, nx - 1, 0, ny), ke=(0, nx, 0, ny),
                 u=(0, nx - 1, 0, ny), v=(0, nx, 0, ny - 1)).items():
             close(reg(got[o][s], i0, i1, j0, j1), reg(ref[o], i0, i1, j0, j1), f"sub{s} {o}")
+
+
+D_NAMES = ["delp", "pt", "w", "u", "v", "uc", "vc", "ua", "va", "crx", "cry", "xfx", "yfx", "cx", "cy", "mfx", "mfy",
+           "ke"]
+
+
+def _d_sw_run(d, inp, npz, fused, ords=(6, 6, 6, 6), tag="f"):
+    sh = d.shape(npz)
+    for k, v in inp.items():
+        d.upload(tag + k, v)
+    for k in ("cx", "cy", "mfx", "mfy"):
+        d.upload(tag + k, 0.5 * np.ones(sh))  # accumulators start non-zero: the += is checked
+    d.stencil("d_sw", [tag + n for n in D_NAMES], [600.0, 0.2, 0.0075, *ords, 1.0 if fused else 0.0])
+    return {n: d.download(tag + n) for n in D_NAMES}
+
+
+@pytest.mark.parametrize("npx,layout", [(13, (1, 1)), (181, (1, 1)), (181, (1, 4))])
+def test_d_sw_thermo_march_matches_separate_launches(pkg, require_gpu, npx, layout):
+    """The fused thermo march (delp / w / pt transport with in-register mass fluxes, the
+    flux accumulation and the ds_thermo update in one launch) against the separate
+    fv_tp_2d launches + ds_accum + ds_thermo, bit for bit on every output, at C12 and at
+    C180 (interior strips, strip seams, multi-segment marches; band layout 1x4)."""
+    npz = 2
+    d = pkg.Domain(npx=npx, npz=npz, nq=1, layout_x=layout[0], layout_y=layout[1])
+    r = rng(77)
+    inp = sw_inputs(d, npz, r)
+    sh = d.shape(npz)
+    inp.update(uc=15.0 * r.standard_normal(sh), vc=15.0 * r.standard_normal(sh),
+               ua=15.0 * r.standard_normal(sh), va=15.0 * r.standard_normal(sh))
+    a = _d_sw_run(d, inp, npz, True, tag="f_")
+    b = _d_sw_run(d, inp, npz, False, tag="s_")
+    nx, ny = d.nx, d.ny
+    for n in ("delp", "pt", "w", "mfx", "mfy", "cx", "cy", "u", "v"):
+        ga = a[n][..., NG:NG + ny + 1, NG:NG + nx + 1]
+        gb = b[n][..., NG:NG + ny + 1, NG:NG + nx + 1]
+        assert np.array_equal(ga, gb), f"{n}: fused thermo march differs from the separate launches"
+    d.close()
+
+
+def test_d_sw_parity_c180(pkg, require_gpu):
+    """d_sw (fused thermo march) against the oracle at C180 on two levels."""
+    npz = 2
+    d = pkg.Domain(npx=181, npz=npz, nq=1)
+    r = rng(78)
+    inp = sw_inputs(d, npz, r)
+    sh = d.shape(npz)
+    inp.update(uc=15.0 * r.standard_normal(sh), vc=15.0 * r.standard_normal(sh),
+               ua=15.0 * r.standard_normal(sh), va=15.0 * r.standard_normal(sh))
+    got = _d_sw_run(d, inp, npz, True, tag="o_")
+    ms = metrics_of(d)
+    nx, ny = d.nx, d.ny
+    dmc = d.scalars()["da_min_c"]
+    for s in (0, 3, 5):
+        ref = sw_core.d_sw(inp["delp"][s], inp["pt"][s], inp["u"][s], inp["v"][s], inp["w"][s], inp["uc"][s],
+                           inp["vc"][s], inp["ua"][s], inp["va"][s], d.subs[s], ms[s], nx, ny, 600.0, (6, 6, 6, 6),
+                           0.2, 0.0075, dmc)
+        ref["mfx"], ref["mfy"] = 0.5 + ref["fx"], 0.5 + ref["fy"]
+        for o, (i0, i1, j0, j1) in dict(delp=(0, nx - 1, 0, ny - 1), pt=(0, nx - 1, 0, ny - 1),
+                                        w=(0, nx - 1, 0, ny - 1), mfx=(0, nx, 0, ny - 1), mfy=(0, nx - 1, 0, ny),
+                                        u=(0, nx - 1, 0, ny), v=(0, nx, 0, ny - 1)).items():
+            close(reg(got[o][s], i0, i1, j0, j1), reg(ref[o], i0, i1, j0, j1), f"sub{s} {o}")
+    d.close()
