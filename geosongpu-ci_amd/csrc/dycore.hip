@@ -82,6 +82,8 @@ Dycore::~Dycore() {
   debug_canary_drop(dsubs);
   debug_canary_drop(dmet);
   debug_canary_drop(dcornerw);
+  if (h_cmax) (void)hipHostFree(h_cmax);
+  if (ev_cmax) (void)hipEventDestroy(ev_cmax);
   if (dsubs) (void)hipFree(dsubs);
   if (dmet) (void)hipFree(dmet);
   if (dcornerw) (void)hipFree(dcornerw);
@@ -194,7 +196,7 @@ void Dycore::set_vertical(const double* ak_, const double* bk_, int ks_) {
 // tracer_2d_1l (FV3 fv_tracer2d): large-time-step transport of nq tracers with
 // the mass fluxes (mfx,mfy) and Courant numbers (cx,cy) accumulated over the
 // acoustic sub-steps; dp1 = delp at the start of the step.
-void Dycore::tracer_2d(int nq, double /*dt*/) {
+void Dycore::tracer_2d(int nq, double /*dt*/, int fused_mode) {
   const int npz = nl.npz;
   Ctx c = ctx();
   Field& q = field("q", nq * npz);
@@ -208,36 +210,65 @@ void Dycore::tracer_2d(int nq, double /*dt*/) {
   Field& dp2 = field("tr_dp2", npz);
   Field& cmax = field("tr_cmax", 1);  // first npz doubles used
   Field& nspl = field("tr_nsplt", 1);
-  Field& fx = field("tr_fx", nq * npz);
-  Field& fy = field("tr_fy", nq * npz);
   if ((long)npz > d.plane) throw std::runtime_error("tracer cmax scratch too small");
+  static const bool fused_env = [] {
+    const char* e = getenv("GTFV3_TRACER_FUSED");  // 0: flux planes + tracer_dp2 + tracer_update
+    return !(e && e[0] == '0');
+  }();
+  const bool fused = fused_mode < 0 ? fused_env : fused_mode != 0;
 
   tracer_prep(c, npz, cx.p, cy.p, xfx.p, yfx.p, cmax.p);
   allreduce_max(cmax.p, npz);
-  std::vector<double> hcm(npz);
-  HIP_CHECK(hipMemcpyAsync(hcm.data(), cmax.p, sizeof(double) * npz, hipMemcpyDeviceToHost, st));
-  HIP_CHECK(hipStreamSynchronize(st));
-  std::vector<int> ns(npz);
-  int nmax = 1;
-  for (int k = 0; k < npz; ++k) {
-    ns[k] = (int)(1.0 + hcm[k]);
-    nmax = std::max(nmax, ns[k]);
-  }
+  // nsplt[k] = int(1 + cmax[k]) on the device; the host needs only the largest count (the
+  // number of sub-steps to launch): it comes through pinned memory, and the host waits for
+  // it only after the first sub-step is queued, so the GPU does not idle on the round trip
   int* dns = reinterpret_cast<int*>(nspl.p);
-  HIP_CHECK(hipMemcpyAsync(dns, ns.data(), sizeof(int) * npz, hipMemcpyHostToDevice, st));
+  tracer_nsplt(c, npz, cmax.p, dns);
+  if (!h_cmax) {
+    HIP_CHECK(hipHostMalloc(reinterpret_cast<void**>(&h_cmax), sizeof(double) * std::max(npz, 1)));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_cmax, hipEventDisableTiming));
+  }
+  HIP_CHECK(hipMemcpyAsync(h_cmax, cmax.p, sizeof(double) * npz, hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipEventRecord(ev_cmax, st));
   tracer_split(c, npz, dns, cx.p, cy.p, xfx.p, yfx.p, mfx.p, mfy.p);
+  int nmax = -1;
+  auto sub_steps = [&]() {
+    if (nmax < 0) {
+      HIP_CHECK(hipEventSynchronize(ev_cmax));
+      nmax = 1;
+      for (int k = 0; k < npz; ++k) nmax = std::max(nmax, (int)(1.0 + h_cmax[k]));
+    }
+    return nmax;
+  };
+  TpArgs a{};
+  a.nt = nq; a.nk = npz;
+  a.crx = cx.p; a.cry = cy.p; a.xfx = xfx.p; a.yfx = yfx.p;
+  a.mfx = mfx.p; a.mfy = mfy.p;
+  a.ord = nl.hord_tr;
+  if (fused) {
+    // each sub-step updates the tracers into a second set of planes, which then become "q"
+    // (the march reads neighbouring columns' tracers as its halo: no in-place update)
+    Field& qa = field("_q_alt", nq * npz);
+    for (int it = 0; it < (it == 0 ? 1 : sub_steps()); ++it) {
+      if (it > 0) copy_levels(c, field_elems(npz), dp2.p, dp1.p);
+      halo_update({{"q", 'c'}});
+      a.q = q.p; a.q_out = qa.p;
+      a.dp1 = dp1.p; a.dp2 = dp2.p; a.nsplt = dns; a.it = it;
+      fv_tp_2d(c, a);
+      std::swap(q.p, qa.p);
+    }
+    return;
+  }
+  Field& fx = field("tr_fx", nq * npz);
+  Field& fy = field("tr_fy", nq * npz);
   halo_update({{"q", 'c'}});
-  for (int it = 0; it < nmax; ++it) {
+  for (int it = 0; it < (it == 0 ? 1 : sub_steps()); ++it) {
     tracer_dp2(c, npz, dp1.p, mfx.p, mfy.p, dp2.p);
-    TpArgs a{};
-    a.q = q.p; a.nt = nq; a.nk = npz;
-    a.crx = cx.p; a.cry = cy.p; a.xfx = xfx.p; a.yfx = yfx.p;
-    a.mfx = mfx.p; a.mfy = mfy.p;
+    a.q = q.p;
     a.fx = fx.p; a.fy = fy.p;
-    a.ord = nl.hord_tr;
     fv_tp_2d(c, a);
     tracer_update(c, npz, nq, q.p, nullptr, dp1.p, dp2.p, fx.p, fy.p, dns, it);
-    if (it + 1 < nmax) {
+    if (it + 1 < sub_steps()) {
       copy_levels(c, field_elems(npz), dp2.p, dp1.p);
       halo_update({{"q", 'c'}});
     }

@@ -51,6 +51,10 @@ class Dycore {
   std::vector<double> ak, bk;  // npz+1
   int ks = 0;
   std::map<std::string, double> timers;  // accumulated ms per phase (events)
+  // tracer_2d: the reduced per-level Courant maxima come back to the host through pinned
+  // memory after an event, while the first tracer sub-step already runs
+  double* h_cmax = nullptr;
+  hipEvent_t ev_cmax = nullptr;
 
   Field& field(const std::string& name, int nk);  // get or create (zeroed)
   Field* find(const std::string& name);
@@ -69,7 +73,8 @@ class Dycore {
   void allreduce_max(double* dev, int n);
 
   // algorithm blocks
-  void tracer_2d(int nq, double dt);
+  // fused: 1 update inside the march, 0 flux planes + separate update, -1 GTFV3_TRACER_FUSED
+  void tracer_2d(int nq, double dt, int fused = -1);
   void set_vertical(const double* ak_, const double* bk_, int ks_);
   void step();  // one fv_dynamics call on device-resident state
   // Aquaplanet moist column step on the state (tracers 0..5 = qv ql qr qi qs qg, nq >= 6)

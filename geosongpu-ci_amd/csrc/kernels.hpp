@@ -44,6 +44,14 @@ struct TpArgs {
   double *fx, *fy;
   int ord;
   int cfg = -1;  // tile variant (tuning); -1: default
+  // tracer_2d_1l update fused into the march (mfx / mfy required): the nt tracers are
+  // updated into q_out (no flux planes), dp2 = dp1 + mass-flux divergence written to dp2;
+  // levels with it >= nsplt[k] are copied unchanged
+  double* q_out = nullptr;
+  const double* dp1 = nullptr;
+  double* dp2 = nullptr;
+  const int* nsplt = nullptr;
+  int it = 0;
 };
 void fv_tp_2d(const Ctx& c, const TpArgs& a);
 
@@ -64,6 +72,8 @@ void d_sw_thermo_march(const Ctx& c, const ThermoArgs& a);
 // tracer_2d_1l pieces
 void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, double* xfx, double* yfx,
                  double* cmax_dev);
+// per-level sub-step counts nsplt[k] = int(1 + cmax[k]) (fv_tracer2d), on the device
+void tracer_nsplt(const Ctx& c, int npz, const double* cmax_dev, int* nsplt_dev);
 void tracer_split(const Ctx& c, int npz, const int* nsplt_dev, double* cx, double* cy, double* xfx, double* yfx,
                   double* mfx, double* mfy);
 void tracer_dp2(const Ctx& c, int npz, const double* dp1, const double* mfx, const double* mfy, double* dp2);

@@ -304,12 +304,13 @@ std::map<std::string, Fn>& reg() {
          if (F(dy, f[0]).nk != pt.nk + 1) throw std::runtime_error("held_suarez: pe must have npz+1 levels");
          held_suarez(dy.ctx(), pt.nk, p.at(0), F(dy, f[0]).p, pt.p, F(dy, f[2]).p, F(dy, f[3]).p);
        }},
-      // tracer_2d_1l: uses state fields q, dp1, cx, cy, mfx, mfy. params: nq
+      // tracer_2d_1l: uses state fields q, dp1, cx, cy, mfx, mfy. params: nq[, fused (1: the
+      // update inside the march, 0: flux planes and the separate update)]
       {"tracer_2d_1l",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
          (void)f;
          int nq = p.size() > 0 ? (int)p[0] : dy.nl.nq;
-         dy.tracer_2d(nq, dy.nl.dt_atmos);
+         dy.tracer_2d(nq, dy.nl.dt_atmos, p.size() > 1 ? (int)p[1] : -1);
        }},
   };
   return r;

@@ -49,7 +49,13 @@ struct TpM {
   const SubInfo* subs;
   const double* M;
   const double* qf[3];
-  double* qo[3];  // TM = 1: the updated delp, w, pt
+  double* qo[3];  // TM = 1: the updated delp, w, pt; TM = 2: the updated tracers
+  // TM = 2 (tracer_2d_1l update fused): dp1 in, dp2 out (written by field group 0), the
+  // per-level sub-step counts and this sub-step (levels with it >= nsplt[k] are copied)
+  const double* dp1;
+  double* dp2o;
+  const int* nsplt;
+  int it;
   int nt, nk, ntg;
   const double *crx, *cry, *xfx, *yfx, *mx, *my;
   double* fxf[2];
@@ -153,6 +159,7 @@ struct MarchIn {
   double crx, xfx, area_r, dxr;     // row r
   double cry, yfx, my;              // edge r-2
   double mx, dxm;                   // row r-3
+  double dp1;                       // row r-3 (TM = 2)
 };
 
 // y-direction PPM state rolled along the march: al at the last interface computed and
@@ -169,9 +176,13 @@ struct YRoll {
 //   accumulated into mfx / mfy (MX / MY planes, read-modify-write: the flux capacitor),
 //   and the three fields are updated on row r-3 from the fluxes of its four edges
 //   (ds_thermo's expressions) into qo -- no flux plane is written or re-read.
+// TM = 2: tracer_2d_1l's update fused (NF tracers with the mass fluxes mfx / mfy): dp2 of
+//   row r-3 is formed from the mass fluxes the march holds (tracer_dp2's expression) and the
+//   tracers are updated from their outer fluxes (tracer_update's expression) into qo.
 template <int ORD, bool EX, bool AHEAD2, bool MF, int NF, int TM>
 __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
-  static_assert(TM == 0 || (NF == 3 && MF), "thermo march: delp, w, pt with the accumulators as MX / MY");
+  static_assert(TM == 0 || (TM == 1 && NF == 3 && MF) || (TM == 2 && MF),
+                "thermo march: delp, w, pt with the accumulators as MX / MY; tracer march: mass fluxes");
   const Dims& d = a.d;
   const int lane = threadIdx.x & (MW - 1);
   // z: (sub-domain, field group, level); the NF fields of a group share the Courant
@@ -202,6 +213,9 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   const auto rCRX = rsrc(a.crx + fo), rCRY = rsrc(a.cry + fo), rXFX = rsrc(a.xfx + fo);
   const auto rYFX = rsrc(a.yfx + fo);
   const auto rMX = rsrc(a.mx + fo), rMY = rsrc(a.my + fo), rAR = rsrc(area), rDXA = rsrc(dxa);
+  const auto rDP1 = rsrc(TM == 2 ? a.dp1 + fo : a.mx + fo);
+  const auto rDP2 = rsrc(TM == 2 ? a.dp2o + fo : a.mx + fo);
+  const bool dp2_group = TM == 2 && tg == 0;  // one field group writes dp2
   const uint32_t vx = (uint32_t)xo * 8u;
   // dxa only enters the tile-edge interface values (ppm_al at g = 0, N reads the four
   // cells g-2 .. g+1): the other lanes read one shared word instead of their own column
@@ -252,6 +266,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     const uint32_t sm = (uint32_t)(rm + NG) * rowb;
     v.mx = MF ? bl(rMX, vx, sm) : 0.0;
     v.dxm = EX ? bl(rDXA, vxd, sm) : 0.0;
+    v.dp1 = TM == 2 ? bl(rDP1, vx, sm) : 0.0;
     return v;
   };
 
@@ -273,7 +288,8 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   double hxf[4];                  // xfx of rows r-3 .. r (the mass flux mfx when MF = false)
   YRoll ry[NF], rj[NF];           // q (y fill) and q_j
   double fyy_prev[NF];
-  double fyo_prev[NF];            // TM = 1: outer y flux of edge r-3
+  double fyo_prev[NF];            // TM = 1, 2: outer y flux of edge r-3
+  double my_prev = 0.0;           // TM = 2: mfy of edge r-3
 #pragma unroll
   for (int m = 0; m < 4; ++m) hcx[m] = arw[m] = hxf[m] = 0.0;
 #pragma unroll
@@ -297,8 +313,10 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     if (TM == 0) {
       rFX[f] = rsrc(a.fxf[f < 2 ? f : 0] + zo);
       rFY[f] = rsrc(a.fyf[f < 2 ? f : 0] + zo);
-    } else {
+    } else if (TM == 1) {
       rFX[f] = rsrc(a.qo[f] + fo);  // updated field f (TM = 1 groups are one field each)
+    } else {
+      rFX[f] = rsrc(a.qo[f < 2 ? f : 0] + zo);  // updated tracer f of the group
     }
   }
   auto bst = [&](__amdgpu_buffer_rsrc_t r, uint32_t soff, double v) {
@@ -336,6 +354,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
       nxt.my = MF ? bl(rMY, vx, se) : 0.0;
       nxt.mx = MF ? bl(rMX, vx, sm) : 0.0;
       nxt.dxm = EX ? bl(rDXA, vxd, sm) : 0.0;
+      nxt.dp1 = TM == 2 ? bl(rDP1, vx, sm) : 0.0;
   };
   // ahead: how many rows ahead the steady step prefetches (1, or 2 in the three-buffer loop)
   auto step = [&](auto gen, int r, const MarchIn<NF>& cur, MarchIn<NF>& nxt, int ahead) {
@@ -483,6 +502,32 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
 #pragma unroll
         for (int f = 0; f < NF; ++f) fyo_prev[f] = fyo[f];
       }
+      if constexpr (TM == 2) {
+        if (rowm) {
+          // tracer_dp2 then tracer_update on row m (same expressions and order)
+          const double ra = 1.0 / arw[0];  // == rarea
+          const double dp1 = cur.dp1;
+          const double dp2 = dp1 + (cur.mx - dpp_next(cur.mx) + my_prev - cur.my) * ra;
+          double qn[NF];
+#pragma unroll
+          for (int f = 0; f < NF; ++f)
+            qn[f] = (qyw[f][0] * dp1 + (fxo[f] - dpp_next(fxo[f]) + fyo_prev[f] - fyo[f]) * ra) / dp2;
+          if (GEN) {
+            if (s_fy && mrow < j1) {
+#pragma unroll
+              for (int f = 0; f < NF; ++f) bst(rFX[f], se - rowb, qn[f]);
+              if (dp2_group) bst(rDP2, se - rowb, dp2);
+            }
+          } else {
+#pragma unroll
+            for (int f = 0; f < NF; ++f) bstv(rFX[f], vfy, se - rowb, qn[f]);
+            if (dp2_group) bstv(rDP2, vfy, se - rowb, dp2);
+          }
+        }
+#pragma unroll
+        for (int f = 0; f < NF; ++f) fyo_prev[f] = fyo[f];
+        my_prev = cur.my;
+      }
     }
     yfx_prev = cur.yfx;
   };
@@ -532,6 +577,23 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
 
 // AHEAD2: steady rows prefetch two rows ahead (three row buffers, 149 VGPRs, three
 // waves per SIMD); otherwise one row ahead (two buffers, <= 128 VGPRs, four waves)
+// copy of the strip's output cells of rows [j0, j1) from the tracers to qo (and dp1 to dp2)
+template <int NF>
+__device__ void tracer_carry(const TpM& a, int z, int strip, int j0, int j1) {
+  const Dims& d = a.d;
+  const int lane = threadIdx.x & (MW - 1);
+  const int k = z % a.nk, s = z / a.nk / a.ntg, tg = (z / a.nk) % a.ntg;
+  const int x = strip * MOUT - NG + lane;
+  if (!(lane >= NG && lane < NG + MOUT && x < d.nx)) return;
+  const long zo = ((long)(s * a.nt + tg * NF) * a.nk + k) * d.plane, fo = ((long)s * a.nk + k) * d.plane;
+  const long tstride = (long)a.nk * d.plane;
+  for (int j = j0; j < j1; ++j) {
+    const long o = (long)(j + NG) * d.pitch + x + NG;
+    for (int f = 0; f < NF; ++f) a.qo[0][zo + f * tstride + o] = a.qf[0][zo + f * tstride + o];
+    if (tg == 0) a.dp2o[fo + o] = a.dp1[fo + o];
+  }
+}
+
 // OCC: minimum workgroups per CU the register budget must allow (0: 1 with AHEAD2, else 4)
 // EXS: 1 = only the strips reaching a tile edge (tile-edge PPM forms), 2 = only interior
 // strips (fewer registers, so more waves per SIMD), 0 = both; the other waves leave at once
@@ -563,6 +625,14 @@ __global__ void __launch_bounds__(MW * MWAVES, OCC ? OCC : (AHEAD2 ? 1 : 4)) tp_
   const SubInfo& sub = a.subs[s];
   const int j0 = seg * a.seg;
   const int j1 = j0 + a.seg < a.d.ny ? j0 + a.seg : a.d.ny;
+  if constexpr (TM == 2) {
+    // tracer sub-steps past this level's count: the level's tracers carry over unchanged
+    const int k = z % a.nk;
+    if (a.it >= a.nsplt[k]) {
+      tracer_carry<NF>(a, z, strip, j0, j1);
+      return;
+    }
+  }
   const int A = strip * MOUT + sub.ioff;
   const bool ex = !(A - 1 >= 2 && A + MOUT + 1 <= sub.N - 2);
   if constexpr (EXS == 1) {
@@ -743,6 +813,11 @@ __global__ void __launch_bounds__(256) tracer_update_k(Dims d, const double* __r
   }
 }
 
+__global__ void tracer_nsplt_k(int npz, const double* __restrict__ cmax, int* __restrict__ nsplt) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < npz) nsplt[k] = (int)(1.0 + cmax[k]);
+}
+
 __global__ void copy_k(long n, const double* __restrict__ a, double* __restrict__ b) {
   long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long stride = (long)gridDim.x * blockDim.x;
@@ -776,6 +851,17 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     m.fyf[0] = a.fy;
     m.fxf[1] = pair2 ? a.fx_2 : a.fx + tstride;
     m.fyf[1] = pair2 ? a.fy_2 : a.fy + tstride;
+    const bool tupd = a.q_out != nullptr;
+    if (tupd) {
+      if (pair2 || !a.mfx || !a.dp1 || !a.dp2 || !a.nsplt)
+        throw std::runtime_error("fv_tp_2d tracer update: tracer array, mass fluxes, dp1, dp2, nsplt needed");
+      m.qo[0] = a.q_out;
+      m.qo[1] = a.q_out + tstride;
+      m.dp1 = a.dp1;
+      m.dp2o = a.dp2;
+      m.nsplt = a.nsplt;
+      m.it = a.it;
+    }
     m.nt = a.nt;
     m.nk = a.nk;
     m.ntg = pair2 ? 1 : a.nt / NFw;
@@ -802,7 +888,10 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     // read once per (sub-domain, level) however many fields share them (ra_x, ra_y are
     // formed in the kernel, the 2-D area plane is not counted)
     const Ext e = ext(d);
-    const double bytes = 8.0 * a.nk * (nfields * (e.C + e.X + e.Y) + (a.mfx ? 3 : 2) * (e.X + e.Y));
+    const double bytes = tupd
+        // per tracer q read and written; crx cry xfx yfx mfx mfy dp1 read, dp2 written once
+        ? 8.0 * a.nk * (nfields * 2 * e.C + 3 * (e.X + e.Y) + 2 * e.C)
+        : 8.0 * a.nk * (nfields * (e.C + e.X + e.Y) + (a.mfx ? 3 : 2) * (e.X + e.Y));
     // (the one-row-ahead form measured 3 % slower at C180; tile-edge and interior strips
     // as two kernels -- the interior one at four waves per SIMD for single fields --
     // measured 314 against 245 us per single-field launch at C180: two launch tails, and
@@ -817,7 +906,17 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     HIP_LAUNCH_CHECK();                                                                            \
     gt_bytes(bytes / 8.0);                                                                         \
   } while (0)
-    if (a.mfx) {
+    if (tupd) {
+#define TQ_GO(O, F_)                                                                                  \
+  do {                                                                                                \
+    GT_LAUNCH_N("tp_march_tracer<" #O ", " #F_ ">", (tp_march<O, true, true, F_, 2>), g, b, 0, c.st, m); \
+    HIP_LAUNCH_CHECK();                                                                               \
+    gt_bytes(bytes / 8.0);                                                                            \
+  } while (0)
+      if (NFw == 2) { if (a.ord == 5) TQ_GO(5, 2); else TQ_GO(6, 2); }
+      else { if (a.ord == 5) TQ_GO(5, 1); else TQ_GO(6, 1); }
+#undef TQ_GO
+    } else if (a.mfx) {
       if (NFw == 2) { if (a.ord == 5) TP_GO(5, true, 2); else TP_GO(6, true, 2); }
       else { if (a.ord == 5) TP_GO(5, true, 1); else TP_GO(6, true, 1); }
     } else {
@@ -871,6 +970,11 @@ void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, doub
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   gt_bytes(npz * (2 * e.X + 2 * e.Y) + 4 * e.C);
+}
+
+void tracer_nsplt(const Ctx& c, int npz, const double* cmax_dev, int* nsplt_dev) {
+  GT_LAUNCH(tracer_nsplt_k, dim3(cdiv(npz, 64)), dim3(64), 0, c.st, npz, cmax_dev, nsplt_dev);
+  HIP_LAUNCH_CHECK();
 }
 
 void tracer_split(const Ctx& c, int npz, const int* nsplt_dev, double* cx, double* cy, double* xfx, double* yfx,

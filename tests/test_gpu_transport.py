@@ -150,3 +150,32 @@ def test_fv_tp_2d_field_pairs_bitwise(pkg, require_gpu, ord_, mf, layout):
     assert np.array_equal(d.download("p_ay"), single[0][1])
     assert np.array_equal(d.download("p_bx"), single[1][0])
     assert np.array_equal(d.download("p_by"), single[1][1])
+
+
+def _tracer_inputs(d, npz, nq, cmax_amp, seed):
+    r = rng(seed)
+    area = d.metric("area")[:, None]
+    sh = d.shape(npz)
+    return dict(q=np.abs(1e-3 * (1.0 + 0.5 * r.standard_normal(d.shape(nq * npz)))), dp1=500.0 + 100.0 * r.random(sh),
+                cx=r.uniform(-cmax_amp, cmax_amp, sh), cy=r.uniform(-cmax_amp, cmax_amp, sh),
+                mfx=0.02 * r.uniform(-1, 1, sh) * area * 500.0, mfy=0.02 * r.uniform(-1, 1, sh) * area * 500.0)
+
+
+@pytest.mark.parametrize("npx,npz,nq,cmax_amp", [(13, 6, 3, 1.2), (13, 6, 4, 0.35), (181, 2, 4, 0.45),
+                                                 (181, 2, 3, 1.3)])
+def test_tracer_update_in_march_matches_separate_update(pkg, require_gpu, npx, npz, nq, cmax_amp):
+    """tracer_2d_1l with the update inside the march (dp2 and the flux-form update from the
+    mass fluxes and tracer fluxes held in registers, ping-pong tracer planes) against the
+    flux planes + tracer_dp2 + tracer_update, bit for bit: single tracers (nq odd) and pairs,
+    one and several sub-steps (nsplt >= 2 where cmax > 1: the finished levels carry over),
+    at C12 and C180 (interior strips, seams, segments)."""
+    d = make_dom(pkg, npx, npz, nq)
+    inp = _tracer_inputs(d, npz, nq, cmax_amp, 17)
+    out = []
+    for fused in (1, 0):
+        for name, v in inp.items():
+            d.upload(name, v)
+        d.stencil("tracer_2d_1l", [], [nq, fused])
+        out.append(d.download("q")[:, :, NG:NG + d.ny, NG:NG + d.nx])
+    assert np.array_equal(out[0], out[1])
+    d.close()
