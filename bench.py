@@ -135,7 +135,7 @@ def parse():
     p.add_argument("--npz", type=int, default=72)
     p.add_argument("--nq", type=int, default=4)
     p.add_argument("--layout", default="", help="sub-domain layout per tile, e.g. 2x2 (default: by rank count)")
-    p.add_argument("--dt", type=float, default=450.0)
+    p.add_argument("--dt", type=float, default=0.0, help="dt_atmos (default 450 s x 180 / N: C180 450 s)")
     p.add_argument("--cpu-npx", type=int, default=25, help="cpu_baseline sample grid (C24)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timing", action="store_true")
@@ -191,6 +191,8 @@ def cpu_baseline(pkg, npx, npz, nq, dt, moist=False):
 
 def main():
     a = parse()
+    if a.dt <= 0.0:
+        a.dt = 450.0 * 180.0 / (a.npx - 1)
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
@@ -217,12 +219,21 @@ def main():
     nq = max(a.nq, 6) if a.moist else a.nq
     d = pkg.Domain(rank, world, nccl_id, npx=a.npx, npz=a.npz, nq=nq, layout_x=lx, layout_y=ly, dt=a.dt)
     ak, bk, ks = state.hybrid_levels(a.npz)
-    st = state.jablonowski_williamson(d, ak, bk)
+    # large tracer sets (the C720 L137 x 54 configuration's per-GPU share) go up one tracer
+    # at a time, so the host never holds all of them
+    big_q = nq > 8 and not a.moist
+    st = state.jablonowski_williamson(d, ak, bk, tracers=1 if big_q else None)
     if a.moist:
         state.aquaplanet_tracers(d, st, ak, bk)
     d.set_vertical(ak, bk, ks)
     for k, v in st.items():
-        d.upload(k, v)
+        if k == "q" and big_q:
+            d.create("q", nq * a.npz)
+            d.upload_levels("q", 0, v)
+            for iq in range(1, nq):
+                d.upload_levels("q", iq * a.npz, state.tracer_planes(d, iq))
+        else:
+            d.upload(k, v)
     del st
     torch.cuda.synchronize()
     t_init = time.perf_counter() - t_init
@@ -329,7 +340,8 @@ def main():
     if rank == 0:
         out = {
             "metric": "grid-cell-updates/sec per dycore step, " +
-                      ("Aquaplanet C180 L72 + moist physics" if a.moist else "Held-Suarez C180 L72"),
+                      (f"Aquaplanet C{N} L{npz} + moist physics" if a.moist else f"Held-Suarez C{N} L{npz}") +
+                      (f" with {nq} tracers" if nq != 4 and not a.moist else ""),
             "value": value,
             "unit": "grid-cell-updates/s",
             "n_gpus": world,
@@ -345,7 +357,8 @@ def main():
                                     if a.moist else f"Held-Suarez C{N} L{npz} dycore step (fv_dynamics)") +
                                    f", 6 tiles on {world} MI355X", "npx": N + 1, "npz": npz, "nq": nq,
                        "layout": f"{lx}x{ly}",
-                       "dt_atmos": a.dt, "n_split": 6, "k_split": 1, "cells_per_step": cells},
+                       "dt_atmos": a.dt, "n_split": 6, "k_split": 1, "cells_per_step": cells,
+                       "tracer_cell_updates_per_step": cells * nq},
             "roofline": roof,
             "cpu_baseline": cpu,
             "state_check": check,

@@ -182,6 +182,12 @@ int gtfv3_field_upload(void* h, const char* name, int nk, const double* host) {
   API_CATCH
 }
 
+int gtfv3_field_upload_levels(void* h, const char* name, int k0, int nk, const double* host) {
+  API_TRY
+  D(h)->upload_levels(name, host, k0, nk);
+  API_CATCH
+}
+
 int gtfv3_field_download(void* h, const char* name, double* host) {
   API_TRY
   D(h)->download(name, host);

@@ -146,6 +146,17 @@ void Dycore::upload(const std::string& name, const double* host, int nk) {
   HIP_CHECK(hipStreamSynchronize(st));
 }
 
+void Dycore::upload_levels(const std::string& name, const double* host, int k0, int nk) {
+  Field* f = find(name);
+  if (!f) throw std::runtime_error("no field '" + name + "'");
+  if (k0 < 0 || nk < 1 || k0 + nk > f->nk) throw std::runtime_error("upload_levels: level range outside the field");
+  // host (nsub, nk, plane) -> levels k0 .. k0+nk-1 of every sub-domain
+  HIP_CHECK(hipMemcpy2DAsync(f->p + (long)k0 * d.plane, sizeof(double) * f->nk * d.plane, host,
+                             sizeof(double) * nk * d.plane, sizeof(double) * nk * d.plane, d.nsub,
+                             hipMemcpyHostToDevice, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+}
+
 void Dycore::download(const std::string& name, double* host) {
   Field* f = find(name);
   if (!f) throw std::runtime_error("no field '" + name + "'");
@@ -527,7 +538,7 @@ void Dycore::step() {
   // ---- vertical remap to the hybrid Eulerian coordinate ----
   RemapState rs{pe, peln, pk, pkz, delp.p, delz.p, pt.p, w.p, q.p, u.p, v.p, ps, ws};
   RemapScratch rsc;
-  for (int n = 0; n < 3; ++n) rsc.s[n] = S(("_rmj" + std::to_string(n)).c_str(), remap_jobs(nq) * k1);
+  for (int n = 0; n < 3; ++n) rsc.s[n] = S(("_rmj" + std::to_string(n)).c_str(), remap_scratch_slots(nq) * k1);
   lagrangian_to_eulerian(c, npz, nq, ptop, nl.fill != 0, ak_dev, bk_dev, rs, rsc);
   HIP_CHECK(hipEventRecord(ev[3], st));
 

@@ -66,6 +66,9 @@ class Dycore {
   // host <-> device copies of a whole named field in the padded device layout
   void upload(const std::string& name, const double* host, int nk);
   void download(const std::string& name, double* host);
+  // host (nsub, nk, plane) into levels [k0, k0+nk) of an existing field (large tracer sets
+  // are uploaded tracer by tracer)
+  void upload_levels(const std::string& name, const double* host, int k0, int nk);
 
   // halo update of named fields; kinds: 'c' cell, 'b' corner, 'd' D-grid pair, 'C' C-grid pair, 'a' A-grid pair
   void halo_update(const std::vector<std::pair<std::string, char>>& items);

@@ -64,9 +64,10 @@ struct RemapState {
   double *pe, *peln, *pk, *pkz, *delp, *delz, *pt, *w, *q, *u, *v, *ps, *ws;
 };
 struct RemapScratch {
-  double* s[3];  // q edges, gam, source copy: remap_jobs(nq) * (npz+1) levels each
+  double* s[3];  // q edges, gam, source copy: remap_scratch_slots(nq) * (npz+1) levels each
 };
 int remap_jobs(int nq);
+int remap_scratch_slots(int nq);  // scratch column sets (jobs run in chunks of this many)
 // variant: 0 = register-resident columns where instantiated (L10/12/20/72), else the
 // scratch-column jobs; 1 = force the scratch-column jobs (remap_job_k, the bitwise reference)
 void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fill, const double* ak_dev,

@@ -327,6 +327,7 @@ __device__ __forceinline__ void fillz_col(const Col& q, const DPF& dp, int km) {
 struct RemapArgs {
   Dims d;
   int npz, nq, fill, njob;
+  int job0, nslot;  // scratch slots per sub-domain: jobs job0 .. job0+nslot-1 of a launch
   double ptop;
   const double *ak, *bk;
   RemapState S;
@@ -348,8 +349,8 @@ __global__ void __launch_bounds__(BLOCK) remap_prep_k(RemapArgs a) {
   const double* DELP = a.S.delp + (long)s * km * P + o;
   const double* DELZ = a.S.delz + (long)s * km * P + o;
   const double* PT = a.S.pt + (long)s * km * P + o;
-  double* TV = a.src + ((long)s * a.njob + J_PT) * k1 * P + o;
-  double* DZ = a.src + ((long)s * a.njob + J_DZ) * k1 * P + o;
+  double* TV = a.src + ((long)s * a.nslot + J_PT) * k1 * P + o;
+  double* DZ = a.src + ((long)s * a.nslot + J_DZ) * k1 * P + o;
   for (int k = 0; k < km; ++k) {
     const double pt = PT[k * P];
     TV[k * P] = pt * exp(k1k * log(rrg * DELP[k * P] / DELZ[k * P] * pt));
@@ -360,7 +361,7 @@ __global__ void __launch_bounds__(BLOCK) remap_prep_k(RemapArgs a) {
 __global__ void __launch_bounds__(BLOCK) remap_job_k(RemapArgs a) {
   const Dims& d = a.d;
   const int km = a.npz, k1 = km + 1;
-  const int job = blockIdx.y;
+  const int job = a.job0 + blockIdx.y;
   const int s = blockIdx.z;
   const int nxe = d.nx + 1;
   const int c = blockIdx.x * BLOCK + threadIdx.x;
@@ -375,7 +376,7 @@ __global__ void __launch_bounds__(BLOCK) remap_job_k(RemapArgs a) {
   }
   const long P = d.plane, o = pidx(d, i, j);
   const long b1 = (long)s * k1 * P + o, bk = (long)s * km * P + o;
-  const long slot = ((long)s * a.njob + job) * k1 * P + o;
+  const long slot = ((long)s * a.nslot + job - a.job0) * k1 * P + o;
   Col q{a.qs + slot, P}, gam{a.gs + slot, P}, A{a.src + slot, P};
   const double* pe = a.S.pe + b1;
   Edges E{0, pe, nullptr, P};
@@ -502,7 +503,7 @@ __global__ void __launch_bounds__(64) remap_reg_k(RemapArgs a) {
   const double* src;
   double* out;
   double qs = 0.0;
-  const long slot = ((long)s * a.njob + job) * (KM + 1) * P;
+  const long slot = ((long)s * a.nslot + job) * (KM + 1) * P;  // (T_v, delz only: job < 2)
   if (JK == JK_PT) {
     rEA = rsrc(a.S.peln + (long)s * (KM + 1) * P, KM + 1);
     lntop = ld(rEA, vo, 0);
@@ -839,6 +840,12 @@ __global__ void __launch_bounds__(BLOCK) remap_finish_k(RemapArgs a) {
 
 int remap_jobs(int nq) { return nq + J_Q0; }
 
+// The column-job form keeps three scratch columns (edge values, factors, source copy) per
+// job: at most RM_CHUNK jobs share one set of scratch planes (jobs launched in chunks), so
+// L137 with 54 tracers needs 3 x 8 x 138 planes per sub-domain, not 3 x 59 x 138.
+constexpr int RM_CHUNK = 8;
+int remap_scratch_slots(int nq) { return std::min(remap_jobs(nq), RM_CHUNK); }
+
 void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fill, const double* ak_dev,
                             const double* bk_dev, const RemapState& S, const RemapScratch& R, int variant) {
   if (npz < 6) throw std::runtime_error("remap: npz >= 6 required");
@@ -849,6 +856,8 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
   a.nq = nq;
   a.fill = fill ? 1 : 0;
   a.njob = remap_jobs(nq);
+  a.nslot = remap_scratch_slots(nq);
+  a.job0 = 0;
   a.ptop = ptop;
   a.ak = ak_dev;
   a.bk = bk_dev;
@@ -887,9 +896,15 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
     else if (npz == 12) go(std::integral_constant<int, 12>{}, std::integral_constant<int, 8>{});
     else go(std::integral_constant<int, 20>{}, std::integral_constant<int, 8>{});
   } else {
-    GT_LAUNCH(remap_job_k, dim3(cdiv(nce, BLOCK), a.njob, d.nsub), dim3(BLOCK), 0, c.st, a);
-    // every job reads its source column and writes its field (L each), pe + peln once, ws
-    gt_bytes(L * 2 * ((a.njob - 2) * e.C + e.X + e.Y) + L1 * 2 * e.C + e.C);
+    // every job reads its source column and writes its field (L each), pe + peln once, ws;
+    // each chunk registers its jobs' share
+    const double all = L * 2 * ((a.njob - 2) * e.C + e.X + e.Y) + L1 * 2 * e.C + e.C;
+    for (int j0 = 0; j0 < a.njob; j0 += a.nslot) {
+      a.job0 = j0;
+      const int nj = std::min(a.nslot, a.njob - j0);
+      GT_LAUNCH(remap_job_k, dim3(cdiv(nce, BLOCK), nj, d.nsub), dim3(BLOCK), 0, c.st, a);
+      gt_bytes(all * nj / a.njob);
+    }
   }
   HIP_LAUNCH_CHECK();
   GT_LAUNCH(remap_finish_k, dim3(cdiv(nc, BLOCK), d.nsub), dim3(BLOCK), 0, c.st, a);

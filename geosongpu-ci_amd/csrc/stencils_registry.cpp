@@ -201,7 +201,7 @@ std::map<std::string, Fn>& reg() {
                        dy.need("q", nq * npz).p, dy.need("u", npz).p, dy.need("v", npz).p, dy.field("ps", 1).p,
                        dy.field("ws", 1).p};
          RemapScratch rsc;
-         for (int n = 0; n < 3; ++n) rsc.s[n] = dy.field("_rmj" + std::to_string(n), remap_jobs(nq) * k1).p;
+         for (int n = 0; n < 3; ++n) rsc.s[n] = dy.field("_rmj" + std::to_string(n), remap_scratch_slots(nq) * k1).p;
          lagrangian_to_eulerian(dy.ctx(), npz, nq, dy.ak.at(0), p.empty() || p[0] != 0.0, vert, vert + k1, rs, rsc,
                                 p.size() > 1 ? (int)p[1] : 0);
        }},

@@ -185,9 +185,11 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
                 "thermo march: delp, w, pt with the accumulators as MX / MY; tracer march: mass fluxes");
   const Dims& d = a.d;
   const int lane = threadIdx.x & (MW - 1);
-  // z: (sub-domain, field group, level); the NF fields of a group share the Courant
-  // numbers and fluxes, so those planes are loaded once for all of them
-  const int k = z % a.nk, s = z / a.nk / a.ntg, tg = (z / a.nk) % a.ntg;
+  // z: (sub-domain, level, field group), the field group fastest: the groups of one level
+  // share the Courant numbers and fluxes (loaded once per wave for its NF fields), and with
+  // the groups of a level adjacent in launch order those planes are re-read from the
+  // Infinity Cache, not HBM (54 tracers: 27 groups per level)
+  const int tg = z % a.ntg, k = (z / a.ntg) % a.nk, s = z / a.ntg / a.nk;
   const SubInfo sub = a.subs[s];
   const int nx = d.nx, ny = d.ny, N = sub.N;
   const bool last = j1 >= ny;
@@ -582,7 +584,7 @@ template <int NF>
 __device__ void tracer_carry(const TpM& a, int z, int strip, int j0, int j1) {
   const Dims& d = a.d;
   const int lane = threadIdx.x & (MW - 1);
-  const int k = z % a.nk, s = z / a.nk / a.ntg, tg = (z / a.nk) % a.ntg;
+  const int tg = z % a.ntg, k = (z / a.ntg) % a.nk, s = z / a.ntg / a.nk;
   const int x = strip * MOUT - NG + lane;
   if (!(lane >= NG && lane < NG + MOUT && x < d.nx)) return;
   const long zo = ((long)(s * a.nt + tg * NF) * a.nk + k) * d.plane, fo = ((long)s * a.nk + k) * d.plane;
@@ -627,7 +629,7 @@ __global__ void __launch_bounds__(MW * MWAVES, OCC ? OCC : (AHEAD2 ? 1 : 4)) tp_
   const int j1 = j0 + a.seg < a.d.ny ? j0 + a.seg : a.d.ny;
   if constexpr (TM == 2) {
     // tracer sub-steps past this level's count: the level's tracers carry over unchanged
-    const int k = z % a.nk;
+    const int k = (z / a.ntg) % a.nk;
     if (a.it >= a.nsplt[k]) {
       tracer_carry<NF>(a, z, strip, j0, j1);
       return;

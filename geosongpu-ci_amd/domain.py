@@ -98,6 +98,13 @@ class Domain:
             raise ValueError(f"{name}: array shape {arr.shape} is not (nsub, nk, nj, pitch)")
         check(lib().gtfv3_field_upload(self.h, name.encode(), arr.shape[1], dptr(arr)))
 
+    def upload_levels(self, name, k0, arr):
+        """levels k0 .. k0 + arr.shape[1] - 1 of an existing field (every sub-domain)"""
+        arr = np.ascontiguousarray(arr, dtype=np.float64)
+        if arr.ndim != 4 or arr.shape[0] != self.nsub or arr.shape[2:] != (self.nj, self.pitch):
+            raise ValueError(f"{name}: array shape {arr.shape} is not (nsub, nk, nj, pitch)")
+        check(lib().gtfv3_field_upload_levels(self.h, name.encode(), k0, arr.shape[1], dptr(arr)))
+
     def download(self, name):
         nk = self.nk_of(name)
         if nk <= 0:

@@ -78,9 +78,25 @@ def _jw_phis(lat):
                                      + (1.6 * cl ** 3 * (sl ** 2 + 2.0 / 3.0) - np.pi / 4.0) * RADIUS * OMEGA)
 
 
-def jablonowski_williamson(dom, ak, bk, ps=1.0e5):
-    """dict of host arrays (nsub, nk, nj, pitch): u, v, w, delz, pt, delp, q, phis."""
-    nsub, npz, nq = dom.nsub, dom.npz, max(dom.nq, 1)
+def tracer_planes(dom, iq):
+    """tracer iq of the synthetic state as (nsub, npz, nj, pitch): specific humidity for
+    iq = 0, else a smooth bell pattern shifted in longitude per tracer"""
+    lat, lon = dom.metric("lat"), dom.metric("lon")
+    if iq == 0:
+        t = 1.0e-6 * (1.0 + np.cos(lat))
+    else:
+        t = 0.5 * (1.0 + np.cos(lat) * np.cos(lon - 0.7 * iq))
+    out = np.repeat(t[:, None], dom.npz, axis=1)
+    np.nan_to_num(out, copy=False)
+    return out
+
+
+def jablonowski_williamson(dom, ak, bk, ps=1.0e5, tracers=None):
+    """dict of host arrays (nsub, nk, nj, pitch): u, v, w, delz, pt, delp, q, phis.
+    tracers: how many tracers to put in q (default all dom.nq; large sets go through
+    tracer_planes + Domain.upload_levels one tracer at a time)."""
+    nsub, npz = dom.nsub, dom.npz
+    nq = max(dom.nq, 1) if tracers is None else max(int(tracers), 1)
     nj, pitch, nx, ny = dom.nj, dom.pitch, dom.nx, dom.ny
     H = NG + 1
     xyz = dom.corner_xyz()  # (nsub, ny+2H+1, nx+2H+1, 3), corner (i, j) at [j+H, i+H]

@@ -37,6 +37,8 @@ int gtfv3_field_create(void* h, const char* name, int nk);
 int gtfv3_field_nk(void* h, const char* name);
 int gtfv3_field_upload(void* h, const char* name, int nk, const double* host);
 int gtfv3_field_download(void* h, const char* name, double* host);
+/* levels [k0, k0+nk) of an existing field from host (nsub, nk, nj, pitch) */
+int gtfv3_field_upload_levels(void* h, const char* name, int k0, int nk, const double* host);
 /* raw device pointer of a field (for zero-copy interop), NULL if missing */
 void* gtfv3_field_ptr(void* h, const char* name);
 

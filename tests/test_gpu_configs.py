@@ -109,3 +109,21 @@ def test_c180_l72_step_properties_and_band_layout(pkg, require_gpu):
                 assert np.array_equal(a, b), f"{k}: band layout differs on sub-domain {s}"
     finally:
         d4.close()
+
+
+def test_upload_levels_tracer_by_tracer(pkg, require_gpu):
+    """Domain.upload_levels (gtfv3_field_upload_levels): tracers uploaded one at a time into
+    a created nq*npz field land in their level ranges of every sub-domain (the path bench.py
+    takes for the 54-tracer configuration)."""
+    import importlib
+    state = importlib.import_module(pkg.__name__ + ".state")
+    npz, nq = 5, 4
+    d = pkg.Domain(npx=13, npz=npz, nq=nq, layout_x=2, layout_y=2)
+    ak, bk, ks = state.hybrid_levels(npz)
+    full = state.jablonowski_williamson(d, ak, bk)["q"]
+    d.create("q", nq * npz)
+    for iq in range(nq):
+        d.upload_levels("q", iq * npz, state.tracer_planes(d, iq))
+    got = d.download("q")
+    assert np.array_equal(got, full)
+    d.close()
