@@ -70,7 +70,8 @@ class Dycore {
   // are uploaded tracer by tracer)
   void upload_levels(const std::string& name, const double* host, int k0, int nk);
 
-  // halo update of named fields; kinds: 'c' cell, 'b' corner, 'd' D-grid pair, 'C' C-grid pair, 'a' A-grid pair
+  // halo update of named fields; kinds: 'c' cell, 'b' corner, 'd' D-grid pair, 'C' C-grid pair, 'a' A-grid pair,
+  // 'S' C-grid pair tile-edge synchronisation (east / north edge values from the neighbour)
   void halo_update(const std::vector<std::pair<std::string, char>>& items);
   // max-reduce across ranks (in place, device, n doubles)
   void allreduce_max(double* dev, int n);

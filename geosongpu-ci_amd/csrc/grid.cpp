@@ -161,6 +161,13 @@ Mapped CubedSphere::map(int t, int x2, int y2, bool geometry) const {
   return m;
 }
 
+Mapped CubedSphere::map_across(int t, int edge, int x2, int y2) const {
+  const Xf& xf = xf_[t][edge];
+  int rx, ry;
+  rot_apply(xf.rot, x2, y2, rx, ry);
+  return Mapped{xf.nt, rx + xf.tx, ry + xf.ty, xf.rot, true};
+}
+
 V3 CubedSphere::point(int t, int I, int J) const {
   Mapped m = map(t, 2 * I, 2 * J, true);
   return tile_point(m.t, m.x2 / 2, m.y2 / 2);

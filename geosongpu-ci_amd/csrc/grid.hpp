@@ -46,6 +46,9 @@ class CubedSphere {
   // any lattice point; cube-corner regions use the copy_corners(XDir) rotation
   V3 point(int t, int I, int J) const;
   Mapped map(int t, int x2, int y2, bool geometry) const;
+  // the point in the coordinates of the neighbour across `edge` (W,E,S,N = 0..3) even when it
+  // lies on the edge itself (a shared edge point: its position in the neighbouring tile)
+  Mapped map_across(int t, int edge, int x2, int y2) const;
   int neighbor(int t, int edge) const { return xf_[t][edge].nt; }
   int edge_rot(int t, int edge) const { return xf_[t][edge].rot; }
 

@@ -77,7 +77,10 @@ struct Dims {
 enum Stagger : int { CELL = 0, XEDGE = 1, YEDGE = 2, CORNER = 3 };
 // halo kinds (scalar staggerings + vector pairs)
 enum HaloKind : int {
-  H_CELL = 0, H_CORNER = 1, H_DGRID = 2, H_CGRID = 3, H_AGRID = 4, H_NKIND = 5
+  H_CELL = 0, H_CORNER = 1, H_DGRID = 2, H_CGRID = 3, H_AGRID = 4,
+  // C-grid tile-edge synchronisation: uc on east and vc on north tile edges take the
+  // neighbouring tile's values at the same points (FV3 mpp_get_boundary; see halo.hip)
+  H_CSYNC = 5, H_NKIND = 6
 };
 
 // host-side sub-domain decomposition of the cubed sphere

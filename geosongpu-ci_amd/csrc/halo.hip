@@ -24,7 +24,8 @@ inline int comp_stagger(int kind, int c) {
     case H_CELL: return CELL;
     case H_CORNER: return CORNER;
     case H_DGRID: return c == 0 ? XEDGE : YEDGE;   // u along x-edges, v along y-edges
-    case H_CGRID: return c == 0 ? YEDGE : XEDGE;   // uc normal to y-edges, vc to x-edges
+    case H_CGRID:
+    case H_CSYNC: return c == 0 ? YEDGE : XEDGE;   // uc normal to y-edges, vc to x-edges
     default: return CELL;                           // A-grid pair
   }
 }
@@ -98,6 +99,37 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
     s.zero = false;
     return s;
   };
+  // a point ON the east (edge 1) / north (edge 3) tile edge, as the neighbouring tile holds
+  // it (its west or south edge: the FV3 cube joins every east / north edge to one of those)
+  auto resolve_edge = [&](int g, int kind, int c, int i, int j, int edge) -> Src {
+    SubInfo si = dc.sub(g);
+    int st = comp_stagger(kind, c);
+    int x2 = 2 * (i + si.ioff) + ((st == CELL || st == XEDGE) ? 1 : 0);
+    int y2 = 2 * (j + si.joff) + ((st == CELL || st == YEDGE) ? 1 : 0);
+    Mapped m = cs.map_across(si.tile, edge, x2, y2);
+    if (!(m.x2 == 0 || m.y2 == 0)) throw std::runtime_error("halo: an east / north edge must meet a west / south edge");
+    int found = -1, li = 0, lj = 0;
+    for (int py = 0; py < dc.ly && found < 0; ++py)
+      for (int px = 0; px < dc.lx && found < 0; ++px) {
+        int ii = (m.x2 - (m.x2 & 1)) / 2 - px * nx, jj = (m.y2 - (m.y2 & 1)) / 2 - py * ny;
+        int imax = (m.x2 & 1) ? nx - 1 : nx, jmax = (m.y2 & 1) ? ny - 1 : ny;
+        if (ii >= 0 && ii <= imax && jj >= 0 && jj <= jmax) {
+          found = m.t * dc.lx * dc.ly + py * dc.lx + px;
+          li = ii; lj = jj;
+        }
+      }
+    if (found < 0) throw std::runtime_error("halo: no owner sub-domain of a shared edge point");
+    Src s{};
+    s.rank = dc.owner_rank(found);
+    s.lsub = found % nper;
+    s.off = (int)pidx(d, li, lj);
+    int dx = c == 0 ? 1 : 0, dy = c == 0 ? 0 : 1, ox, oy;
+    rot_dir(m.rot, dx, dy, ox, oy);
+    s.comp = ox != 0 ? 0 : 1;
+    s.sign = ox + oy;
+    s.zero = false;
+    return s;
+  };
 
   for (int kind = 0; kind < H_NKIND; ++kind) {
     h_local_[kind].clear();
@@ -109,6 +141,24 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
           int st = comp_stagger(kind, c);
           int sx = (st == YEDGE || st == CORNER) ? 1 : 0;
           int sy = (st == XEDGE || st == CORNER) ? 1 : 0;
+          if (kind == H_CSYNC) {
+            // targets: uc on the east tile edge, vc on the north tile edge of this sub-domain
+            const SubInfo si = dc.sub(g);
+            const bool east = c == 0 && si.ioff + nx == si.N, north = c == 1 && si.joff + ny == si.N;
+            const int n = east ? ny : (north ? nx : 0);
+            for (int p = 0; p < n; ++p) {
+              const int i = east ? nx : p, j = east ? p : ny;
+              Src s = resolve_edge(g, kind, c, i, j, east ? 1 : 3);
+              if (q != rank_) {
+                if (s.rank == rank_) send[q].push_back({s.lsub, s.off, s.comp, s.sign, 0, 0});
+                continue;
+              }
+              int doff = (int)pidx(d, i, j);
+              if (s.rank == rank_) h_local_[kind].push_back({ls, doff, s.lsub, s.off, c | (s.comp << 1), s.sign});
+              else recv[s.rank].push_back({ls, doff, c, 0, 0, 0});
+            }
+            continue;
+          }
           for (int j = -NG; j <= ny - 1 + NG + sy; ++j)
             for (int i = -NG; i <= nx - 1 + NG + sx; ++i) {
               bool inside = i >= 0 && i <= nx - 1 + sx && j >= 0 && j <= ny - 1 + sy;

@@ -19,7 +19,7 @@ import numpy as np
 
 from . import NG
 from . import fv_mapz, nh_core, sw_core, tp_core
-from .halo import Layout, fill_scalar, fill_vector
+from .halo import Layout, fill_scalar, fill_vector, sync_edges
 from .util import Plane, sh
 
 np.seterr(all="ignore")
@@ -149,6 +149,11 @@ def fv_dynamics(st, ak, bk, g, nl):
             uc, vc = nh_core.p_grad_c(c["uc"], c["vc"], c["delpc"], pef, gzc, m, P, dt2)
             st["uc"][s], st["vc"][s], st["ua"][s], st["va"][s] = uc, vc, c["ua"], c["va"]
             cs.append(c)
+        # one value per shared tile-edge point: east / north edges take the neighbour's winds
+        # (FV3 mpp_get_boundary; without it the cube-corner circulation of c_sw leaves the two
+        # tiles with different winds, hence mass fluxes, next to each corner)
+        if nl.get("edge_sync", 1):
+            sync_edges(st["uc"], st["vc"], g.layout, "cgrid")
         _halo(g, st, [("uc", "C"), ("vc", "C")])
         ds = []
         for s in range(nsub):

@@ -171,3 +171,49 @@ def fill_vector(fx, fy, layout, kind="dgrid"):
         vals[sg < 0] = 0.0
         dsts[c][dg, :, dj, di] = vals
     return fx, fy
+
+
+def _sync_table(layout, kind):
+    """Tile-edge synchronisation (FV3's mpp_get_boundary use in dyn_core): the vector
+    components stored ON the east / north tile edges of a sub-domain take the values the
+    neighbouring tile holds at the same points (its west / south edge; the FV3 connectivity
+    always joins an east or north edge to a west or south one), so both tiles carry one
+    value per shared edge point.  C grid: uc on east edges, vc on north edges; D grid: v on
+    east edges, u on north edges."""
+    key = ("e", layout.N, layout.lx, layout.ly, kind)
+    if key in _TABLES:
+        return _TABLES[key]
+    out = []
+    nx, ny, N = layout.nx, layout.ny, layout.N
+    for c, st in enumerate(VECTOR[kind]):
+        dx2, dy2 = STAGGER[st]
+        dst, src = [], []
+        for g, sd in enumerate(layout.subs()):
+            pts = []
+            if st == "yedge" and sd["ioff"] + nx == N:      # east tile edge, x-normal point
+                pts = [(nx, j, "E") for j in range(ny)]
+            elif st == "xedge" and sd["joff"] + ny == N:    # north tile edge, y-normal point
+                pts = [(i, ny, "N") for i in range(nx)]
+            for i, j, edge in pts:
+                nb, f, rot = _edge_map(sd["tile"], edge, N)
+                X, Y = f(2 * (i + sd["ioff"]) + dx2, 2 * (j + sd["joff"]) + dy2)
+                assert X == 0 or Y == 0, "an east / north edge must meet a west / south edge"
+                dxd, dyd = (1, 0) if c == 0 else (0, 1)
+                ox, oy = _rot(rot, dxd, dyd)
+                gs, ii, jj = layout.owner(nb, X, Y)
+                dst.append((g, j + NG, i + NG))
+                src.append((gs, jj + NG, ii + NG, 0 if ox != 0 else 1, ox + oy))
+        out.append((np.array(dst, dtype=int).reshape(-1, 3).T, np.array(src, dtype=int).reshape(-1, 5).T))
+    _TABLES[key] = out
+    return out
+
+
+def sync_edges(fx, fy, layout, kind="cgrid"):
+    srcs = (fx.copy(), fy.copy())
+    dsts = (fx, fy)
+    for c, ((dg, dj, di), (sg, sj, si, sc, sign)) in enumerate(_sync_table(layout, kind)):
+        if dg.size == 0:
+            continue
+        vals = np.where(sc[:, None] == 0, srcs[0][sg, :, sj, si], srcs[1][sg, :, sj, si]) * sign[:, None]
+        dsts[c][dg, :, dj, di] = vals
+    return fx, fy

@@ -109,3 +109,25 @@ def test_fv_dynamics_decomposition_invariant(pkg, require_gpu):
             a = o2[k][s2][:, NG:NG + d2.ny, NG:NG + d2.nx]
             b = o1[k][t][:, NG + jo:NG + jo + d2.ny, NG + io:NG + io + d2.nx]
             assert np.array_equal(a, b), f"{k} differs on sub {s2}"
+
+
+def test_hip_step_dry_mass_drift(pkg, require_gpu):
+    """Global dry mass (sum of delp x area) after a HIP step: with the C-grid tile-edge
+    synchronisation (Dycore::step, halo kind 'S') it drifts by < 3e-11 of itself per step,
+    as the oracle (tests/test_oracle_props.py); 2.8e-7 before the synchronisation."""
+    state = importlib.import_module(pkg.__name__ + ".state")
+    npz = 10
+    d = pkg.Domain(npx=13, npz=npz, nq=2)
+    ak, bk, ks = state.hybrid_levels(npz)
+    st = state.jablonowski_williamson(d, ak, bk)
+    d.set_vertical(ak, bk, ks)
+    for k, v in st.items():
+        d.upload(k, v)
+    area = d.metric("area")[:, None, NG:NG + d.ny, NG:NG + d.nx]
+    m0 = (st["delp"][..., NG:NG + d.ny, NG:NG + d.nx] * area).sum()
+    for _ in range(2):
+        d.step(1)
+        m1 = (d.download("delp")[..., NG:NG + d.ny, NG:NG + d.nx] * area).sum()
+        assert abs(m1 - m0) / m0 < 3e-11, (m1 - m0) / m0
+        m0 = m1
+    d.close()

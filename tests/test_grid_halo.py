@@ -107,3 +107,12 @@ def test_halo_tables_match_oracle(pkg, layout):
         ohalo.fill_vector(u2, v2, lay, vk)
         np.testing.assert_array_equal(u, u2)
         np.testing.assert_array_equal(v, v2)
+    # C-grid tile-edge synchronisation (kind 5): east / north edge points from the neighbour
+    u = r.standard_normal(shape)
+    v = r.standard_normal(shape)
+    u2, v2 = u.copy(), v.copy()
+    _apply_table(pkg, d, 5, [u, v])
+    ohalo.sync_edges(u2, v2, lay, "cgrid")
+    np.testing.assert_array_equal(u, u2)
+    np.testing.assert_array_equal(v, v2)
+    assert not np.array_equal(u, r.standard_normal(shape))

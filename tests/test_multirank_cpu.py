@@ -14,7 +14,8 @@ import torch.multiprocessing as mp
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
-KINDS = ((0, "cell", None), (1, "corner", None), (2, None, "dgrid"), (3, None, "cgrid"), (4, None, "agrid"))
+KINDS = ((0, "cell", None), (1, "corner", None), (2, None, "dgrid"), (3, None, "cgrid"), (4, None, "agrid"),
+         (5, None, "csync"))
 
 
 def _free_port():
@@ -62,6 +63,8 @@ def _worker(rank, world, port, layout, q, npx=13):
             ref = [c.copy() for c in comps]
             if st:
                 ohalo.fill_scalar(ref[0], lay, st)
+            elif vk == "csync":
+                ohalo.sync_edges(ref[0], ref[1], lay, "cgrid")
             else:
                 ohalo.fill_vector(ref[0], ref[1], lay, vk)
             loc = [c[rank * nper:(rank + 1) * nper].reshape(nper, nk, -1).copy() for c in comps]
