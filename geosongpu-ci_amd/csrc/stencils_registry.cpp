@@ -43,7 +43,9 @@ std::map<std::string, Fn>& reg() {
          TpArgs a{};
          a.q = q.p; a.nt = nt; a.nk = nk;
          a.crx = F(dy, f[1]).p; a.cry = F(dy, f[2]).p; a.xfx = F(dy, f[3]).p; a.yfx = F(dy, f[4]).p;
-         (void)F(dy, f[5]); (void)F(dy, f[6]);  // ra_x, ra_y: checked to exist, not read
+         // ra_x, ra_y: not read (may be "-"); when named they must exist
+         if (f[5] != "-") (void)F(dy, f[5]);
+         if (f[6] != "-") (void)F(dy, f[6]);
          a.mfx = f[7] == "-" ? nullptr : F(dy, f[7]).p;
          a.mfy = f[8] == "-" ? nullptr : F(dy, f[8]).p;
          a.fx = dy.field(f[9], q.nk).p; a.fy = dy.field(f[10], q.nk).p;

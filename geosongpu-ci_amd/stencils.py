@@ -1,5 +1,15 @@
 """NDSL-style stencil surface backed by the HIP library.
 
+Two factories:
+  * get_factories_single_tile(nx, ny, nz, nhalo): host numpy arrays in and out (the DSL
+    pattern programs' single-tile numpy setup);
+  * get_factories_cubed_sphere(npx, npz, nq, layout): device-resident quantities on the whole
+    cubed sphere for the dycore stencils (c_sw, d_sw, fv_tp_2d, riem_solver_c, riem_solver3,
+    update_dz_d, a2b_ord4, held_suarez, the moist columns ...), called the NDSL way --
+    `self.c_sw = stencil_factory.from_dims_halo(func=c_sw, compute_dims=[X_DIM, Y_DIM, Z_DIM])`,
+    `self.c_sw(delp, pt, w, u, v, uc, vc, ua, va, ut, vt, delpc, ptc, wc, dt2=dt2)` -- with the
+    fields staying in HBM between calls (host views are synchronised lazily).
+
 Mirrors the call shapes the reference's DSL pattern programs use
 (dsl_patterns/Do__get_top_of_the_column.py:28-55, Do__while_in_gt_functions.py:15-52,
 WIP__hybrid_index_2dout.py:25-65):
@@ -40,6 +50,23 @@ class StencilDef:
 column_top = StencilDef("column_top", 2, (1,))
 column_while_lt = StencilDef("column_while_lt", 2, (1,), ("thr",))
 column_gather_k = StencilDef("column_gather_k", 4, (3,))
+
+# dycore stencils (csrc/stencils_registry.cpp; argument order = the FV3 routine's)
+c_sw = StencilDef("c_sw", 14, tuple(range(5, 14)), ("dt2",))
+d_sw = StencilDef("d_sw", 18, (0, 1, 2, 3, 4) + tuple(range(9, 18)),
+                  ("dt", "dddmp", "d2_bg", "hord_mt", "hord_vt", "hord_tm", "hord_dp"))
+fv_tp_2d = StencilDef("fv_tp_2d", 11, (9, 10), ("ord", "nt"))
+fv_tp_2d_pair = StencilDef("fv_tp_2d_pair", 12, (8, 9, 10, 11), ("ord",))
+riem_solver_c = StencilDef("riem_solver_c", 6, (4, 5), ("dt2", "ptop", "p_fac", "dz_min"))
+riem_solver3 = StencilDef("riem_solver3", 12, (2, 4) + tuple(range(5, 12)), ("dt", "ptop", "p_fac", "dz_min", "last_call"))
+edge_profile = StencilDef("edge_profile", 8, (4, 5, 6, 7), ("variant",))
+update_dz_d = StencilDef("update_dz_d", 5, (0,), ("hord",))
+a2b_ord4 = StencilDef("a2b_ord4", 2, (1,))
+held_suarez = StencilDef("held_suarez", 4, (1, 2, 3), ("dt",))
+moist_qsat = StencilDef("moist_qsat", 5, (2, 3, 4))
+fillq2zero = StencilDef("fillq2zero", 3, (0, 2))
+gfdl_1m = StencilDef("gfdl_1m", 14, tuple(range(7)) + (10, 11, 12, 13), ("dt",))
+buoyancy = StencilDef("buoyancy", 8, (4, 5, 6, 7))
 
 
 class Quantity:
@@ -126,6 +153,110 @@ class StencilFactory:
 def get_factories_single_tile(nx: int, ny: int, nz: int, nhalo: int):
     """(StencilFactory, QuantityFactory) like ndsl.boilerplate.get_factories_single_tile_numpy."""
     return StencilFactory(nx, ny, nz, nhalo), QuantityFactory(nx, ny, nz, nhalo)
+
+
+class DeviceQuantity:
+    """A Domain field with NDSL Quantity semantics: dims, units, and a host `view`
+    (nsub, nk, nj, pitch) that is downloaded on first access after a stencil wrote the
+    field and uploaded before the next stencil that reads it (every view access marks the
+    host copy as the newer one)."""
+
+    def __init__(self, factory, name, dims, units, nk):
+        self.f, self.name, self.dims, self.units, self.nk = factory, name, tuple(dims), units, nk
+        factory.domain.create(name, nk)
+        self._host = None
+        self._host_newer = False
+
+    @property
+    def view(self):
+        if self._host is None:
+            self._host = self.f.domain.download(self.name)
+        self._host_newer = True
+        return self._host
+
+    @property
+    def data(self):
+        return self.view
+
+    def compute(self):
+        """compute-domain copy indexed [s, k, j, i] (staggered dims +1)"""
+        d = self.f.domain
+        sx = 1 if X_INTERFACE_DIM in self.dims else 0
+        sy = 1 if Y_INTERFACE_DIM in self.dims else 0
+        return self.view[..., NG:NG + d.ny + sy, NG:NG + d.nx + sx].copy()
+
+    def _sync_to_device(self):
+        if self._host_newer:
+            self.f.domain.upload(self.name, self._host)
+            self._host_newer = False
+
+    def _device_written(self):
+        self._host = None
+        self._host_newer = False
+
+
+class DeviceQuantityFactory:
+    def __init__(self, sf: "CubedSphereStencilFactory"):
+        self.sf = sf
+        self._n = 0
+
+    def zeros(self, dims, units, dtype=np.float64, nk=None):
+        if dtype != np.float64:
+            raise TypeError("device quantities are fp64")
+        d = self.sf.domain
+        if nk is None:
+            nk = 1 if Z_DIM not in dims and Z_INTERFACE_DIM not in dims else \
+                (d.npz + 1 if Z_INTERFACE_DIM in dims else d.npz)
+        self._n += 1
+        return DeviceQuantity(self.sf, f"_q{self._n}_{units.replace('/', '_')}", dims, units, nk)
+
+
+class DeviceStencil:
+    def __init__(self, sf, sdef, compute_dims):
+        if not isinstance(sdef, StencilDef):
+            raise TypeError("from_dims_halo: func must be a StencilDef of the HIP library")
+        self.sf, self.sdef, self.compute_dims = sf, sdef, tuple(compute_dims)
+
+    def __call__(self, *args, **params):
+        sd = self.sdef
+        if len(args) != sd.nargs:
+            raise TypeError(f"{sd.name}: expected {sd.nargs} fields, got {len(args)}")
+        names = []
+        for a in args:
+            if a is None:
+                names.append("-")  # optional field (e.g. fv_tp_2d without mass fluxes)
+                continue
+            if not isinstance(a, DeviceQuantity):
+                raise TypeError(f"{sd.name}: arguments are DeviceQuantity objects of this factory")
+            a._sync_to_device()
+            names.append(a.name)
+        missing = [k for k in sd.params if k not in params]
+        if missing:
+            raise TypeError(f"{sd.name}: missing parameters {missing}")
+        self.sf.domain.stencil(sd.name, names, [float(params[k]) for k in sd.params])
+        for n in sd.outputs:
+            if args[n] is not None:
+                args[n]._device_written()
+
+
+class CubedSphereStencilFactory:
+    """All tiles of a cubed sphere on the current GPU; stencils run on every sub-domain."""
+
+    def __init__(self, npx, npz, nq=1, layout=(1, 1)):
+        self.domain = Domain(npx=npx, npz=npz, nq=nq, layout_x=layout[0], layout_y=layout[1])
+
+    def from_dims_halo(self, func, compute_dims, compute_halos=()):
+        return DeviceStencil(self, func, compute_dims)
+
+    def close(self):
+        self.domain.close()
+
+
+def get_factories_cubed_sphere(npx: int, npz: int, nq: int = 1, layout=(1, 1)):
+    """(stencil factory, quantity factory) for device-resident dycore stencils on all six
+    tiles (sub-domain layout per tile), the NDSL surface of pyFV3's DynamicalCore pieces."""
+    sf = CubedSphereStencilFactory(npx, npz, nq, layout)
+    return sf, DeviceQuantityFactory(sf)
 
 
 def orchestrate(obj=None, config=None):
