@@ -49,7 +49,7 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
   for (hipEvent_t* e : {&ev_fork, &ev_b, &ev_c}) HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   {
     const char* e = std::getenv("GTFV3_STREAMS");
-    fork_substep = e ? e[0] == '1' : nranks > 1;
+    fork_substep = e ? e[0] == '1' : true;
   }
   HIP_CHECK(hipMalloc(&dsubs, sizeof(SubInfo) * d.nsub));
   HIP_CHECK(hipMemcpy(dsubs, hsubs.data(), sizeof(SubInfo) * d.nsub, hipMemcpyHostToDevice));
@@ -479,9 +479,22 @@ void Dycore::step() {
   halo_update({{"zh", 'c'}});
   for (int it = 0; it < nl.n_split; ++it) {
     const bool last = it == nl.n_split - 1;
-    c_sw(c, ca);
+    c_sw_transport(c, ca);
+    // c_sw's wind stage (vorticity, uc / vc) beside update_dz_c + riem_solver_c: they share
+    // no field; joined before p_grad_c, which needs both
+    if (fork_substep) {
+      HIP_CHECK(hipEventRecord(ev_fork, st));
+      HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
+      Ctx cb = c;
+      cb.st = st_b;
+      c_sw_winds(cb, ca);
+      HIP_CHECK(hipEventRecord(ev_b, st_b));
+    } else {
+      c_sw_winds(c, ca);
+    }
     update_dz_c(c, npz, dp_ref, ca.ut, ca.vt, zh, gzc);
     riem_solver_c(c, npz, dt2, ptop, nl.p_fac, nl.dz_min, ca.delpc, ca.ptc, ca.wc, phis.p, gzc, pef, nsc);
+    if (fork_substep) HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
     p_grad_c(c, npz, dt2, ca.delpc, pef, gzc, uc, vc);
     // one value per shared tile-edge point: the east / north edges take the C-grid winds
     // the neighbouring tile computed there (otherwise the two tiles' winds differ next to
@@ -491,10 +504,9 @@ void Dycore::step() {
     halo_update({{"uc", 'C'}, {"vc", 'C'}});
     // fork: after the Courant numbers, the wind stage of d_sw (stream b) and update_dz_d
     // (stream c) run beside the mass / thermodynamic transport and its halo update (the
-    // RCCL exchange of delp / pt then overlaps compute).  Multi-rank runs only (or
-    // GTFV3_STREAMS=1): on one GPU the C180 kernels fill the chip by themselves (the fork
-    // gained 0.6 %) and concurrent kernels would stretch the per-kernel event times the
-    // roofline line is built from.
+    // RCCL exchange of delp / pt then overlaps compute).  Default on (GTFV3_STREAMS=0: one
+    // stream): with the thermo march at one or two waves per SIMD the side streams fill
+    // the chip -- C180 on one GPU 43.8 -> 42.4 ms per step.
     d_sw_courant(c, da);
     if (!fork_substep) {
       d_sw_thermo(c, da);

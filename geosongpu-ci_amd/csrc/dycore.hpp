@@ -45,7 +45,7 @@ class Dycore {
   // its thermodynamic transport (fork after the Courant numbers, join before riem_solver3)
   hipStream_t st_b = nullptr, st_c = nullptr;
   hipEvent_t ev_fork = nullptr, ev_b = nullptr, ev_c = nullptr;
-  bool fork_substep = false;  // multi-rank runs (or GTFV3_STREAMS=1)
+  bool fork_substep = true;  // GTFV3_STREAMS=0: one stream
   std::unique_ptr<Transport> comm;  // null for one rank
   std::map<std::string, Field> fields;
   std::vector<double> ak, bk;  // npz+1

@@ -13,7 +13,9 @@ struct CswArgs {
   double *delpc, *ptc, *wc;
   double *utmp, *vtmp, *ke, *vort;  // scratch
 };
-void c_sw(const Ctx& c, const CswArgs& a);
+void c_sw(const Ctx& c, const CswArgs& a);            // the two stages in order
+void c_sw_transport(const Ctx& c, const CswArgs& a);  // d2a2c_vect, delpc / ptc / wc, ke
+void c_sw_winds(const Ctx& c, const CswArgs& a);      // vorticity, uc / vc update
 
 struct DswArgs {
   int npz;

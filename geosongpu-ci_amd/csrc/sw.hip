@@ -596,6 +596,13 @@ inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
 }  // namespace
 
 void c_sw(const Ctx& c, const CswArgs& a) {
+  c_sw_transport(c, a);
+  c_sw_winds(c, a);
+}
+
+// c_sw first stage: d2a2c_vect (uc, vc, ua, va, ut, vt), the half-step transport (delpc,
+// ptc, wc) and the kinetic energy
+void c_sw_transport(const Ctx& c, const CswArgs& a) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
@@ -616,6 +623,15 @@ void c_sw(const Ctx& c, const CswArgs& a) {
                      a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke);
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (9 * e.C + 3 * e.X + 3 * e.Y) + 9 * e.C);
+}
+
+// c_sw second stage: vorticity and the time-centred C-grid winds (touches uc, vc, vort and
+// reads ke: independent of update_dz_c / riem_solver_c, which may run beside it)
+void c_sw_winds(const Ctx& c, const CswArgs& a) {
+  const Dims& d = c.d;
+  const int nz = d.nsub * a.npz;
+  const Ext e = ext(d);
+  const double L = a.npz;
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
   GT_LAUNCH(cs_vort, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.vort);
   HIP_LAUNCH_CHECK();
