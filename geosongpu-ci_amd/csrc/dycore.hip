@@ -548,15 +548,29 @@ void Dycore::step() {
   }
   HIP_CHECK(hipEventRecord(ev[1], st));
 
-  // ---- tracer transport with the accumulated mass fluxes ----
-  tracer_2d(nq, mdt);
+  // ---- tracer transport with the accumulated mass fluxes, beside the remap of T_v, delz,
+  // w and the winds (which touch none of the tracer step's fields); the tracer remap and
+  // the remap's finish wait for both ----
+  RemapScratch rsc;
+  for (int n = 0; n < 3; ++n) rsc.s[n] = S(("_rmj" + std::to_string(n)).c_str(), remap_scratch_slots(nq) * k1);
+  if (fork_substep) {
+    HIP_CHECK(hipEventRecord(ev_fork, st));
+    HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
+    std::swap(st, st_b);  // tracer_2d enqueues (kernels, halo updates, copies) on the side stream
+    tracer_2d(nq, mdt);
+    std::swap(st, st_b);
+    HIP_CHECK(hipEventRecord(ev_b, st_b));
+    RemapState rs1{pe, peln, pk, pkz, delp.p, delz.p, pt.p, w.p, q.p, u.p, v.p, ps, ws};
+    lagrangian_to_eulerian(c, npz, nq, ptop, nl.fill != 0, ak_dev, bk_dev, rs1, rsc, 0, 1);
+    HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
+  } else {
+    tracer_2d(nq, mdt);
+  }
   HIP_CHECK(hipEventRecord(ev[2], st));
 
   // ---- vertical remap to the hybrid Eulerian coordinate ----
   RemapState rs{pe, peln, pk, pkz, delp.p, delz.p, pt.p, w.p, q.p, u.p, v.p, ps, ws};
-  RemapScratch rsc;
-  for (int n = 0; n < 3; ++n) rsc.s[n] = S(("_rmj" + std::to_string(n)).c_str(), remap_scratch_slots(nq) * k1);
-  lagrangian_to_eulerian(c, npz, nq, ptop, nl.fill != 0, ak_dev, bk_dev, rs, rsc);
+  lagrangian_to_eulerian(c, npz, nq, ptop, nl.fill != 0, ak_dev, bk_dev, rs, rsc, 0, fork_substep ? 2 : 0);
   HIP_CHECK(hipEventRecord(ev[3], st));
 
   // ---- exit: T, omega, A-grid winds ----

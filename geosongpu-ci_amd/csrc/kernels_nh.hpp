@@ -71,6 +71,7 @@ int remap_scratch_slots(int nq);  // scratch column sets (jobs run in chunks of 
 // variant: 0 = register-resident columns where instantiated (L10/12/20/72), else the
 // scratch-column jobs; 1 = force the scratch-column jobs (remap_job_k, the bitwise reference)
 void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fill, const double* ak_dev,
-                            const double* bk_dev, const RemapState& S, const RemapScratch& R, int variant = 0);
+                            const double* bk_dev, const RemapState& S, const RemapScratch& R, int variant = 0,
+                            int phase = 0);  // 1: prep + T_v/delz/w/winds, 2: tracers + finish
 
 }  // namespace gtfv3

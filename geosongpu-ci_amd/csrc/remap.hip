@@ -847,8 +847,12 @@ constexpr int RM_CHUNK = 8;
 int remap_scratch_slots(int nq) { return std::min(remap_jobs(nq), RM_CHUNK); }
 
 void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fill, const double* ak_dev,
-                            const double* bk_dev, const RemapState& S, const RemapScratch& R, int variant) {
+                            const double* bk_dev, const RemapState& S, const RemapScratch& R, int variant,
+                            int phase) {
   if (npz < 6) throw std::runtime_error("remap: npz >= 6 required");
+  // phase 1: prep and the T_v / delz / w / wind jobs; phase 2: the tracer jobs and the
+  // finish (so the tracer transport can run beside phase 1); 0: both
+  const bool p1 = phase != 2, p2 = phase != 1;
   const Dims& d = c.d;
   RemapArgs a{};
   a.d = d;
@@ -866,11 +870,13 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
   a.gs = R.s[1];
   a.src = R.s[2];
   const int nc = d.nx * d.ny, nce = (d.nx + 1) * (d.ny + 1);
-  GT_LAUNCH(remap_prep_k, dim3(cdiv(nc, BLOCK), d.nsub), dim3(BLOCK), 0, c.st, a);
-  HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   const double L = npz, L1 = npz + 1;
-  gt_bytes(L * 5 * e.C);  // delp delz pt read, T_v and -delz/delp source columns written
+  if (p1) {
+    GT_LAUNCH(remap_prep_k, dim3(cdiv(nc, BLOCK), d.nsub), dim3(BLOCK), 0, c.st, a);
+    HIP_LAUNCH_CHECK();
+    gt_bytes(L * 5 * e.C);  // delp delz pt read, T_v and -delz/delp source columns written
+  }
   // register-resident columns for the instantiated level counts (L72 of the benchmark and
   // the L10 / L12 / L20 test configurations), the scratch-column jobs otherwise (L137)
   const bool reg = variant != 1 && (npz == 72 || npz == 10 || npz == 12 || npz == 20);
@@ -880,16 +886,20 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
       constexpr int KM = decltype(KMc)::value, CH = decltype(CHc)::value;
       // per launch: each job's source column read and its field written (L levels), the
       // source pressures (pe, + peln for T_v; winds: pe of both neighbours) read once
-      GT_LAUNCH((remap_reg_k<KM, JK_PT, CH>), dim3(gx, 1, d.nsub), dim3(64), 0, c.st, a);
-      gt_bytes(L * 2 * e.C + L1 * 2 * e.C);
-      GT_LAUNCH((remap_reg_k<KM, JK_DZ, CH>), dim3(gx, 1, d.nsub), dim3(64), 0, c.st, a);
-      gt_bytes(L * 2 * e.C + L1 * e.C);
-      GT_LAUNCH((remap_reg_k<KM, JK_W, CH>), dim3(gx, 1, d.nsub), dim3(64), 0, c.st, a);
-      gt_bytes(L * 2 * e.C + L1 * e.C + e.C);
-      GT_LAUNCH((remap_reg_k<KM, JK_UV, CH>), dim3(gx, 2, d.nsub), dim3(64), 0, c.st, a);
-      gt_bytes(L * 2 * (e.X + e.Y) + L1 * e.C);
-      if (nq > 0) GT_LAUNCH((remap_reg_k<KM, JK_Q, CH>), dim3(gx, nq, d.nsub), dim3(64), 0, c.st, a);
-      if (nq > 0) gt_bytes(nq * L * 2 * e.C + L1 * e.C);
+      if (p1) {
+        GT_LAUNCH((remap_reg_k<KM, JK_PT, CH>), dim3(gx, 1, d.nsub), dim3(64), 0, c.st, a);
+        gt_bytes(L * 2 * e.C + L1 * 2 * e.C);
+        GT_LAUNCH((remap_reg_k<KM, JK_DZ, CH>), dim3(gx, 1, d.nsub), dim3(64), 0, c.st, a);
+        gt_bytes(L * 2 * e.C + L1 * e.C);
+        GT_LAUNCH((remap_reg_k<KM, JK_W, CH>), dim3(gx, 1, d.nsub), dim3(64), 0, c.st, a);
+        gt_bytes(L * 2 * e.C + L1 * e.C + e.C);
+        GT_LAUNCH((remap_reg_k<KM, JK_UV, CH>), dim3(gx, 2, d.nsub), dim3(64), 0, c.st, a);
+        gt_bytes(L * 2 * (e.X + e.Y) + L1 * e.C);
+      }
+      if (p2 && nq > 0) {
+        GT_LAUNCH((remap_reg_k<KM, JK_Q, CH>), dim3(gx, nq, d.nsub), dim3(64), 0, c.st, a);
+        gt_bytes(nq * L * 2 * e.C + L1 * e.C);
+      }
     };
     if (npz == 72) go(std::integral_constant<int, 72>{}, std::integral_constant<int, 8>{});
     else if (npz == 10) go(std::integral_constant<int, 10>{}, std::integral_constant<int, 8>{});
@@ -899,14 +909,18 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
     // every job reads its source column and writes its field (L each), pe + peln once, ws;
     // each chunk registers its jobs' share
     const double all = L * 2 * ((a.njob - 2) * e.C + e.X + e.Y) + L1 * 2 * e.C + e.C;
-    for (int j0 = 0; j0 < a.njob; j0 += a.nslot) {
+    // phase 1 the first J_Q0 jobs (T_v, delz, w, u, v: their source slots from the prep),
+    // phase 2 the tracers; within a phase, chunks of nslot jobs share the scratch
+    const int jlo = p1 ? 0 : J_Q0, jhi = p2 ? a.njob : J_Q0;
+    for (int j0 = jlo; j0 < jhi; j0 += a.nslot) {
       a.job0 = j0;
-      const int nj = std::min(a.nslot, a.njob - j0);
+      const int nj = std::min(a.nslot, jhi - j0);
       GT_LAUNCH(remap_job_k, dim3(cdiv(nce, BLOCK), nj, d.nsub), dim3(BLOCK), 0, c.st, a);
       gt_bytes(all * nj / a.njob);
     }
   }
   HIP_LAUNCH_CHECK();
+  if (!p2) return;
   GT_LAUNCH(remap_finish_k, dim3(cdiv(nc, BLOCK), d.nsub), dim3(BLOCK), 0, c.st, a);
   HIP_LAUNCH_CHECK();
   // reads delz pt (L) pe peln (L+1); writes delz delp pkz (L) pk peln pe (L+1) ps
