@@ -47,6 +47,7 @@ DEVICE_SYMBOLS = [
     "gtfv3_halo_remote",
     "gtfv3_kernel_timing",
     "gtfv3_kernel_timing_filter",
+    "gtfv3_set_streams",
     "gtfv3_kernel_stats",
 ]
 
@@ -100,6 +101,7 @@ def lib():
         "gtfv3_halo_remote": (I, [P, I, I, IP, I]),
         "gtfv3_kernel_timing": (I, [P, I]),
         "gtfv3_kernel_timing_filter": (I, [P, ctypes.c_char_p]),
+        "gtfv3_set_streams": (I, [P, I]),
         "gtfv3_kernel_stats": (I, [P, ctypes.c_char_p, I]),
     }
     for name, (res, args) in sig.items():

@@ -332,6 +332,13 @@ int gtfv3_kernel_timing_filter(void* h, const char* kernel) {
   API_CATCH
 }
 
+int gtfv3_set_streams(void* h, int n) {
+  API_TRY
+  if (n != 1 && n != 3) throw std::runtime_error("set_streams: 1 or 3 streams");
+  D(h)->fork_substep = n == 3;
+  API_CATCH
+}
+
 int gtfv3_kernel_stats(void* h, char* buf, int len) {
   API_TRY
   HIP_CHECK(hipStreamSynchronize(D(h)->st));

@@ -40,6 +40,11 @@ constexpr int ZMAX = 65535;
 // results and ran 1.9x slower at C180; removed with the ra_x / ra_y planes it read.)
 constexpr int MW = 64, MOUT = MW - 6, MWAVES = 4;
 constexpr int MAXPAIR = 192;
+// DXL (the thermo march's tile-edge strips): the dxa of the <= 8 tile-edge columns a strip
+// can hold (I = -2 .. 1, N-2 .. N+1) for the segment's rows live in LDS, one region per wave,
+// instead of two dxa loads per row step in the prefetch buffers: 8 fewer VGPRs, which puts
+// the tile-edge kernel at two waves per SIMD without scratch
+constexpr int DXL_ROWS = 64;
 typedef unsigned int TpU2 __attribute__((ext_vector_type(2)));
 
 // NF fields per wave (field group g of a sub-domain = fields g*NF .. g*NF+NF-1, field f
@@ -224,6 +229,25 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   const bool dx_lane = (I >= -2 && I <= 1) || (I >= N - 2 && I <= N + 1);
   const uint32_t vxd = dx_lane ? vx : 0u;
   const uint32_t rowb = (uint32_t)pitch * 8u;
+  constexpr bool DXL = EX && TM == 1;
+  const int r_lo = j0 - NG, r_hi = j1 + 2;
+  // DXL: rows rb .. rb+DXL_ROWS-1 of the tile-edge columns' dxa (every row a step reads:
+  // r_lo-3 .. r_hi+1, clamped to the plane) at sdx[wave][row - rb][slot]
+  __shared__ double sdx[DXL ? MWAVES * DXL_ROWS * 8 : 1];
+  const int rb = r_lo - 3 > -NG ? r_lo - 3 : -NG;
+  const int dslot = I <= 1 ? I + 2 : I - (N - 2) + 4;
+  double* const sdw = sdx + (DXL ? (threadIdx.x / MW) * DXL_ROWS * 8 + dslot : 0);
+  if constexpr (DXL) {
+    const int rt = r_hi + 1 < ny + NG ? r_hi + 1 : ny + NG;
+    if (dx_lane)
+      for (int rr = rb; rr <= rt; ++rr) sdw[(rr - rb) * 8] = dxa[(long)(rr + NG) * pitch + xo];
+    __builtin_amdgcn_wave_barrier();
+  }
+  // dxa of row r (clamped as the loads clamp) for the tile-edge PPM forms
+  auto dxl = [&](int r) {
+    const int rr = r < -NG ? -NG : (r > ny + NG ? ny + NG : r);
+    return dx_lane ? sdw[(rr - rb) * 8] : 0.0;
+  };
   auto bl = [&](__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, voff, soff, 0));
   };
@@ -258,7 +282,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     v.crx = bl(rCRX, vx, so);
     v.xfx = bl(rXFX, vx, so);
     v.area_r = bl(rAR, vx, so);
-    v.dxr = EX ? bl(rDXA, vxd, so) : 0.0;
+    v.dxr = EX && !DXL ? bl(rDXA, vxd, so) : 0.0;
     const int re = r - 2 < -NG ? -NG : r - 2;
     const uint32_t se = (uint32_t)(re + NG) * rowb;
     v.cry = bl(rCRY, vx, se);
@@ -267,7 +291,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     const int rm = r - 3 < -NG ? -NG : r - 3;
     const uint32_t sm = (uint32_t)(rm + NG) * rowb;
     v.mx = MF ? bl(rMX, vx, sm) : 0.0;
-    v.dxm = EX ? bl(rDXA, vxd, sm) : 0.0;
+    v.dxm = EX && !DXL ? bl(rDXA, vxd, sm) : 0.0;
     v.dp1 = TM == 2 ? bl(rDP1, vx, sm) : 0.0;
     return v;
   };
@@ -349,13 +373,13 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
       nxt.crx = bl(rCRX, vx, so);
       nxt.xfx = bl(rXFX, vx, so);
       nxt.area_r = bl(rAR, vx, so);
-      nxt.dxr = EX ? bl(rDXA, vxd, so) : 0.0;
+      nxt.dxr = EX && !DXL ? bl(rDXA, vxd, so) : 0.0;
       const uint32_t se = so - 2 * rowb, sm = so - 3 * rowb;
       nxt.cry = bl(rCRY, vx, se);
       nxt.yfx = bl(rYFX, vx, se);
       nxt.my = MF ? bl(rMY, vx, se) : 0.0;
       nxt.mx = MF ? bl(rMX, vx, sm) : 0.0;
-      nxt.dxm = EX ? bl(rDXA, vxd, sm) : 0.0;
+      nxt.dxm = EX && !DXL ? bl(rDXA, vxd, sm) : 0.0;
       nxt.dp1 = TM == 2 ? bl(rDP1, vx, sm) : 0.0;
   };
   // ahead: how many rows ahead the steady step prefetches (1, or 2 in the three-buffer loop)
@@ -367,10 +391,11 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     const double rax = cur.area_r + cur.xfx - dpp_next(cur.xfx);
     // ---- row r: inner x flux fx2, q_j (per field)
     double fx2[NF], qj[NF];
+    const double dxr = DXL ? dxl(r) : cur.dxr, dxm = DXL ? dxl(r - 3) : cur.dxm;
 #pragma unroll
     for (int f = 0; f < NF; ++f) {
       {
-        const double v = ppm_x_dpp<ORD, EX>(cur.qx[f], cur.dxr, I, N, cur.crx);
+        const double v = ppm_x_dpp<ORD, EX>(cur.qx[f], dxr, I, N, cur.crx);
         const bool ok = GEN ? l_fx2 && r >= -NG && r <= ny + NG - 1 : l_fx2;
         fx2[f] = ok ? v : 0.0;
       }
@@ -453,7 +478,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
         if (rowm) {
           const double v = (qyw[f][0] * arw[0] + fyy_prev[f] - fyy) / ray;
           const double qi = cin ? v : 0.0;
-          const double fo_ = ppm_x_dpp<ORD, EX>(qi, cur.dxm, I, N, hcx[0]);
+          const double fo_ = ppm_x_dpp<ORD, EX>(qi, dxm, I, N, hcx[0]);
           const double mxf = TM == 1 ? (f == 0 ? hxf[0] : fxo[0]) : mx;
           fxo[f] = 0.5 * (fo_ + hf2[f][0]) * mxf;
           if (TM == 0) {
@@ -537,7 +562,6 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   // steady rows: 2 <= G <= N-2 for the y interpolant's interface G = r-1, rows r+1 (the
   // prefetch), r-2, r-3 inside the plane and the tile (no corner fills), edge e = r-2 and
   // row r-3 inside the segment's outputs
-  const int r_lo = j0 - NG, r_hi = j1 + 2;
   int rs0 = j0 + 3, rs1 = j1 + 1;  // [rs0, rs1] candidate steady rows
   rs0 = rs0 > 3 - sub.joff ? rs0 : 3 - sub.joff;
   rs1 = rs1 < N - 2 - sub.joff ? rs1 : N - 2 - sub.joff;
@@ -553,6 +577,12 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   }
   // steady rows whose two-ahead loads stay in the steady range: three rotating buffers,
   // each step prefetching two rows ahead (one more step of HBM latency covered)
+  // steady rows hold no cube-corner fill, so their x- and y-filled q are one value: with
+  // that stated at the loop entry the loop carries one register set for both
+  if (r <= rs1) {
+#pragma unroll
+    for (int f = 0; f < NF; ++f) cur.qy[f] = cur.qx[f];
+  }
   {
     const int lmax = ny + NG - 1 < N - 1 - sub.joff ? ny + NG - 1 : N - 1 - sub.joff;
     const int rs1b = rs1 < lmax - 2 ? rs1 : lmax - 2;
@@ -666,7 +696,7 @@ double ex_fraction(const Ctx& c, int nstrip, std::vector<int>* pex = nullptr, st
 // One march as two kernels: the tile-edge strips (EX forms, AHEAD2, their register count)
 // and the interior strips (A2_IN prefetch depth, OCC_IN workgroups per CU).  Each launch
 // registers its share of the algorithmic bytes.
-template <int ORD, bool MF, int NF, int TM, int OCC_IN, bool A2_IN>
+template <int ORD, bool MF, int NF, int TM, int OCC_IN, bool A2_IN, int OCC_EX = 0, bool A2_EX = true>
 void march2(const Ctx& c, const TpM& m0, double bytes, const char* name_ex, const char* name_in) {
   std::vector<int> pex, pin;
   const double fex = ex_fraction(c, m0.nstrip, &pex, &pin);
@@ -679,7 +709,7 @@ void march2(const Ctx& c, const TpM& m0, double bytes, const char* name_ex, cons
     const long waves = (long)m.ntg * m.nk * m.npair * m.nseg;
     if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
     const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
-    if (ex) GT_LAUNCH_N(name_ex, (tp_march<ORD, true, MF, NF, TM, 0, 1>), g, b, 0, c.st, m);
+    if (ex) GT_LAUNCH_N(name_ex, (tp_march<ORD, A2_EX, MF, NF, TM, OCC_EX, 1>), g, b, 0, c.st, m);
     else GT_LAUNCH_N(name_in, (tp_march<ORD, A2_IN, MF, NF, TM, OCC_IN, 2>), g, b, 0, c.st, m);
     HIP_LAUNCH_CHECK();
   };
@@ -953,13 +983,14 @@ void d_sw_thermo_march(const Ctx& c, const ThermoArgs& a) {
   m.seg = (int)((d.ny + nseg - 1) / nseg);
   m.nstrip = nstrip;
   m.nseg = (d.ny + m.seg - 1) / m.seg;
+  if (m.seg + 10 > DXL_ROWS) throw std::runtime_error("d_sw thermo march: segment longer than the LDS dxa rows");
   // delp w pt read and written, crx cry xfx yfx read, mfx mfy read and written; the
   // interior strips prefetch one row ahead to fit two waves per SIMD (233 VGPRs; the
   // tile-edge form takes 292 with the two-ahead prefetch)
   const Ext e = ext(d);
   const double bytes = 8.0 * a.npz * (6 * e.C + 4 * (e.X + e.Y));
-  if (a.ord == 5) march2<5, true, 3, 1, 2, false>(c, m, bytes, "tp_march_thermo<5, ex>", "tp_march_thermo<5, in>");
-  else march2<6, true, 3, 1, 2, false>(c, m, bytes, "tp_march_thermo<6, ex>", "tp_march_thermo<6, in>");
+  if (a.ord == 5) march2<5, true, 3, 1, 2, false, 2, false>(c, m, bytes, "tp_march_thermo<5, ex>", "tp_march_thermo<5, in>");
+  else march2<6, true, 3, 1, 2, false, 2, false>(c, m, bytes, "tp_march_thermo<6, ex>", "tp_march_thermo<6, in>");
 }
 
 void tracer_prep(const Ctx& c, int npz, const double* cx, const double* cy, double* xfx, double* yfx,

@@ -145,6 +145,10 @@ class Domain:
         """time only `kernel` (its launch name) while timing is on; None: every kernel"""
         check(lib().gtfv3_kernel_timing_filter(self.h, kernel.encode() if kernel else None))
 
+    def set_streams(self, n):
+        """1: every kernel of the step on one stream; 3: the default fork onto side streams"""
+        check(lib().gtfv3_set_streams(self.h, int(n)))
+
     def kernel_stats(self):
         """{kernel: (total_ms, launches, algorithmic_bytes)} since kernel_timing(True)"""
         buf = ctypes.create_string_buffer(1 << 16)

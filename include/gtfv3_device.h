@@ -76,6 +76,9 @@ int gtfv3_timers(void* h, char* buf, int len);
 int gtfv3_kernel_timing(void* h, int on);
 /* time only this kernel family (name without template arguments, e.g. "tp_march"); NULL or "": all */
 int gtfv3_kernel_timing_filter(void* h, const char* kernel);
+/* streams of the step: 1 = every kernel on the library stream; 3 (the default) = c_sw's and
+   d_sw's wind stages, update_dz_d and the tracer transport forked onto two side streams */
+int gtfv3_set_streams(void* h, int n);
 /* per-kernel totals since enabling, "kernel=ms,launches;..." into buf */
 int gtfv3_kernel_stats(void* h, char* buf, int len);
 
