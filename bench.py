@@ -146,8 +146,9 @@ def parse():
     p.add_argument("--roofline-steps", type=int, default=3,
                    help="steps of the single-stream roofline pass after the timed region")
     p.add_argument("--moist", action="store_true",
-                   help="Aquaplanet configuration: nq=6 moist tracers and the moist column step "
-                        "(gfdl_1m) after every fv_dynamics call, inside the timed region")
+                   help="Aquaplanet configuration: nq=6 moist tracers and the moist physics (aer_activation, "
+                        "evap_subl_pdf, GFDL microphysics, radcouple) after every fv_dynamics call, inside the "
+                        "timed region")
     p.add_argument("--geos-log", default="", help="also write a GEOS-style log (geoslog.py) of K individually "
                    "synchronised steps run after the timed region, for tcn.benchmark's parse_geos_log")
     return p.parse_args()
@@ -179,12 +180,11 @@ def cpu_baseline(pkg, npx, npz, nq, dt, moist=False):
     t0 = time.perf_counter()
     out = fvd.fv_dynamics(st, ak, bk, g, nl)
     if moist:
-        from oracle import moist as om
+        from oracle import geos_moist as gm
         for s in range(d.nsub):
-            pe = out["pe"][s]
             q = out["q"][s]
             sp = [q[n * npz:(n + 1) * npz] for n in range(6)]
-            om.gfdl_1m(out["pt"][s], out["delp"][s], out["delz"][s], 0.5 * (pe[1:] + pe[:-1]), *sp, dt)
+            gm.aquaplanet_physics(dt, out["pt"][s], *sp, out["delp"][s], out["delz"][s], out["pe"][s], out["w"][s])
     el = time.perf_counter() - t0
     cells = 6 * d.N * d.N * npz
     d.close()
@@ -367,7 +367,8 @@ def main():
             "vs_baseline": None,
             "dtype": "f64",
             "data": "synthetic (Jablonowski-Williamson baroclinic state on an analytic hybrid L%d grid)" % npz,
-            "config": {"workload": (f"Aquaplanet C{N} L{npz} dycore step + moist column step (gfdl_1m)"
+            "config": {"workload": (f"Aquaplanet C{N} L{npz} dycore step + moist physics (aer_activation, "
+                                    f"evap_subl_pdf, GFDL microphysics, radcouple)"
                                     if a.moist else f"Held-Suarez C{N} L{npz} dycore step (fv_dynamics)") +
                                    f", 6 tiles on {world} MI355X", "npx": N + 1, "npz": npz, "nq": nq,
                        "layout": f"{lx}x{ly}",

@@ -313,26 +313,56 @@ const double* Dycore::vertical_dev() {
 // One fv_dynamics call (FV3 fv_dynamics.F90 / dyn_core.F90 sequence, non-hydrostatic,
 // k_split remap cycles of n_split acoustic sub-steps, tracer_2d_1l, Lagrangian-to-
 // Eulerian remap, then T/omega/A-grid winds for the caller).
-// Aquaplanet moist column step on the device-resident state after
-// fv_dynamics: T = pt, species = tracers 0..5 (qv ql qr qi qs qg), layer pressure from
-// the interfaces pe; surface precipitation accumulates into prec_{rain,snow,graupel,ice}.
+// Aquaplanet moist physics on the device-resident state after
+// fv_dynamics, in the order of GEOS's GFDL_1M run (GFDL_1M.drawio): aerosol activation,
+// the evap_subl_pdf loop (anvil evaporation / sublimation, large-scale PDF condensation),
+// the GFDL cloud microphysics driver, RADCOUPLE.  T = pt, species = tracers 0..5 (qv ql qr
+// qi qs qg; ql / qi are the large-scale condensate), anvil condensate and the cloud
+// fractions in their own fields (qlcn, qicn, clcn, clls), surface precipitation into
+// prec_{rain,snow,graupel,ice}, the radiation's view into rad_*.
 void Dycore::moist_physics(double dt) {
   const int npz = nl.npz, nq = nl.nq;
   if (nq < 6) throw std::runtime_error("moist_physics: needs nq >= 6 (qv ql qr qi qs qg)");
+  Ctx c = ctx();
   Field& q = need("q", nq * npz);
   const long sp = (long)npz * d.plane;  // one species of sub-domain 0
+  const long qsub = (long)nq * npz;
+  double* qv = q.p;
+  double *ql = q.p + sp, *qr = q.p + 2 * sp, *qi = q.p + 3 * sp, *qs = q.p + 4 * sp, *qg = q.p + 5 * sp;
+  double* T = need("pt", npz).p;
+  const double* delz = need("delz", npz).p;
+  auto F = [&](const char* n) { return field(n, npz).p; };
+  double *pl = F("_m_pl"), *zm = F("_m_zm"), *nactl = F("nactl"), *nacti = F("nacti"), *smax = F("_m_smax");
+  double *qlcn = F("qlcn"), *qicn = F("qicn"), *clls = F("clls"), *clcn = F("clcn");
+  moist_prep(c, npz, need("pe", npz + 1).p, delz, pl, zm);
+  aer_activation(c, npz, qsub, pl, T, qv, zm, need("w", npz).p, nactl, nacti, smax);
+  EvapSublArgs e{};
+  e.nk = npz;
+  e.dt = dt;
+  e.T = T; e.qv = qv; e.qlls = ql; e.qils = qi; e.qlcn = qlcn; e.qicn = qicn; e.clls = clls; e.clcn = clcn;
+  e.qv_sub = e.ql_sub = e.qi_sub = qsub;
+  e.pl = pl; e.nactl = nactl; e.nacti = nacti;
+  evap_subl_pdf(c, e);
   Gfdl1mArgs g{};
   g.nk = npz;
-  g.qsub = nq * npz;
+  g.qsub = (int)qsub;
   g.dt = dt;
-  g.T = need("pt", npz).p;
-  g.qv = q.p; g.ql = q.p + sp; g.qr = q.p + 2 * sp; g.qi = q.p + 3 * sp; g.qs = q.p + 4 * sp; g.qg = q.p + 5 * sp;
+  g.T = T;
+  g.qv = qv; g.ql = ql; g.qr = qr; g.qi = qi; g.qs = qs; g.qg = qg;
   g.dp = need("delp", npz).p;
-  g.dz = need("delz", npz).p;
-  g.pe = need("pe", npz + 1).p;
+  g.dz = delz;
+  g.scr = field("_mp_scr", gfdl_mp_scratch_levels(npz)).p;
   g.pr = field("prec_rain", 1).p; g.ps = field("prec_snow", 1).p; g.pg = field("prec_graupel", 1).p;
   g.pi = field("prec_ice", 1).p;
-  gfdl_1m(ctx(), g);
+  gfdl_1m(c, g);
+  RadcoupleArgs r{};
+  r.nk = npz;
+  r.qv_sub = r.ql_sub = r.qi_sub = r.qr_sub = r.qs_sub = r.qg_sub = qsub;
+  r.T = T; r.pl = pl; r.cf = clls; r.af = clcn; r.qv = qv; r.qlls = ql; r.qils = qi; r.qlcn = qlcn; r.qicn = qicn;
+  r.qr = qr; r.qs = qs; r.qg = qg; r.nl = nactl;
+  r.rqv = F("rad_qv"); r.rql = F("rad_ql"); r.rqi = F("rad_qi"); r.rqr = F("rad_qr"); r.rqs = F("rad_qs");
+  r.rqg = F("rad_qg"); r.rcf = F("rad_cf"); r.rrl = F("rad_rl"); r.rri = F("rad_ri");
+  radcouple(c, r);
 }
 
 void Dycore::step() {

@@ -10,16 +10,46 @@ void moist_qsat(const Ctx& c, int nk, const double* t, const double* p, double* 
 // column fill of negative q keeping sum(q dp); fill = -sum(min(q,0) dp)
 void fillq2zero(const Ctx& c, int nk, double* q, const double* dp, double* fill);
 
+// GFDL single-moment cloud microphysics (gfdl_cloud_microphys_driver -> mpdrv per column:
+// neg_adj, terminal_fall with Lagrangian PPM sedimentation + sedi_heat, warm_rain, icloud)
 struct Gfdl1mArgs {
   int nk;
   int qsub = 0;  // levels per sub-domain of the species arrays (0: nk; nq*nk for slices of the tracer array q)
   double dt;
   double *T, *qv, *ql, *qr, *qi, *qs, *qg;  // updated in place
   const double *dp, *dz;                   // delp (Pa), delz (m, < 0)
-  const double *pm = nullptr, *pe = nullptr;  // layer pressure (Pa), or interface pressure (L+1)
+  double* scr;                             // gfdl_mp_scratch_levels(nk) planes per sub-domain
   double *pr, *ps, *pg, *pi;               // surface rain / snow / graupel / ice (kg m-2 per step)
 };
+int gfdl_mp_scratch_levels(int nk);
 void gfdl_1m(const Ctx& c, const Gfdl1mArgs& a);
+
+// GEOS evap_subl_pdf loop: MELTFRZ of anvil and large-scale condensate, EVAP3 / SUBL3 of the
+// anvil condensate, hystpdf large-scale condensation (uniform PDF); all in place
+struct EvapSublArgs {
+  int nk;
+  double dt;
+  double *T, *qv, *qlls, *qils, *qlcn, *qicn, *clls, *clcn;
+  long qv_sub = 0, ql_sub = 0, qi_sub = 0;  // levels per sub-domain of qv / qlls / qils (0: nk)
+  const double *pl, *nactl, *nacti;
+};
+void evap_subl_pdf(const Ctx& c, const EvapSublArgs& a);
+
+// GEOS RADCOUPLE: in-cloud water contents, total cloud fraction and effective radii
+struct RadcoupleArgs {
+  int nk;
+  long qv_sub = 0, ql_sub = 0, qi_sub = 0, qr_sub = 0, qs_sub = 0, qg_sub = 0;
+  const double *T, *pl, *cf, *af, *qv, *qlls, *qils, *qlcn, *qicn, *qr, *qs, *qg, *nl;
+  double *rqv, *rql, *rqi, *rqr, *rqs, *rqg, *rcf, *rrl, *rri;
+};
+void radcouple(const Ctx& c, const RadcoupleArgs& a);
+
+// aerosol activation (Abdul-Razzak & Ghan 2000, three lognormal modes) and ice nuclei
+void aer_activation(const Ctx& c, int nk, long qv_sub, const double* pl, const double* t, const double* qv,
+                    const double* zm, const double* w, double* nactl, double* nacti, double* smax);
+
+// layer pressure from the interfaces pe and layer-mid heights from delz (surface at 0)
+void moist_prep(const Ctx& c, int nk, const double* pe, const double* dz, double* pl, double* zm);
 
 // parcel buoyancy (per level), CAPE, CIN and the LCL level index (-1: none)
 void buoyancy(const Ctx& c, int nk, const double* t, const double* qv, const double* pm, const double* zm,

@@ -1,21 +1,20 @@
 // moist.hip — moist column physics for gfx950.
 //
-// The GEOS moist schemes the Aquaplanet configuration runs (GFDL 1M driver chain,
+// The GEOS moist schemes the Aquaplanet configuration runs (GFDL_1M run sequence:
+// aer_activation, the evap_subl_pdf loop, gfdl_cloud_microphys_driver, RADCOUPLE;
 // buoyancy, fillq2zero: geos_documentation/moist/GFDL_1M.drawio:70-618,
-// experiments.yaml:42-110) live outside the reference; these kernels restate the
-// published algorithms (Lin et al. 1983, Chen & Lin 2013, Kessler 1969, Klemp &
-// Wilhelmson 1978; GFDL MP qs_table / implicit_fall) — oracle/moist.py holds the same
-// expressions in numpy, parity unpinned by reference data.
+// experiments.yaml:42-110) live outside the reference.  The oracles restate the published
+// algorithms independently of this file (oracle/gfdl_mp.py: Lin et al. 1983, Chen & Lin
+// 2013, Zhou et al. 2019; oracle/geos_moist.py: Abdul-Razzak & Ghan 2000, Wyser 1998, ...)
+// and these kernels follow them expression by expression; parity unpinned by reference data.
 //
-// Decomposition: the K axis is never split; one lane per column,
-// i-fastest, so every level access of a wavefront is one coalesced 64-wide row.  The
-// whole GFDL-style step is ONE top-down pass per column: the implicit sedimentation of
-// each species at level k depends only on the levels above (a carried flux), and every
-// other process is pointwise in the column, so level k is final once it is reached —
-// each field is read once and written once (no column scratch, unlike the dycore's
-// tridiagonal sweeps).  Saturation vapour pressure comes from 0.1 K tables built on the
-// host with the C library's exp/log (bit-identical to the oracle's tables) and read
-// with linear interpolation (GFDL wqs1 / iqs1 style).
+// Decomposition: the K axis is never split.  Column schemes (the GFDL driver,
+// fillq2zero, buoyancy) run one lane per column, i-fastest, so every level access of a
+// wavefront is one coalesced 64-wide row; the GEOS pieces are pointwise, one lane per
+// (column, level).  Saturation vapour pressure comes from 0.1 K tables built on the host
+// with the C library's exp/log (bit-identical to the oracle's tables) and read with linear
+// interpolation (GFDL wqs1 / iqs1 style).
+#include <algorithm>
 #include <cmath>
 #include <map>
 #include <mutex>
@@ -54,14 +53,7 @@ constexpr double TABLE_DT = 0.1;
 constexpr double VCONR = 2503.23638966667, NORMR = 25132741228.7183;
 constexpr double VCONS = 6.6280504, NORMS = 942477796.076938;
 constexpr double VCONG = 87.2382675, NORMG = 5026548245.74367;
-constexpr double RHO_SFC = 1.2;
 constexpr double VR_MIN = 1.0e-3, VR_MAX = 12.0, VS_MAX = 2.0, VG_MAX = 12.0, VI_MAX = 1.0;
-constexpr double QMIN_FALL = 1.0e-8;
-// process constants
-constexpr double C_AUT = 1.0e-3, QL_CRIT = 5.0e-4;  // Kessler autoconversion
-constexpr double C_ACC = 2.2;                       // Kessler accretion
-constexpr double T_HOM = T_ICE - 40.0;              // homogeneous freezing
-constexpr double TAU_DEP = 600.0, TAU_MLT = 600.0;  // deposition / melting relaxation (s)
 
 struct Tables {
   const double *tw, *ti, *dw, *di;
@@ -132,138 +124,710 @@ __global__ void __launch_bounds__(256) fillq2zero_k(Dims d, int nk, double* __re
   fill[(long)s * d.plane + o] = -neg;
 }
 
-// ---- GFDL-1M-style column step (one top-down pass) ----
-struct Fall {  // implicit_fall carry: dd(k-1) * qm(k-1)
-  double carry = 0.0;
-  // new mixing ratio at level k, given the level's mass, fall distance and thickness
-  __device__ __forceinline__ double step(double q, double dp, double dz, double dd) {
-    const double m = q * dp / GRAV;
-    const double qm = (m + carry) / (dz + dd);
-    carry = dd * qm;
-    return qm * dz * GRAV / dp;
-  }
+// ---- GFDL cloud microphysics, one column per lane (oracle/gfdl_mp.py mpdrv) ----
+//
+// The column driver of GEOS's gfdl_cloud_microphys_driver (GFDL_1M.drawio :122-618):
+// ntimes sub-steps of neg_adj, terminal_fall (melting of falling ice species, Lagrangian
+// PPM sedimentation of ice / snow / graupel with sedi_heat), warm_rain (revap_racc half
+// steps around the rain sedimentation, autoconversion) and icloud (+ subgrid_z_proc).
+// Every expression and its operand order follow oracle/gfdl_mp.py.  The sedimentation
+// remap walks the column with data-dependent indices, so its working columns (interface
+// heights, fallen heights, the PPM profile, masses, fluxes) live in HBM scratch planes
+// at the lane's column (coalesced across the wave's consecutive columns), not in
+// registers; everything pointwise streams the fields in place.
+constexpr double CV_AIR = CP_AIR - RDGAS;
+constexpr double CV_VAP = 3.0 * RVGAS;
+constexpr double D0_VAP = CV_VAP - C_LIQ;
+constexpr double DC_ICE = C_LIQ - C_ICE;
+constexpr double LV00 = HLV - D0_VAP * T_ICE;
+constexpr double LI00 = HLF - DC_ICE * T_ICE;
+constexpr double SFCRHO = 1.2;
+constexpr double QI0_CRIT = 1.0e-4, QS0_CRIT = 1.0e-3;
+constexpr double C_PSACI = 0.02, C_PAUT = 0.55, QL0_AUT = 5.0e-4;
+constexpr double T_WFR = T_ICE - 40.0;
+constexpr double QRMIN = 1.0e-8, QCMIN = 1.0e-12, QVMIN = 1.0e-20;
+constexpr double DZ_MIN_FALL = 1.0e-2;
+constexpr double TAU_I2S = 1000.0;
+constexpr double MP_R3 = 1.0 / 3.0, MP_R23 = 2.0 / 3.0;
+constexpr int MP_NSCR = 12;  // scratch columns of nk+1 levels per sub-domain
+
+// host-computed coefficients (oracle/gfdl_mp.py module constants; exp(-dts / tau) factors)
+struct MpConst {
+  double cracw, csacw, cgacw, crevp[5];
+  double e_imlt, e_smlt, e_gmlt, e_l2v, e_v2l, e_i2v;
 };
 
-struct M1Args {
+struct MpArgs {
   Dims d;
-  int nk, qsub;  // levels; levels per sub-domain of the species arrays (nk, or nq*nk in q)
-  double dt;
+  int nk, qsub, ntimes;
+  double dts;
   Tables tb;
+  MpConst k;
   double *T, *qv, *ql, *qr, *qi, *qs, *qg;
-  const double *dp, *dz, *pm, *pe;  // pm null: layer pressure from the interfaces pe (L+1)
+  const double *dp, *dz;
+  double* scr;  // MP_NSCR * (nk+1) planes per sub-domain
   double *pr, *ps, *pg, *pi;
 };
 
-__global__ void __launch_bounds__(256) gfdl_1m_k(M1Args a) {
+// strided column
+struct MCol {
+  double* p;
+  long st;
+  __device__ __forceinline__ double& operator[](int k) const { return p[(long)k * st]; }
+};
+
+__device__ __forceinline__ double lhl_(double t) { return LV00 + D0_VAP * t; }
+__device__ __forceinline__ double lhi_(double t) { return LI00 + DC_ICE * t; }
+__device__ __forceinline__ double cvm_(double qv, double ql, double qr, double qi, double qs, double qg) {
+  return CV_AIR + qv * CV_VAP + (qr + ql) * C_LIQ + (qi + qs + qg) * C_ICE;
+}
+// density-form saturation mixing ratio and its T derivative (oracle wqs2 / iqs2)
+__device__ __forceinline__ void qs2(const Tables& tb, bool ice, double t, double den, double& q, double& dq) {
+  double es, des;
+  es_lookup(ice ? tb.ti : tb.tw, ice ? tb.di : tb.dw, t, es, des);
+  q = es / (RVGAS * t * den);
+  dq = (des - es / t) / (RVGAS * t * den);
+}
+
+struct MpCol {
+  int nk;
+  MCol t, qv, ql, qr, qi, qs, qg, dp, dz;
+  MCol ze, zt, den, a, aL, aR, a6, gam, qe, qm, m1, qm0;
+  __device__ __forceinline__ double cvm(int k) const { return cvm_(qv[k], ql[k], qr[k], qi[k], qs[k], qg[k]); }
+};
+
+__device__ void mp_neg_adj(const MpCol& c) {
+  const int n = c.nk;
+  for (int k = 0; k < n; ++k) {
+    double t = c.t[k], qv = c.qv[k], ql = c.ql[k], qr = c.qr[k], qi = c.qi[k], qs = c.qs[k], qg = c.qg[k];
+    const double cvm = cvm_(qv, ql, qr, qi, qs, qg);
+    const double lcpk = lhl_(t) / cvm, icpk = lhi_(t) / cvm;
+    if (qi < 0.0) { qs = qs + qi; qi = 0.0; }
+    if (qs < 0.0) { qg = qg + qs; qs = 0.0; }
+    {
+      const double dq = qg < 0.0 ? qg : 0.0;
+      qv = qv + dq;
+      t = t - dq * (lcpk + icpk);
+      if (qg < 0.0) qg = 0.0;
+    }
+    if (qr < 0.0) { ql = ql + qr; qr = 0.0; }
+    {
+      const double dq = ql < 0.0 ? ql : 0.0;
+      qv = qv + dq;
+      t = t - dq * lcpk;
+      if (ql < 0.0) ql = 0.0;
+    }
+    c.t[k] = t; c.qv[k] = qv; c.ql[k] = ql; c.qr[k] = qr; c.qi[k] = qi; c.qs[k] = qs; c.qg[k] = qg;
+  }
+  for (int k = 0; k < n - 1; ++k) {
+    const double q0 = c.qv[k];
+    if (q0 < 0.0) {
+      c.qv[k + 1] = c.qv[k + 1] + q0 * c.dp[k] / c.dp[k + 1];
+      c.qv[k] = 0.0;
+    }
+  }
+  const int k = n - 1;
+  const double qb = c.qv[k], qa = c.qv[k - 1];
+  double dq = fmin(-qb * c.dp[k], qa * c.dp[k - 1]);
+  if (!(qb < 0.0 && qa > 0.0)) dq = 0.0;
+  c.qv[k - 1] = qa - dq / c.dp[k - 1];
+  c.qv[k] = qb + dq / c.dp[k];
+}
+
+// monotone PPM of the per-height amounts a[] on the fallen layers (oracle cs_profile_mono)
+__device__ void mp_cs_profile(const MpCol& c) {
+  const int n = c.nk;
+  const MCol &a = c.a, &q = c.qe, &gam = c.gam;
+  auto dz = [&](int k) { return c.zt[k] - c.zt[k + 1]; };
+  {
+    const double grat = dz(1) / dz(0);
+    const double bet = grat * (grat + 0.5);
+    q[0] = ((grat + grat) * (grat + 1.0) * a[0] + a[1]) / bet;
+    gam[0] = (1.0 + grat * (grat + 1.5)) / bet;
+  }
+  for (int k = 1; k < n; ++k) {
+    const double d4 = dz(k - 1) / dz(k);
+    const double bet = 2.0 + d4 + d4 - gam[k - 1];
+    q[k] = (3.0 * (a[k - 1] + d4 * a[k]) - q[k - 1]) / bet;
+    gam[k] = d4 / bet;
+  }
+  {
+    const double d4 = dz(n - 2) / dz(n - 1);
+    const double a_bot = 1.0 + d4 * (d4 + 1.5);
+    q[n] = (2.0 * d4 * (d4 + 1.0) * a[n - 1] + a[n - 2] - a_bot * q[n - 1]) / (d4 * (d4 + 0.5) - a_bot * gam[n - 1]);
+  }
+  for (int k = n - 1; k >= 0; --k) q[k] = q[k] - gam[k] * q[k + 1];
+  for (int k = 1; k < n; ++k) q[k] = fmin(fmax(q[k], fmin(a[k - 1], a[k])), fmax(a[k - 1], a[k]));
+  q[0] = fmax(q[0], 0.0);
+  q[n] = fmax(q[n], 0.0);
+  for (int k = 0; k < n; ++k) {
+    double aL = q[k], aR = q[k + 1], a6;
+    const double av = a[k];
+    const double da1 = aR - aL;
+    if ((av - aL) * (av - aR) >= 0.0) {
+      aL = av; aR = av; a6 = 0.0;
+    } else {
+      a6 = 3.0 * (2.0 * av - (aL + aR));
+      if (a6 * da1 < -da1 * da1) {
+        a6 = 3.0 * (aL - av);
+        aR = aL - a6;
+      } else if (a6 * da1 > da1 * da1) {
+        a6 = 3.0 * (aR - av);
+        aL = aR - a6;
+      }
+    }
+    c.aL[k] = aL; c.aR[k] = aR; c.a6[k] = a6;
+  }
+}
+
+// fallen interface heights (oracle fallen_edges), vt[k] held in c.qm for the call
+__device__ void mp_fallen_edges(const MpCol& c, double dts) {
+  const int n = c.nk;
+  const MCol& vt = c.qm;
+  c.zt[0] = c.ze[0];
+  for (int k = 1; k < n; ++k) c.zt[k] = c.ze[k] - 0.5 * dts * (vt[k - 1] + vt[k]);
+  c.zt[n] = c.ze[n] - dts * vt[n - 1];
+  for (int k = 0; k < n; ++k)
+    if (c.zt[k + 1] >= c.zt[k]) c.zt[k + 1] = c.zt[k] - DZ_MIN_FALL;
+}
+
+// Lagrangian sedimentation of species q (oracle lagrangian_fall_ppm); the flux out of the
+// bottom of each layer in c.m1; returns m1[n-1]
+__device__ double mp_lagrangian_fall(const MpCol& c, const MCol& q) {
+  const int n = c.nk;
+  for (int k = 0; k < n; ++k) {
+    const double m0 = q[k] * c.dp[k];
+    c.qm0[k] = m0;
+    c.a[k] = m0 / (c.zt[k] - c.zt[k + 1]);
+  }
+  mp_cs_profile(c);
+  int k0 = 0;
+  for (int k = 0; k < n; ++k) {
+    const double top = c.ze[k], bot = c.ze[k + 1];
+    double qmk = 0.0;
+    for (int m = k0; m < n; ++m) {
+      const double ztm = c.zt[m], ztm1 = c.zt[m + 1];
+      if (top <= ztm && top >= ztm1) {
+        const double dzm = ztm - ztm1;
+        const double pl = (ztm - top) / dzm;
+        const double aL = c.aL[m], aR = c.aR[m], a6 = c.a6[m];
+        if (ztm1 <= bot) {
+          const double pr = (ztm - bot) / dzm;
+          qmk = (aL + 0.5 * (a6 + aR - aL) * (pr + pl) - a6 * MP_R3 * (pr * (pr + pl) + pl * pl)) * (top - bot);
+          k0 = m;
+        } else {
+          double s = (top - ztm1) * (aL + 0.5 * (a6 + aR - aL) * (1.0 + pl) - a6 * (MP_R3 * (1.0 + pl * (1.0 + pl))));
+          for (int mm = m + 1; mm < n; ++mm) {
+            const double zb = c.zt[mm + 1];
+            if (bot < zb) {
+              s = s + c.qm0[mm];
+            } else {
+              const double dzz = c.zt[mm] - bot;
+              const double esl = dzz / (c.zt[mm] - zb);
+              s = s + dzz * (c.aL[mm] + 0.5 * esl * (c.aR[mm] - c.aL[mm] + c.a6[mm] * (1.0 - MP_R23 * esl)));
+              k0 = mm;
+              break;
+            }
+          }
+          qmk = s;
+        }
+        break;
+      }
+    }
+    c.qm[k] = qmk;
+  }
+  double acc = 0.0;
+  for (int k = 0; k < n; ++k) {
+    acc = acc + c.qm0[k] - c.qm[k];
+    c.m1[k] = acc;
+    q[k] = c.qm[k] / c.dp[k];
+  }
+  return acc;
+}
+
+__device__ void mp_sedi_heat(const MpCol& c, double cw) {
+  for (int k = 1; k < c.nk; ++k) {
+    const double dgz = -0.5 * GRAV * c.dz[k];
+    const double cv0 = c.dp[k] * c.cvm(k) + cw * (c.m1[k] - c.m1[k - 1]);
+    c.t[k] = (cv0 * c.t[k] + c.m1[k - 1] * (cw * c.t[k - 1] + dgz)) / (cv0 + cw * c.m1[k - 1]);
+  }
+}
+
+__device__ void mp_terminal_fall(const MpCol& c, const MpConst& kc, double dts, double& pi_, double& ps_,
+                                 double& pg_) {
+  const int n = c.nk;
+  for (int k = 0; k < n; ++k) {
+    if (c.t[k] > T_ICE) {
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        const double fq = w == 0 ? kc.e_imlt : (w == 1 ? kc.e_smlt : kc.e_gmlt);
+        const MCol& q = w == 0 ? c.qi : (w == 1 ? c.qs : c.qg);
+        const double cvm = c.cvm(k);
+        const double t = c.t[k];
+        const double icpk = lhi_(t) / cvm;
+        const double mlt = fmin(fq * q[k], (t - T_ICE) / icpk);
+        if (mlt > 0.0) {
+          q[k] = q[k] - mlt;
+          if (w == 0) c.ql[k] = c.ql[k] + mlt;
+          else c.qr[k] = c.qr[k] + mlt;
+          c.t[k] = t - mlt * icpk;
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int w = 0; w < 3; ++w) {
+    double& out = w == 0 ? pi_ : (w == 1 ? ps_ : pg_);
+    const MCol& q = w == 0 ? c.qi : (w == 1 ? c.qs : c.qg);
+    bool any = false;
+    for (int k = 0; k < n; ++k) any = any || q[k] > QCMIN;
+    if (!any) {
+      out = 0.0;
+      continue;
+    }
+    // fall speeds (oracle fall_speed), into the qm column for mp_fallen_edges
+    for (int k = 0; k < n; ++k) {
+      const double den = c.den[k], qq = q[k];
+      const double rhof = sqrt(fmin(10.0, SFCRHO / den));
+      const double q_ = fmax(qq, QCMIN);
+      double v;
+      if (w == 0) v = qq > QCMIN ? fmin(VI_MAX, 3.29 * exp(0.16 * log(q_ * den))) : 0.0;
+      else if (w == 1) v = qq > QCMIN ? fmin(VS_MAX, VCONS * rhof * exp(0.0625 * log(q_ * den / NORMS))) : 0.0;
+      else v = qq > QCMIN ? fmin(VG_MAX, VCONG * rhof * sqrt(sqrt(sqrt(q_ * den / NORMG)))) : 0.0;
+      c.qm[k] = v;
+    }
+    mp_fallen_edges(c, dts);
+    const double m = mp_lagrangian_fall(c, q);
+    mp_sedi_heat(c, C_ICE);
+    out = m / GRAV;
+  }
+}
+
+__device__ void mp_revap_racc(const Tables& tb, const MpConst& kc, double dt, double den, double& t, double& qv,
+                              double& ql, double& qr, double qi, double qs, double qg) {
+  const double cvm = cvm_(qv, ql, qr, qi, qs, qg);
+  const double lcpk = lhl_(t) / cvm;
+  double qsat, dqsdt;
+  qs2(tb, false, t, den, qsat, dqsdt);
+  const double dqv = qsat - qv;
+  const double qden = fmax(qr, QRMIN) * den;
+  const double t2 = t * t;
+  const double ev = kc.crevp[0] * t2 * dqv * (kc.crevp[1] * sqrt(qden) + kc.crevp[2] * exp(0.725 * log(qden))) /
+                    (kc.crevp[3] * t2 + kc.crevp[4] * qsat * den);
+  double evap = fmin(fmin(qr, dt * ev), dqv / (1.0 + lcpk * dqsdt));
+  if (!(dqv > QVMIN && qr > QRMIN)) evap = 0.0;
+  qr = qr - evap;
+  qv = qv + evap;
+  t = t - evap * lcpk;
+  const double denfac = sqrt(SFCRHO / den);
+  double sink = dt * denfac * kc.cracw * exp(0.95 * log(fmax(qr, QRMIN) * den));
+  sink = sink / (1.0 + sink) * ql;
+  if (!(qr > QRMIN && ql > QCMIN)) sink = 0.0;
+  ql = ql - sink;
+  qr = qr + sink;
+}
+
+__device__ double mp_warm_rain(const MpCol& c, const Tables& tb, const MpConst& kc, double dts) {
+  const int n = c.nk;
+  const double dt5 = 0.5 * dts;
+  auto revap = [&]() {
+    for (int k = 0; k < n; ++k) {
+      double t = c.t[k], qv = c.qv[k], ql = c.ql[k], qr = c.qr[k];
+      mp_revap_racc(tb, kc, dt5, c.den[k], t, qv, ql, qr, c.qi[k], c.qs[k], c.qg[k]);
+      c.t[k] = t; c.qv[k] = qv; c.ql[k] = ql; c.qr[k] = qr;
+    }
+  };
+  revap();
+  double rain = 0.0;
+  bool any = false;
+  for (int k = 0; k < n; ++k) {
+    const double den = c.den[k], qr = c.qr[k];
+    const double rhof = sqrt(fmin(10.0, SFCRHO / den));
+    const double q_ = fmax(qr, QRMIN);
+    c.qm[k] = qr > QRMIN ? fmin(VR_MAX, fmax(VR_MIN, VCONR * rhof * exp(0.2 * log(q_ * den / NORMR)))) : 0.0;
+    any = any || qr > QRMIN;
+  }
+  if (any) {
+    mp_fallen_edges(c, dts);
+    const double m = mp_lagrangian_fall(c, c.qr);
+    mp_sedi_heat(c, C_LIQ);
+    rain = m / GRAV;
+  }
+  revap();
+  for (int k = 0; k < n; ++k) {
+    const double ql = c.ql[k];
+    const double dq = ql - QL0_AUT;
+    double aut = dts * C_PAUT * 1.0e-3 * dq * dq / (dq + 1.0e-3);
+    aut = dq > 0.0 ? fmin(aut, dq) : 0.0;
+    c.ql[k] = ql - aut;
+    c.qr[k] = c.qr[k] + aut;
+  }
+  return rain;
+}
+
+__device__ void mp_icloud(const Tables& tb, const MpConst& kc, double dts, double den, double& t, double& qv,
+                          double& ql, double& qr, double& qi, double& qs, double& qg) {
+  const double denfac = sqrt(SFCRHO / den);
+  double tc = t - T_ICE;
+  {  // pimlt
+    const double icpk = lhi_(t) / cvm_(qv, ql, qr, qi, qs, qg);
+    double mlt = fmin(qi * kc.e_imlt, fmax(tc, 0.0) / icpk);
+    if (!(tc > 0.0)) mlt = 0.0;
+    qi = qi - mlt; ql = ql + mlt; t = t - mlt * icpk;
+  }
+  {  // pifr
+    const double icpk = lhi_(t) / cvm_(qv, ql, qr, qi, qs, qg);
+    const double frz = t < T_WFR ? ql : 0.0;
+    ql = ql - frz; qi = qi + frz; t = t + frz * icpk;
+  }
+  tc = t - T_ICE;
+  const bool cold = tc < 0.0;
+  {  // psacw
+    const double fac = dts * denfac * kc.csacw * exp(0.8125 * log(fmax(qs, QCMIN) * den));
+    const double psacw = (qs > QCMIN && ql > QCMIN) ? fac / (1.0 + fac) * ql : 0.0;
+    ql = ql - psacw;
+    const double icpk = lhi_(t) / cvm_(qv, ql, qr, qi, qs, qg);
+    qs = qs + (cold ? psacw : 0.0);
+    qr = qr + (cold ? 0.0 : psacw);
+    t = t + (cold ? psacw * icpk : 0.0);
+  }
+  {  // psaut
+    const double qim = QI0_CRIT / den;
+    const double aut = (cold && qi > qim) ? (1.0 - exp(-dts * exp(0.025 * tc) / TAU_I2S)) * (qi - qim) : 0.0;
+    qi = qi - aut; qs = qs + aut;
+  }
+  {  // psaci
+    const double fac = dts * denfac * kc.csacw * C_PSACI * exp(0.05 * tc + 0.8125 * log(fmax(qs, QCMIN) * den));
+    const double saci = (cold && qs > QCMIN && qi > QCMIN) ? fac / (1.0 + fac) * qi : 0.0;
+    qi = qi - saci; qs = qs + saci;
+  }
+  {  // pgaut
+    double gaut = (cold && qs > QS0_CRIT) ? dts * 1.0e-3 * exp(0.09 * tc) * (qs - QS0_CRIT) : 0.0;
+    gaut = fmin(gaut, fmax(qs, 0.0));
+    qs = qs - gaut; qg = qg + gaut;
+  }
+  {  // pgacw
+    const double fac = dts * kc.cgacw * exp(0.875 * log(fmax(qg, QCMIN) * den)) * denfac;
+    const double gacw = (qg > QCMIN && ql > QCMIN) ? fac / (1.0 + fac) * ql : 0.0;
+    ql = ql - gacw;
+    const double icpk = lhi_(t) / cvm_(qv, ql, qr, qi, qs, qg);
+    qg = qg + (cold ? gacw : 0.0);
+    qr = qr + (cold ? 0.0 : gacw);
+    t = t + (cold ? gacw * icpk : 0.0);
+  }
+  for (int w = 0; w < 2; ++w) {  // smlt, gmlt
+    double& q = w == 0 ? qs : qg;
+    const double e = w == 0 ? kc.e_smlt : kc.e_gmlt;
+    const double icpk = lhi_(t) / cvm_(qv, ql, qr, qi, qs, qg);
+    const double tcm = t - T_ICE;
+    double m = fmin(q * e, fmax(tcm, 0.0) / icpk);
+    if (!(tcm > 0.0 && q > QCMIN)) m = 0.0;
+    q = q - m; qr = qr + m; t = t - m * icpk;
+  }
+  // subgrid_z_proc
+  {
+    const double lcpk = lhl_(t) / cvm_(qv, ql, qr, qi, qs, qg);
+    double qsw, dwsdt;
+    qs2(tb, false, t, den, qsw, dwsdt);
+    const double dq0 = (qv - qsw) / (1.0 + lcpk * dwsdt);
+    double cond = dq0 > 0.0 ? dq0 * kc.e_v2l : fmax(dq0 * kc.e_l2v, -ql);
+    if (dq0 > 0.0 && t < T_WFR) cond = 0.0;
+    qv = qv - cond; ql = ql + cond; t = t + cond * lcpk;
+  }
+  const double fdep = kc.e_i2v;
+  {
+    const double tcpk = (lhl_(t) + lhi_(t)) / cvm_(qv, ql, qr, qi, qs, qg);
+    double qsi, dqsidt;
+    qs2(tb, true, t, den, qsi, dqsidt);
+    const double dq = (qv - qsi) / (1.0 + tcpk * dqsidt);
+    double dep = dq > 0.0 ? fdep * dq : fmax(fdep * dq, -qi);
+    if (!(t < T_ICE)) dep = 0.0;
+    qv = qv - dep; qi = qi + dep; t = t + dep * tcpk;
+  }
+  for (int w = 0; w < 2; ++w) {
+    double& q = w == 0 ? qs : qg;
+    const double tcpk = (lhl_(t) + lhi_(t)) / cvm_(qv, ql, qr, qi, qs, qg);
+    double qsi, dqsidt;
+    qs2(tb, true, t, den, qsi, dqsidt);
+    const double dq = (qsi - qv) / (1.0 + tcpk * dqsidt);
+    const double sub = (dq > 0.0 && q > QCMIN) ? fmin(q, fdep * dq) : 0.0;
+    q = q - sub; qv = qv + sub; t = t - sub * tcpk;
+  }
+}
+
+__global__ void __launch_bounds__(256) mpdrv_k(MpArgs a) {
   int s;
   long o;
   if (!col_point(a.d, s, o)) return;
-  const Col3 c{a.d, s, a.nk, o};
-  const double dt = a.dt;
-  const double lcp = HLV / CP_AIR, icp = HLF / CP_AIR, scp = HLS / CP_AIR;
-  const double fdep = 1.0 - exp(-dt / TAU_DEP), fmlt = 1.0 - exp(-dt / TAU_MLT);
-  Fall fi, fs, fg, fr;
-  for (int k = 0; k < a.nk; ++k) {
-    const long x = c.at(k);
-    const long y = ((long)s * a.qsub + k) * a.d.plane + o;  // species
-    double T = a.T[x], qv = a.qv[y], ql = a.ql[y], qr = a.qr[y], qi = a.qi[y], qs = a.qs[y], qg = a.qg[y];
-    double pm;
-    if (a.pm) {
-      pm = a.pm[x];
-    } else {
-      const long e = ((long)s * (a.nk + 1) + k) * a.d.plane + o;
-      pm = 0.5 * (a.pe[e] + a.pe[e + a.d.plane]);
+  const long P = a.d.plane;
+  const int n = a.nk;
+  auto col = [&](double* base, int nkk) { return MCol{base + (long)s * nkk * P + o, P}; };
+  auto ccol = [&](const double* base, int nkk) { return MCol{const_cast<double*>(base) + (long)s * nkk * P + o, P}; };
+  MpCol c;
+  c.nk = n;
+  c.t = col(a.T, n);
+  c.qv = col(a.qv, a.qsub); c.ql = col(a.ql, a.qsub); c.qr = col(a.qr, a.qsub);
+  c.qi = col(a.qi, a.qsub); c.qs = col(a.qs, a.qsub); c.qg = col(a.qg, a.qsub);
+  c.dp = ccol(a.dp, n);
+  c.dz = ccol(a.dz, n);
+  double* sb = a.scr + (long)s * MP_NSCR * (n + 1) * P + o;
+  auto scol = [&](int b) { return MCol{sb + (long)b * (n + 1) * P, P}; };
+  c.ze = scol(0); c.zt = scol(1); c.den = scol(2); c.a = scol(3); c.aL = scol(4); c.aR = scol(5);
+  c.a6 = scol(6); c.gam = scol(7); c.qe = scol(8); c.qm = scol(9); c.m1 = scol(10); c.qm0 = scol(11);
+  c.ze[n] = 0.0;
+  for (int k = n - 1; k >= 0; --k) c.ze[k] = c.ze[k + 1] - c.dz[k];
+  for (int k = 0; k < n; ++k) c.den[k] = -c.dp[k] / (GRAV * c.dz[k]);
+  double prr = 0.0, prs = 0.0, prg = 0.0, pri = 0.0;
+  for (int it = 0; it < a.ntimes; ++it) {
+    mp_neg_adj(c);
+    double pi_, ps_, pg_;
+    mp_terminal_fall(c, a.k, a.dts, pi_, ps_, pg_);
+    const double pr_ = mp_warm_rain(c, a.tb, a.k, a.dts);
+    prr = prr + pr_;
+    prs = prs + ps_;
+    prg = prg + pg_;
+    pri = pri + pi_;
+    for (int k = 0; k < n; ++k) {
+      double t = c.t[k], qv = c.qv[k], ql = c.ql[k], qr = c.qr[k], qi = c.qi[k], qs = c.qs[k], qg = c.qg[k];
+      mp_icloud(a.tb, a.k, a.dts, c.den[k], t, qv, ql, qr, qi, qs, qg);
+      c.t[k] = t; c.qv[k] = qv; c.ql[k] = ql; c.qr[k] = qr; c.qi[k] = qi; c.qs[k] = qs; c.qg[k] = qg;
     }
-    const double dp = a.dp[x], thick = -a.dz[x];
-    // 1. neg_adj
-    {
-      double n;
-      n = fmin(ql, 0.0); qv += n; T -= n * lcp; ql -= n;
-      n = fmin(qr, 0.0); qv += n; T -= n * lcp; qr -= n;
-      n = fmin(qi, 0.0); qv += n; T -= n * scp; qi -= n;
-      n = fmin(qs, 0.0); qv += n; T -= n * scp; qs -= n;
-      n = fmin(qg, 0.0); qv += n; T -= n * scp; qg -= n;
-    }
-    // 2-3. fall speeds, implicit sedimentation (carried from the level above)
-    const double den = dp / (GRAV * thick);
-    const double rhof = sqrt(fmin(10.0, RHO_SFC / den));
-    const double vr = qr > QMIN_FALL
-                          ? fmin(VR_MAX, fmax(VR_MIN, VCONR * rhof * exp(0.2 * log(fmax(qr, QMIN_FALL) * den / NORMR))))
-                          : VR_MIN;
-    const double vs =
-        qs > QMIN_FALL ? fmin(VS_MAX, VCONS * rhof * exp(0.0625 * log(fmax(qs, QMIN_FALL) * den / NORMS))) : 0.0;
-    const double vg =
-        qg > QMIN_FALL ? fmin(VG_MAX, VCONG * rhof * sqrt(sqrt(sqrt(fmax(qg, QMIN_FALL) * den / NORMG)))) : 0.0;
-    const double vi = qi > QMIN_FALL ? fmin(VI_MAX, 3.29 * exp(0.16 * log(fmax(qi, QMIN_FALL) * den))) : 0.0;
-    qi = fi.step(qi, dp, thick, dt * vi);
-    qs = fs.step(qs, dp, thick, dt * vs);
-    qg = fg.step(qg, dp, thick, dt * vg);
-    qr = fr.step(qr, dp, thick, dt * vr);
-    // 4. warm rain
-    const double aut = fmin(ql, dt * C_AUT * fmax(ql - QL_CRIT, 0.0));
-    ql = ql - aut;
-    qr = qr + aut;
-    const double acc = qr > 0.0 ? fmin(ql, dt * C_ACC * ql * exp(0.875 * log(fmax(qr, 1.0e-30)))) : 0.0;
-    ql = ql - acc;
-    qr = qr + acc;
-    double qsw, dqsw;
-    qsat(a.tb, false, T, pm, qsw, dqsw);
-    {
-      const double rq = den * qr;
-      const double cvent = 1.6 + 124.9 * exp(0.2046 * log(fmax(rq, 1.0e-30)));
-      const double erate =
-          (1.0 - qv / qsw) * cvent * exp(0.525 * log(fmax(rq, 1.0e-30))) / (den * (5.4e5 + 2.55e8 / (pm * qsw)));
-      const double evap =
-          (qv < qsw && qr > 0.0) ? fmin(fmin(qr, dt * erate), (qsw - qv) / (1.0 + lcp * dqsw)) : 0.0;
-      qr = qr - evap;
-      qv = qv + evap;
-      T = T - evap * lcp;
-    }
-    // 5. saturation adjustment of cloud water
-    qsat(a.tb, false, T, pm, qsw, dqsw);
-    {
-      double dq = (qv - qsw) / (1.0 + lcp * dqsw);
-      dq = dq > 0.0 ? dq : fmax(dq, -ql);
-      qv = qv - dq;
-      ql = ql + dq;
-      T = T + dq * lcp;
-    }
-    // 6. homogeneous freezing
-    {
-      const double frz = T < T_HOM ? ql : 0.0;
-      ql = ql - frz;
-      qi = qi + frz;
-      T = T + frz * icp;
-    }
-    // 7. ice deposition / sublimation
-    {
-      double qsi, dqsi;
-      qsat(a.tb, true, T, pm, qsi, dqsi);
-      double ddep = fdep * (qv - qsi) / (1.0 + scp * dqsi);
-      ddep = T < T_ICE ? (ddep > 0.0 ? ddep : fmax(ddep, -qi)) : 0.0;
-      qv = qv - ddep;
-      qi = qi + ddep;
-      T = T + ddep * scp;
-    }
-    // 8. melting: ice -> cloud water, snow and graupel -> rain
-    {
-      double cap = fmax(T - T_ICE, 0.0) / icp;
-      double mlt = T > T_ICE ? fmin(fmlt * qi, cap) : 0.0;
-      qi -= mlt; ql = ql + mlt; T = T - mlt * icp;
-      cap = fmax(T - T_ICE, 0.0) / icp;
-      mlt = T > T_ICE ? fmin(fmlt * qs, cap) : 0.0;
-      qs -= mlt; qr = qr + mlt; T = T - mlt * icp;
-      cap = fmax(T - T_ICE, 0.0) / icp;
-      mlt = T > T_ICE ? fmin(fmlt * qg, cap) : 0.0;
-      qg -= mlt; qr = qr + mlt; T = T - mlt * icp;
-    }
-    a.T[x] = T; a.qv[y] = qv; a.ql[y] = ql; a.qr[y] = qr; a.qi[y] = qi; a.qs[y] = qs; a.qg[y] = qg;
   }
-  const long p2 = (long)s * a.d.plane + o;
-  a.pr[p2] = fr.carry;
-  a.ps[p2] = fs.carry;
-  a.pg[p2] = fg.carry;
-  a.pi[p2] = fi.carry;
+  const long p2 = (long)s * P + o;
+  a.pr[p2] = prr;
+  a.ps[p2] = prs;
+  a.pg[p2] = prg;
+  a.pi[p2] = pri;
+}
+
+// ---- GEOS pieces around the microphysics (oracle/geos_moist.py), pointwise ----
+constexpr double RHO_W = 1000.0, RHO_I = 917.0;
+constexpr double K_COND = 2.4e-2, DIFFU = 2.2e-5;
+constexpr double A_EFF_L = 0.8, A_EFF_I = 0.5;
+constexpr double QC_MAX = 0.01;
+constexpr double PI_ = 3.14159265358979323846;
+
+__device__ __forceinline__ double ice_fraction(double t) { return fmin(fmax((T_ICE - t) / 40.0, 0.0), 1.0); }
+__device__ __forceinline__ double rhcrit(double pl) {
+  const double x = fmin(fmax((75000.0 - pl) / 75000.0, 0.0), 1.0);
+  return 0.80 + 0.19 * x * x;
+}
+__device__ double ldradius4(double pl, double t, double qc, double nnl, int itype) {
+  const double rho = pl / (RDGAS * t);
+  const double wc = rho * fmax(qc, 0.0);
+  if (itype == 1) {
+    const double nnx = fmax(nnl, 1.0e7);
+    const double r = 1.1 * cbrt(3.0 * wc / (4.0 * PI_ * RHO_W * nnx));
+    return fmin(60.0e-6, fmax(2.5e-6, r));
+  }
+  const double wcg = fmax(1.0e3 * wc, 1.0e-12);
+  double bb = (t > T_ICE || qc <= 0.0) ? -2.0
+                                       : -2.0 + log10(wcg / 50.0) * (1.0e-3 * pow(fmax(T_ICE - t, 0.0), 1.5));
+  bb = fmin(fmax(bb, -6.0), -2.0);
+  const double r = 377.4 + 203.3 * bb + 37.91 * bb * bb + 2.3696 * bb * bb * bb;
+  return fmin(150.0e-6, fmax(5.0e-6, 1.0e-6 * r));
+}
+
+struct EspArgs {
+  Dims d;
+  int nk;
+  double dt, e_frz, e_mlt;
+  Tables tb;
+  double *T, *qv, *qlls, *qils, *qlcn, *qicn, *clls, *clcn;
+  long qv_sub, ql_sub, qi_sub;  // levels per sub-domain of qv / qlls / qils (tracer slices)
+  const double *pl, *nactl, *nacti;
+};
+
+__device__ __forceinline__ void meltfrz(double e_frz, double e_mlt, double& t, double& ql, double& qi) {
+  const double fqi = ice_fraction(t);
+  const double frz = t <= T_ICE ? ql * fqi * e_frz : 0.0;
+  const double mlt = t > T_ICE ? qi * e_mlt : 0.0;
+  ql = ql + (mlt - frz);
+  qi = qi + (frz - mlt);
+  t = t + (frz - mlt) * (HLF / CP_AIR);
+}
+
+__global__ void __launch_bounds__(256) evap_subl_pdf_k(EspArgs a) {
+  const Dims& d = a.d;
+  const int i = blockIdx.x * BX + threadIdx.x, j = blockIdx.y * BY + threadIdx.y;
+  if (i >= d.nx || j >= d.ny) return;
+  const int z = blockIdx.z, s = z / a.nk, k = z % a.nk;
+  const long o = pidx(d, i, j);
+  const long x = (long)z * d.plane + o;
+  const long xv = ((long)s * a.qv_sub + k) * d.plane + o;
+  const long xl = ((long)s * a.ql_sub + k) * d.plane + o;
+  const long xi = ((long)s * a.qi_sub + k) * d.plane + o;
+  const double pl = a.pl[x], nl = a.nactl[x];
+  double t = a.T[x], qv = a.qv[xv], qlls = a.qlls[xl], qils = a.qils[xi], qlcn = a.qlcn[x], qicn = a.qicn[x];
+  double clls = a.clls[x], clcn = a.clcn[x];
+  const double rhcr = rhcrit(pl);
+  meltfrz(a.e_frz, a.e_mlt, t, qlcn, qicn);
+  meltfrz(a.e_frz, a.e_mlt, t, qlls, qils);
+  {  // evap3 (anvil liquid)
+    double qs, dqs;
+    qsat(a.tb, false, t, pl, qs, dqs);
+    const double es = pl * qs / (EPS + (1.0 - EPS) * qs);
+    const double rhx = fmin(qv / qs, 1.0);
+    const double k1 = HLV * HLV * RHO_W / (K_COND * RVGAS * t * t);
+    const double k2 = RVGAS * t * RHO_W / (DIFFU * (1.0e5 / pl) * es);
+    const double qcm = (clcn > 0.0 && qlcn > 0.0) ? qlcn / clcn : 0.0;
+    const double rad = ldradius4(pl, t, qcm, nl, 1);
+    const double teff = rhx < rhcr ? (rhcr - rhx) / ((k1 + k2) * rad * rad) : 0.0;
+    double ev = fmin(A_EFF_L * qlcn * a.dt * teff, qlcn);
+    if (!(qlcn > 0.0)) ev = 0.0;
+    qv = qv + ev; qlcn = qlcn - ev; t = t - ev * (HLV / CP_AIR);
+  }
+  {  // subl3 (anvil ice)
+    double qs, dqs;
+    qsat(a.tb, true, t, pl, qs, dqs);
+    const double es = pl * qs / (EPS + (1.0 - EPS) * qs);
+    const double rhx = fmin(qv / qs, 1.0);
+    const double k1 = HLS * HLS * RHO_I / (K_COND * RVGAS * t * t);
+    const double k2 = RVGAS * t * RHO_I / (DIFFU * (1.0e5 / pl) * es);
+    const double qcm = (clcn > 0.0 && qicn > 0.0) ? qicn / clcn : 0.0;
+    const double rad = ldradius4(pl, t, qcm, nl, 2);
+    const double teff = rhx < rhcr ? (rhcr - rhx) / ((k1 + k2) * rad * rad) : 0.0;
+    double sb = fmin(A_EFF_I * qicn * a.dt * teff, qicn);
+    if (!(qicn > 0.0)) sb = 0.0;
+    qv = qv + sb; qicn = qicn - sb; t = t - sb * (HLS / CP_AIR);
+  }
+  if (!(qlcn + qicn > 0.0)) clcn = 0.0;
+  for (int it = 0; it < 3; ++it) {  // hystpdf
+    double qs, dqs;
+    qsat(a.tb, false, t, pl, qs, dqs);
+    const double sig = (1.0 - rhcr) * qs;
+    const double qt = qv + qlls + qils;
+    const bool full = qt - sig >= qs, none = qt + sig <= qs;
+    const double cf = full ? 1.0 : (none ? 0.0 : (qt + sig - qs) / (2.0 * sig));
+    const double qcn = full ? qt - qs : (none ? 0.0 : (qt + sig - qs) * (qt + sig - qs) / (4.0 * sig));
+    const double fqi = ice_fraction(t);
+    const double lat = HLV / CP_AIR + fqi * (HLF / CP_AIR);
+    const double dqc = (qcn - (qlls + qils)) / (1.0 + lat * dqs * cf);
+    const double dl = dqc > 0.0 ? dqc * (1.0 - fqi) : fmax(dqc, -qlls);
+    const double di = dqc > 0.0 ? dqc * fqi : fmax(dqc - dl, -qils);
+    qlls = qlls + dl;
+    qils = qils + di;
+    qv = qv - (dl + di);
+    t = t + (dl * (HLV / CP_AIR) + di * (HLS / CP_AIR));
+    clls = cf;
+  }
+  a.T[x] = t; a.qv[xv] = qv; a.qlls[xl] = qlls; a.qils[xi] = qils; a.qlcn[x] = qlcn; a.qicn[x] = qicn;
+  a.clls[x] = clls; a.clcn[x] = clcn;
+}
+
+struct RadArgs {
+  Dims d;
+  int nk;
+  long qv_sub, ql_sub, qi_sub, qr_sub, qs_sub, qg_sub;
+  const double *T, *pl, *cf, *af, *qv, *qlls, *qils, *qlcn, *qicn, *qr, *qs, *qg, *nl;
+  double *rqv, *rql, *rqi, *rqr, *rqs, *rqg, *rcf, *rrl, *rri;
+};
+
+__global__ void __launch_bounds__(256) radcouple_k(RadArgs a) {
+  const Dims& d = a.d;
+  const int i = blockIdx.x * BX + threadIdx.x, j = blockIdx.y * BY + threadIdx.y;
+  if (i >= d.nx || j >= d.ny) return;
+  const int z = blockIdx.z, s = z / a.nk, k = z % a.nk;
+  const long o = pidx(d, i, j);
+  const long x = (long)z * d.plane + o;
+  auto sp = [&](long sub) { return ((long)s * sub + k) * d.plane + o; };
+  double rcf = fmin(fmax(a.cf[x] + a.af[x], 0.0), 1.0);
+  const bool cloudy = rcf >= 1.0e-5;
+  const double div = cloudy ? rcf : 1.0;
+  auto incloud = [&](double v) { return (cloudy && v >= 1.0e-8) ? v / div : 0.0; };
+  const double rql = fmin(incloud(a.qlls[sp(a.ql_sub)] + a.qlcn[x]), QC_MAX);
+  const double rqi = fmin(incloud(a.qils[sp(a.qi_sub)] + a.qicn[x]), QC_MAX);
+  a.rqr[x] = fmin(incloud(a.qr[sp(a.qr_sub)]), QC_MAX);
+  a.rqs[x] = fmin(incloud(a.qs[sp(a.qs_sub)]), QC_MAX);
+  a.rqg[x] = fmin(incloud(a.qg[sp(a.qg_sub)]), QC_MAX);
+  a.rql[x] = rql;
+  a.rqi[x] = rqi;
+  a.rcf[x] = cloudy ? rcf : 0.0;
+  a.rqv[x] = a.qv[sp(a.qv_sub)];
+  const double t = a.T[x], pl = a.pl[x], nl = a.nl[x];
+  a.rrl[x] = ldradius4(pl, t, rql, nl, 1);
+  a.rri[x] = ldradius4(pl, t, rqi, nl, 2);
+}
+
+// Abdul-Razzak & Ghan (2000) activation of three lognormal modes + Meyers (1992) ice nuclei
+struct AerMode {
+  double n0, h, rd, sg, kap;
+};
+__constant__ AerMode c_aer_modes[3] = {{1.0e9, 2000.0, 0.02e-6, 1.6, 0.6},
+                                      {3.0e8, 2000.0, 0.08e-6, 1.8, 0.6},
+                                      {1.0e6, 1000.0, 1.00e-6, 2.0, 1.2}};
+constexpr double MW = 0.018015, MA = 0.028965, RGAS_U = 8.314462618, SURF_T = 0.0761, W_MIN = 0.1;
+
+struct AerArgs {
+  Dims d;
+  int nk;
+  long qv_sub;
+  Tables tb;
+  const double *pl, *T, *qv, *zm, *w;
+  double *nactl, *nacti, *smax;
+};
+
+__global__ void __launch_bounds__(256) aer_activation_k(AerArgs a) {
+  const Dims& d = a.d;
+  const int i = blockIdx.x * BX + threadIdx.x, j = blockIdx.y * BY + threadIdx.y;
+  if (i >= d.nx || j >= d.ny) return;
+  const int z = blockIdx.z, s = z / a.nk, k = z % a.nk;
+  const long o = pidx(d, i, j);
+  const long x = (long)z * d.plane + o;
+  const double pl = a.pl[x], t = a.T[x], zm = a.zm[x];
+  const double qv = a.qv[((long)s * a.qv_sub + k) * d.plane + o];
+  const double wv = fmax(a.w[x], 0.0) + W_MIN;
+  double qs, dqs;
+  qsat(a.tb, false, t, pl, qs, dqs);
+  const double es = pl * qs / (EPS + (1.0 - EPS) * qs);
+  const double a_k = 2.0 * SURF_T * MW / (RHO_W * RGAS_U * t);
+  const double alpha = GRAV * MW * HLV / (CP_AIR * RGAS_U * t * t) - GRAV * MA / (RGAS_U * t);
+  const double gamma = RGAS_U * t / (es * MW) + MW * HLV * HLV / (CP_AIR * pl * MA * t);
+  const double dv = DIFFU * (1.0e5 / pl);
+  const double gg = 1.0 / (RHO_W * RGAS_U * t / (es * dv * MW) + HLV * RHO_W / (K_COND * t) * (HLV * MW / (RGAS_U * t) - 1.0));
+  const double aw = alpha * wv / gg;
+  const double zeta = 2.0 * a_k / 3.0 * sqrt(aw);
+  double ssum = 0.0, sm[3], nn[3], ls[3];
+  for (int m = 0; m < 3; ++m) {
+    const AerMode md = c_aer_modes[m];
+    nn[m] = md.n0 * exp(-fmax(zm, 0.0) / md.h);
+    sm[m] = 2.0 / sqrt(md.kap) * pow(a_k / (3.0 * md.rd), 1.5);
+    ls[m] = log(md.sg);
+    const double eta = pow(aw, 1.5) / (2.0 * PI_ * RHO_W * gamma * nn[m]);
+    const double f = 0.5 * exp(2.5 * ls[m] * ls[m]);
+    const double g = 1.0 + 0.25 * ls[m];
+    ssum = ssum + (f * pow(zeta / eta, 1.5) + g * pow(sm[m] * sm[m] / (eta + 3.0 * zeta), 0.75)) / (sm[m] * sm[m]);
+  }
+  const double smax = 1.0 / sqrt(ssum);
+  double nact = 0.0;
+  for (int m = 0; m < 3; ++m) {
+    const double u = 2.0 * log(sm[m] / smax) / (3.0 * sqrt(2.0) * ls[m]);
+    nact = nact + nn[m] * 0.5 * erfc(u);
+  }
+  double qsi, dqsi;
+  qsat(a.tb, true, t, pl, qsi, dqsi);
+  const double si = fmin(fmax(qv / qsi - 1.0, -0.2), 0.25);
+  a.nactl[x] = nact;
+  a.nacti[x] = t < T_ICE - 5.0 ? 1.0e3 * exp(-0.639 + 12.96 * si) : 0.0;
+  a.smax[x] = smax;
+}
+
+// layer pressure from the interfaces and layer-mid heights from delz (surface at 0)
+__global__ void __launch_bounds__(256) moist_prep_k(Dims d, int nk, const double* __restrict__ pe,
+                                                     const double* __restrict__ dz, double* __restrict__ pl,
+                                                     double* __restrict__ zm) {
+  int s;
+  long o;
+  if (!col_point(d, s, o)) return;
+  const long P = d.plane;
+  const long b = (long)s * nk * P + o, be = (long)s * (nk + 1) * P + o;
+  double zb = 0.0;
+  for (int k = nk - 1; k >= 0; --k) {
+    const double zt = zb - dz[b + k * P];
+    zm[b + k * P] = 0.5 * (zt + zb);
+    pl[b + k * P] = 0.5 * (pe[be + k * P] + pe[be + (k + 1) * P]);
+    zb = zt;
+  }
 }
 
 // ---- buoyancy, CAPE / CIN, LCL index (one bottom-up pass) ----
@@ -347,6 +911,34 @@ Tables device_tables() {
 }
 
 inline dim3 colgrid(const Dims& d) { return dim3(cdiv(d.nx, BX), cdiv(d.ny, BY), d.nsub); }
+inline dim3 ptgrid(const Dims& d, int nk) { return dim3(cdiv(d.nx, BX), cdiv(d.ny, BY), d.nsub * nk); }
+
+// GFDL MP coefficients on the host, as oracle/gfdl_mp.py forms them
+MpConst mp_const(double dts) {
+  const double PIE = 3.14159265358979323846;
+  const double RNZR = 8.0e6, RNZS = 3.0e6, RNZG = 4.0e6, RHOR = 1.0e3, RHOS = 1.0e2, RHOG = 4.0e2;
+  const double ALIN = 842.0, CLIN = 4.8, GCON = 40.74 * std::sqrt(1.2);
+  const double VDIFU = 2.11e-5, TCOND = 2.36e-2, VISK = 1.259e-5;
+  const double ACT_S = PIE * RNZS * RHOS, ACT_R = PIE * RNZR * RHOR, ACT_G = PIE * RNZG * RHOG;
+  const double SCM3 = std::pow(VISK / VDIFU, 1.0 / 3.0);
+  MpConst k{};
+  k.cracw = PIE * RNZR * ALIN * std::tgamma(3.8) / (4.0 * std::pow(ACT_R, 0.95));
+  k.csacw = PIE * RNZS * CLIN * std::tgamma(3.25) / (4.0 * std::pow(ACT_S, 0.8125));
+  k.cgacw = PIE * RNZG * std::tgamma(3.5) * GCON / (4.0 * std::pow(ACT_G, 0.875));
+  k.crevp[0] = 2.0 * PIE * VDIFU * TCOND * RVGAS * RNZR;
+  k.crevp[1] = 0.78 / std::sqrt(ACT_R);
+  k.crevp[2] = 0.31 * SCM3 * std::tgamma(2.9) * std::sqrt(ALIN / VISK) / std::pow(ACT_R, 0.725);
+  k.crevp[3] = TCOND * RVGAS;
+  k.crevp[4] = HLV * HLV * VDIFU;
+  k.e_imlt = 1.0 - std::exp(-dts / 600.0);
+  k.e_smlt = 1.0 - std::exp(-dts / 900.0);
+  k.e_gmlt = 1.0 - std::exp(-dts / 600.0);
+  k.e_l2v = 1.0 - std::exp(-dts / 300.0);
+  k.e_v2l = 1.0 - std::exp(-dts / 150.0);
+  k.e_i2v = 1.0 - std::exp(-dts / 300.0);
+  return k;
+}
+
 
 }  // namespace moist
 
@@ -362,14 +954,55 @@ void fillq2zero(const Ctx& c, int nk, double* q, const double* dp, double* fill)
   HIP_LAUNCH_CHECK();
 }
 
+int gfdl_mp_scratch_levels(int nk) { return moist::MP_NSCR * (nk + 1); }
+
 void gfdl_1m(const Ctx& c, const Gfdl1mArgs& g) {
-  if (!g.pm && !g.pe) throw std::runtime_error("gfdl_1m: layer pressure (pm) or interfaces (pe) required");
-  moist::M1Args a{c.d, g.nk, g.qsub > 0 ? g.qsub : g.nk, g.dt, moist::device_tables(), g.T, g.qv, g.ql, g.qr,
-                  g.qi, g.qs, g.qg, g.dp, g.dz, g.pm, g.pe, g.pr, g.ps, g.pg, g.pi};
-  GT_LAUNCH(moist::gfdl_1m_k, moist::colgrid(c.d), dim3(BX, BY), 0, c.st, a);
+  if (!g.scr) throw std::runtime_error("gfdl_1m: scratch planes required");
+  if (g.nk < 3) throw std::runtime_error("gfdl_1m: nk >= 3 required");
+  const double mp_time = 150.0;
+  const int ntimes = std::max(1, (int)std::ceil(g.dt / mp_time - 1.0e-9));
+  const double dts = g.dt / ntimes;
+  moist::MpArgs a{c.d, g.nk, g.qsub > 0 ? g.qsub : g.nk, ntimes, dts, moist::device_tables(), moist::mp_const(dts),
+                  g.T, g.qv, g.ql, g.qr, g.qi, g.qs, g.qg, g.dp, g.dz, g.scr, g.pr, g.ps, g.pg, g.pi};
+  GT_LAUNCH(moist::mpdrv_k, moist::colgrid(c.d), dim3(BX, BY), 0, c.st, a);
   HIP_LAUNCH_CHECK();
-  // algorithmic bytes: T + 6 species read and written, dp dz pm read (L each), 4 surface fields
-  ktimer_bytes(8.0 * c.d.nx * c.d.ny * c.d.nsub * (17.0 * g.nk + 4.0));
+  // algorithmic bytes: T + 6 species read and written, dp dz read (L each), 4 surface fields
+  ktimer_bytes(8.0 * c.d.nx * c.d.ny * c.d.nsub * (16.0 * g.nk + 4.0));
+}
+
+void evap_subl_pdf(const Ctx& c, const EvapSublArgs& g) {
+  const double e_frz = 1.0 - std::exp(-g.dt / 450.0), e_mlt = 1.0 - std::exp(-g.dt / 450.0);
+  moist::EspArgs a{c.d, g.nk, g.dt, e_frz, e_mlt, moist::device_tables(), g.T, g.qv, g.qlls, g.qils, g.qlcn, g.qicn,
+                   g.clls, g.clcn, g.qv_sub > 0 ? g.qv_sub : g.nk, g.ql_sub > 0 ? g.ql_sub : g.nk,
+                   g.qi_sub > 0 ? g.qi_sub : g.nk, g.pl, g.nactl, g.nacti};
+  GT_LAUNCH(moist::evap_subl_pdf_k, moist::ptgrid(c.d, g.nk), dim3(BX, BY), 0, c.st, a);
+  HIP_LAUNCH_CHECK();
+  // T qv qlls qils qlcn qicn clls clcn read and written, pl nactl read
+  ktimer_bytes(8.0 * c.d.nx * c.d.ny * c.d.nsub * g.nk * 18.0);
+}
+
+void radcouple(const Ctx& c, const RadcoupleArgs& g) {
+  auto sub = [&](long v) { return v > 0 ? v : (long)g.nk; };
+  moist::RadArgs a{c.d, g.nk, sub(g.qv_sub), sub(g.ql_sub), sub(g.qi_sub), sub(g.qr_sub), sub(g.qs_sub), sub(g.qg_sub),
+                   g.T, g.pl, g.cf, g.af, g.qv, g.qlls, g.qils, g.qlcn, g.qicn, g.qr, g.qs, g.qg, g.nl,
+                   g.rqv, g.rql, g.rqi, g.rqr, g.rqs, g.rqg, g.rcf, g.rrl, g.rri};
+  GT_LAUNCH(moist::radcouple_k, moist::ptgrid(c.d, g.nk), dim3(BX, BY), 0, c.st, a);
+  HIP_LAUNCH_CHECK();
+  ktimer_bytes(8.0 * c.d.nx * c.d.ny * c.d.nsub * g.nk * 22.0);
+}
+
+void aer_activation(const Ctx& c, int nk, long qv_sub, const double* pl, const double* t, const double* qv,
+                    const double* zm, const double* w, double* nactl, double* nacti, double* smax) {
+  moist::AerArgs a{c.d, nk, qv_sub > 0 ? qv_sub : nk, moist::device_tables(), pl, t, qv, zm, w, nactl, nacti, smax};
+  GT_LAUNCH(moist::aer_activation_k, moist::ptgrid(c.d, nk), dim3(BX, BY), 0, c.st, a);
+  HIP_LAUNCH_CHECK();
+  ktimer_bytes(8.0 * c.d.nx * c.d.ny * c.d.nsub * nk * 8.0);
+}
+
+void moist_prep(const Ctx& c, int nk, const double* pe, const double* dz, double* pl, double* zm) {
+  GT_LAUNCH(moist::moist_prep_k, moist::colgrid(c.d), dim3(BX, BY), 0, c.st, c.d, nk, pe, dz, pl, zm);
+  HIP_LAUNCH_CHECK();
+  ktimer_bytes(8.0 * c.d.nx * c.d.ny * c.d.nsub * (4.0 * nk + 1.0));
 }
 
 void buoyancy(const Ctx& c, int nk, const double* t, const double* qv, const double* pm, const double* zm,

@@ -265,11 +265,11 @@ std::map<std::string, Fn>& reg() {
          Field& q = F(dy, f[0]);
          fillq2zero(dy.ctx(), q.nk, q.p, F(dy, f[1]).p, dy.field(f[2], 1).p);
        }},
-      // gfdl_1m(T, qv, ql, qr, qi, qs, qg, delp, delz, pm | prec_r, prec_s, prec_g, prec_i) params: dt;
-      // the first seven fields are updated in place
+      // gfdl_1m(T, qv, ql, qr, qi, qs, qg, delp, delz | prec_r, prec_s, prec_g, prec_i) params: dt;
+      // the GFDL cloud microphysics column driver; the first seven fields are updated in place
       {"gfdl_1m",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
-         need(f, 14, "gfdl_1m");
+         need(f, 13, "gfdl_1m");
          Field& t = F(dy, f[0]);
          Gfdl1mArgs a{};
          a.nk = t.nk;
@@ -277,12 +277,65 @@ std::map<std::string, Fn>& reg() {
          a.T = t.p;
          a.qv = F(dy, f[1]).p; a.ql = F(dy, f[2]).p; a.qr = F(dy, f[3]).p; a.qi = F(dy, f[4]).p;
          a.qs = F(dy, f[5]).p; a.qg = F(dy, f[6]).p;
-         a.dp = F(dy, f[7]).p; a.dz = F(dy, f[8]).p; a.pm = F(dy, f[9]).p;
-         for (int n = 1; n <= 9; ++n)
+         a.dp = F(dy, f[7]).p; a.dz = F(dy, f[8]).p;
+         for (int n = 1; n <= 8; ++n)
            if (F(dy, f[n]).nk != t.nk) throw std::runtime_error("gfdl_1m: fields must share the level count");
-         a.pr = dy.field(f[10], 1).p; a.ps = dy.field(f[11], 1).p; a.pg = dy.field(f[12], 1).p;
-         a.pi = dy.field(f[13], 1).p;
+         a.scr = dy.field("_mp_scr", gfdl_mp_scratch_levels(t.nk)).p;
+         a.pr = dy.field(f[9], 1).p; a.ps = dy.field(f[10], 1).p; a.pg = dy.field(f[11], 1).p;
+         a.pi = dy.field(f[12], 1).p;
          gfdl_1m(dy.ctx(), a);
+       }},
+      // evap_subl_pdf(T, qv, qlls, qils, qlcn, qicn, clls, clcn, pl, nactl, nacti) params: dt;
+      // the first eight fields are updated in place
+      {"evap_subl_pdf",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 11, "evap_subl_pdf");
+         Field& t = F(dy, f[0]);
+         for (int n = 1; n <= 10; ++n)
+           if (F(dy, f[n]).nk != t.nk) throw std::runtime_error("evap_subl_pdf: fields must share the level count");
+         EvapSublArgs a{};
+         a.nk = t.nk;
+         a.dt = p.at(0);
+         a.T = t.p;
+         a.qv = F(dy, f[1]).p; a.qlls = F(dy, f[2]).p; a.qils = F(dy, f[3]).p; a.qlcn = F(dy, f[4]).p;
+         a.qicn = F(dy, f[5]).p; a.clls = F(dy, f[6]).p; a.clcn = F(dy, f[7]).p;
+         a.pl = F(dy, f[8]).p; a.nactl = F(dy, f[9]).p; a.nacti = F(dy, f[10]).p;
+         evap_subl_pdf(dy.ctx(), a);
+       }},
+      // GEOS RADCOUPLE, fields in / out:
+      // radcouple(T, pl, cf, af, qv, qlls, qils, qlcn, qicn, qr, qs, qg, nactl | rad_qv, rad_ql, rad_qi, rad_qr, rad_qs, rad_qg, rad_cf, rad_rl, rad_ri)
+      {"radcouple",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
+         need(f, 22, "radcouple");
+         Field& t = F(dy, f[0]);
+         for (int n = 1; n <= 12; ++n)
+           if (F(dy, f[n]).nk != t.nk) throw std::runtime_error("radcouple: fields must share the level count");
+         RadcoupleArgs a{};
+         a.nk = t.nk;
+         a.T = t.p; a.pl = F(dy, f[1]).p; a.cf = F(dy, f[2]).p; a.af = F(dy, f[3]).p; a.qv = F(dy, f[4]).p;
+         a.qlls = F(dy, f[5]).p; a.qils = F(dy, f[6]).p; a.qlcn = F(dy, f[7]).p; a.qicn = F(dy, f[8]).p;
+         a.qr = F(dy, f[9]).p; a.qs = F(dy, f[10]).p; a.qg = F(dy, f[11]).p; a.nl = F(dy, f[12]).p;
+         double** outs[9] = {&a.rqv, &a.rql, &a.rqi, &a.rqr, &a.rqs, &a.rqg, &a.rcf, &a.rrl, &a.rri};
+         for (int n = 0; n < 9; ++n) *outs[n] = dy.field(f[13 + n], t.nk).p;
+         radcouple(dy.ctx(), a);
+       }},
+      // aer_activation(pl, T, qv, zm, w | nactl, nacti, smax)
+      {"aer_activation",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
+         need(f, 8, "aer_activation");
+         Field& t = F(dy, f[1]);
+         for (int n = 0; n <= 4; ++n)
+           if (F(dy, f[n]).nk != t.nk) throw std::runtime_error("aer_activation: fields must share the level count");
+         aer_activation(dy.ctx(), t.nk, 0, F(dy, f[0]).p, t.p, F(dy, f[2]).p, F(dy, f[3]).p, F(dy, f[4]).p,
+                        dy.field(f[5], t.nk).p, dy.field(f[6], t.nk).p, dy.field(f[7], t.nk).p);
+       }},
+      // moist_prep(pe, delz | pl, zm): layer pressure and layer-mid heights
+      {"moist_prep",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
+         need(f, 4, "moist_prep");
+         Field& dz = F(dy, f[1]);
+         if (F(dy, f[0]).nk != dz.nk + 1) throw std::runtime_error("moist_prep: pe must have nk+1 levels");
+         moist_prep(dy.ctx(), dz.nk, F(dy, f[0]).p, dz.p, dy.field(f[2], dz.nk).p, dy.field(f[3], dz.nk).p);
        }},
       // buoyancy(T, qv, pm, zm | buoy, cape, cin, klcl)
       {"buoyancy",

@@ -65,7 +65,11 @@ a2b_ord4 = StencilDef("a2b_ord4", 2, (1,))
 held_suarez = StencilDef("held_suarez", 4, (1, 2, 3), ("dt",))
 moist_qsat = StencilDef("moist_qsat", 5, (2, 3, 4))
 fillq2zero = StencilDef("fillq2zero", 3, (0, 2))
-gfdl_1m = StencilDef("gfdl_1m", 14, tuple(range(7)) + (10, 11, 12, 13), ("dt",))
+gfdl_1m = StencilDef("gfdl_1m", 13, tuple(range(7)) + (9, 10, 11, 12), ("dt",))
+evap_subl_pdf = StencilDef("evap_subl_pdf", 11, tuple(range(8)), ("dt",))
+radcouple = StencilDef("radcouple", 22, tuple(range(13, 22)))
+aer_activation = StencilDef("aer_activation", 8, (5, 6, 7))
+moist_prep = StencilDef("moist_prep", 4, (2, 3))
 buoyancy = StencilDef("buoyancy", 8, (4, 5, 6, 7))
 
 

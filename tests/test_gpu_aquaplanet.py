@@ -1,9 +1,11 @@
 """The Aquaplanet configuration's coupled step on the device (BASELINE.json configs[3]:
-dycore + moist column physics): one fv_dynamics call followed by the moist column step
-(Dycore::moist_physics: gfdl_1m on pt, the six moist tracers, delp, delz and the layer
-pressure from pe), against oracle fv_dynamics followed by oracle gfdl_1m.  Bar as the
-dycore step test: each field within 1e-9 of its mean magnitude; column water plus
-surface precipitation conserved by the moist step on the device."""
+dycore + moist column physics): one fv_dynamics call followed by the moist physics in
+GEOS's GFDL_1M order (Dycore::moist_physics: aer_activation, evap_subl_pdf, the GFDL cloud
+microphysics driver, radcouple, on pt, the six moist tracers, the anvil condensate and
+cloud fractions, delp, delz, pe, w), against oracle fv_dynamics followed by
+oracle/geos_moist.py aquaplanet_physics.  Bar: each field within 1e-9 of its scale (and
+the reference's 0.01 % per value); column water plus surface precipitation conserved by
+the moist step on the device."""
 import importlib
 
 import numpy as np
@@ -12,6 +14,7 @@ import pytest
 from conftest import metrics_of
 from oracle import NG
 from oracle import fv_dynamics as fvd
+from oracle import geos_moist as gm
 from oracle import moist as om
 
 pytestmark = pytest.mark.gpu
@@ -40,18 +43,27 @@ def test_aquaplanet_step_matches_oracle(pkg, require_gpu):
         g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
         ref = fvd.fv_dynamics(st, ak, bk, g, dict(NL, nq=nq))
         J, I = slice(NG, NG + d.ny), slice(NG, NG + d.nx)
+        gotx = {k: d.download(k) for k in ("qlcn", "qicn", "clls", "clcn", "nactl", "rad_cf", "rad_ql", "rad_ri",
+                                           "prec_rain", "prec_snow")}
+
+        def close(a, b, what, floor=1e-30):
+            scale = max(np.abs(b).max(), floor)
+            assert np.abs(a - b).max() <= 1e-9 * scale + 1e-18, (what, np.abs(a - b).max() / scale)
+            np.testing.assert_allclose(a, b, rtol=1e-4, atol=1e-9 * scale + 1e-18, err_msg=str(what))
+
         for s in range(d.nsub):
-            pe = ref["pe"][s]
-            sp = [ref["q"][s][n * npz:(n + 1) * npz] for n in range(6)]
-            (T, *qs), rp = om.gfdl_1m(ref["pt"][s], ref["delp"][s], ref["delz"][s], 0.5 * (pe[1:] + pe[:-1]),
-                                      *sp, dt)
-            a, b = got["pt"][s][:, J, I], T[:, J, I]
-            assert np.abs(a - b).max() <= 1e-9 * np.abs(b).mean(), ("pt", s)
-            for n in range(6):
-                a = got["q"][s][n * npz:(n + 1) * npz][:, J, I]
-                b = qs[n][:, J, I]
-                scale = max(np.abs(b).mean(), 1e-30)
-                assert np.abs(a - b).max() <= 1e-9 * scale + 1e-18, ("q", n, s)
+            c = lambda a: a[..., J, I]
+            sp = [c(ref["q"][s][n * npz:(n + 1) * npz]) for n in range(6)]
+            o = gm.aquaplanet_physics(dt, c(ref["pt"][s]), *sp, c(ref["delp"][s]), c(ref["delz"][s]),
+                                      c(ref["pe"][s]), c(ref["w"][s]))
+            close(got["pt"][s][:, J, I], o["t"], ("pt", s))
+            for n, k in enumerate(("qv", "ql", "qr", "qi", "qs", "qg")):
+                close(got["q"][s][n * npz:(n + 1) * npz][:, J, I], o[k], (k, s))
+            for k in ("qlcn", "qicn", "clls", "clcn", "nactl", "rad_cf", "rad_ql", "rad_ri"):
+                close(gotx[k][s][:, J, I], o[k], (k, s))
+            for k in ("prec_rain", "prec_snow"):   # (melted-out species arrive as round-off)
+                cw = (sum(sp) * c(ref["delp"][s])).sum(0).max() / om.GRAV
+                close(gotx[k][s][0][J, I], o[k], (k, s), floor=1e-6 * cw)
             # the device moist step conserves column water + precipitation
             w0 = np.einsum("kji,kji->ji", sum(before["q"][s][n * npz:(n + 1) * npz] for n in range(6)),
                            before["delp"][s]) / om.GRAV
