@@ -66,10 +66,11 @@ def test_layout_rule_matches_reference():
 
 
 def test_no_kernel_uses_scratch(pkg, tmp_path):
-    """Every gfx950 kernel of the library runs without private (scratch) memory: the
-    multi-rank loopback runs (several host threads launching on concurrent streams)
-    faulted in a kernel that had a stack object in scratch, and scratch traffic is
-    slow anyway.  Reads .private_segment_fixed_size from the code-object metadata."""
+    """Every gfx950 kernel of the library runs without private (scratch) memory: a
+    stack object or a register spill in scratch costs HBM round trips on the hot path.
+    (The round-1 multi-rank loopback fault was traced to an out-of-plane read in
+    a2b_march_k -- the prefetched J == 1 edge row below a segment, fixed in 27fdd8c --
+    not to scratch.)  Reads .private_segment_fixed_size from the code-object metadata."""
     import shutil
     import subprocess
     llvm = "/opt/rocm/lib/llvm/bin"
