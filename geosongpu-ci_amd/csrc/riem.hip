@@ -291,9 +291,10 @@ __global__ void __launch_bounds__(BLOCK) riem_col_k(RiemArgs a) {
 //
 // One wavefront owns 16 columns; its 64 lanes are 4 level blocks x 16 columns
 // (lane = 16 b + column), block b holding layers [b M, b M + M) and interfaces
-// b M .. b M + M of its column in registers (M = 18 at L72).  Every input is read from
-// HBM once (PT, W1 a second time, from cache) and every output written once: the
-// sweeps of the column form above never touch memory.
+// b M .. b M + M of its column in registers (M = 18 at L72).  Every output is written
+// once; inputs the registers cannot hold across all sweeps (DP, PT, W1, G) are re-read
+// from cache where a later sweep needs them, and the clamped heights and interface
+// pressures are recomputed there (nothing is parked in HBM and read back).
 //
 //   * pointwise work (the transcendentals of pm, pl, pk3, dz2; aa, the numerators) runs
 //     on all 64 lanes at once;
@@ -313,10 +314,6 @@ typedef unsigned int RbU2 __attribute__((ext_vector_type(2)));
 // alone the scheduler interleaves all M of them and runs out of registers.  A fence per
 // level keeps one or two in flight (two waves per SIMD hide the latency instead).
 #define RB_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
-// Values parked in HBM and read back later by the same lane: the stores must have
-// completed before the loads are issued (a vector-memory load does not wait for an
-// earlier store of the same wave), and neither side may be moved across by the compiler.
-#define RB_PARK_DRAIN() asm volatile("s_waitcnt vmcnt(0)" ::: "memory")
 
 __device__ __forceinline__ double from_below(double v, int lane) { return __shfl(v, (lane + RB_NC) & 63); }
 __device__ __forceinline__ double from_above(double v, int lane) { return __shfl(v, (lane - RB_NC) & 63); }
@@ -393,52 +390,48 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.ws_out + (long)s * P), 0, (int)PB, 0x00020000), o8, 0, 0);
   }
 
-  RB_SCHED_FENCE();
-  // ---- S0: dz_min clamp (bottom-up), speculative per block
-  double gl[M + 1];
-  {
-    double gin = gr[M];  // unclamped interface kb1
+  // dz_min clamp of the heights g (bottom-up), speculative per block: each block clamps from
+  // the unclamped interface below it, and repeats only if the block below changed it
+  auto clamp = [&](const double (&g)[M + 1], double (&gl)[M + 1]) {
+    double gin = g[M];  // unclamped interface kb1
     for (int it = 0; it <= RB_NB; ++it) {
       gl[M] = gin;
 #pragma unroll
-      for (int m = M - 1; m >= 0; --m) gl[m] = fmax(gr[m], gl[m + 1] + a.dz_min);
+      for (int m = M - 1; m >= 0; --m) gl[m] = fmax(g[m], gl[m + 1] + a.dz_min);
       const double gn = from_below(gl[0], lane);
       const double want = lastblk || !act ? gin : gn;
       if (!__any(want != gin)) break;
       gin = want;
     }
-  }
-  // park the clamped heights in G until S3 (own slots: same-lane ordering)
-  if (act) {
+  };
+  // interface pressures pem = ptop + prefix sums of DP (top-down, block after block)
+  auto prefix = [&](const double (&dpv)[M], double (&pe_)[M + 1]) {
 #pragma unroll
-    for (int m = 0; m < M; ++m) st(rG, m, gl[m]);
-  }
-  RB_PARK_DRAIN();
-
-  RB_SCHED_FENCE();
-  // ---- S1a: pem prefix (top-down, block after block)
-  double pem[M + 1];
-#pragma unroll
-  for (int m = 0; m <= M; ++m) pem[m] = 0.0;
-  {
+    for (int m = 0; m <= M; ++m) pe_[m] = 0.0;
     double carry = a.ptop;
 #pragma unroll 1
     for (int r = 0; r < nblk; ++r) {
       if (b == r) {
-        pem[0] = carry;
+        pe_[0] = carry;
 #pragma unroll
-        for (int m = 0; m < M; ++m) pem[m + 1] = pem[m] + DP[m];
+        for (int m = 0; m < M; ++m) pe_[m + 1] = pe_[m] + dpv[m];
       }
-      carry = from_above(pem[M], lane);
+      carry = from_above(pe_[M], lane);
     }
-  }
-  // park pem in the output array until S3 / S6
-  if (act) {
-#pragma unroll
-    for (int m = 0; m < M; ++m) st(rPO, m, pem[m]);
-    if (lastblk) st(rPO, M, pem[M]);
-  }
-  RB_PARK_DRAIN();
+  };
+  // The clamped heights and pem are recomputed where S3 / S6 need them again (same
+  // operations, same values) instead of being parked in HBM between the sweeps: the parked
+  // copies cost a write and one or two re-reads per level (riem traffic was 2.4-3x its
+  // algorithmic bytes).
+  RB_SCHED_FENCE();
+  // ---- S0: dz_min clamp
+  double gl[M + 1];
+  clamp(gr, gl);
+
+  RB_SCHED_FENCE();
+  // ---- S1a: pem prefix
+  double pem[M + 1];
+  prefix(DP, pem);
 
   RB_SCHED_FENCE();
   // ---- S1b: pointwise layer quantities
@@ -553,23 +546,19 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
   double aat[M], num[M], aab_last;
   {
     double pemr[M + 1], glr[M + 1], dz[M];
+    {
+      double dpv[M], g0[M + 1];
 #pragma unroll
-    for (int m = 0; m <= M; ++m) {
-      pemr[m] = ld(rPO, m);
-      glr[m] = ld(rG, m);  // parked clamped heights; interface km is never clamped
-    }
-    {  // interface kb1 belongs to the block below (shuffle outside any divergent branch)
-      const double pb = from_below(pemr[0], lane), gb = from_below(glr[0], lane);
-      if (!lastblk) {
-        pemr[M] = pb;
-        glr[M] = gb;
-      }
+      for (int m = 0; m < M; ++m) dpv[m] = ld(rDP, m);
+#pragma unroll
+      for (int m = 0; m <= M; ++m) g0[m] = ld(rG, m);  // the unclamped heights (G is written in S6)
+      prefix(dpv, pemr);
+      clamp(g0, glr);
+#pragma unroll
+      for (int m = 0; m < M; ++m) dm[m] = dpv[m] * (1.0 / GRAV);
     }
 #pragma unroll
-    for (int m = 0; m < M; ++m) {
-      dz[m] = glr[m + 1] - glr[m];
-      dm[m] = ld(rDP, m) * (1.0 / GRAV);
-    }
+    for (int m = 0; m < M; ++m) dz[m] = glr[m + 1] - glr[m];
     const double dz_ab = from_above(dz[M - 1], lane);
 #pragma unroll
     for (int m = 0; m < M; ++m) {
@@ -729,10 +718,19 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
       }
       cg_in = from_below(gz[0], lane);
     }
-    if (valid) {
-      double pemr[M + 1];
+    // C grid: pem again for the full pressure (outside the divergent branch: the prefix
+    // hands its carry between lanes)
+    double pemr[M + 1];
+    if (cg) {
+      double dpv[M];
 #pragma unroll
-      for (int m = 0; m <= M; ++m) pemr[m] = cg ? ld(rPO, m) : 0.0;
+      for (int m = 0; m < M; ++m) dpv[m] = ld(rDP, m);
+      prefix(dpv, pemr);
+    } else {
+#pragma unroll
+      for (int m = 0; m <= M; ++m) pemr[m] = 0.0;
+    }
+    if (valid) {
       const auto rDZ = rs(a.delz, false);
 #pragma unroll
       for (int m = 0; m < M; ++m) {
