@@ -189,221 +189,284 @@ __device__ __forceinline__ void qs2(const Tables& tb, bool ice, double t, double
   dq = (des - es / t) / (RVGAS * t * den);
 }
 
-struct MpCol {
-  int nk;
-  MCol t, qv, ql, qr, qi, qs, qg, dp, dz;
-  MCol ze, zt, den, a, aL, aR, a6, gam, qe, qm, m1, qm0;
-  __device__ __forceinline__ double cvm(int k) const { return cvm_(qv[k], ql[k], qr[k], qi[k], qs[k], qg[k]); }
-};
+// Every column pass below is a function whose arrays are __restrict__ parameters (the
+// lane's column at stride P): a level's loads may then be issued before the previous
+// level's stores complete, instead of each level waiting out a store -> load round trip
+// through memory (the passes are otherwise chains of dependent HBM / L2 latencies).
+// Recurrences carry their previous level in registers; values and operation order are
+// those of oracle/gfdl_mp.py.
+#define RP double* __restrict__
+#define CRP const double* __restrict__
 
-__device__ void mp_neg_adj(const MpCol& c) {
-  const int n = c.nk;
+__device__ __forceinline__ void mp_neg_adj(int n, long P, RP t, RP qv, RP ql, RP qr, RP qi, RP qs, RP qg, CRP dp) {
   for (int k = 0; k < n; ++k) {
-    double t = c.t[k], qv = c.qv[k], ql = c.ql[k], qr = c.qr[k], qi = c.qi[k], qs = c.qs[k], qg = c.qg[k];
-    const double cvm = cvm_(qv, ql, qr, qi, qs, qg);
-    const double lcpk = lhl_(t) / cvm, icpk = lhi_(t) / cvm;
-    if (qi < 0.0) { qs = qs + qi; qi = 0.0; }
-    if (qs < 0.0) { qg = qg + qs; qs = 0.0; }
+    const long x = (long)k * P;
+    double tt = t[x], v = qv[x], l = ql[x], r = qr[x], ii = qi[x], sn = qs[x], g = qg[x];
+    const double cvm = cvm_(v, l, r, ii, sn, g);
+    const double lcpk = lhl_(tt) / cvm, icpk = lhi_(tt) / cvm;
+    if (ii < 0.0) { sn = sn + ii; ii = 0.0; }
+    if (sn < 0.0) { g = g + sn; sn = 0.0; }
     {
-      const double dq = qg < 0.0 ? qg : 0.0;
-      qv = qv + dq;
-      t = t - dq * (lcpk + icpk);
-      if (qg < 0.0) qg = 0.0;
+      const double dq = g < 0.0 ? g : 0.0;
+      v = v + dq;
+      tt = tt - dq * (lcpk + icpk);
+      if (g < 0.0) g = 0.0;
     }
-    if (qr < 0.0) { ql = ql + qr; qr = 0.0; }
+    if (r < 0.0) { l = l + r; r = 0.0; }
     {
-      const double dq = ql < 0.0 ? ql : 0.0;
-      qv = qv + dq;
-      t = t - dq * lcpk;
-      if (ql < 0.0) ql = 0.0;
+      const double dq = l < 0.0 ? l : 0.0;
+      v = v + dq;
+      tt = tt - dq * lcpk;
+      if (l < 0.0) l = 0.0;
     }
-    c.t[k] = t; c.qv[k] = qv; c.ql[k] = ql; c.qr[k] = qr; c.qi[k] = qi; c.qs[k] = qs; c.qg[k] = qg;
+    t[x] = tt; qv[x] = v; ql[x] = l; qr[x] = r; qi[x] = ii; qs[x] = sn; qg[x] = g;
   }
+  // negative vapour borrows from below (the level below carried in a register)
+  double cur = qv[0];
   for (int k = 0; k < n - 1; ++k) {
-    const double q0 = c.qv[k];
-    if (q0 < 0.0) {
-      c.qv[k + 1] = c.qv[k + 1] + q0 * c.dp[k] / c.dp[k + 1];
-      c.qv[k] = 0.0;
+    double nxt = qv[(long)(k + 1) * P];
+    if (cur < 0.0) {
+      nxt = nxt + cur * dp[(long)k * P] / dp[(long)(k + 1) * P];
+      qv[(long)k * P] = 0.0;
+      cur = 0.0;
     }
+    if (k + 1 < n - 1) qv[(long)(k + 1) * P] = nxt;
+    else {
+      // bottom: qb = nxt (level n-1), qa = cur (level n-2)
+      const double qb = nxt, qa = cur;
+      double dq = fmin(-qb * dp[(long)k * P + P], qa * dp[(long)k * P]);
+      if (!(qb < 0.0 && qa > 0.0)) dq = 0.0;
+      qv[(long)k * P] = qa - dq / dp[(long)k * P];
+      qv[(long)(k + 1) * P] = qb + dq / dp[(long)(k + 1) * P];
+    }
+    cur = nxt;
   }
-  const int k = n - 1;
-  const double qb = c.qv[k], qa = c.qv[k - 1];
-  double dq = fmin(-qb * c.dp[k], qa * c.dp[k - 1]);
-  if (!(qb < 0.0 && qa > 0.0)) dq = 0.0;
-  c.qv[k - 1] = qa - dq / c.dp[k - 1];
-  c.qv[k] = qb + dq / c.dp[k];
 }
 
-// monotone PPM of the per-height amounts a[] on the fallen layers (oracle cs_profile_mono)
-__device__ void mp_cs_profile(const MpCol& c) {
-  const int n = c.nk;
-  const MCol &a = c.a, &q = c.qe, &gam = c.gam;
-  auto dz = [&](int k) { return c.zt[k] - c.zt[k + 1]; };
-  {
-    const double grat = dz(1) / dz(0);
-    const double bet = grat * (grat + 0.5);
-    q[0] = ((grat + grat) * (grat + 1.0) * a[0] + a[1]) / bet;
-    gam[0] = (1.0 + grat * (grat + 1.5)) / bet;
-  }
-  for (int k = 1; k < n; ++k) {
-    const double d4 = dz(k - 1) / dz(k);
-    const double bet = 2.0 + d4 + d4 - gam[k - 1];
-    q[k] = (3.0 * (a[k - 1] + d4 * a[k]) - q[k - 1]) / bet;
-    gam[k] = d4 / bet;
-  }
-  {
-    const double d4 = dz(n - 2) / dz(n - 1);
-    const double a_bot = 1.0 + d4 * (d4 + 1.5);
-    q[n] = (2.0 * d4 * (d4 + 1.0) * a[n - 1] + a[n - 2] - a_bot * q[n - 1]) / (d4 * (d4 + 0.5) - a_bot * gam[n - 1]);
-  }
-  for (int k = n - 1; k >= 0; --k) q[k] = q[k] - gam[k] * q[k + 1];
-  for (int k = 1; k < n; ++k) q[k] = fmin(fmax(q[k], fmin(a[k - 1], a[k])), fmax(a[k - 1], a[k]));
-  q[0] = fmax(q[0], 0.0);
-  q[n] = fmax(q[n], 0.0);
+// melting of the falling ice species in layers above freezing (oracle terminal_fall)
+__device__ __forceinline__ void mp_melt(int n, long P, const MpConst& kc, RP t, CRP qv, RP ql, RP qr, RP qi, RP qs,
+                                        RP qg) {
   for (int k = 0; k < n; ++k) {
-    double aL = q[k], aR = q[k + 1], a6;
-    const double av = a[k];
-    const double da1 = aR - aL;
-    if ((av - aL) * (av - aR) >= 0.0) {
-      aL = av; aR = av; a6 = 0.0;
-    } else {
-      a6 = 3.0 * (2.0 * av - (aL + aR));
-      if (a6 * da1 < -da1 * da1) {
-        a6 = 3.0 * (aL - av);
-        aR = aL - a6;
-      } else if (a6 * da1 > da1 * da1) {
-        a6 = 3.0 * (aR - av);
-        aL = aR - a6;
+    const long x = (long)k * P;
+    double tt = t[x];
+    if (!(tt > T_ICE)) continue;
+    double v = qv[x], l = ql[x], r = qr[x], ii = qi[x], sn = qs[x], g = qg[x];
+#pragma unroll
+    for (int w = 0; w < 3; ++w) {
+      double& q = w == 0 ? ii : (w == 1 ? sn : g);
+      const double fq = w == 0 ? kc.e_imlt : (w == 1 ? kc.e_smlt : kc.e_gmlt);
+      const double icpk = lhi_(tt) / cvm_(v, l, r, ii, sn, g);
+      const double mlt = fmin(fq * q, (tt - T_ICE) / icpk);
+      if (mlt > 0.0) {
+        q = q - mlt;
+        if (w == 0) l = l + mlt;
+        else r = r + mlt;
+        tt = tt - mlt * icpk;
       }
     }
-    c.aL[k] = aL; c.aR[k] = aR; c.a6[k] = a6;
+    t[x] = tt; ql[x] = l; qr[x] = r; qi[x] = ii; qs[x] = sn; qg[x] = g;
   }
 }
 
-// fallen interface heights (oracle fallen_edges), vt[k] held in c.qm for the call
-__device__ void mp_fallen_edges(const MpCol& c, double dts) {
-  const int n = c.nk;
-  const MCol& vt = c.qm;
-  c.zt[0] = c.ze[0];
-  for (int k = 1; k < n; ++k) c.zt[k] = c.ze[k] - 0.5 * dts * (vt[k - 1] + vt[k]);
-  c.zt[n] = c.ze[n] - dts * vt[n - 1];
-  for (int k = 0; k < n; ++k)
-    if (c.zt[k + 1] >= c.zt[k]) c.zt[k + 1] = c.zt[k] - DZ_MIN_FALL;
-}
-
-// Lagrangian sedimentation of species q (oracle lagrangian_fall_ppm); the flux out of the
-// bottom of each layer in c.m1; returns m1[n-1]
-__device__ double mp_lagrangian_fall(const MpCol& c, const MCol& q) {
-  const int n = c.nk;
+// fall speeds of species w (0 ice, 1 snow, 2 graupel, 3 rain) into vt; returns whether
+// any level holds more than the species' threshold
+__device__ __forceinline__ bool mp_speeds(int n, long P, int w, CRP q, CRP den, RP vt) {
+  bool any = false;
   for (int k = 0; k < n; ++k) {
-    const double m0 = q[k] * c.dp[k];
-    c.qm0[k] = m0;
-    c.a[k] = m0 / (c.zt[k] - c.zt[k + 1]);
+    const long x = (long)k * P;
+    const double dn = den[x], qq = q[x];
+    const double rhof = sqrt(fmin(10.0, SFCRHO / dn));
+    double v;
+    if (w == 3) {
+      const double q_ = fmax(qq, QRMIN);
+      v = qq > QRMIN ? fmin(VR_MAX, fmax(VR_MIN, VCONR * rhof * exp(0.2 * log(q_ * dn / NORMR)))) : 0.0;
+      any = any || qq > QRMIN;
+    } else {
+      const double q_ = fmax(qq, QCMIN);
+      if (w == 0) v = qq > QCMIN ? fmin(VI_MAX, 3.29 * exp(0.16 * log(q_ * dn))) : 0.0;
+      else if (w == 1) v = qq > QCMIN ? fmin(VS_MAX, VCONS * rhof * exp(0.0625 * log(q_ * dn / NORMS))) : 0.0;
+      else v = qq > QCMIN ? fmin(VG_MAX, VCONG * rhof * sqrt(sqrt(sqrt(q_ * dn / NORMG)))) : 0.0;
+      any = any || qq > QCMIN;
+    }
+    vt[x] = v;
   }
-  mp_cs_profile(c);
+  return any;
+}
+
+// fallen interface heights (oracle fallen_edges; the monotone fix carried in one pass: each
+// raw height depends only on ze and vt, the fix of k+1 on the fixed k)
+__device__ __forceinline__ void mp_fallen_edges(int n, long P, double dts, CRP ze, CRP vt, RP zt) {
+  double zp = ze[0];
+  zt[0] = zp;
+  double vprev = vt[0];
+  for (int k = 1; k <= n; ++k) {
+    const long x = (long)k * P;
+    double z;
+    if (k < n) {
+      const double v = vt[x];
+      z = ze[x] - 0.5 * dts * (vprev + v);
+      vprev = v;
+    } else {
+      z = ze[x] - dts * vprev;
+    }
+    if (z >= zp) z = zp - DZ_MIN_FALL;
+    zt[x] = z;
+    zp = z;
+  }
+}
+
+// Lagrangian sedimentation of q (oracle lagrangian_fall_ppm + cs_profile_mono); the flux
+// out of the bottom of each layer into m1; returns m1[n-1]
+__device__ __forceinline__ double mp_lagrangian_fall(int n, long P, CRP ze, CRP zt, CRP dp, RP q, RP qm0, RP a,
+                                                     RP qe, RP gam, RP aL, RP aR, RP a6, RP qm, RP m1) {
+  for (int k = 0; k < n; ++k) {
+    const long x = (long)k * P;
+    const double m0 = q[x] * dp[x];
+    qm0[x] = m0;
+    a[x] = m0 / (zt[x] - zt[x + P]);
+  }
+  // cs_profile: forward elimination (carries: q, gam, a and dz of the level above)
+  {
+    const double z0 = zt[0], z1 = zt[P], z2 = zt[2 * P];
+    const double dz0 = z0 - z1, dz1 = z1 - z2;
+    const double a0 = a[0], a1 = a[P];
+    const double grat = dz1 / dz0;
+    const double bet = grat * (grat + 0.5);
+    double qp = ((grat + grat) * (grat + 1.0) * a0 + a1) / bet;
+    double gp = (1.0 + grat * (grat + 1.5)) / bet;
+    qe[0] = qp;
+    gam[0] = gp;
+    double dzp = dz0, ap = a0, zb = z1;
+    for (int k = 1; k < n; ++k) {
+      const long x = (long)k * P;
+      const double zn = zt[x + P];
+      const double dzk = zb - zn;
+      const double ak = a[x];
+      const double d4 = dzp / dzk;
+      const double bt = 2.0 + d4 + d4 - gp;
+      qp = (3.0 * (ap + d4 * ak) - qp) / bt;
+      gp = d4 / bt;
+      qe[x] = qp;
+      gam[x] = gp;
+      dzp = dzk;
+      ap = ak;
+      zb = zn;
+    }
+    // bottom edge: dz(n-2) / dz(n-1) (dzp is dz(n-1); dz(n-2) recomputed from zt)
+    const long xn = (long)n * P;
+    const double d4 = (zt[xn - 2 * P] - zt[xn - P]) / dzp;
+    const double a_bot = 1.0 + d4 * (d4 + 1.5);
+    qe[xn] = (2.0 * d4 * (d4 + 1.0) * ap + a[xn - 2 * P] - a_bot * qp) / (d4 * (d4 + 0.5) - a_bot * gp);
+  }
+  // back substitution (on the unbounded values), each edge bounded by its neighbouring
+  // means as it is finalised; both end edges non-negative
+  {
+    const long xn = (long)n * P;
+    double x = qe[xn];
+    qe[xn] = fmax(x, 0.0);
+    double anext = a[xn - P];
+    for (int k = n - 1; k >= 0; --k) {
+      const long y = (long)k * P;
+      x = qe[y] - gam[y] * x;
+      if (k >= 1) {
+        const double ap = a[y - P];
+        qe[y] = fmin(fmax(x, fmin(ap, anext)), fmax(ap, anext));
+        anext = ap;
+      } else {
+        qe[y] = fmax(x, 0.0);
+      }
+    }
+  }
+  // monotone limiter (cs_limiters)
+  {
+    double qL = qe[0];
+    for (int k = 0; k < n; ++k) {
+      const long x = (long)k * P;
+      const double qR = qe[x + P];
+      double l = qL, r = qR, a6v;
+      const double av = a[x];
+      const double da1 = r - l;
+      if ((av - l) * (av - r) >= 0.0) {
+        l = av; r = av; a6v = 0.0;
+      } else {
+        a6v = 3.0 * (2.0 * av - (l + r));
+        if (a6v * da1 < -da1 * da1) {
+          a6v = 3.0 * (l - av);
+          r = l - a6v;
+        } else if (a6v * da1 > da1 * da1) {
+          a6v = 3.0 * (r - av);
+          l = r - a6v;
+        }
+      }
+      aL[x] = l; aR[x] = r; a6[x] = a6v;
+      qL = qR;
+    }
+  }
+  // integrate the fallen profile over the fixed layers
   int k0 = 0;
   for (int k = 0; k < n; ++k) {
-    const double top = c.ze[k], bot = c.ze[k + 1];
+    const double top = ze[(long)k * P], bot = ze[(long)(k + 1) * P];
     double qmk = 0.0;
     for (int m = k0; m < n; ++m) {
-      const double ztm = c.zt[m], ztm1 = c.zt[m + 1];
+      const long y = (long)m * P;
+      const double ztm = zt[y], ztm1 = zt[y + P];
       if (top <= ztm && top >= ztm1) {
         const double dzm = ztm - ztm1;
         const double pl = (ztm - top) / dzm;
-        const double aL = c.aL[m], aR = c.aR[m], a6 = c.a6[m];
+        const double l = aL[y], r = aR[y], a6v = a6[y];
         if (ztm1 <= bot) {
           const double pr = (ztm - bot) / dzm;
-          qmk = (aL + 0.5 * (a6 + aR - aL) * (pr + pl) - a6 * MP_R3 * (pr * (pr + pl) + pl * pl)) * (top - bot);
+          qmk = (l + 0.5 * (a6v + r - l) * (pr + pl) - a6v * MP_R3 * (pr * (pr + pl) + pl * pl)) * (top - bot);
           k0 = m;
         } else {
-          double s = (top - ztm1) * (aL + 0.5 * (a6 + aR - aL) * (1.0 + pl) - a6 * (MP_R3 * (1.0 + pl * (1.0 + pl))));
+          double sm = (top - ztm1) * (l + 0.5 * (a6v + r - l) * (1.0 + pl) - a6v * (MP_R3 * (1.0 + pl * (1.0 + pl))));
           for (int mm = m + 1; mm < n; ++mm) {
-            const double zb = c.zt[mm + 1];
+            const long yy = (long)mm * P;
+            const double zb = zt[yy + P];
             if (bot < zb) {
-              s = s + c.qm0[mm];
+              sm = sm + qm0[yy];
             } else {
-              const double dzz = c.zt[mm] - bot;
-              const double esl = dzz / (c.zt[mm] - zb);
-              s = s + dzz * (c.aL[mm] + 0.5 * esl * (c.aR[mm] - c.aL[mm] + c.a6[mm] * (1.0 - MP_R23 * esl)));
+              const double dzz = zt[yy] - bot;
+              const double esl = dzz / (zt[yy] - zb);
+              sm = sm + dzz * (aL[yy] + 0.5 * esl * (aR[yy] - aL[yy] + a6[yy] * (1.0 - MP_R23 * esl)));
               k0 = mm;
               break;
             }
           }
-          qmk = s;
+          qmk = sm;
         }
         break;
       }
     }
-    c.qm[k] = qmk;
+    qm[(long)k * P] = qmk;
   }
   double acc = 0.0;
   for (int k = 0; k < n; ++k) {
-    acc = acc + c.qm0[k] - c.qm[k];
-    c.m1[k] = acc;
-    q[k] = c.qm[k] / c.dp[k];
+    const long x = (long)k * P;
+    const double qmk = qm[x];
+    acc = acc + qm0[x] - qmk;
+    m1[x] = acc;
+    q[x] = qmk / dp[x];
   }
   return acc;
 }
 
-__device__ void mp_sedi_heat(const MpCol& c, double cw) {
-  for (int k = 1; k < c.nk; ++k) {
-    const double dgz = -0.5 * GRAV * c.dz[k];
-    const double cv0 = c.dp[k] * c.cvm(k) + cw * (c.m1[k] - c.m1[k - 1]);
-    c.t[k] = (cv0 * c.t[k] + c.m1[k - 1] * (cw * c.t[k - 1] + dgz)) / (cv0 + cw * c.m1[k - 1]);
+__device__ __forceinline__ void mp_sedi_heat(int n, long P, double cw, RP t, CRP dp, CRP dz, CRP m1, CRP qv, CRP ql,
+                                             CRP qr, CRP qi, CRP qs, CRP qg) {
+  double tp = t[0], mp = m1[0];
+  for (int k = 1; k < n; ++k) {
+    const long x = (long)k * P;
+    const double mk = m1[x];
+    const double dgz = -0.5 * GRAV * dz[x];
+    const double cv0 = dp[x] * cvm_(qv[x], ql[x], qr[x], qi[x], qs[x], qg[x]) + cw * (mk - mp);
+    const double tn = (cv0 * t[x] + mp * (cw * tp + dgz)) / (cv0 + cw * mp);
+    t[x] = tn;
+    tp = tn;
+    mp = mk;
   }
 }
 
-__device__ void mp_terminal_fall(const MpCol& c, const MpConst& kc, double dts, double& pi_, double& ps_,
-                                 double& pg_) {
-  const int n = c.nk;
-  for (int k = 0; k < n; ++k) {
-    if (c.t[k] > T_ICE) {
-#pragma unroll
-      for (int w = 0; w < 3; ++w) {
-        const double fq = w == 0 ? kc.e_imlt : (w == 1 ? kc.e_smlt : kc.e_gmlt);
-        const MCol& q = w == 0 ? c.qi : (w == 1 ? c.qs : c.qg);
-        const double cvm = c.cvm(k);
-        const double t = c.t[k];
-        const double icpk = lhi_(t) / cvm;
-        const double mlt = fmin(fq * q[k], (t - T_ICE) / icpk);
-        if (mlt > 0.0) {
-          q[k] = q[k] - mlt;
-          if (w == 0) c.ql[k] = c.ql[k] + mlt;
-          else c.qr[k] = c.qr[k] + mlt;
-          c.t[k] = t - mlt * icpk;
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int w = 0; w < 3; ++w) {
-    double& out = w == 0 ? pi_ : (w == 1 ? ps_ : pg_);
-    const MCol& q = w == 0 ? c.qi : (w == 1 ? c.qs : c.qg);
-    bool any = false;
-    for (int k = 0; k < n; ++k) any = any || q[k] > QCMIN;
-    if (!any) {
-      out = 0.0;
-      continue;
-    }
-    // fall speeds (oracle fall_speed), into the qm column for mp_fallen_edges
-    for (int k = 0; k < n; ++k) {
-      const double den = c.den[k], qq = q[k];
-      const double rhof = sqrt(fmin(10.0, SFCRHO / den));
-      const double q_ = fmax(qq, QCMIN);
-      double v;
-      if (w == 0) v = qq > QCMIN ? fmin(VI_MAX, 3.29 * exp(0.16 * log(q_ * den))) : 0.0;
-      else if (w == 1) v = qq > QCMIN ? fmin(VS_MAX, VCONS * rhof * exp(0.0625 * log(q_ * den / NORMS))) : 0.0;
-      else v = qq > QCMIN ? fmin(VG_MAX, VCONG * rhof * sqrt(sqrt(sqrt(q_ * den / NORMG)))) : 0.0;
-      c.qm[k] = v;
-    }
-    mp_fallen_edges(c, dts);
-    const double m = mp_lagrangian_fall(c, q);
-    mp_sedi_heat(c, C_ICE);
-    out = m / GRAV;
-  }
-}
-
-__device__ void mp_revap_racc(const Tables& tb, const MpConst& kc, double dt, double den, double& t, double& qv,
+__device__ __forceinline__ void mp_revap_racc(const Tables& tb, const MpConst& kc, double dt, double den, double& t, double& qv,
                               double& ql, double& qr, double qi, double qs, double qg) {
   const double cvm = cvm_(qv, ql, qr, qi, qs, qg);
   const double lcpk = lhl_(t) / cvm;
@@ -427,45 +490,29 @@ __device__ void mp_revap_racc(const Tables& tb, const MpConst& kc, double dt, do
   qr = qr + sink;
 }
 
-__device__ double mp_warm_rain(const MpCol& c, const Tables& tb, const MpConst& kc, double dts) {
-  const int n = c.nk;
-  const double dt5 = 0.5 * dts;
-  auto revap = [&]() {
-    for (int k = 0; k < n; ++k) {
-      double t = c.t[k], qv = c.qv[k], ql = c.ql[k], qr = c.qr[k];
-      mp_revap_racc(tb, kc, dt5, c.den[k], t, qv, ql, qr, c.qi[k], c.qs[k], c.qg[k]);
-      c.t[k] = t; c.qv[k] = qv; c.ql[k] = ql; c.qr[k] = qr;
-    }
-  };
-  revap();
-  double rain = 0.0;
-  bool any = false;
+__device__ __forceinline__ void mp_revap_pass(int n, long P, const Tables& tb, const MpConst& kc, double dt, CRP den,
+                                              RP t, RP qv, RP ql, RP qr, CRP qi, CRP qs, CRP qg) {
   for (int k = 0; k < n; ++k) {
-    const double den = c.den[k], qr = c.qr[k];
-    const double rhof = sqrt(fmin(10.0, SFCRHO / den));
-    const double q_ = fmax(qr, QRMIN);
-    c.qm[k] = qr > QRMIN ? fmin(VR_MAX, fmax(VR_MIN, VCONR * rhof * exp(0.2 * log(q_ * den / NORMR)))) : 0.0;
-    any = any || qr > QRMIN;
+    const long x = (long)k * P;
+    double tt = t[x], v = qv[x], l = ql[x], r = qr[x];
+    mp_revap_racc(tb, kc, dt, den[x], tt, v, l, r, qi[x], qs[x], qg[x]);
+    t[x] = tt; qv[x] = v; ql[x] = l; qr[x] = r;
   }
-  if (any) {
-    mp_fallen_edges(c, dts);
-    const double m = mp_lagrangian_fall(c, c.qr);
-    mp_sedi_heat(c, C_LIQ);
-    rain = m / GRAV;
-  }
-  revap();
-  for (int k = 0; k < n; ++k) {
-    const double ql = c.ql[k];
-    const double dq = ql - QL0_AUT;
-    double aut = dts * C_PAUT * 1.0e-3 * dq * dq / (dq + 1.0e-3);
-    aut = dq > 0.0 ? fmin(aut, dq) : 0.0;
-    c.ql[k] = ql - aut;
-    c.qr[k] = c.qr[k] + aut;
-  }
-  return rain;
 }
 
-__device__ void mp_icloud(const Tables& tb, const MpConst& kc, double dts, double den, double& t, double& qv,
+__device__ __forceinline__ void mp_autoconv(int n, long P, double dts, RP ql, RP qr) {
+  for (int k = 0; k < n; ++k) {
+    const long x = (long)k * P;
+    const double l = ql[x];
+    const double dq = l - QL0_AUT;
+    double aut = dts * C_PAUT * 1.0e-3 * dq * dq / (dq + 1.0e-3);
+    aut = dq > 0.0 ? fmin(aut, dq) : 0.0;
+    ql[x] = l - aut;
+    qr[x] = qr[x] + aut;
+  }
+}
+
+__device__ __forceinline__ void mp_icloud(const Tables& tb, const MpConst& kc, double dts, double den, double& t, double& qv,
                           double& ql, double& qr, double& qi, double& qs, double& qg) {
   const double denfac = sqrt(SFCRHO / den);
   double tc = t - T_ICE;
@@ -555,43 +602,81 @@ __device__ void mp_icloud(const Tables& tb, const MpConst& kc, double dts, doubl
   }
 }
 
+__device__ __forceinline__ void mp_icloud_pass(int n, long P, const Tables& tb, const MpConst& kc, double dts,
+                                               CRP den, RP t, RP qv, RP ql, RP qr, RP qi, RP qs, RP qg) {
+  for (int k = 0; k < n; ++k) {
+    const long x = (long)k * P;
+    double tt = t[x], v = qv[x], l = ql[x], r = qr[x], ii = qi[x], sn = qs[x], g = qg[x];
+    mp_icloud(tb, kc, dts, den[x], tt, v, l, r, ii, sn, g);
+    t[x] = tt; qv[x] = v; ql[x] = l; qr[x] = r; qi[x] = ii; qs[x] = sn; qg[x] = g;
+  }
+}
+
 __global__ void __launch_bounds__(256) mpdrv_k(MpArgs a) {
   int s;
   long o;
   if (!col_point(a.d, s, o)) return;
   const long P = a.d.plane;
   const int n = a.nk;
-  auto col = [&](double* base, int nkk) { return MCol{base + (long)s * nkk * P + o, P}; };
-  auto ccol = [&](const double* base, int nkk) { return MCol{const_cast<double*>(base) + (long)s * nkk * P + o, P}; };
-  MpCol c;
-  c.nk = n;
-  c.t = col(a.T, n);
-  c.qv = col(a.qv, a.qsub); c.ql = col(a.ql, a.qsub); c.qr = col(a.qr, a.qsub);
-  c.qi = col(a.qi, a.qsub); c.qs = col(a.qs, a.qsub); c.qg = col(a.qg, a.qsub);
-  c.dp = ccol(a.dp, n);
-  c.dz = ccol(a.dz, n);
+  const double dts = a.dts;
+  const MpConst& kc = a.k;
+  double* t = a.T + (long)s * n * P + o;
+  const long qo = (long)s * a.qsub * P + o;
+  double *qv = a.qv + qo, *ql = a.ql + qo, *qr = a.qr + qo, *qi = a.qi + qo, *qs = a.qs + qo, *qg = a.qg + qo;
+  const double* dp = a.dp + (long)s * n * P + o;
+  const double* dz = a.dz + (long)s * n * P + o;
   double* sb = a.scr + (long)s * MP_NSCR * (n + 1) * P + o;
-  auto scol = [&](int b) { return MCol{sb + (long)b * (n + 1) * P, P}; };
-  c.ze = scol(0); c.zt = scol(1); c.den = scol(2); c.a = scol(3); c.aL = scol(4); c.aR = scol(5);
-  c.a6 = scol(6); c.gam = scol(7); c.qe = scol(8); c.qm = scol(9); c.m1 = scol(10); c.qm0 = scol(11);
-  c.ze[n] = 0.0;
-  for (int k = n - 1; k >= 0; --k) c.ze[k] = c.ze[k + 1] - c.dz[k];
-  for (int k = 0; k < n; ++k) c.den[k] = -c.dp[k] / (GRAV * c.dz[k]);
+  const long SB = (long)(n + 1) * P;
+  double *ze = sb, *zt = sb + SB, *den = sb + 2 * SB, *aa = sb + 3 * SB, *aL = sb + 4 * SB, *aR = sb + 5 * SB;
+  double *a6 = sb + 6 * SB, *gam = sb + 7 * SB, *qe = sb + 8 * SB, *vt = sb + 9 * SB, *m1 = sb + 10 * SB;
+  double* qm0 = sb + 11 * SB;
+  double* qm = vt;  // the fall speeds are consumed (fallen heights) before the remap writes qm
+  {
+    double z = 0.0;
+    ze[(long)n * P] = z;
+    for (int k = n - 1; k >= 0; --k) {
+      z = z - dz[(long)k * P];
+      ze[(long)k * P] = z;
+    }
+    for (int k = 0; k < n; ++k) den[(long)k * P] = -dp[(long)k * P] / (GRAV * dz[(long)k * P]);
+  }
   double prr = 0.0, prs = 0.0, prg = 0.0, pri = 0.0;
   for (int it = 0; it < a.ntimes; ++it) {
-    mp_neg_adj(c);
-    double pi_, ps_, pg_;
-    mp_terminal_fall(c, a.k, a.dts, pi_, ps_, pg_);
-    const double pr_ = mp_warm_rain(c, a.tb, a.k, a.dts);
-    prr = prr + pr_;
-    prs = prs + ps_;
-    prg = prg + pg_;
-    pri = pri + pi_;
-    for (int k = 0; k < n; ++k) {
-      double t = c.t[k], qv = c.qv[k], ql = c.ql[k], qr = c.qr[k], qi = c.qi[k], qs = c.qs[k], qg = c.qg[k];
-      mp_icloud(a.tb, a.k, a.dts, c.den[k], t, qv, ql, qr, qi, qs, qg);
-      c.t[k] = t; c.qv[k] = qv; c.ql[k] = ql; c.qr[k] = qr; c.qi[k] = qi; c.qs[k] = qs; c.qg[k] = qg;
+    mp_neg_adj(n, P, t, qv, ql, qr, qi, qs, qg, dp);
+    // terminal_fall: melting, then ice, snow, graupel
+    mp_melt(n, P, kc, t, qv, ql, qr, qi, qs, qg);
+    double pf0 = 0.0, pf1 = 0.0, pf2 = 0.0;
+#pragma unroll 1
+    for (int w = 0; w < 3; ++w) {
+      double* q = w == 0 ? qi : (w == 1 ? qs : qg);
+      double pfw = 0.0;
+      if (mp_speeds(n, P, w, q, den, vt)) {
+        mp_fallen_edges(n, P, dts, ze, vt, zt);
+        const double m = mp_lagrangian_fall(n, P, ze, zt, dp, q, qm0, aa, qe, gam, aL, aR, a6, qm, m1);
+        mp_sedi_heat(n, P, C_ICE, t, dp, dz, m1, qv, ql, qr, qi, qs, qg);
+        pfw = m / GRAV;
+      }
+      if (w == 0) pf0 = pfw;
+      else if (w == 1) pf1 = pfw;
+      else pf2 = pfw;
     }
+    // warm_rain
+    const double dt5 = 0.5 * dts;
+    mp_revap_pass(n, P, a.tb, kc, dt5, den, t, qv, ql, qr, qi, qs, qg);
+    double pr_ = 0.0;
+    if (mp_speeds(n, P, 3, qr, den, vt)) {
+      mp_fallen_edges(n, P, dts, ze, vt, zt);
+      const double m = mp_lagrangian_fall(n, P, ze, zt, dp, qr, qm0, aa, qe, gam, aL, aR, a6, qm, m1);
+      mp_sedi_heat(n, P, C_LIQ, t, dp, dz, m1, qv, ql, qr, qi, qs, qg);
+      pr_ = m / GRAV;
+    }
+    mp_revap_pass(n, P, a.tb, kc, dt5, den, t, qv, ql, qr, qi, qs, qg);
+    mp_autoconv(n, P, dts, ql, qr);
+    prr = prr + pr_;
+    prs = prs + pf1;
+    prg = prg + pf2;
+    pri = pri + pf0;
+    mp_icloud_pass(n, P, a.tb, kc, dts, den, t, qv, ql, qr, qi, qs, qg);
   }
   const long p2 = (long)s * P + o;
   a.pr[p2] = prr;
@@ -599,6 +684,8 @@ __global__ void __launch_bounds__(256) mpdrv_k(MpArgs a) {
   a.pg[p2] = prg;
   a.pi[p2] = pri;
 }
+#undef RP
+#undef CRP
 
 // ---- GEOS pieces around the microphysics (oracle/geos_moist.py), pointwise ----
 constexpr double RHO_W = 1000.0, RHO_I = 917.0;

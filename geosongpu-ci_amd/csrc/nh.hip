@@ -320,23 +320,37 @@ __device__ __forceinline__ bool ring2_point(int t, int nx, int ny, int& i, int& 
   return false;
 }
 
-__global__ void __launch_bounds__(256) pk3_pe_halo_k(Dims d, int npz, double ptop, int do_pe,
-                                                     const double* __restrict__ delp, double* __restrict__ pk3,
-                                                     double* __restrict__ pe) {
+// One lane per ring column walking the levels top-down: the interface pressure is the
+// running sum ptop + delp[0] + ... + delp[k] (the same additions in the same order as a
+// per-level sum from the top), pk3 = exp(kappa log pe) per interface; the loads of a block
+// of levels are issued together and the transcendentals of different levels overlap.
+__global__ void __launch_bounds__(64) pk3_pe_halo_k(Dims d, int npz, double ptop, int do_pe,
+                                                    const double* __restrict__ delp, double* __restrict__ pk3,
+                                                    double* __restrict__ pe) {
   int i, j;
   if (!ring2_point(blockIdx.x * blockDim.x + threadIdx.x, d.nx, d.ny, i, j)) return;
-  const int s = blockIdx.z / npz, k = blockIdx.z % npz;
+  const int s = blockIdx.y;
   const long o = pidx(d, i, j);
   const int km = npz, k1 = npz + 1;
-  const double* DP = delp + (long)s * km * d.plane + o;
+  const long P = d.plane;
+  const double* DP = delp + (long)s * km * P + o;
   const bool ring1 = i >= -1 && i <= d.nx && j >= -1 && j <= d.ny;
+  const long b1 = (long)s * k1 * P + o;
+  if (do_pe && ring1) pe[b1] = ptop;
   double pei = ptop;
-  for (int m = 0; m <= k; ++m) pei = pei + DP[(long)m * d.plane];
-  const long b1 = (long)s * k1 * d.plane + o;
-  pk3[b1 + (long)(k + 1) * d.plane] = exp(KAPPA * log(pei));
-  if (do_pe && ring1) {
-    pe[b1 + (long)(k + 1) * d.plane] = pei;
-    if (k == 0) pe[b1] = ptop;
+  constexpr int KB = 8;
+  for (int k0 = 0; k0 < km; k0 += KB) {
+    double dv[KB];
+#pragma unroll
+    for (int m = 0; m < KB; ++m) dv[m] = k0 + m < km ? DP[(long)(k0 + m) * P] : 0.0;
+#pragma unroll
+    for (int m = 0; m < KB; ++m) {
+      if (k0 + m >= km) break;
+      pei = pei + dv[m];
+      const long x = b1 + (long)(k0 + m + 1) * P;
+      pk3[x] = exp(KAPPA * log(pei));
+      if (do_pe && ring1) pe[x] = pei;
+    }
   }
 }
 
@@ -869,8 +883,8 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
 void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* delp, double* pk3, double* pe) {
   const Dims& d = c.d;
   const int nring = 4 * (d.nx + 4) + 4 * d.ny;
-  GT_LAUNCH(pk3_pe_halo_k, dim3(cdiv(nring, 256), 1, d.nsub * npz), dim3(256), 0, c.st, d, npz, ptop, do_pe ? 1 : 0, delp, pk3,
-                     pe);
+  GT_LAUNCH(pk3_pe_halo_k, dim3(cdiv(nring, 64), d.nsub), dim3(64), 0, c.st, d, npz, ptop, do_pe ? 1 : 0, delp, pk3,
+            pe);
   HIP_LAUNCH_CHECK();
   gt_bytes((double)d.nsub * npz * (4.0 * (d.nx + 2) + 4.0 * d.ny) * (do_pe ? 3 : 2));  // halo ring only
 }
