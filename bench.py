@@ -18,7 +18,8 @@ Prints ONE JSON line on rank 0 (contract in DESIGN.md §Measurement):
                    step_bytes (every kernel's algorithmic bytes, bytes_manifest.yaml, as
                    registered by the launchers on the probe step) / ms_per_step -> step_frac
   cpu_baseline     the numpy oracle (oracle/fv_dynamics.py) timed for one step on a
-                   bounded sample (C24 L72, 6 tiles) on the host, rank 0 only
+                   bounded sample (C48 L72, 6 tiles, ~20 s of one core) on the host, rank 0
+                   only; the host's CPU count and this process's affinity are recorded
 """
 import argparse
 import json
@@ -136,7 +137,8 @@ def parse():
     p.add_argument("--nq", type=int, default=4)
     p.add_argument("--layout", default="", help="sub-domain layout per tile, e.g. 2x2 (default: by rank count)")
     p.add_argument("--dt", type=float, default=0.0, help="dt_atmos (default 450 s x 180 / N: C180 450 s)")
-    p.add_argument("--cpu-npx", type=int, default=25, help="cpu_baseline sample grid (C24)")
+    p.add_argument("--cpu-npx", type=int, default=49,
+                   help="cpu_baseline sample grid (C48 L72, 6 tiles: ~20 s of one host core)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--kernel-report", default="", help="write per-kernel stats JSON here")
@@ -188,10 +190,16 @@ def cpu_baseline(pkg, npx, npz, nq, dt, moist=False):
     el = time.perf_counter() - t0
     cells = 6 * d.N * d.N * npz
     d.close()
+    try:
+        aff = sorted(os.sched_getaffinity(0))
+    except AttributeError:
+        aff = []
     return dict(value=cells / el, unit="grid-cell-updates/s", cores=1, kind="port",
-                sample=f"one fv_dynamics step{' + moist column step' if moist else ''}, C{d.N} L{npz} nq={nq}, "
+                host_cpus=os.cpu_count(), affinity=f"{len(aff)} cpus ({aff[0]}-{aff[-1]})" if aff else None,
+                sample=f"one fv_dynamics step{' + moist physics' if moist else ''}, C{d.N} L{npz} nq={nq}, "
                        f"6 tiles, numpy fp64 oracle "
-                       f"(oracle/fv_dynamics.py), {el:.1f} s on 1 host core")
+                       f"(oracle/fv_dynamics.py), {el:.1f} s on 1 host core (numpy single-threaded; the "
+                       f"process may run on any of the affinity set)")
 
 
 def main():
