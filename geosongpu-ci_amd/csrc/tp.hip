@@ -39,6 +39,12 @@ constexpr int ZMAX = 65535;
 // (An LDS-tiled form with 64 x 8 tiles, the first fused version, gave bit-identical
 // results and ran 1.9x slower at C180; removed with the ra_x / ra_y planes it read.)
 constexpr int MW = 64, MOUT = MW - 6, MWAVES = 4;
+// Paired last strip (the thermo march's split launches): when the last strip of a row has at
+// most MOUT_H outputs (C180: 181 edges = 3 x 58 + 7), one wave runs it for two levels at
+// once -- lanes 0-31 level k, lanes 32-63 level k+1, each half a 32-lane strip with three
+// halo lanes on either side (the DPP shifts that cross the halves only reach halo lanes) --
+// instead of one wave per level: the tile-edge kernel 460 -> 393 us per launch at C180.
+constexpr int MOUT_H = 32 - 6;
 constexpr int MAXPAIR = 192;
 // DXL (the thermo march's tile-edge strips): the dxa of the <= 8 tile-edge columns a strip
 // can hold (I = -2 .. 1, N-2 .. N+1) for the segment's rows live in LDS, one region per wave,
@@ -53,6 +59,7 @@ struct TpM {
   Dims d;
   const SubInfo* subs;
   const double* M;
+  const double* area2;  // [nsub][2][plane]
   const double* qf[3];
   double* qo[3];  // TM = 1: the updated delp, w, pt; TM = 2: the updated tracers
   // TM = 2 (tracer_2d_1l update fused): dp1 in, dp2 out (written by field group 0), the
@@ -71,6 +78,9 @@ struct TpM {
   // all have work (a workgroup holds its CU slots until its last wave ends)
   int npair;
   int pairs[MAXPAIR];
+  // paired last strips (split launches, pairlast set): the paired (sub-domain, strip) entries
+  // follow the npair full ones
+  int pairlast, npairh;
 };
 
 // Wavefront-wide lane shifts through DPP (no LDS): dpp_prev(v) in lane L is v of lane
@@ -184,12 +194,16 @@ struct YRoll {
 // TM = 2: tracer_2d_1l's update fused (NF tracers with the mass fluxes mfx / mfy): dp2 of
 //   row r-3 is formed from the mass fluxes the march holds (tracer_dp2's expression) and the
 //   tracers are updated from their outer fluxes (tracer_update's expression) into qo.
+// pair: 0 one level per wave; 1 the wave's upper half runs level k+1; 2 paired strip without
+// a level k+1 (odd level count: the upper half repeats level k and stores nothing)
 template <int ORD, bool EX, bool AHEAD2, bool MF, int NF, int TM>
-__device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
+__device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, int pair) {
   static_assert(TM == 0 || (TM == 1 && NF == 3 && MF) || (TM == 2 && MF),
                 "thermo march: delp, w, pt with the accumulators as MX / MY; tracer march: mass fluxes");
   const Dims& d = a.d;
   const int lane = threadIdx.x & (MW - 1);
+  const int hl = pair ? (lane & 31) : lane;  // lane within the strip
+  const bool upper = pair && lane >= 32;
   // z: (sub-domain, level, field group), the field group fastest: the groups of one level
   // share the Courant numbers and fluxes (loaded once per wave for its NF fields), and with
   // the groups of a level adjacent in launch order those planes are re-read from the
@@ -198,32 +212,38 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
   const SubInfo sub = a.subs[s];
   const int nx = d.nx, ny = d.ny, N = sub.N;
   const bool last = j1 >= ny;
-  const int x = strip * MOUT - NG + lane;
+  const int x = strip * MOUT - NG + hl;
   const int I = x + sub.ioff;
   const int xc = x < -NG ? -NG : (x > nx + NG ? nx + NG : x);  // addressable column
   const long pitch = d.pitch;
   const long zo = ((long)(s * a.nt + tg * NF) * a.nk + k) * d.plane, fo = ((long)s * a.nk + k) * d.plane;
-  const double* area = met(a.M, d, M_AREA, s);
   const double* dxa = met(a.M, d, M_DXA, s);
   const double* dya = met(a.M, d, M_DYA, s);
   const bool cin = x >= -NG && x < nx + NG;              // q exists (cell halo)
-  const bool out_lane = lane >= NG && lane < NG + MOUT;  // owns an output edge / column
+  // owns an output edge / column (the upper half of an unpaired odd tail owns nothing)
+  const bool out_lane = hl >= NG && hl < NG + (pair ? MOUT_H : MOUT) && !(upper && pair == 2);
   const long xo = xc + NG;
   // Buffer descriptors (wave-uniform) for every plane the march reads or writes; a lane
   // addresses column xo of row r with the constant voffset vx and the row offset as the
   // scalar offset, so the loads of a row step cost no vector address arithmetic.
   const int PBy = (int)(d.plane * 8);
+  // metric planes: one plane; level fields: two planes when the upper half runs level k+1
+  const int PBf = pair == 1 ? 2 * PBy : PBy;
   auto rsrc = [&](const double* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, PBy, 0x00020000); };
+  auto rsrcf = [&](const double* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, PBf, 0x00020000); };
   __amdgpu_buffer_rsrc_t rQ[NF];
 #pragma unroll
-  for (int f = 0; f < NF; ++f) rQ[f] = rsrc(a.qf[f] + zo);
-  const auto rCRX = rsrc(a.crx + fo), rCRY = rsrc(a.cry + fo), rXFX = rsrc(a.xfx + fo);
-  const auto rYFX = rsrc(a.yfx + fo);
-  const auto rMX = rsrc(a.mx + fo), rMY = rsrc(a.my + fo), rAR = rsrc(area), rDXA = rsrc(dxa);
-  const auto rDP1 = rsrc(TM == 2 ? a.dp1 + fo : a.mx + fo);
-  const auto rDP2 = rsrc(TM == 2 ? a.dp2o + fo : a.mx + fo);
+  for (int f = 0; f < NF; ++f) rQ[f] = rsrcf(a.qf[f] + zo);
+  const auto rCRX = rsrcf(a.crx + fo), rCRY = rsrcf(a.cry + fo), rXFX = rsrcf(a.xfx + fo);
+  const auto rYFX = rsrcf(a.yfx + fo);
+  // the area through the level fields' offset: a2 holds it twice, for both halves
+  const auto rMX = rsrcf(a.mx + fo), rMY = rsrcf(a.my + fo), rDXA = rsrc(dxa);
+  const auto rAR = __builtin_amdgcn_make_buffer_rsrc((void*)(a.area2 + (long)s * 2 * d.plane), 0, 2 * PBy, 0x00020000);
+  const auto rDP1 = rsrcf(TM == 2 ? a.dp1 + fo : a.mx + fo);
+  const auto rDP2 = rsrcf(TM == 2 ? a.dp2o + fo : a.mx + fo);
   const bool dp2_group = TM == 2 && tg == 0;  // one field group writes dp2
-  const uint32_t vx = (uint32_t)xo * 8u;
+  const uint32_t vx = (uint32_t)xo * 8u;  // metric planes
+  const uint32_t vf = vx + (upper && pair == 1 ? (uint32_t)PBy : 0u);  // level fields
   // dxa only enters the tile-edge interface values (ppm_al at g = 0, N reads the four
   // cells g-2 .. g+1): the other lanes read one shared word instead of their own column
   const bool dx_lane = (I >= -2 && I <= 1) || (I >= N - 2 && I <= N + 1);
@@ -263,8 +283,9 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     const bool qin = cin && r >= -NG && r < ny + NG;
     if (EX && (J < 0 || J >= N)) {  // cube-corner halo cells read the copy_corners source
       const bool cc = qin && (I < 0 || I >= N);
-      const uint32_t ox = cc ? (uint32_t)cc_off(d, sub, x, r, 1) * 8u : vx + so;
-      const uint32_t oy = cc ? (uint32_t)cc_off(d, sub, x, r, 2) * 8u : vx + so;
+      const uint32_t hof = vf - vx;
+      const uint32_t ox = cc ? (uint32_t)cc_off(d, sub, x, r, 1) * 8u + hof : vf + so;
+      const uint32_t oy = cc ? (uint32_t)cc_off(d, sub, x, r, 2) * 8u + hof : vf + so;
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
         const double q1 = bl(rQ[f], ox, 0), q2 = bl(rQ[f], oy, 0);
@@ -274,25 +295,25 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
     } else {
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
-        const double q1 = bl(rQ[f], vx, so);
+        const double q1 = bl(rQ[f], vf, so);
         v.qx[f] = qin ? q1 : 0.0;
         v.qy[f] = v.qx[f];
       }
     }
-    v.crx = bl(rCRX, vx, so);
-    v.xfx = bl(rXFX, vx, so);
-    v.area_r = bl(rAR, vx, so);
+    v.crx = bl(rCRX, vf, so);
+    v.xfx = bl(rXFX, vf, so);
+    v.area_r = bl(rAR, vf, so);
     v.dxr = EX && !DXL ? bl(rDXA, vxd, so) : 0.0;
     const int re = r - 2 < -NG ? -NG : r - 2;
     const uint32_t se = (uint32_t)(re + NG) * rowb;
-    v.cry = bl(rCRY, vx, se);
-    v.yfx = bl(rYFX, vx, se);
-    v.my = MF ? bl(rMY, vx, se) : 0.0;
+    v.cry = bl(rCRY, vf, se);
+    v.yfx = bl(rYFX, vf, se);
+    v.my = MF ? bl(rMY, vf, se) : 0.0;
     const int rm = r - 3 < -NG ? -NG : r - 3;
     const uint32_t sm = (uint32_t)(rm + NG) * rowb;
-    v.mx = MF ? bl(rMX, vx, sm) : 0.0;
+    v.mx = MF ? bl(rMX, vf, sm) : 0.0;
     v.dxm = EX && !DXL ? bl(rDXA, vxd, sm) : 0.0;
-    v.dp1 = TM == 2 ? bl(rDP1, vx, sm) : 0.0;
+    v.dp1 = TM == 2 ? bl(rDP1, vf, sm) : 0.0;
     return v;
   };
 
@@ -337,22 +358,22 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
     if (TM == 0) {
-      rFX[f] = rsrc(a.fxf[f < 2 ? f : 0] + zo);
-      rFY[f] = rsrc(a.fyf[f < 2 ? f : 0] + zo);
+      rFX[f] = rsrcf(a.fxf[f < 2 ? f : 0] + zo);
+      rFY[f] = rsrcf(a.fyf[f < 2 ? f : 0] + zo);
     } else if (TM == 1) {
-      rFX[f] = rsrc(a.qo[f] + fo);  // updated field f (TM = 1 groups are one field each)
+      rFX[f] = rsrcf(a.qo[f] + fo);  // updated field f (TM = 1 groups are one field each)
     } else {
-      rFX[f] = rsrc(a.qo[f < 2 ? f : 0] + zo);  // updated tracer f of the group
+      rFX[f] = rsrcf(a.qo[f < 2 ? f : 0] + zo);  // updated tracer f of the group
     }
   }
   auto bst = [&](__amdgpu_buffer_rsrc_t r, uint32_t soff, double v) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(TpU2, v), r, vx, soff, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(TpU2, v), r, vf, soff, 0);
   };
   // lane-predicated store without a branch: a lane that must not store addresses past the
   // end of the plane (the descriptor's range check drops the write), so the steady rows
   // stay one basic block the scheduler can interleave across the three unrolled rows
   constexpr uint32_t OOB = 0x80000000u;
-  const uint32_t vfy = s_fy ? vx : OOB, vfx = s_fx ? vx : OOB;
+  const uint32_t vfy = s_fy ? vf : OOB, vfx = s_fx ? vf : OOB;
   auto bstv = [&](__amdgpu_buffer_rsrc_t r, uint32_t voff, uint32_t soff, double v) {
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(TpU2, v), r, voff, soff, 0);
   };
@@ -366,21 +387,21 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1) {
       const uint32_t so = (uint32_t)(rl + NG) * rowb;
 #pragma unroll
       for (int f = 0; f < NF; ++f) {
-        nxt.qx[f] = bl(rQ[f], vx, so);
+        nxt.qx[f] = bl(rQ[f], vf, so);
         if (!cin) nxt.qx[f] = 0.0;
         nxt.qy[f] = nxt.qx[f];
       }
-      nxt.crx = bl(rCRX, vx, so);
-      nxt.xfx = bl(rXFX, vx, so);
-      nxt.area_r = bl(rAR, vx, so);
+      nxt.crx = bl(rCRX, vf, so);
+      nxt.xfx = bl(rXFX, vf, so);
+      nxt.area_r = bl(rAR, vf, so);
       nxt.dxr = EX && !DXL ? bl(rDXA, vxd, so) : 0.0;
       const uint32_t se = so - 2 * rowb, sm = so - 3 * rowb;
-      nxt.cry = bl(rCRY, vx, se);
-      nxt.yfx = bl(rYFX, vx, se);
-      nxt.my = MF ? bl(rMY, vx, se) : 0.0;
-      nxt.mx = MF ? bl(rMX, vx, sm) : 0.0;
+      nxt.cry = bl(rCRY, vf, se);
+      nxt.yfx = bl(rYFX, vf, se);
+      nxt.my = MF ? bl(rMY, vf, se) : 0.0;
+      nxt.mx = MF ? bl(rMX, vf, sm) : 0.0;
       nxt.dxm = EX && !DXL ? bl(rDXA, vxd, sm) : 0.0;
-      nxt.dp1 = TM == 2 ? bl(rDP1, vx, sm) : 0.0;
+      nxt.dp1 = TM == 2 ? bl(rDP1, vf, sm) : 0.0;
   };
   // ahead: how many rows ahead the steady step prefetches (1, or 2 in the three-buffer loop)
   auto step = [&](auto gen, int r, const MarchIn<NF>& cur, MarchIn<NF>& nxt, int ahead) {
@@ -635,7 +656,14 @@ __global__ void __launch_bounds__(MW * MWAVES, OCC ? OCC : (AHEAD2 ? 1 : 4)) tp_
   // buffer descriptors, row offsets) is then provably wave-uniform (SGPRs, no waterfalls)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / MW);
   const unsigned w = blockIdx.x * MWAVES + wv;  // < 2^31 (launch_tp checks)
-  int strip, seg, z;
+  int strip, seg, z, pair = 0;
+  const int kh = (a.nk + 1) / 2;  // level pairs of a paired strip
+  // paired-strip wave: (level pair kk, field group tg) of sub-domain s, tg fastest
+  auto paired_z = [&](int s_, unsigned zz) {
+    const int tg = (int)(zz % (unsigned)a.ntg), k = 2 * (int)(zz / (unsigned)a.ntg);
+    pair = k + 1 < a.nk ? 1 : 2;
+    return (s_ * a.nk + k) * a.ntg + tg;
+  };
   if constexpr (EXS == 0) {
     strip = (int)(w % (unsigned)a.nstrip);
     const unsigned t = w / (unsigned)a.nstrip;
@@ -643,15 +671,29 @@ __global__ void __launch_bounds__(MW * MWAVES, OCC ? OCC : (AHEAD2 ? 1 : 4)) tp_
     z = (int)(t / (unsigned)a.nseg);
     if (z >= a.nz) return;  // whole wavefront leaves; no workgroup barrier follows
   } else {
-    // pair p = (sub-domain, strip) of this kind; then segment; then (field group, level)
-    const unsigned p = w % (unsigned)a.npair;
-    const unsigned t = w / (unsigned)a.npair;
-    seg = (int)(t % (unsigned)a.nseg);
-    const int zz = (int)(t / (unsigned)a.nseg);
-    const int pr = a.pairs[p];
-    strip = pr & 255;
-    if (zz >= a.ntg * a.nk) return;
-    z = (pr >> 8) * a.ntg * a.nk + zz;
+    // pair p = (sub-domain, strip) of this kind; then segment; then (field group, level);
+    // the paired entries (pairs[npair ..]) after the full ones
+    const unsigned nfull = (unsigned)a.npair * (unsigned)a.nseg * (unsigned)(a.ntg * a.nk);
+    if (w < nfull) {
+      const unsigned p = w % (unsigned)a.npair;
+      const unsigned t = w / (unsigned)a.npair;
+      seg = (int)(t % (unsigned)a.nseg);
+      const int zz = (int)(t / (unsigned)a.nseg);
+      const int pr = a.pairs[p];
+      strip = pr & 255;
+      z = (pr >> 8) * a.ntg * a.nk + zz;
+    } else {
+      if (a.npairh == 0) return;
+      const unsigned w2 = w - nfull;
+      const unsigned p = (unsigned)a.npair + w2 % (unsigned)a.npairh;
+      const unsigned t = w2 / (unsigned)a.npairh;
+      seg = (int)(t % (unsigned)a.nseg);
+      const unsigned zz = t / (unsigned)a.nseg;
+      if (zz >= (unsigned)(kh * a.ntg)) return;
+      const int pr = a.pairs[p];
+      strip = pr & 255;
+      z = paired_z(pr >> 8, zz);
+    }
   }
   const int s = z / a.nk / a.ntg;
   const SubInfo& sub = a.subs[s];
@@ -668,13 +710,22 @@ __global__ void __launch_bounds__(MW * MWAVES, OCC ? OCC : (AHEAD2 ? 1 : 4)) tp_
   const int A = strip * MOUT + sub.ioff;
   const bool ex = !(A - 1 >= 2 && A + MOUT + 1 <= sub.N - 2);
   if constexpr (EXS == 1) {
-    if (ex) tp_march_strip<ORD, true, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1);
+    if (ex) tp_march_strip<ORD, true, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1, pair);
   } else if constexpr (EXS == 2) {
-    if (!ex) tp_march_strip<ORD, false, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1);
+    if (!ex) tp_march_strip<ORD, false, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1, pair);
   } else {
-    if (ex) tp_march_strip<ORD, true, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1);
-    else tp_march_strip<ORD, false, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1);
+    if (ex) tp_march_strip<ORD, true, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1, pair);
+    else tp_march_strip<ORD, false, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1, pair);
   }
+}
+
+// whether the last strip of a row has at most MOUT_H outputs (edges 0 .. nx), so that one
+// wave runs it for two levels
+bool pair_last_strip(const Dims& d, int nstrip) {
+  if (nstrip < 2) return false;
+  const int rem = d.nx + 1 - (nstrip - 1) * MOUT;
+  if (getenv("GTFV3_TP_NOPAIR")) return false;
+  return rem >= 1 && rem <= MOUT_H;
 }
 
 // Fraction of the (sub-domain, strip) pairs of a launch whose strip reaches a tile edge
@@ -704,9 +755,15 @@ void march2(const Ctx& c, const TpM& m0, double bytes, const char* name_ex, cons
     throw std::runtime_error("fv_tp_2d: too many (sub-domain, strip) pairs for one launch");
   auto go = [&](const std::vector<int>& pr, bool ex) {
     TpM m = m0;
-    m.npair = (int)pr.size();
-    for (int q = 0; q < m.npair; ++q) m.pairs[q] = pr[q];
-    const long waves = (long)m.ntg * m.nk * m.npair * m.nseg;
+    // full strips first, then the paired last strips
+    std::vector<int> full, half;
+    for (int v : pr) ((m0.pairlast && (v & 255) == m0.nstrip - 1) ? half : full).push_back(v);
+    m.npair = (int)full.size();
+    m.npairh = (int)half.size();
+    for (int q = 0; q < m.npair; ++q) m.pairs[q] = full[q];
+    for (int q = 0; q < m.npairh; ++q) m.pairs[m.npair + q] = half[q];
+    const long kh = (m.nk + 1) / 2;
+    const long waves = (long)m.ntg * m.nseg * ((long)m.nk * m.npair + kh * m.npairh);
     if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
     const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
     if (ex) GT_LAUNCH_N(name_ex, (tp_march<ORD, A2_EX, MF, NF, TM, OCC_EX, 1>), g, b, 0, c.st, m);
@@ -876,6 +933,7 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     m.d = d;
     m.subs = c.subs;
     m.M = c.met;
+  m.area2 = c.area2;
     const long tstride = (long)a.nk * d.plane;  // next tracer of the same sub-domain
     m.qf[0] = a.q;
     m.qf[1] = pair2 ? a.q2 : a.q + tstride;
@@ -929,7 +987,9 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     // measured 314 against 245 us per single-field launch at C180: two launch tails, and
     // the interior strips' rows are not 128-B aligned, so they are no cheaper)
     // MF: separate mass fluxes (w, pt and the tracers) or xfx / yfx themselves
-    const long waves = nz * m.nstrip * m.nseg;
+    // (the paired last strip of the split thermo march measured 7 us slower per launch here,
+    // 242 -> 249 us at C180, in either wave order: single-kernel marches keep one level per wave)
+    const long waves = (long)m.nseg * nz * m.nstrip;
     if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
     const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
 #define TP_GO(O, M_, F_)                                                                           \
@@ -966,6 +1026,7 @@ void d_sw_thermo_march(const Ctx& c, const ThermoArgs& a) {
   m.d = d;
   m.subs = c.subs;
   m.M = c.met;
+  m.area2 = c.area2;
   m.qf[0] = a.delp; m.qf[1] = a.w; m.qf[2] = a.pt;
   m.qo[0] = a.delp_o; m.qo[1] = a.w_o; m.qo[2] = a.pt_o;
   m.nt = 1;
@@ -984,6 +1045,7 @@ void d_sw_thermo_march(const Ctx& c, const ThermoArgs& a) {
   m.nstrip = nstrip;
   m.nseg = (d.ny + m.seg - 1) / m.seg;
   if (m.seg + 10 > DXL_ROWS) throw std::runtime_error("d_sw thermo march: segment longer than the LDS dxa rows");
+  m.pairlast = pair_last_strip(d, nstrip) ? 1 : 0;
   // delp w pt read and written, crx cry xfx yfx read, mfx mfy read and written; the
   // interior strips prefetch one row ahead to fit two waves per SIMD (233 VGPRs; the
   // tile-edge form takes 292 with the two-ahead prefetch)

@@ -134,6 +134,30 @@ def test_d_sw_thermo_march_matches_separate_launches(pkg, require_gpu, npx, layo
     d.close()
 
 
+def test_paired_last_strip_bitwise(pkg, require_gpu, monkeypatch):
+    """At C180 the last strip of a march row has 7 outputs (181 edges = 3 x 58 + 7), so one
+    wave runs it for two levels (lanes 0-31 level k, 32-63 level k+1).  d_sw -- the split
+    thermo march and the single-kernel vorticity / delp marches -- with and without the
+    pairing, bit for bit, on an odd level count (the last level unpaired)."""
+    npz = 3
+    d = pkg.Domain(npx=181, npz=npz, nq=1)
+    r = rng(79)
+    inp = sw_inputs(d, npz, r)
+    sh = d.shape(npz)
+    inp.update(uc=15.0 * r.standard_normal(sh), vc=15.0 * r.standard_normal(sh),
+               ua=15.0 * r.standard_normal(sh), va=15.0 * r.standard_normal(sh))
+    monkeypatch.setenv("GTFV3_TP_NOPAIR", "1")
+    b = _d_sw_run(d, inp, npz, True, tag="n_")
+    monkeypatch.delenv("GTFV3_TP_NOPAIR")
+    a = _d_sw_run(d, inp, npz, True, tag="p_")
+    nx, ny = d.nx, d.ny
+    for n in ("delp", "pt", "w", "mfx", "mfy", "cx", "cy", "u", "v"):
+        ga = a[n][..., NG:NG + ny + 1, NG:NG + nx + 1]
+        gb = b[n][..., NG:NG + ny + 1, NG:NG + nx + 1]
+        assert np.array_equal(ga, gb), f"{n}: paired last strip differs from one level per wave"
+    d.close()
+
+
 def test_d_sw_parity_c180(pkg, require_gpu):
     """d_sw (fused thermo march) against the oracle at C180 on two levels."""
     npz = 2
