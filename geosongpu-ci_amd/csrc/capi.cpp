@@ -308,6 +308,7 @@ void* gtfv3_stream(void* h) {
 
 int gtfv3_timers(void* h, char* buf, int len) {
   API_TRY
+  D(h)->flush_all_timers();
   std::string s;
   for (auto& kv : D(h)->timers) s += kv.first + "=" + std::to_string(kv.second) + ";";
   if (buf && len > 0) {

@@ -101,6 +101,9 @@ Dycore::~Dycore() {
   if (darea2) (void)hipFree(darea2);
   for (hipEvent_t e : {ev_fork, ev_b, ev_c})
     if (e) (void)hipEventDestroy(e);
+  for (auto& set : ev_ph)
+    for (hipEvent_t e : set)
+      if (e) (void)hipEventDestroy(e);
   if (st_b) (void)hipStreamDestroy(st_b);
   if (st_c) (void)hipStreamDestroy(st_c);
   if (st) (void)hipStreamDestroy(st);
@@ -215,6 +218,7 @@ void Dycore::set_vertical(const double* ak_, const double* bk_, int ks_) {
   ak.assign(ak_, ak_ + nl.npz + 1);
   bk.assign(bk_, bk_ + nl.npz + 1);
   ks = ks_;
+  vert_dirty = true;
 }
 
 // tracer_2d_1l (FV3 fv_tracer2d): large-time-step transport of nq tracers with
@@ -312,6 +316,7 @@ const double* Dycore::vertical_dev() {
   if ((int)ak.size() != k1) throw std::runtime_error("step: set_vertical() was not called");
   if (3L * k1 > d.plane) throw std::runtime_error("vertical table larger than one plane");
   Field& v = field("_vert", 1);
+  if (!vert_dirty) return v.p;  // uploaded once per set_vertical(), not per step
   std::vector<double> h(3 * k1, 0.0);
   for (int k = 0; k < k1; ++k) {
     h[k] = ak[k];
@@ -320,6 +325,7 @@ const double* Dycore::vertical_dev() {
   for (int k = 0; k < nl.npz; ++k) h[2 * k1 + k] = (ak[k + 1] - ak[k]) + (bk[k + 1] - bk[k]) * 1.0e5;
   HIP_CHECK(hipMemcpyAsync(v.p, h.data(), sizeof(double) * h.size(), hipMemcpyHostToDevice, st));
   HIP_CHECK(hipStreamSynchronize(st));
+  vert_dirty = false;
   return v.p;
 }
 
@@ -396,8 +402,15 @@ void Dycore::step() {
   const double* bk_dev = vert + k1;
   const double* dp_ref = vert + 2 * k1;
 
-  hipEvent_t ev[5];
-  for (auto& e : ev) HIP_CHECK(hipEventCreate(&e));
+  // phase events in a two-step ring: the slot's previous step (two steps ago) has completed
+  // by now -- the tracer step's pinned-memory read waits for its own step mid-way, so the
+  // host is never more than one step ahead -- and its times are read without a stall
+  const int slot = ev_slot;
+  ev_slot ^= 1;
+  if (ev_pending[slot]) flush_timers(slot);
+  if (!ev_ph[slot][0])
+    for (auto& e : ev_ph[slot]) HIP_CHECK(hipEventCreate(&e));
+  hipEvent_t* ev = ev_ph[slot];
   HIP_CHECK(hipEventRecord(ev[0], st));
 
   Field& u = need("u", npz);
@@ -621,6 +634,12 @@ void Dycore::step() {
   halo_update({{"u", 'd'}, {"v", 'd'}});
   c2l_ord4(c, npz, u.p, v.p, ua, va);
   HIP_CHECK(hipEventRecord(ev[4], st));
+  ev_pending[slot] = true;
+  if (ktimer_enabled()) ktimer_flush();
+}
+
+void Dycore::flush_timers(int slot) {
+  hipEvent_t* ev = ev_ph[slot];
   HIP_CHECK(hipEventSynchronize(ev[4]));
   const char* names[4] = {"dyn_core", "tracer_2d", "remap", "exit"};
   for (int n = 0; n < 4; ++n) {
@@ -632,8 +651,15 @@ void Dycore::step() {
   HIP_CHECK(hipEventElapsedTime(&tot, ev[0], ev[4]));
   timers["fv_dynamics"] += tot;
   timers["steps"] += 1;
-  if (ktimer_enabled()) ktimer_flush();
-  for (auto& e : ev) (void)hipEventDestroy(e);
+  ev_pending[slot] = false;
+}
+
+void Dycore::flush_all_timers() {
+  // oldest first
+  for (int n = 0; n < 2; ++n) {
+    const int slot = (ev_slot + n) & 1;
+    if (ev_pending[slot]) flush_timers(slot);
+  }
 }
 
 }  // namespace gtfv3

@@ -52,6 +52,14 @@ class Dycore {
   std::vector<double> ak, bk;  // npz+1
   int ks = 0;
   std::map<std::string, double> timers;  // accumulated ms per phase (events)
+  // phase events of the last two steps (the step does not wait for its own end: a step's
+  // events are read two steps later, or when the timers are queried)
+  hipEvent_t ev_ph[2][5] = {};
+  bool ev_pending[2] = {false, false};
+  int ev_slot = 0;
+  bool vert_dirty = true;
+  void flush_timers(int slot);  // accumulate a completed step's phase times
+  void flush_all_timers();
   // tracer_2d: the reduced per-level Courant maxima come back to the host through pinned
   // memory after an event, while the first tracer sub-step already runs
   double* h_cmax = nullptr;
