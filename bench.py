@@ -145,6 +145,10 @@ def parse():
     p.add_argument("--streams", type=int, default=3, choices=(1, 3),
                    help="streams of the timed steps (3: wind stages, update_dz_d and the tracer "
                         "transport beside the main chain; 1: everything on one stream)")
+    p.add_argument("--rank-proxy", type=int, default=0,
+                   help="measurement aid, one GPU: run rank 0 of an N-rank layout alone with the null "
+                        "transport (cross-rank messages dropped) -- the per-GPU compute time of an N-GPU "
+                        "run without the exchange; not a numerical result")
     p.add_argument("--roofline-steps", type=int, default=3,
                    help="steps of the single-stream roofline pass after the timed region")
     p.add_argument("--moist", action="store_true",
@@ -227,10 +231,14 @@ def main():
         obj = [pkg.unique_id() if rank == 0 else None]
         dist.broadcast_object_list(obj, src=0)
         nccl_id = obj[0]
-    lx, ly = (tuple(int(v) for v in a.layout.split("x")) if a.layout else layout_for(world))
+    proxy = a.rank_proxy if world == 1 and a.rank_proxy > 1 else 0
+    lx, ly = (tuple(int(v) for v in a.layout.split("x")) if a.layout else layout_for(proxy or world))
     t_init = time.perf_counter()
     nq = max(a.nq, 6) if a.moist else a.nq
-    d = pkg.Domain(rank, world, nccl_id, npx=a.npx, npz=a.npz, nq=nq, layout_x=lx, layout_y=ly, dt=a.dt)
+    if proxy:
+        d = pkg.Domain(0, proxy, None, npx=a.npx, npz=a.npz, nq=nq, layout_x=lx, layout_y=ly, dt=a.dt, loopback=-1)
+    else:
+        d = pkg.Domain(rank, world, nccl_id, npx=a.npx, npz=a.npz, nq=nq, layout_x=lx, layout_y=ly, dt=a.dt)
     ak, bk, ks = state.hybrid_levels(a.npz)
     # large tracer sets (the C720 L137 x 54 configuration's per-GPU share) go up one tracer
     # at a time, so the host never holds all of them
@@ -353,7 +361,13 @@ def main():
                                    backend="hip-gfx950-f64", step_seconds=per_step, init_s=t_init,
                                    run_s=sum(per_step), finalize_s=time.perf_counter() - t_fin)
 
-    check = state_check(d, ak[0])  # every rank checks its own sub-domains
+    if proxy:
+        try:
+            check = state_check(d, ak[0])
+        except SystemExit as e:  # remote halos never refreshed: the state is not meaningful
+            check = dict(not_checked=str(e)[:80])
+    else:
+        check = state_check(d, ak[0])  # every rank checks its own sub-domains
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
@@ -386,6 +400,9 @@ def main():
             "cpu_baseline": cpu,
             "state_check": check,
         }
+        if proxy:
+            out["metric"] += f" (rank proxy: one rank of {proxy}, no halo exchange; not a measured N-GPU run)"
+            out["rank_proxy"] = proxy
         print(json.dumps(out))
     d.close()
     if world > 1:

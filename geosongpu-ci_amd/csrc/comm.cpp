@@ -163,6 +163,20 @@ class LoopbackTransport : public Transport {
   std::vector<Pending> sends_, recvs_;
 };
 
+// ---- null (measurement only) ----
+// One rank of a multi-rank layout alone on a device: cross-rank messages are dropped (the
+// remote halo points keep their values), so the rank's kernels run exactly the work of its
+// share of the layout -- the per-GPU compute time of an N-GPU run without the exchange
+// (bench.py --rank-proxy).  Never a numerical path.
+class NullTransport : public Transport {
+ public:
+  void group_start() override {}
+  void send(const double*, size_t, int, hipStream_t) override {}
+  void recv(double*, size_t, int, hipStream_t) override {}
+  void group_end(hipStream_t) override {}
+  void allreduce_max(double*, int, hipStream_t) override {}
+};
+
 }  // namespace
 
 std::unique_ptr<Transport> make_nccl_transport(int nranks, int rank, const void* nccl_id) {
@@ -170,6 +184,7 @@ std::unique_ptr<Transport> make_nccl_transport(int nranks, int rank, const void*
 }
 
 std::unique_ptr<Transport> make_loopback_transport(int group, int nranks, int rank) {
+  if (group < 0) return std::make_unique<NullTransport>();
   return std::make_unique<LoopbackTransport>(group, nranks, rank);
 }
 

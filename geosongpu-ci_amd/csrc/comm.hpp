@@ -25,6 +25,7 @@ class Transport {
 };
 
 std::unique_ptr<Transport> make_nccl_transport(int nranks, int rank, const void* nccl_id);
+// group < 0: the null transport (one rank alone, messages dropped: measurement only)
 std::unique_ptr<Transport> make_loopback_transport(int group, int nranks, int rank);
 
 }  // namespace gtfv3

@@ -320,15 +320,21 @@ __device__ __forceinline__ bool ring2_point(int t, int nx, int ny, int& i, int& 
   return false;
 }
 
-// One lane per ring column walking the levels top-down: the interface pressure is the
-// running sum ptop + delp[0] + ... + delp[k] (the same additions in the same order as a
-// per-level sum from the top), pk3 = exp(kappa log pe) per interface; the loads of a block
-// of levels are issued together and the transcendentals of different levels overlap.
+// One lane per (ring column, block of PK_B levels): the interface pressure of level k+1
+// is the running sum ptop + delp[0] + ... + delp[k], which each lane forms from the top
+// with the same additions in the same order (bit-identical to one sequential walk, and to
+// the interior columns' values); pk3 = exp(kappa log pe).  The blocks give the ring's few
+// columns (a band of 180 x 45: ~900 per sub-domain) nine lanes each, so the transcendentals
+// of a column's levels run in parallel instead of one after another.
+constexpr int PK_B = 8;
 __global__ void __launch_bounds__(64) pk3_pe_halo_k(Dims d, int npz, double ptop, int do_pe,
                                                     const double* __restrict__ delp, double* __restrict__ pk3,
                                                     double* __restrict__ pe) {
+  const int nb = (npz + PK_B - 1) / PK_B;
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = t % nb;
   int i, j;
-  if (!ring2_point(blockIdx.x * blockDim.x + threadIdx.x, d.nx, d.ny, i, j)) return;
+  if (!ring2_point(t / nb, d.nx, d.ny, i, j)) return;
   const int s = blockIdx.y;
   const long o = pidx(d, i, j);
   const int km = npz, k1 = npz + 1;
@@ -336,18 +342,25 @@ __global__ void __launch_bounds__(64) pk3_pe_halo_k(Dims d, int npz, double ptop
   const double* DP = delp + (long)s * km * P + o;
   const bool ring1 = i >= -1 && i <= d.nx && j >= -1 && j <= d.ny;
   const long b1 = (long)s * k1 * P + o;
-  if (do_pe && ring1) pe[b1] = ptop;
+  const int k0 = b * PK_B, k1e = k0 + PK_B < km ? k0 + PK_B : km;
+  if (do_pe && ring1 && b == 0) pe[b1] = ptop;
   double pei = ptop;
-  constexpr int KB = 8;
-  for (int k0 = 0; k0 < km; k0 += KB) {
-    double dv[KB];
+  // the sum in blocks of PK_B loads issued together (one memory latency per block)
+  for (int m0 = 0; m0 < k0; m0 += PK_B) {
+    double v[PK_B];
 #pragma unroll
-    for (int m = 0; m < KB; ++m) dv[m] = k0 + m < km ? DP[(long)(k0 + m) * P] : 0.0;
+    for (int u = 0; u < PK_B; ++u) v[u] = DP[(long)(m0 + u) * P];
 #pragma unroll
-    for (int m = 0; m < KB; ++m) {
-      if (k0 + m >= km) break;
-      pei = pei + dv[m];
-      const long x = b1 + (long)(k0 + m + 1) * P;
+    for (int u = 0; u < PK_B; ++u) pei = pei + v[u];
+  }
+  double v[PK_B];
+#pragma unroll
+  for (int u = 0; u < PK_B; ++u) v[u] = k0 + u < k1e ? DP[(long)(k0 + u) * P] : 0.0;
+#pragma unroll
+  for (int u = 0; u < PK_B; ++u) {
+    if (k0 + u < k1e) {
+      pei = pei + v[u];
+      const long x = b1 + (long)(k0 + u + 1) * P;
       pk3[x] = exp(KAPPA * log(pei));
       if (do_pe && ring1) pe[x] = pei;
     }
@@ -883,8 +896,9 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
 void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* delp, double* pk3, double* pe) {
   const Dims& d = c.d;
   const int nring = 4 * (d.nx + 4) + 4 * d.ny;
-  GT_LAUNCH(pk3_pe_halo_k, dim3(cdiv(nring, 64), d.nsub), dim3(64), 0, c.st, d, npz, ptop, do_pe ? 1 : 0, delp, pk3,
-            pe);
+  const int nb = (npz + PK_B - 1) / PK_B;
+  GT_LAUNCH(pk3_pe_halo_k, dim3(cdiv(nring * nb, 64), d.nsub), dim3(64), 0, c.st, d, npz, ptop, do_pe ? 1 : 0, delp,
+            pk3, pe);
   HIP_LAUNCH_CHECK();
   gt_bytes((double)d.nsub * npz * (4.0 * (d.nx + 2) + 4.0 * d.ny) * (do_pe ? 3 : 2));  // halo ring only
 }

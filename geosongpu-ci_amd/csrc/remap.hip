@@ -335,27 +335,24 @@ struct RemapArgs {
 };
 
 // theta_v -> T_v (kord_tm < 0 remaps T_v in log p) and delz -> -delz/delp, into the
-// source slots of the T and delz jobs, before any job overwrites delz / pt
+// source slots of the T and delz jobs, before any job overwrites delz / pt; one lane per
+// (column, level) (pointwise: the levels run in parallel)
 __global__ void __launch_bounds__(BLOCK) remap_prep_k(RemapArgs a) {
   const Dims& d = a.d;
   const int km = a.npz, k1 = km + 1;
   const int c = blockIdx.x * BLOCK + threadIdx.x;
-  const int s = blockIdx.y;
+  const int s = blockIdx.y / km, k = blockIdx.y % km;
   if (c >= d.nx * d.ny) return;
   const int i = c % d.nx, j = c / d.nx;
   const long P = d.plane, o = pidx(d, i, j);
   const double rrg = -RDGAS / GRAV;
   const double k1k = KAPPA / (1.0 - KAPPA);
-  const double* DELP = a.S.delp + (long)s * km * P + o;
-  const double* DELZ = a.S.delz + (long)s * km * P + o;
-  const double* PT = a.S.pt + (long)s * km * P + o;
+  const long x = ((long)s * km + k) * P + o;
   double* TV = a.src + ((long)s * a.nslot + J_PT) * k1 * P + o;
   double* DZ = a.src + ((long)s * a.nslot + J_DZ) * k1 * P + o;
-  for (int k = 0; k < km; ++k) {
-    const double pt = PT[k * P];
-    TV[k * P] = pt * exp(k1k * log(rrg * DELP[k * P] / DELZ[k * P] * pt));
-    DZ[k * P] = -DELZ[k * P] / DELP[k * P];
-  }
+  const double pt = a.S.pt[x], dp = a.S.delp[x], dz = a.S.delz[x];
+  TV[k * P] = pt * exp(k1k * log(rrg * dp / dz * pt));
+  DZ[k * P] = -dz / dp;
 }
 
 __global__ void __launch_bounds__(BLOCK) remap_job_k(RemapArgs a) {
@@ -797,12 +794,14 @@ __global__ void __launch_bounds__(64) remap_reg_k(RemapArgs a) {
   }
 }
 
-// Eulerian state from the remapped fields
+// Eulerian state from the remapped fields, one lane per (column, interface k = 0 .. km): the
+// top interface of layer k is ptop (k = 0) or ak + bk ps, its log the stored peln (k = 0, km)
+// or the log of that -- the same values a top-down walk carries from layer to layer
 __global__ void __launch_bounds__(BLOCK) remap_finish_k(RemapArgs a) {
   const Dims& d = a.d;
   const int km = a.npz, k1 = km + 1;
   const int c = blockIdx.x * BLOCK + threadIdx.x;
-  const int s = blockIdx.y;
+  const int s = blockIdx.y / k1, k = blockIdx.y % k1;
   if (c >= d.nx * d.ny) return;
   const int i = c % d.nx, j = c / d.nx;
   const long P = d.plane, o = pidx(d, i, j);
@@ -811,29 +810,29 @@ __global__ void __launch_bounds__(BLOCK) remap_finish_k(RemapArgs a) {
   double* PE = a.S.pe + b1;
   double* PELN = a.S.peln + b1;
   double* PK = a.S.pk + b1;
+  const double psurf = PE[km * P];
+  if (k == km) {  // bottom interface: peln kept, pk from it
+    const double pn = PELN[km * P];
+    PK[km * P] = exp(KAPPA * pn);
+    PELN[km * P] = pn;
+    return;
+  }
+  if (k == 0) a.S.ps[(long)s * P + o] = psurf;
   double* DELP = a.S.delp + bk;
   double* DELZ = a.S.delz + bk;
   double* PT = a.S.pt + bk;
   double* PKZ = a.S.pkz + bk;
-  const double psurf = PE[km * P];
-  a.S.ps[(long)s * P + o] = psurf;
-  double pe_t = a.ptop, pn_t = PELN[0];
-  for (int k = 0; k < km; ++k) {
-    const double pe_b = k + 1 == km ? psurf : a.ak[k + 1] + a.bk[k + 1] * psurf;
-    const double pn_b = k + 1 == km ? PELN[km * P] : log(pe_b);
-    const double dp2 = pe_b - pe_t;
-    const double dz = -DELZ[k * P] * dp2;
-    DELZ[k * P] = dz;
-    DELP[k * P] = dp2;
-    PK[k * P] = exp(KAPPA * pn_t);
-    PELN[k * P] = pn_t;
-    PKZ[k * P] = exp(KAPPA * log(rrg * dp2 / dz * PT[k * P]));
-    if (k >= 1) PE[k * P] = pe_t;
-    pe_t = pe_b;
-    pn_t = pn_b;
-  }
-  PK[km * P] = exp(KAPPA * pn_t);
-  PELN[km * P] = pn_t;
+  const double pe_t = k == 0 ? a.ptop : a.ak[k] + a.bk[k] * psurf;
+  const double pn_t = k == 0 ? PELN[0] : log(pe_t);
+  const double pe_b = k + 1 == km ? psurf : a.ak[k + 1] + a.bk[k + 1] * psurf;
+  const double dp2 = pe_b - pe_t;
+  const double dz = -DELZ[k * P] * dp2;
+  DELZ[k * P] = dz;
+  DELP[k * P] = dp2;
+  PK[k * P] = exp(KAPPA * pn_t);
+  PELN[k * P] = pn_t;
+  PKZ[k * P] = exp(KAPPA * log(rrg * dp2 / dz * PT[k * P]));
+  if (k >= 1) PE[k * P] = pe_t;
 }
 
 }  // namespace
@@ -873,7 +872,7 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
   const Ext e = ext(d);
   const double L = npz, L1 = npz + 1;
   if (p1) {
-    GT_LAUNCH(remap_prep_k, dim3(cdiv(nc, BLOCK), d.nsub), dim3(BLOCK), 0, c.st, a);
+    GT_LAUNCH(remap_prep_k, dim3(cdiv(nc, BLOCK), d.nsub * npz), dim3(BLOCK), 0, c.st, a);
     HIP_LAUNCH_CHECK();
     gt_bytes(L * 5 * e.C);  // delp delz pt read, T_v and -delz/delp source columns written
   }
@@ -921,7 +920,7 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
   }
   HIP_LAUNCH_CHECK();
   if (!p2) return;
-  GT_LAUNCH(remap_finish_k, dim3(cdiv(nc, BLOCK), d.nsub), dim3(BLOCK), 0, c.st, a);
+  GT_LAUNCH(remap_finish_k, dim3(cdiv(nc, BLOCK), d.nsub * (npz + 1)), dim3(BLOCK), 0, c.st, a);
   HIP_LAUNCH_CHECK();
   // reads delz pt (L) pe peln (L+1); writes delz delp pkz (L) pk peln pe (L+1) ps
   gt_bytes(L * 5 * e.C + L1 * 5 * e.C + e.C);
