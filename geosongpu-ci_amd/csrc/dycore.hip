@@ -333,8 +333,8 @@ const double* Dycore::vertical_dev() {
 // k_split remap cycles of n_split acoustic sub-steps, tracer_2d_1l, Lagrangian-to-
 // Eulerian remap, then T/omega/A-grid winds for the caller).
 // Aquaplanet moist physics on the device-resident state after
-// fv_dynamics, in the order of GEOS's GFDL_1M run (GFDL_1M.drawio): aerosol activation,
-// the evap_subl_pdf loop (anvil evaporation / sublimation, large-scale PDF condensation),
+// fv_dynamics, in the order of GEOS's moist run (GFDL_1M.drawio): aerosol activation, the
+// shallow cumulus (cup_gf_sh), the evap_subl_pdf loop (anvil evaporation / sublimation, large-scale PDF condensation),
 // the GFDL cloud microphysics driver, RADCOUPLE.  T = pt, species = tracers 0..5 (qv ql qr
 // qi qs qg; ql / qi are the large-scale condensate), anvil condensate and the cloud
 // fractions in their own fields (qlcn, qicn, clcn, clls), surface precipitation into
@@ -353,8 +353,24 @@ void Dycore::moist_physics(double dt) {
   auto F = [&](const char* n) { return field(n, npz).p; };
   double *pl = F("_m_pl"), *zm = F("_m_zm"), *nactl = F("nactl"), *nacti = F("nacti"), *smax = F("_m_smax");
   double *qlcn = F("qlcn"), *qicn = F("qicn"), *clls = F("clls"), *clcn = F("clcn");
-  moist_prep(c, npz, need("pe", npz + 1).p, delz, pl, zm);
+  double* kpbl = field("_m_kpbl", 1).p;
+  if (!find("hfx")) {  // no surface model here: a uniform sensible heat flux drives the shallow plumes
+    Field& h = field("hfx", 1);
+    fill_field(c, field_elems(1), kSurfaceHfx, h.p);
+  }
+  moist_prep(c, npz, need("pe", npz + 1).p, delz, pl, zm, kpbl);
   aer_activation(c, npz, qsub, pl, T, qv, zm, need("w", npz).p, nactl, nacti, smax);
+  GfShArgs gf{};
+  gf.nk = npz;
+  gf.qv_sub = qsub;
+  gf.dt = dt;
+  gf.T = T; gf.qv = qv; gf.pl = pl; gf.zm = zm; gf.dp = need("delp", npz).p;
+  gf.kpbl = kpbl; gf.hfx = need("hfx", 1).p; gf.qlcn = qlcn; gf.qicn = qicn;
+  gf.cf = F("_m_cfcn"); gf.mb = field("gf_mb", 1).p; gf.k22 = field("gf_k22", 1).p;
+  gf.kbcon = field("gf_kbcon", 1).p; gf.ktop = field("gf_ktop", 1).p;
+  gf.scr = field("_gf_scr", gf_scratch_levels(npz)).p;
+  cup_gf_sh(c, gf);
+  max_field(c, field_elems(npz), gf.cf, clcn);  // convective cloud fraction into the anvil fraction
   EvapSublArgs e{};
   e.nk = npz;
   e.dt = dt;

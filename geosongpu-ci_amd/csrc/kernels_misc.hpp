@@ -13,5 +13,7 @@ void fv_wrapup(const Ctx& c, int npz, int nq, double zvir, const double* q, cons
 void c2l_ord4(const Ctx& c, int npz, const double* u, const double* v, double* ua, double* va);
 void held_suarez(const Ctx& c, int npz, double dt, const double* pe, double* pt, double* u, double* v);
 void fill_field(const Ctx& c, long n, double a, double* x);
+// y = max(y, x) elementwise
+void max_field(const Ctx& c, long n, const double* x, double* y);
 
 }  // namespace gtfv3

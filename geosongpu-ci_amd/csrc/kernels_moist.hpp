@@ -48,8 +48,29 @@ void radcouple(const Ctx& c, const RadcoupleArgs& a);
 void aer_activation(const Ctx& c, int nk, long qv_sub, const double* pl, const double* t, const double* qv,
                     const double* zm, const double* w, double* nactl, double* nacti, double* smax);
 
-// layer pressure from the interfaces pe and layer-mid heights from delz (surface at 0)
-void moist_prep(const Ctx& c, int nk, const double* pe, const double* dz, double* pl, double* zm);
+// GEOS cup_gf_sh shallow cumulus (Grell-Freitas shallow plume): source level, cloud base,
+// entraining updraft, cloud top, convective-velocity closure, flux-form tendencies of T and
+// qv, detrained condensate added to qlcn / qicn, convective cloud fraction, index fields
+struct GfShArgs {
+  int nk;
+  long qv_sub = 0;  // levels per sub-domain of qv (0: nk)
+  double dt;
+  double *T, *qv;                             // updated in place
+  const double *pl, *zm, *dp;                 // layer pressure (Pa), mid heights (m), delp (Pa)
+  const double *kpbl, *hfx;                   // 2-D: PBL-top level index, sensible heat flux (W m-2)
+  double *qlcn, *qicn;                        // detrained condensate added
+  double *cf, *mb, *k22, *kbcon, *ktop;       // cloud fraction (L); 2-D mass flux and indices (-1: none)
+  double* scr;                                // gf_scratch_levels(nk) planes per sub-domain
+};
+int gf_scratch_levels(int nk);
+// uniform surface sensible heat flux (W m-2) of the Aquaplanet coupling when no "hfx" field
+// was uploaded (no surface model on this path)
+constexpr double kSurfaceHfx = 15.0;
+void cup_gf_sh(const Ctx& c, const GfShArgs& a);
+
+// layer pressure from the interfaces pe, layer-mid heights from delz (surface at 0) and the
+// PBL-top level index (the highest level below 1 km)
+void moist_prep(const Ctx& c, int nk, const double* pe, const double* dz, double* pl, double* zm, double* kpbl);
 
 // parcel buoyancy (per level), CAPE, CIN and the LCL level index (-1: none)
 void buoyancy(const Ctx& c, int nk, const double* t, const double* qv, const double* pm, const double* zm,

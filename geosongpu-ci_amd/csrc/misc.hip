@@ -137,6 +137,12 @@ __global__ void fill_k(long n, double a, double* __restrict__ x) {
   for (; t < n; t += stride) x[t] = a;
 }
 
+__global__ void max_k(long n, const double* __restrict__ x, double* __restrict__ y) {
+  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  long stride = (long)gridDim.x * blockDim.x;
+  for (; t < n; t += stride) y[t] = fmax(y[t], x[t]);
+}
+
 inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
   (void)d;
   return plane_grid(L, nz);
@@ -194,6 +200,12 @@ void fill_field(const Ctx& c, long n, double a, double* x) {
   GT_LAUNCH(fill_k, dim3(cdiv(n, 256) < 8192 ? cdiv(n, 256) : 8192), dim3(256), 0, c.st, n, a, x);
   HIP_LAUNCH_CHECK();
   gt_bytes((double)n);
+}
+
+void max_field(const Ctx& c, long n, const double* x, double* y) {
+  GT_LAUNCH(max_k, dim3(cdiv(n, 256) < 8192 ? cdiv(n, 256) : 8192), dim3(256), 0, c.st, n, x, y);
+  HIP_LAUNCH_CHECK();
+  gt_bytes(3.0 * n);
 }
 
 }  // namespace gtfv3

@@ -899,22 +899,211 @@ __global__ void __launch_bounds__(256) aer_activation_k(AerArgs a) {
   a.smax[x] = smax;
 }
 
-// layer pressure from the interfaces and layer-mid heights from delz (surface at 0)
+// ---- shallow cumulus (GEOS cup_gf_sh; oracle/gf_shallow.py), one lane per column ----
+// Source level, cloud base, entraining plume and cloud top are column walks; the plume's
+// moist static energy, total water, normalised mass flux and condensate live in HBM scratch
+// columns between the walk and the flux-form tendencies.  Same expressions and order as the
+// oracle; the level indices k22 / kbcon / ktop come out bit-exact.
+constexpr double GF_DT_PERT = 0.5, GF_DP_BASE = 1.5e4, GF_DP_DEPTH = 3.0e4, GF_EPS = 1.0e-3, GF_DEL = 0.75e-3;
+constexpr double GF_C_MB = 0.03, GF_W_UP = 1.0, GF_CF_MAX = 0.3;
+constexpr int GF_NSCR = 4;
+
+struct GfArgs {
+  Dims d;
+  int nk;
+  long qsub;
+  double dt;
+  Tables tb;
+  double *T, *qv;
+  const double *pl, *zm, *dp, *kpbl, *hfx;
+  double *qlcn, *qicn, *cf, *mb, *k22, *kbcon, *ktop;
+  double* scr;  // GF_NSCR * nk planes per sub-domain
+};
+
+__global__ void __launch_bounds__(256) cup_gf_sh_k(GfArgs a) {
+  int s;
+  long o;
+  if (!col_point(a.d, s, o)) return;
+  const long P = a.d.plane;
+  const int n = a.nk;
+  double* __restrict__ T = a.T + (long)s * n * P + o;
+  double* __restrict__ QV = a.qv + (long)s * a.qsub * P + o;
+  const double* __restrict__ PL = a.pl + (long)s * n * P + o;
+  const double* __restrict__ ZM = a.zm + (long)s * n * P + o;
+  const double* __restrict__ DP = a.dp + (long)s * n * P + o;
+  double* __restrict__ HC = a.scr + (long)s * GF_NSCR * n * P + o;
+  double* __restrict__ QT = HC + (long)n * P;
+  double* __restrict__ ZU = QT + (long)n * P;
+  double* __restrict__ QC = ZU + (long)n * P;
+  const long p2 = (long)s * P + o;
+  const double kpd = a.kpbl[p2], hf = a.hfx[p2];
+  a.mb[p2] = 0.0;
+  a.k22[p2] = -1.0;
+  a.kbcon[p2] = -1.0;
+  a.ktop[p2] = -1.0;
+  for (int k = 0; k < n; ++k) a.cf[(long)(s * n + k) * P + o] = 0.0;
+  auto L = [&](int k) { return (long)k * P; };
+  // environment at level k: h, h*, qsat, gamma
+  auto env = [&](int k, double& h, double& hs, double& qs, double& gm) {
+    const double t = T[L(k)];
+    double dqs;
+    qsat(a.tb, false, t, PL[L(k)], qs, dqs);
+    h = CP_AIR * t + GRAV * ZM[L(k)] + HLV * QV[L(k)];
+    hs = CP_AIR * t + GRAV * ZM[L(k)] + HLV * qs;
+    gm = HLV / CP_AIR * dqs;
+  };
+  const int kp = (int)kpd;
+  double hx, hsx, qsx, gx;
+  env(n - 1, hx, hsx, qsx, gx);
+  int k22 = n - 1;
+  double h22 = hx;
+  for (int k = n - 2; k >= kp; --k) {
+    env(k, hx, hsx, qsx, gx);
+    if (hx > h22) {
+      k22 = k;
+      h22 = hx;
+    }
+  }
+  const double hp = h22 + CP_AIR * GF_DT_PERT;
+  const double qp = QV[L(k22)];
+  const double pl22 = PL[L(k22)];
+  int kb = -1;
+  for (int k = k22; k >= 0; --k) {
+    if (PL[L(k)] < pl22 - GF_DP_BASE) break;
+    env(k, hx, hsx, qsx, gx);
+    if (hp >= hsx) {
+      kb = k;
+      break;
+    }
+  }
+  if (kb < 1 || hf <= 0.0) return;
+  HC[L(kb)] = hp;
+  QT[L(kb)] = qp;
+  ZU[L(kb)] = 1.0;
+  int kt = kb;
+  const double plb = PL[L(kb)];
+  {
+    double hcp = hp, qtp = qp, zup = 1.0, zp = ZM[L(kb)];
+    for (int k = kb - 1; k >= 0; --k) {
+      if (PL[L(k)] < plb - GF_DP_DEPTH) break;
+      const double zk = ZM[L(k)];
+      const double dz = zk - zp;
+      const double aa = 0.5 * GF_EPS * dz;
+      env(k, hx, hsx, qsx, gx);
+      const double hn = (hcp * (1.0 - aa) + 2.0 * aa * hx) / (1.0 + aa);
+      if (hn < hsx) break;
+      const double qn = (qtp * (1.0 - aa) + 2.0 * aa * QV[L(k)]) / (1.0 + aa);
+      const double zn = zup * (1.0 + (GF_EPS - GF_DEL) * dz);
+      HC[L(k)] = hn;
+      QT[L(k)] = qn;
+      ZU[L(k)] = zn;
+      hcp = hn;
+      qtp = qn;
+      zup = zn;
+      zp = zk;
+      kt = k;
+    }
+  }
+  if (kt == kb) return;
+  for (int k = k22; k > kb; --k) {
+    HC[L(k)] = hp;
+    QT[L(k)] = qp;
+    ZU[L(k)] = 1.0;
+  }
+  for (int k = kt; k <= kb; ++k) {
+    env(k, hx, hsx, qsx, gx);
+    const double qsat_c = qsx + gx / (1.0 + gx) * (HC[L(k)] - hsx) / HLV;
+    QC[L(k)] = fmax(QT[L(k)] - qsat_c, 0.0);
+  }
+  // flux-form tendencies per unit mb (the eddy flux through the upper interface of layer k
+  // is zero at kt and below k22)
+  auto eflux = [&](int k, double& eh, double& eq) {
+    if (k <= kt || k > k22) {
+      eh = 0.0;
+      eq = 0.0;
+      return;
+    }
+    double h, hs, qs, gm;
+    env(k, h, hs, qs, gm);
+    const double zu = ZU[L(k)];
+    eh = zu * (HC[L(k)] - h);
+    eq = zu * (QT[L(k)] - QV[L(k)]);
+  };
+  const double dc = GRAV * ZU[L(kt + 1)] * QC[L(kt + 1)] / DP[L(kt)];
+  const double dt = a.dt;
+  // closure and the vapour limiter
+  const double tb = T[L(n - 1)];
+  const double rhob = PL[L(n - 1)] / (RDGAS * tb);
+  const double zi = ZM[L(kp)];
+  const double wst = cbrt(GRAV / tb * hf / (rhob * CP_AIR) * zi);
+  double mb = GF_C_MB * (PL[L(k22)] / (RDGAS * T[L(k22)])) * wst;
+  {
+    double eha, eqa, ehb, eqb;
+    eflux(kt, eha, eqa);
+    for (int k = kt; k <= k22; ++k) {
+      eflux(k + 1, ehb, eqb);
+      double dqv = GRAV * (eqb - eqa) / DP[L(k)];
+      if (k == kt) dqv = dqv - dc;
+      if (dqv < 0.0) mb = fmin(mb, 0.9 * QV[L(k)] / (-dt * dqv));
+      eha = ehb;
+      eqa = eqb;
+    }
+  }
+  if (!(mb > 0.0)) return;
+  // cloud fraction (initial-state density), then the tendencies (fluxes from the initial
+  // state: each level's two interface fluxes are formed before the level is updated)
+  for (int k = kt; k <= kb; ++k) {
+    const double rho = PL[L(k)] / (RDGAS * T[L(k)]);
+    a.cf[(long)(s * n + k) * P + o] = fmin(GF_CF_MAX, mb * ZU[L(k)] / (rho * GF_W_UP));
+  }
+  {
+    double eha, eqa, ehb, eqb;
+    eflux(kt, eha, eqa);
+    for (int k = kt; k <= k22; ++k) {
+      eflux(k + 1, ehb, eqb);
+      const double dh = GRAV * (ehb - eha) / DP[L(k)];
+      double dq = GRAV * (eqb - eqa) / DP[L(k)];
+      if (k == kt) dq = dq - dc;
+      const double dqk = mb * dq;
+      const double t0 = T[L(k)], q0 = QV[L(k)];
+      QV[L(k)] = q0 + dt * dqk;
+      T[L(k)] = t0 + dt * (mb * dh - HLV * dqk) / CP_AIR;
+      eha = ehb;
+      eqa = eqb;
+    }
+  }
+  const double fi = fmin(fmax((T_ICE - T[L(kt)]) / 40.0, 0.0), 1.0);
+  const long xt = (long)(s * n + kt) * P + o;
+  a.qicn[xt] = a.qicn[xt] + dt * mb * dc * fi;
+  a.qlcn[xt] = a.qlcn[xt] + dt * mb * dc * (1.0 - fi);
+  a.mb[p2] = mb;
+  a.k22[p2] = (double)k22;
+  a.kbcon[p2] = (double)kb;
+  a.ktop[p2] = (double)kt;
+}
+
+// layer pressure from the interfaces, layer-mid heights from delz (surface at 0), and the
+// PBL-top level index: the highest level whose mid height is below Z_PBL
+constexpr double Z_PBL = 1000.0;
 __global__ void __launch_bounds__(256) moist_prep_k(Dims d, int nk, const double* __restrict__ pe,
                                                      const double* __restrict__ dz, double* __restrict__ pl,
-                                                     double* __restrict__ zm) {
+                                                     double* __restrict__ zm, double* __restrict__ kpbl) {
   int s;
   long o;
   if (!col_point(d, s, o)) return;
   const long P = d.plane;
   const long b = (long)s * nk * P + o, be = (long)s * (nk + 1) * P + o;
   double zb = 0.0;
+  int kp = nk - 1;
   for (int k = nk - 1; k >= 0; --k) {
     const double zt = zb - dz[b + k * P];
-    zm[b + k * P] = 0.5 * (zt + zb);
+    const double z = 0.5 * (zt + zb);
+    zm[b + k * P] = z;
     pl[b + k * P] = 0.5 * (pe[be + k * P] + pe[be + (k + 1) * P]);
+    if (z < Z_PBL) kp = k;
     zb = zt;
   }
+  kpbl[(long)s * P + o] = (double)kp;
 }
 
 // ---- buoyancy, CAPE / CIN, LCL index (one bottom-up pass) ----
@@ -1086,8 +1275,21 @@ void aer_activation(const Ctx& c, int nk, long qv_sub, const double* pl, const d
   ktimer_bytes(8.0 * c.d.nx * c.d.ny * c.d.nsub * nk * 8.0);
 }
 
-void moist_prep(const Ctx& c, int nk, const double* pe, const double* dz, double* pl, double* zm) {
-  GT_LAUNCH(moist::moist_prep_k, moist::colgrid(c.d), dim3(BX, BY), 0, c.st, c.d, nk, pe, dz, pl, zm);
+int gf_scratch_levels(int nk) { return moist::GF_NSCR * nk; }
+
+void cup_gf_sh(const Ctx& c, const GfShArgs& g) {
+  if (!g.scr) throw std::runtime_error("cup_gf_sh: scratch planes required");
+  if (g.nk < 3) throw std::runtime_error("cup_gf_sh: nk >= 3 required");
+  moist::GfArgs a{c.d, g.nk, g.qv_sub > 0 ? g.qv_sub : g.nk, g.dt, moist::device_tables(), g.T, g.qv, g.pl, g.zm, g.dp,
+                  g.kpbl, g.hfx, g.qlcn, g.qicn, g.cf, g.mb, g.k22, g.kbcon, g.ktop, g.scr};
+  GT_LAUNCH(moist::cup_gf_sh_k, moist::colgrid(c.d), dim3(BX, BY), 0, c.st, a);
+  HIP_LAUNCH_CHECK();
+  // T qv read and written, pl zm dp read, cf written (L each); qlcn qicn at one level
+  ktimer_bytes(8.0 * c.d.nx * c.d.ny * c.d.nsub * (8.0 * g.nk + 9.0));
+}
+
+void moist_prep(const Ctx& c, int nk, const double* pe, const double* dz, double* pl, double* zm, double* kpbl) {
+  GT_LAUNCH(moist::moist_prep_k, moist::colgrid(c.d), dim3(BX, BY), 0, c.st, c.d, nk, pe, dz, pl, zm, kpbl);
   HIP_LAUNCH_CHECK();
   ktimer_bytes(8.0 * c.d.nx * c.d.ny * c.d.nsub * (4.0 * nk + 1.0));
 }

@@ -329,13 +329,32 @@ std::map<std::string, Fn>& reg() {
          aer_activation(dy.ctx(), t.nk, 0, F(dy, f[0]).p, t.p, F(dy, f[2]).p, F(dy, f[3]).p, F(dy, f[4]).p,
                         dy.field(f[5], t.nk).p, dy.field(f[6], t.nk).p, dy.field(f[7], t.nk).p);
        }},
-      // moist_prep(pe, delz | pl, zm): layer pressure and layer-mid heights
+      // cup_gf_sh(T, qv, pl, zm, delp, kpbl, hfx, qlcn, qicn | cf, mb, k22, kbcon, ktop) params: dt; T, qv, qlcn, qicn in place
+      {"cup_gf_sh",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 14, "cup_gf_sh");
+         Field& t = F(dy, f[0]);
+         for (int n : {1, 2, 3, 4, 7, 8})
+           if (F(dy, f[n]).nk != t.nk) throw std::runtime_error("cup_gf_sh: fields must share the level count");
+         GfShArgs a{};
+         a.nk = t.nk;
+         a.dt = p.at(0);
+         a.T = t.p; a.qv = F(dy, f[1]).p; a.pl = F(dy, f[2]).p; a.zm = F(dy, f[3]).p; a.dp = F(dy, f[4]).p;
+         a.kpbl = F(dy, f[5]).p; a.hfx = F(dy, f[6]).p; a.qlcn = F(dy, f[7]).p; a.qicn = F(dy, f[8]).p;
+         a.cf = dy.field(f[9], t.nk).p;
+         a.mb = dy.field(f[10], 1).p; a.k22 = dy.field(f[11], 1).p; a.kbcon = dy.field(f[12], 1).p;
+         a.ktop = dy.field(f[13], 1).p;
+         a.scr = dy.field("_gf_scr", gf_scratch_levels(t.nk)).p;
+         cup_gf_sh(dy.ctx(), a);
+       }},
+      // moist_prep(pe, delz | pl, zm, kpbl): layer pressure, layer-mid heights, PBL-top level
       {"moist_prep",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
-         need(f, 4, "moist_prep");
+         need(f, 5, "moist_prep");
          Field& dz = F(dy, f[1]);
          if (F(dy, f[0]).nk != dz.nk + 1) throw std::runtime_error("moist_prep: pe must have nk+1 levels");
-         moist_prep(dy.ctx(), dz.nk, F(dy, f[0]).p, dz.p, dy.field(f[2], dz.nk).p, dy.field(f[3], dz.nk).p);
+         moist_prep(dy.ctx(), dz.nk, F(dy, f[0]).p, dz.p, dy.field(f[2], dz.nk).p, dy.field(f[3], dz.nk).p,
+                    dy.field(f[4], 1).p);
        }},
       // buoyancy(T, qv, pm, zm | buoy, cape, cin, klcl)
       {"buoyancy",

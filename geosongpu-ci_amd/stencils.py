@@ -69,7 +69,8 @@ gfdl_1m = StencilDef("gfdl_1m", 13, tuple(range(7)) + (9, 10, 11, 12), ("dt",))
 evap_subl_pdf = StencilDef("evap_subl_pdf", 11, tuple(range(8)), ("dt",))
 radcouple = StencilDef("radcouple", 22, tuple(range(13, 22)))
 aer_activation = StencilDef("aer_activation", 8, (5, 6, 7))
-moist_prep = StencilDef("moist_prep", 4, (2, 3))
+moist_prep = StencilDef("moist_prep", 5, (2, 3, 4))
+cup_gf_sh = StencilDef("cup_gf_sh", 14, (0, 1, 7, 8, 9, 10, 11, 12, 13), ("dt",))
 buoyancy = StencilDef("buoyancy", 8, (4, 5, 6, 7))
 
 

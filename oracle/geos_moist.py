@@ -229,39 +229,54 @@ def aer_activation(pl, t, qv, zm, w):
     return nact, nacti, smax
 
 
+Z_PBL = 1000.0
+HFX_SURF = 15.0   # the Aquaplanet coupling's uniform surface sensible heat flux (W m-2)
+
+
 def moist_prep(pe, dz):
-    """layer pressure from the interfaces and layer-mid heights from delz (surface at 0)"""
+    """layer pressure from the interfaces, layer-mid heights from delz (surface at 0) and the
+    PBL-top level index (the highest level whose mid height is below Z_PBL)"""
     nk = dz.shape[0]
     pl = 0.5 * (pe[:-1] + pe[1:])
     zm = np.empty_like(dz)
     zb = np.zeros(dz.shape[1:])
+    kp = np.full(dz.shape[1:], float(nk - 1))
     for k in range(nk - 1, -1, -1):
         zt = zb - dz[k]
         zm[k] = 0.5 * (zt + zb)
+        kp = np.where(zm[k] < Z_PBL, float(k), kp)
         zb = zt
-    return pl, zm
+    return pl, zm, kp
 
 
-def aquaplanet_physics(dt, t, qv, ql, qr, qi, qs, qg, dp, dz, pe, w, qlcn=None, qicn=None, clls=None, clcn=None):
-    """GEOS GFDL_1M run order on column arrays [k, ...]: aer_activation, evap_subl_pdf,
-    the GFDL microphysics driver (oracle/gfdl_mp.py mpdrv), radcouple.  Returns a dict of
+def aquaplanet_physics(dt, t, qv, ql, qr, qi, qs, qg, dp, dz, pe, w, qlcn=None, qicn=None, clls=None, clcn=None,
+                       hfx=HFX_SURF):
+    """GEOS moist run order on column arrays [k, ...]: aer_activation, cup_gf_sh (the shallow
+    cumulus, oracle/gf_shallow.py), evap_subl_pdf, the GFDL microphysics driver
+    (oracle/gfdl_mp.py mpdrv), radcouple.  Returns a dict of
     the updated state (t, qv, ql, qr, qi, qs, qg, qlcn, qicn, clls, clcn), the surface
     precipitation (prec_rain, prec_snow, prec_graupel, prec_ice), nactl, nacti and the
     radiation fields rad_*."""
-    from . import gfdl_mp
+    from . import gf_shallow, gfdl_mp
     z = np.zeros_like(t)
     qlcn = z if qlcn is None else qlcn
     qicn = z if qicn is None else qicn
     clls = z if clls is None else clls
     clcn = z if clcn is None else clcn
-    pl, zm = moist_prep(pe, dz)
+    pl, zm, kpbl = moist_prep(pe, dz)
     nactl, nacti, _ = aer_activation(pl, t, qv, zm, w)
+    g = gf_shallow.cup_gf_sh(dt, t, qv, pl, zm, dp, kpbl, np.full(t.shape[1:], hfx))
+    t, qv = g["t"], g["qv"]
+    qlcn = qlcn + g["dqlcn"]
+    qicn = qicn + g["dqicn"]
+    clcn = np.maximum(clcn, g["cf"])
     e = evap_subl_pdf(dt, pl, t, qv, ql, qi, qlcn, qicn, clls, clcn, nactl, nacti)
     (t1, qv1, ql1, qr1, qi1, qs1, qg1), prec = gfdl_mp.mpdrv(e["t"], dp, dz, e["qv"], e["qlls"], qr, e["qils"],
                                                              qs, qg, dt)
     r = radcouple(t1, pl, e["clls"], e["clcn"], qv1, ql1, qi1, e["qlcn"], e["qicn"], qr1, qs1, qg1, nactl, nacti)
     out = dict(t=t1, qv=qv1, ql=ql1, qr=qr1, qi=qi1, qs=qs1, qg=qg1, qlcn=e["qlcn"], qicn=e["qicn"],
                clls=e["clls"], clcn=e["clcn"], prec_rain=prec[0], prec_snow=prec[1], prec_graupel=prec[2],
-               prec_ice=prec[3], nactl=nactl, nacti=nacti)
+               prec_ice=prec[3], nactl=nactl, nacti=nacti, gf_mb=g["mb"], gf_k22=g["k22"], gf_kbcon=g["kbcon"],
+               gf_ktop=g["ktop"])
     out.update(r)
     return out

@@ -12,6 +12,7 @@ import pytest
 from moist_inputs import moist_state
 from oracle import NG
 from oracle import geos_moist as gm
+from oracle import gf_shallow as gf
 from oracle import gfdl_mp as mp
 from oracle import moist as om
 
@@ -148,6 +149,48 @@ def test_aer_activation_matches_oracle(dom, require_gpu):
     close(comp(dom, dom.download("m_nactl")), comp(dom, na), "nactl")
     close(comp(dom, dom.download("m_nacti")), comp(dom, ni), "nacti")
     close(comp(dom, dom.download("m_smax")), comp(dom, sm), "smax")
+
+
+def test_cup_gf_sh_matches_oracle(dom, require_gpu):
+    """the shallow cumulus on the device against oracle/gf_shallow.py on a sample of columns:
+    T, qv, the detrained condensate, the cloud fraction and the cloud-base mass flux within
+    the bars; the source / cloud-base / cloud-top level indices bit-exact"""
+    st = moist_state(dom.shape(NK), seed=31)
+    sh = st["T"].shape
+    r = np.random.default_rng(32)
+    kpbl = np.zeros((sh[0], 1) + sh[2:])
+    for s in range(sh[0]):   # PBL top: the highest level below 1 km
+        z = st["zm"][s]
+        kpbl[s, 0] = np.where(z < 1000.0, np.arange(NK)[:, None, None], NK - 1).min(axis=0)
+    hfx = 5.0 + 30.0 * r.random((sh[0], 1) + sh[2:])
+    z0 = np.zeros(sh)
+    upload_state(dom, dict(st, kpbl=kpbl, hfx=hfx, qlcn=z0, qicn=z0))
+    dt = 450.0
+    names = ["m_T", "m_qv", "m_pm", "m_zm", "m_delp", "m_kpbl", "m_hfx", "m_qlcn", "m_qicn",
+             "m_cf", "m_mb", "m_k22", "m_kbcon", "m_ktop"]
+    dom.stencil("cup_gf_sh", names, [dt])
+    got = {n: dom.download(n) for n in names}
+    active = 0
+    for s, rows in SAMPLE:
+        c = {k: cols_of(dom, st[k], s, rows) for k in ("T", "qv", "pm", "zm", "delp")}
+        kp = cols_of(dom, kpbl, s, rows)[0]
+        hf = cols_of(dom, hfx, s, rows)[0]
+        ref = gf.cup_gf_sh(dt, c["T"], c["qv"], c["pm"], c["zm"], c["delp"], kp, hf)
+        for n, k in (("m_T", "t"), ("m_qv", "qv"), ("m_qlcn", "dqlcn"), ("m_qicn", "dqicn"), ("m_cf", "cf")):
+            close(cols_of(dom, got[n], s, rows), ref[k], (n, s), floor=1e-30)
+        close(cols_of(dom, got["m_mb"], s, rows)[0], ref["mb"], ("mb", s), floor=1e-30)
+        for n, k in (("m_k22", "k22"), ("m_kbcon", "kbcon"), ("m_ktop", "ktop")):
+            np.testing.assert_array_equal(cols_of(dom, got[n], s, rows)[0], ref[k], err_msg=n)
+        active += int((ref["ktop"] >= 0).sum())
+    assert active > 0, "no shallow convection in the sample"
+    # column moist static energy and water are conserved on the device everywhere
+    cp, lv = om.CP_AIR, om.HLV
+    h0 = np.einsum("skji,skji->sji", cp * st["T"] + lv * st["qv"], st["delp"])
+    h1 = np.einsum("skji,skji->sji", cp * got["m_T"] + lv * got["m_qv"], st["delp"])
+    w0 = np.einsum("skji,skji->sji", st["qv"], st["delp"])
+    w1 = np.einsum("skji,skji->sji", got["m_qv"] + got["m_qlcn"] + got["m_qicn"], st["delp"])
+    assert rel(comp(dom, h1), comp(dom, h0)) <= 1e-14
+    assert rel(comp(dom, w1), comp(dom, w0)) <= 1e-14
 
 
 def test_buoyancy_matches_oracle(dom, require_gpu):

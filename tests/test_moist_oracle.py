@@ -172,3 +172,27 @@ def test_buoyancy_lcl_and_cape():
     assert 0.0 <= klcl[2] < nk - 1.0
     assert np.all(cape >= 0.0) and np.all(cin <= 0.0)
     assert cape[1] > cape[0]
+
+
+def test_gf_shallow_conserves_and_finds_clouds():
+    """cup_gf_sh on the synthetic columns: column moist static energy and water conserved to
+    round-off, vapour non-negative, cloud base at or above the source level and below the
+    top, detrained condensate only in the top layer"""
+    from oracle import gf_shallow as gf
+    st = moist_state(SHAPE, seed=3)
+    T, qv, pl, zm, dp = cols(st, ("T", "qv", "pm", "zm", "delp"), n=60)
+    kp = np.where(zm < 1000.0, np.arange(T.shape[0])[:, None], T.shape[0] - 1).min(axis=0).astype(float)
+    r = gf.cup_gf_sh(450.0, T, qv, pl, zm, dp, kp, np.full(T.shape[1], 25.0))
+    act = r["ktop"] >= 0
+    assert act.sum() > 0
+    assert np.all(r["ktop"][act] < r["kbcon"][act]) and np.all(r["kbcon"][act] <= r["k22"][act])
+    h0 = ((om.CP_AIR * T + om.HLV * qv) * dp).sum(0)
+    h1 = ((om.CP_AIR * r["t"] + om.HLV * r["qv"]) * dp).sum(0)
+    w0 = (qv * dp).sum(0)
+    w1 = ((r["qv"] + r["dqlcn"] + r["dqicn"]) * dp).sum(0)
+    assert np.allclose(h1, h0, rtol=1e-14) and np.allclose(w1, w0, rtol=1e-14)
+    assert r["qv"].min() >= 0.0
+    cond = r["dqlcn"] + r["dqicn"]
+    for c in np.nonzero(act)[0]:
+        nz = np.nonzero(cond[:, c])[0]
+        assert set(nz) <= {int(r["ktop"][c])}
