@@ -602,7 +602,9 @@ void Dycore::step() {
     halo_update({{"delp", 'c'}, {"pt", 'c'}});
     HIP_CHECK(hipEventRecord(ev_b, st_b));
     HIP_CHECK(hipEventRecord(ev_c, st_c));
-    HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
+    // riem_solver3 needs update_dz_d's heights, not d_sw's winds: the wind stage (u, v) keeps
+    // running beside the Riemann solver, the halo updates, pk3 and gz, and is joined only
+    // before nh_p_grad, which updates u and v
     HIP_CHECK(hipStreamWaitEvent(st, ev_c, 0));
     }
     ra.last_call = last ? 1 : 0;
@@ -610,6 +612,7 @@ void Dycore::step() {
     halo_update({{"zh", 'c'}, {"ppe", 'c'}, {"w", 'c'}});
     pk3_pe_halo(c, npz, ptop, last, delp.p, pk3, pe);
     scale_field(c, field_elems(k1), Constants::grav, zh, gz);
+    if (fork_substep) HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
     nh_p_grad(c, pa);
     if (!last) halo_update({{"u", 'd'}, {"v", 'd'}});
   }
