@@ -268,40 +268,61 @@ __device__ __forceinline__ HaloSel halo_sel(const HaloBatch b, int f) {  // by v
   return r;
 }
 
+// Each thread moves one halo point for HK consecutive levels: the table entry is read once
+// per HK levels instead of once per level, and the HK loads are issued together.
+constexpr int HK = 8;
+
 __global__ void halo_local_kernel(HaloBatch b, long plane) {
   const HaloSel F = halo_sel(b, blockIdx.z);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const int k = blockIdx.y;
-  if (e >= F.n || k >= F.nk) return;
+  const int k0 = blockIdx.y * HK;
+  if (e >= F.n || k0 >= F.nk) return;
   const HaloEntry h = static_cast<const HaloEntry*>(F.tab)[e];
-  double v = 0.0;
-  if (h.src_sub >= 0) {
-    const double* src = (h.comp & 2) ? F.p1 : F.p0;
-    v = h.sign * src[((long)h.src_sub * F.nk + k) * plane + h.src_off];
-  }
+  const double* src = (h.comp & 2) ? F.p1 : F.p0;
   double* dst = (h.comp & 1) ? F.p1 : F.p0;
-  dst[((long)h.dst_sub * F.nk + k) * plane + h.dst_off] = v;
+  double v[HK];
+#pragma unroll
+  for (int u = 0; u < HK; ++u) {
+    const int k = k0 + u;
+    v[u] = (h.src_sub >= 0 && k < F.nk) ? h.sign * src[((long)h.src_sub * F.nk + k) * plane + h.src_off] : 0.0;
+  }
+#pragma unroll
+  for (int u = 0; u < HK; ++u) {
+    const int k = k0 + u;
+    if (k < F.nk) dst[((long)h.dst_sub * F.nk + k) * plane + h.dst_off] = v[u];
+  }
 }
 
 __global__ void halo_pack_kernel(HaloBatch b, long plane, double* __restrict__ buf) {
   const HaloSel F = halo_sel(b, blockIdx.z);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const int k = blockIdx.y;
-  if (e >= F.n || k >= F.nk) return;
+  const int k0 = blockIdx.y * HK;
+  if (e >= F.n || k0 >= F.nk) return;
   const PackEntry h = static_cast<const PackEntry*>(F.tab)[e];
   const double* src = h.comp ? F.p1 : F.p0;
-  buf[F.boff + (long)h.pstart * F.nk + (long)k * h.pcount + (e - h.pstart)] =
-      h.sign * src[((long)h.sub * F.nk + k) * plane + h.off];
+#pragma unroll
+  for (int u = 0; u < HK; ++u) {
+    const int k = k0 + u;
+    if (k < F.nk)
+      buf[F.boff + (long)h.pstart * F.nk + (long)k * h.pcount + (e - h.pstart)] =
+          h.sign * src[((long)h.sub * F.nk + k) * plane + h.off];
+  }
 }
 
 __global__ void halo_unpack_kernel(HaloBatch b, long plane, const double* __restrict__ buf) {
   const HaloSel F = halo_sel(b, blockIdx.z);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const int k = blockIdx.y;
-  if (e >= F.n || k >= F.nk) return;
+  const int k0 = blockIdx.y * HK;
+  if (e >= F.n || k0 >= F.nk) return;
   const PackEntry h = static_cast<const PackEntry*>(F.tab)[e];
   double* dst = h.comp ? F.p1 : F.p0;
-  dst[((long)h.sub * F.nk + k) * plane + h.off] = buf[F.boff + (long)h.pstart * F.nk + (long)k * h.pcount + (e - h.pstart)];
+#pragma unroll
+  for (int u = 0; u < HK; ++u) {
+    const int k = k0 + u;
+    if (k < F.nk)
+      dst[((long)h.sub * F.nk + k) * plane + h.off] =
+          buf[F.boff + (long)h.pstart * F.nk + (long)k * h.pcount + (e - h.pstart)];
+  }
 }
 
 }  // namespace
@@ -339,7 +360,7 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
         ++nb;
       }
       if (!nb) continue;
-      const dim3 g(cdiv(maxn, 256), maxk, nb);
+      const dim3 g(cdiv(maxn, 256), cdiv(maxk, HK), nb);
       if (stage == 0) GT_LAUNCH(halo_local_kernel, g, dim3(256), 0, stream, b, d_.plane);
       else if (stage == 1) GT_LAUNCH(halo_pack_kernel, g, dim3(256), 0, stream, b, d_.plane, sendbuf_);
       else GT_LAUNCH(halo_unpack_kernel, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
