@@ -269,9 +269,11 @@ __device__ __forceinline__ HaloSel halo_sel(const HaloBatch b, int f) {  // by v
 }
 
 // Each thread moves one halo point for HK consecutive levels: the table entry is read once
-// per HK levels instead of once per level, and the HK loads are issued together.
-constexpr int HK = 8;
-
+// per HK levels instead of once per level, and the HK loads are issued together.  HK = 8
+// where the exchange has work enough to fill the chip that way (one rank holding whole
+// tiles: C180 halo_local 0.93 -> 0.90 ms/step); HK = 1 for the smaller per-rank exchanges
+// (8-rank share: pack / unpack 0.29 -> 0.34-0.36 ms/step with HK = 8, too few threads).
+template <int HK>
 __global__ void halo_local_kernel(HaloBatch b, long plane) {
   const HaloSel F = halo_sel(b, blockIdx.z);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -293,6 +295,7 @@ __global__ void halo_local_kernel(HaloBatch b, long plane) {
   }
 }
 
+template <int HK>
 __global__ void halo_pack_kernel(HaloBatch b, long plane, double* __restrict__ buf) {
   const HaloSel F = halo_sel(b, blockIdx.z);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -309,6 +312,7 @@ __global__ void halo_pack_kernel(HaloBatch b, long plane, double* __restrict__ b
   }
 }
 
+template <int HK>
 __global__ void halo_unpack_kernel(HaloBatch b, long plane, const double* __restrict__ buf) {
   const HaloSel F = halo_sel(b, blockIdx.z);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -360,10 +364,17 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
         ++nb;
       }
       if (!nb) continue;
-      const dim3 g(cdiv(maxn, 256), cdiv(maxk, HK), nb);
-      if (stage == 0) GT_LAUNCH(halo_local_kernel, g, dim3(256), 0, stream, b, d_.plane);
-      else if (stage == 1) GT_LAUNCH(halo_pack_kernel, g, dim3(256), 0, stream, b, d_.plane, sendbuf_);
-      else GT_LAUNCH(halo_unpack_kernel, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
+      if ((long)cdiv(maxn, 256) * cdiv(maxk, 8) * nb >= 2048) {  // >= 8 workgroups per CU at HK = 8
+        const dim3 g(cdiv(maxn, 256), cdiv(maxk, 8), nb);
+        if (stage == 0) GT_LAUNCH_N("halo_local_kernel", halo_local_kernel<8>, g, dim3(256), 0, stream, b, d_.plane);
+        else if (stage == 1) GT_LAUNCH_N("halo_pack_kernel", halo_pack_kernel<8>, g, dim3(256), 0, stream, b, d_.plane, sendbuf_);
+        else GT_LAUNCH_N("halo_unpack_kernel", halo_unpack_kernel<8>, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
+      } else {
+        const dim3 g(cdiv(maxn, 256), maxk, nb);
+        if (stage == 0) GT_LAUNCH_N("halo_local_kernel", halo_local_kernel<1>, g, dim3(256), 0, stream, b, d_.plane);
+        else if (stage == 1) GT_LAUNCH_N("halo_pack_kernel", halo_pack_kernel<1>, g, dim3(256), 0, stream, b, d_.plane, sendbuf_);
+        else GT_LAUNCH_N("halo_unpack_kernel", halo_unpack_kernel<1>, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
+      }
       HIP_LAUNCH_CHECK();
       // every halo point of every level: one value read, one written
       double pts = 0.0;

@@ -308,18 +308,29 @@ __global__ void __launch_bounds__(BLOCK) riem_col_k(RiemArgs a) {
 //     neighbour changed that interface (exact; the clamp is rarely active).
 // Two per-layer arrays that live from the first sweep to the last (pm, g_rat) are
 // kept in LDS, the rest in VGPRs.
-constexpr int RB_NB = 4, RB_NC = 16, RB_WAVES = 4;
+//
+// A column whose level count is not a multiple of M (L137 = 7 x 18 + 11) runs as eight
+// blocks of eight columns with a partial last block (PARTIAL, MV < M real layers, a template
+// constant): its lanes' loads past the surface are masked to zero and their stores dropped,
+// and every recurrence starts or stops at the real bottom MV instead of M.
+constexpr int RB_WAVES = 4;
 typedef unsigned int RbU2 __attribute__((ext_vector_type(2)));
 // The pointwise loops are long straight-line runs of independent transcendentals; left
 // alone the scheduler interleaves all M of them and runs out of registers.  A fence per
 // level keeps one or two in flight (two waves per SIMD hide the latency instead).
 #define RB_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
-__device__ __forceinline__ double from_below(double v, int lane) { return __shfl(v, (lane + RB_NC) & 63); }
-__device__ __forceinline__ double from_above(double v, int lane) { return __shfl(v, (lane - RB_NC) & 63); }
+template <int NC>
+__device__ __forceinline__ double rb_below(double v, int lane) { return __shfl(v, (lane + NC) & 63); }
+template <int NC>
+__device__ __forceinline__ double rb_above(double v, int lane) { return __shfl(v, (lane - NC) & 63); }
 
-template <int M, bool CG>
+template <int M, bool CG, int NB = 4, int MV = M>
 __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
+  constexpr int RB_NB = NB, RB_NC = 64 / NB;
+  constexpr bool PARTIAL = MV < M;  // the last block holds MV < M layers (km = (nblk - 1) M + MV)
+  auto from_below = [](double v, int ln) { return rb_below<RB_NC>(v, ln); };
+  auto from_above = [](double v, int ln) { return rb_above<RB_NC>(v, ln); };
   __shared__ double lds_pm[RB_WAVES][M][64];
   __shared__ double lds_g[RB_WAVES][M][64];
   constexpr bool cg = CG;
@@ -327,7 +338,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
   const int b = lane / RB_NC;
   const Dims& d = a.d;
   const int km = a.npz;
-  const int nblk = km / M;  // launch_riem guarantees km = nblk * M, nblk <= 4
+  const int nblk = (km + M - 1) / M;  // launch_riem: nblk <= NB, km = (nblk - 1) M + MV
   const int ni = d.nx + 2 * a.ring, nj = d.ny + 2 * a.ring;
   const int ncol = ni * nj;
   const int s = blockIdx.y;
@@ -359,10 +370,20 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
     const long so = (long)s * (itf ? km + 1 : km) * P;
     return __builtin_amdgcn_make_buffer_rsrc((void*)(p + so), 0, itf ? li : ll, 0x00020000);
   };
-  auto ld = [&](__amdgpu_buffer_rsrc_t r, int m) {
+  // itf: an interface field (levels 0 .. km).  In a partial block the levels past the surface
+  // (static m >= MV, or > MV for interface fields) exist only for the other blocks' lanes: the
+  // last block's lanes read zero there and store nothing (masked, no access).
+  auto past = [&](int m, bool itf) { return PARTIAL && m >= MV + (itf ? 1 : 0); };
+  auto ld = [&](__amdgpu_buffer_rsrc_t r, int m, bool itf = false) {
+    if (past(m, itf)) {
+      double v = 0.0;
+      if (!lastblk) v = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lo, (uint32_t)m * PB, 0));
+      return v;
+    }
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lo, (uint32_t)m * PB, 0));
   };
-  auto st = [&](__amdgpu_buffer_rsrc_t r, int m, double v) {
+  auto st = [&](__amdgpu_buffer_rsrc_t r, int m, double v, bool itf = false) {
+    if (past(m, itf) && lastblk) return;
     __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), r, lo, (uint32_t)m * PB, 0);
   };
   const auto rG = rs(a.G, true), rPO = rs(a.pout, true);
@@ -371,7 +392,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
   // ---- loads
   double gr[M + 1], DP[M];
 #pragma unroll
-  for (int m = 0; m <= M; ++m) gr[m] = ld(rG, m);
+  for (int m = 0; m <= M; ++m) gr[m] = ld(rG, m, true);
 #pragma unroll
   for (int m = 0; m < M; ++m) DP[m] = ld(rDP, m);
   // surface values (re-read where used instead of held in registers)
@@ -394,10 +415,12 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
   // the unclamped interface below it, and repeats only if the block below changed it
   auto clamp = [&](const double (&g)[M + 1], double (&gl)[M + 1]) {
     double gin = g[M];  // unclamped interface kb1
+    if (PARTIAL && lastblk) gin = ld(rG, MV, true);  // the partial block's is the surface at MV
     for (int it = 0; it <= RB_NB; ++it) {
       gl[M] = gin;
 #pragma unroll
-      for (int m = M - 1; m >= 0; --m) gl[m] = fmax(g[m], gl[m + 1] + a.dz_min);
+      for (int m = M - 1; m >= 0; --m)
+        gl[m] = PARTIAL && lastblk && m >= MV ? gin : fmax(g[m], gl[m + 1] + a.dz_min);
       const double gn = from_below(gl[0], lane);
       const double want = lastblk || !act ? gin : gn;
       if (!__any(want != gin)) break;
@@ -446,11 +469,11 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
         if (valid && (m < M || lastblk)) {
           RB_SCHED_FENCE();
           const double pkk = exp(KAPPA * pln[m]);
-          st(rK3, m, pkk);
+          st(rK3, m, pkk, true);
           if (a.last_call) {
-            st(rs(a.pe, true), m, pem[m]);
-            st(rs(a.peln, true), m, pln[m]);
-            st(rs(a.pk, true), m, pkk);
+            st(rs(a.pe, true), m, pem[m], true);
+            st(rs(a.peln, true), m, pln[m], true);
+            st(rs(a.pk, true), m, pkk, true);
           }
         }
       }
@@ -471,7 +494,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
     const double dm_nb = from_below(dm[0], lane), pl_nb = from_below(pl[0], lane);
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      const bool bot = m == M - 1 && lastblk;
+      const bool bot = lastblk && m == MV - 1;
       const double dmn = m + 1 < M ? dm[m + 1 < M ? m + 1 : 0] : dm_nb;
       const double pln_ = m + 1 < M ? pl[m + 1 < M ? m + 1 : 0] : pl_nb;
       const double g = bot ? 0.0 : dm[m] / dmn;
@@ -498,7 +521,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
         pp[0] = cpp;
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          const bool bot = m == M - 1 && lastblk;
+          const bool bot = lastblk && m == MV - 1;
           const double g = sg[m][lane];
           const double bbk = bot ? 2.0 : 2.0 * (1.0 + g);
           double ppn;
@@ -511,6 +534,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
             bet = bbk - gm;
             ppn = (dd[m] - ppk) / bet;
           }
+          if (PARTIAL && lastblk && m >= MV) ppn = ppk;  // past the surface: pp[M] = pp[MV] for S2 and S3
           pp[m + 1] = ppn;
           ppk = ppn;
         }
@@ -531,7 +555,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
         double x = pp[M];
 #pragma unroll
         for (int m = M - 1; m >= 0; --m) {
-          if (m > 0 || b > 0) {
+          if ((m > 0 || b > 0) && !(PARTIAL && lastblk && m >= MV)) {
             x = pp[m] - gam[m] * x;
             pp[m] = x;
           }
@@ -551,7 +575,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
 #pragma unroll
       for (int m = 0; m < M; ++m) dpv[m] = ld(rDP, m);
 #pragma unroll
-      for (int m = 0; m <= M; ++m) g0[m] = ld(rG, m);  // the unclamped heights (G is written in S6)
+      for (int m = 0; m <= M; ++m) g0[m] = ld(rG, m, true);  // the unclamped heights (G is written in S6)
       prefix(dpv, pemr);
       clamp(g0, glr);
 #pragma unroll
@@ -570,8 +594,15 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
     const double aab_nb = from_below(aat[0], lane);
     double hs, zs, ws;
     surf(hs, zs, ws);
-    const double p1 = t1g / dz[M - 1] * (pemr[M] + pp[M]);
-    if (lastblk) num[M - 1] = num[M - 1] - p1 * ws;
+    double dzb = dz[M - 1];
+    if (PARTIAL && lastblk) {  // the bottom layer MV-1 of the partial block, clamped as in clamp()
+      const double gs = ld(rG, MV, true);
+      dzb = gs - fmax(ld(rG, MV - 1, true), gs + a.dz_min);
+    }
+    const double p1 = t1g / dzb * (pemr[M] + pp[M]);  // pemr, pp constant past the surface
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (lastblk && m == MV - 1) num[m] = num[m] - p1 * ws;
     aab_last = lastblk ? p1 : aab_nb;
   }
   double w2[M];
@@ -586,7 +617,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
         double bet = cbet, wp = cw;
 #pragma unroll
         for (int m = 0; m < M; ++m) {
-          const double aab = m + 1 < M ? aat[m + 1 < M ? m + 1 : 0] : aab_last;
+          const double aab = m + 1 < M && !(PARTIAL && lastblk && m == MV - 1) ? aat[m + 1 < M ? m + 1 : 0] : aab_last;
           if (m == 0 && b == 0) {
             bet = dm[m] - aab;
             wp = num[m] / bet;
@@ -616,9 +647,9 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
         double x = cx;
 #pragma unroll
         for (int m = M - 1; m >= 0; --m) {
-          if (m == M - 1 && lastblk) {
+          if (lastblk && m == MV - 1) {
             x = w2[m];
-          } else {
+          } else if (!(PARTIAL && lastblk && m >= MV)) {
             x = w2[m] - (m + 1 < M ? gam[m + 1 < M ? m + 1 : 0] : gam_nb) * x;
             w2[m] = x;
           }
@@ -641,8 +672,8 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
     const auto rw = rs(a.w2, true), rg = rs(a.gam, true);
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      st(rw, m, w2[m]);
-      st(rg, m, gam[m]);
+      st(rw, m, w2[m], true);
+      st(rg, m, gam[m], true);
     }
   }
   auto& pe = pp;  // pe replaces pp
@@ -662,7 +693,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
   if (a.dump && valid) {
     const auto rp = rs(a.pp, true);
 #pragma unroll
-    for (int m = 0; m < M; ++m) st(rp, m, pe[m]);
+    for (int m = 0; m < M; ++m) st(rp, m, pe[m], true);
   }
   RB_SCHED_FENCE();
   // ---- S6: p1 recurrence, dz2, heights (bottom-up)
@@ -673,7 +704,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
     for (int m = 0; m < M; ++m) {
       const double g = sg[m][lane];
       const double pe2 = m + 2 <= M ? pe[m + 2 <= M ? m + 2 : 0] : pe2_nb;
-      if (m == M - 1 && lastblk) t[m] = (pe[m] + 2.0 * pe[m + 1]) * R3;
+      if (lastblk && m == MV - 1) t[m] = (pe[m] + 2.0 * pe[m + 1]) * R3;
       else t[m] = (pe[m] + 2.0 * (1.0 + g) * pe[m + 1] + g * pe2) * R3;
     }
     double cp = 0.0;
@@ -683,7 +714,8 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
         double p1 = cp;
 #pragma unroll
         for (int m = M - 1; m >= 0; --m) {
-          if (m == M - 1 && lastblk) p1 = t[m];
+          if (PARTIAL && lastblk && m >= MV) continue;
+          if (lastblk && m == MV - 1) p1 = t[m];
           else p1 = t[m] - sg[m][lane] * p1;
           t[m] = p1;
         }
@@ -712,8 +744,8 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
         gz[M] = go;
 #pragma unroll
         for (int m = M - 1; m >= 0; --m) {
-          go = cg ? go - dz2[m] * GRAV : go - dz2[m];
-          gz[m] = go;
+          if (!(PARTIAL && lastblk && m >= MV)) go = cg ? go - dz2[m] * GRAV : go - dz2[m];
+          gz[m] = go;  // the partial block: the surface up to MV
         }
       }
       cg_in = from_below(gz[0], lane);
@@ -734,17 +766,17 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
       const auto rDZ = rs(a.delz, false);
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        st(rG, m, gz[m]);
+        st(rG, m, gz[m], true);
         if (cg) {
-          st(rPO, m, m == 0 && b == 0 ? a.ptop : pe[m] + pemr[m]);
+          st(rPO, m, m == 0 && b == 0 ? a.ptop : pe[m] + pemr[m], true);
         } else {
           st(rDZ, m, dz2[m]);
-          st(rPO, m, pe[m]);
+          st(rPO, m, pe[m], true);
         }
       }
       if (lastblk) {
-        st(rG, M, cg ? hs : zs);
-        st(rPO, M, cg ? pe[M] + pemr[M] : pe[M]);
+        st(rG, M, cg ? hs : zs, true);
+        st(rPO, M, cg ? pe[M] + pemr[M] : pe[M], true);
       }
     }
   }
@@ -755,11 +787,14 @@ void launch_riem(const Ctx& c, const RiemArgs& a) {
   if (a.npz < 2) throw std::runtime_error("riem: npz >= 2 required");
   const int km = a.npz;
   const int ncol = (c.d.nx + 2 * a.ring) * (c.d.ny + 2 * a.ring);
-  const dim3 gb(cdiv(cdiv(ncol, RB_NC), RB_WAVES), c.d.nsub);
+  const dim3 gb(cdiv(cdiv(ncol, 16), RB_WAVES), c.d.nsub);
+  const dim3 gb8(cdiv(cdiv(ncol, 8), RB_WAVES), c.d.nsub);
   const dim3 tb(64 * RB_WAVES);
   // blocked form when the column splits into at most four blocks of an instantiated size
-  auto fits = [&](int m) { return km % m == 0 && km / m <= RB_NB; };
+  // (16 columns a wave), or into up to eight blocks of 18 with a partial last one (8 columns)
+  auto fits = [&](int m) { return km % m == 0 && km / m <= 4; };
   const bool blk = riem_variant() != 1;
+  const bool part = blk && km == 7 * 18 + 11;  // L137
   if (blk && fits(3)) {
     if (a.cgrid) GT_LAUNCH((riem_blk_k<3, true>), gb, tb, 0, c.st, a);
     else GT_LAUNCH((riem_blk_k<3, false>), gb, tb, 0, c.st, a);
@@ -769,6 +804,9 @@ void launch_riem(const Ctx& c, const RiemArgs& a) {
   } else if (blk && fits(18)) {
     if (a.cgrid) GT_LAUNCH((riem_blk_k<18, true>), gb, tb, 0, c.st, a);
     else GT_LAUNCH((riem_blk_k<18, false>), gb, tb, 0, c.st, a);
+  } else if (part) {
+    if (a.cgrid) GT_LAUNCH((riem_blk_k<18, true, 8, 11>), gb8, tb, 0, c.st, a);
+    else GT_LAUNCH((riem_blk_k<18, false, 8, 11>), gb8, tb, 0, c.st, a);
   } else {
     GT_LAUNCH(riem_col_k, dim3(cdiv(ncol, BLOCK), c.d.nsub), dim3(BLOCK), 0, c.st, a);
   }

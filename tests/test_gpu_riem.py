@@ -64,7 +64,7 @@ def close(a, b, what, rtol=1e-11, atol=0.0):
     assert worst <= rtol, f"{what}: max scaled error {worst:.3e}"
 
 
-@pytest.mark.parametrize("npz,thin", [(12, True), (10, False), (72, True), (7, True)])
+@pytest.mark.parametrize("npz,thin", [(12, True), (10, False), (72, True), (7, True), (137, True), (137, False)])
 def test_riem_solver_c(pkg, require_gpu, npz, thin):
     d = pkg.Domain(npx=13, npz=npz, nq=1)
     r = rng(100 + npz)
@@ -90,7 +90,7 @@ def test_riem_solver_c(pkg, require_gpu, npz, thin):
         close(got[0]["rc_gz"][s], region(gzo, 1, d.nx, d.ny), f"sub{s} gz")
 
 
-@pytest.mark.parametrize("npz,last", [(12, 1), (72, 0), (10, 1)])
+@pytest.mark.parametrize("npz,last", [(12, 1), (72, 0), (10, 1), (137, 1), (137, 0)])
 def test_riem_solver3(pkg, require_gpu, npz, last):
     d = pkg.Domain(npx=13, npz=npz, nq=1)
     r = rng(200 + npz)
