@@ -90,6 +90,11 @@ def pmc_traffic(fam, launches):
             t = json.load(fh)
         keys = {k: k.strip("()").replace(" ", "") for k in launches}
         tk = {k.replace(" ", ""): v for k, v in t.items()}
+        for k, v in keys.items():  # rocprof spells out defaulted template arguments
+            if v not in tk and v.endswith(">"):
+                ext = [x for x in tk if x.startswith(v[:-1] + ",")]
+                if len(ext) == 1:
+                    keys[k] = ext[0]
         if keys and all(v in tk for v in keys.values()):
             tot = sum(tk[keys[k]]["traffic_bytes"] * n for k, n in launches.items())
             return tot / sum(launches.values()), os.path.basename(f)
