@@ -202,7 +202,7 @@ void Dycore::halo_update(const std::vector<std::pair<std::string, char>>& items)
       h.p[0] = fx->p;
       h.p[1] = fy->p;
       h.nk = fx->nk;
-      h.kind = k == 'd' ? H_DGRID : (k == 'C' ? H_CGRID : (k == 'S' ? H_CSYNC : H_AGRID));
+      h.kind = k == 'd' ? H_DGRID : k == 'C' ? H_CGRID : k == 'S' ? H_CSYNC : k == 'X' ? H_CSC : H_AGRID;
       ++n;
     }
     hf.push_back(h);
@@ -571,9 +571,9 @@ void Dycore::step() {
     // one value per shared tile-edge point: the east / north edges take the C-grid winds
     // the neighbouring tile computed there (otherwise the two tiles' winds differ next to
     // the cube corners -- the corner circulation of c_sw -- and so do their mass fluxes:
-    // a dry-mass drift of 3e-7 per step, 1.5e-11 with the sync)
-    halo_update({{"uc", 'S'}, {"vc", 'S'}});
-    halo_update({{"uc", 'C'}, {"vc", 'C'}});
+    // a dry-mass drift of 3e-7 per step, 1.5e-11 with the sync); the sync and the C halo
+    // as one exchange (H_CSC, bit-identical to 'S' then 'C')
+    halo_update({{"uc", 'X'}, {"vc", 'X'}});
     // fork: after the Courant numbers, the wind stage of d_sw (stream b) and update_dz_d
     // (stream c) run beside the mass / thermodynamic transport and its halo update (the
     // RCCL exchange of delp / pt then overlaps compute).  Default on (GTFV3_STREAMS=0: one

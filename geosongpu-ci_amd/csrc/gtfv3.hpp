@@ -80,7 +80,12 @@ enum HaloKind : int {
   H_CELL = 0, H_CORNER = 1, H_DGRID = 2, H_CGRID = 3, H_AGRID = 4,
   // C-grid tile-edge synchronisation: uc on east and vc on north tile edges take the
   // neighbouring tile's values at the same points (FV3 mpp_get_boundary; see halo.hip)
-  H_CSYNC = 5, H_NKIND = 6
+  H_CSYNC = 5,
+  // H_CSYNC then H_CGRID as ONE exchange: a C halo point whose source is a synchronised
+  // tile-edge point reads that point's own source instead (signs and components composed),
+  // so every value the exchange reads is one it does not write -- bit-identical to the two
+  // updates in sequence, with one message round per sub-step fewer
+  H_CSC = 6, H_NKIND = 7
 };
 
 // host-side sub-domain decomposition of the cubed sphere

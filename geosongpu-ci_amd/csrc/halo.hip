@@ -25,7 +25,8 @@ inline int comp_stagger(int kind, int c) {
     case H_CORNER: return CORNER;
     case H_DGRID: return c == 0 ? XEDGE : YEDGE;   // u along x-edges, v along y-edges
     case H_CGRID:
-    case H_CSYNC: return c == 0 ? YEDGE : XEDGE;   // uc normal to y-edges, vc to x-edges
+    case H_CSYNC:
+    case H_CSC: return c == 0 ? YEDGE : XEDGE;     // uc normal to y-edges, vc to x-edges
     default: return CELL;                           // A-grid pair
   }
 }
@@ -34,6 +35,7 @@ inline int ncomp(int kind) { return (kind == H_CELL || kind == H_CORNER) ? 1 : 2
 struct Src {
   int rank, lsub, off, comp, sign;
   bool zero;
+  int gsub, li, lj;  // global owner sub-domain and local point (for the H_CSC redirect)
 };
 
 }  // namespace
@@ -86,6 +88,7 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
         }
       }
     if (found < 0) throw std::runtime_error("halo: no owner sub-domain");
+    s.gsub = found; s.li = li; s.lj = lj;
     s.rank = dc.owner_rank(found);
     s.lsub = found % nper;
     s.off = (int)pidx(d, li, lj);
@@ -131,6 +134,18 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
     return s;
   };
 
+  // H_CSC: a C halo source that is itself a synchronised tile-edge point (uc on an east,
+  // vc on a north tile edge) is replaced by that point's synchronisation source
+  auto csc_redirect = [&](int kind, Src s) -> Src {
+    if (kind != H_CSC || s.zero) return s;
+    const SubInfo so = dc.sub(s.gsub);
+    const bool east = s.comp == 0 && so.ioff + nx == so.N && s.li == nx && s.lj >= 0 && s.lj < ny;
+    const bool north = s.comp == 1 && so.joff + ny == so.N && s.lj == ny && s.li >= 0 && s.li < nx;
+    if (!east && !north) return s;
+    Src t = resolve_edge(s.gsub, H_CSYNC, s.comp, s.li, s.lj, east ? 1 : 3);
+    t.sign *= s.sign;
+    return t;
+  };
   for (int kind = 0; kind < H_NKIND; ++kind) {
     h_local_[kind].clear();
     std::vector<std::vector<PackEntry>> send(nranks_), recv(nranks_);
@@ -141,14 +156,14 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
           int st = comp_stagger(kind, c);
           int sx = (st == YEDGE || st == CORNER) ? 1 : 0;
           int sy = (st == XEDGE || st == CORNER) ? 1 : 0;
-          if (kind == H_CSYNC) {
+          if (kind == H_CSYNC || kind == H_CSC) {
             // targets: uc on the east tile edge, vc on the north tile edge of this sub-domain
             const SubInfo si = dc.sub(g);
             const bool east = c == 0 && si.ioff + nx == si.N, north = c == 1 && si.joff + ny == si.N;
             const int n = east ? ny : (north ? nx : 0);
             for (int p = 0; p < n; ++p) {
               const int i = east ? nx : p, j = east ? p : ny;
-              Src s = resolve_edge(g, kind, c, i, j, east ? 1 : 3);
+              Src s = resolve_edge(g, H_CSYNC, c, i, j, east ? 1 : 3);
               if (q != rank_) {
                 if (s.rank == rank_) send[q].push_back({s.lsub, s.off, s.comp, s.sign, 0, 0});
                 continue;
@@ -157,7 +172,7 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
               if (s.rank == rank_) h_local_[kind].push_back({ls, doff, s.lsub, s.off, c | (s.comp << 1), s.sign});
               else recv[s.rank].push_back({ls, doff, c, 0, 0, 0});
             }
-            continue;
+            if (kind == H_CSYNC) continue;
           }
           for (int j = -NG; j <= ny - 1 + NG + sy; ++j)
             for (int i = -NG; i <= nx - 1 + NG + sx; ++i) {
@@ -165,11 +180,11 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
               if (inside) continue;
               if (q != rank_) {
                 // only needed when this rank is the owner of the source
-                Src s = resolve(g, kind, c, i, j);
+                Src s = csc_redirect(kind, resolve(g, kind, c, i, j));
                 if (!s.zero && s.rank == rank_) send[q].push_back({s.lsub, s.off, s.comp, s.sign, 0, 0});
                 continue;
               }
-              Src s = resolve(g, kind, c, i, j);
+              Src s = csc_redirect(kind, resolve(g, kind, c, i, j));
               int doff = (int)pidx(d, i, j);
               if (s.zero) h_local_[kind].push_back({ls, doff, -1, 0, c, 0});
               else if (s.rank == rank_)

@@ -116,3 +116,27 @@ def test_halo_tables_match_oracle(pkg, layout):
     np.testing.assert_array_equal(u, u2)
     np.testing.assert_array_equal(v, v2)
     assert not np.array_equal(u, r.standard_normal(shape))
+
+
+@pytest.mark.parametrize("layout", [(1, 1), (2, 2), (1, 2)])
+def test_merged_sync_and_cgrid_halo(pkg, layout):
+    """Kind 6 (H_CSC, the step's single exchange of uc / vc per sub-step) equals the tile-edge
+    synchronisation (kind 5) followed by the C-grid halo (kind 3), bit for bit, and so the
+    oracle's sync_edges + fill_vector("cgrid")."""
+    lx, ly = layout
+    d = host_domain(pkg, 13, lx, ly)
+    lay = ohalo.Layout(d.N, lx, ly)
+    r = rng(11)
+    shape = (d.nsub, 2, d.nj, d.pitch)
+    u = r.standard_normal(shape)
+    v = r.standard_normal(shape)
+    u2, v2, u3, v3 = u.copy(), v.copy(), u.copy(), v.copy()
+    _apply_table(pkg, d, 6, [u, v])
+    _apply_table(pkg, d, 5, [u2, v2])
+    _apply_table(pkg, d, 3, [u2, v2])
+    np.testing.assert_array_equal(u, u2)
+    np.testing.assert_array_equal(v, v2)
+    ohalo.sync_edges(u3, v3, lay, "cgrid")
+    ohalo.fill_vector(u3, v3, lay, "cgrid")
+    np.testing.assert_array_equal(u, u3)
+    np.testing.assert_array_equal(v, v3)

@@ -15,7 +15,7 @@ import torch.multiprocessing as mp
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 KINDS = ((0, "cell", None), (1, "corner", None), (2, None, "dgrid"), (3, None, "cgrid"), (4, None, "agrid"),
-         (5, None, "csync"))
+         (5, None, "csync"), (6, None, "csc"))
 
 
 def _free_port():
@@ -65,6 +65,9 @@ def _worker(rank, world, port, layout, q, npx=13):
                 ohalo.fill_scalar(ref[0], lay, st)
             elif vk == "csync":
                 ohalo.sync_edges(ref[0], ref[1], lay, "cgrid")
+            elif vk == "csc":  # the sync and the C halo as one exchange
+                ohalo.sync_edges(ref[0], ref[1], lay, "cgrid")
+                ohalo.fill_vector(ref[0], ref[1], lay, "cgrid")
             else:
                 ohalo.fill_vector(ref[0], ref[1], lay, vk)
             loc = [c[rank * nper:(rank + 1) * nper].reshape(nper, nk, -1).copy() for c in comps]
