@@ -546,9 +546,8 @@ void Dycore::step() {
     da.delp_o = alt[0]->p; da.w_o = alt[1]->p; da.pt_o = alt[2]->p;
   }
 
-  halo_update({{"u", 'd'}, {"v", 'd'}, {"delp", 'c'}, {"pt", 'c'}, {"w", 'c'}, {"phis", 'c'}});
-  zh_init(c, npz, phis.p, delz.p, zh);
-  halo_update({{"zh", 'c'}});
+  zh_init(c, npz, phis.p, delz.p, zh);  // compute domain: reads no halo
+  halo_update({{"u", 'd'}, {"v", 'd'}, {"delp", 'c'}, {"pt", 'c'}, {"w", 'c'}, {"phis", 'c'}, {"zh", 'c'}});
   for (int it = 0; it < nl.n_split; ++it) {
     const bool last = it == nl.n_split - 1;
     c_sw_transport(c, ca);
@@ -575,15 +574,14 @@ void Dycore::step() {
     // as one exchange (H_CSC, bit-identical to 'S' then 'C')
     halo_update({{"uc", 'X'}, {"vc", 'X'}});
     // fork: after the Courant numbers, the wind stage of d_sw (stream b) and update_dz_d
-    // (stream c) run beside the mass / thermodynamic transport and its halo update (the
-    // RCCL exchange of delp / pt then overlaps compute).  Default on (GTFV3_STREAMS=0: one
+    // (stream c) run beside the mass / thermodynamic transport (and the wind stage on beside
+    // riem_solver3 and the exchange of delp, pt, zh, ppe, w).  Default on (GTFV3_STREAMS=0: one
     // stream): with the thermo march at one or two waves per SIMD the side streams fill
     // the chip -- C180 on one GPU 43.8 -> 42.4 ms per step.
     d_sw_courant(c, da);
     if (!fork_substep) {
       d_sw_thermo(c, da);
       if (tfused) thermo_swap();
-      halo_update({{"delp", 'c'}, {"pt", 'c'}});
       d_sw_winds(c, da);
       update_dz_d(c, za);
     } else {
@@ -599,7 +597,6 @@ void Dycore::step() {
     }
     d_sw_thermo(c, da);
     if (tfused) thermo_swap();
-    halo_update({{"delp", 'c'}, {"pt", 'c'}});
     HIP_CHECK(hipEventRecord(ev_b, st_b));
     HIP_CHECK(hipEventRecord(ev_c, st_c));
     // riem_solver3 needs update_dz_d's heights, not d_sw's winds: the wind stage (u, v) keeps
@@ -609,7 +606,10 @@ void Dycore::step() {
     }
     ra.last_call = last ? 1 : 0;
     riem_solver3(c, ra, nsc);
-    halo_update({{"zh", 'c'}, {"ppe", 'c'}, {"w", 'c'}});
+    // delp / pt (d_sw's thermodynamic update) join riem_solver3's fields in one exchange:
+    // nothing between reads their halos (riem_solver3 works on the compute domain; the wind
+    // stage and update_dz_d do not read them), pk3_pe_halo and the next c_sw do
+    halo_update({{"delp", 'c'}, {"pt", 'c'}, {"zh", 'c'}, {"ppe", 'c'}, {"w", 'c'}});
     pk3_pe_halo(c, npz, ptop, last, delp.p, pk3, pe);
     scale_field(c, field_elems(k1), Constants::grav, zh, gz);
     if (fork_substep) HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
