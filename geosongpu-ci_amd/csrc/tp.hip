@@ -1042,6 +1042,11 @@ void d_sw_thermo_march(const Ctx& c, const ThermoArgs& a) {
   const long want = (6912 + fw - 1) / fw;
   const long nseg = std::max<long>((d.ny + 44) / 45, std::min<long>((d.ny + 14) / 15, want));
   m.seg = (int)((d.ny + nseg - 1) / nseg);
+  static const int seg_env = [] {
+    const char* e = getenv("GTFV3_TP_SEG");  // tuning override of the default segment
+    return e ? atoi(e) : 0;
+  }();
+  if (seg_env >= 8) m.seg = seg_env;
   m.nstrip = nstrip;
   m.nseg = (d.ny + m.seg - 1) / m.seg;
   if (m.seg + 10 > DXL_ROWS) throw std::runtime_error("d_sw thermo march: segment longer than the LDS dxa rows");
