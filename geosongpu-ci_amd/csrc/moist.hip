@@ -149,7 +149,7 @@ constexpr double QRMIN = 1.0e-8, QCMIN = 1.0e-12, QVMIN = 1.0e-20;
 constexpr double DZ_MIN_FALL = 1.0e-2;
 constexpr double TAU_I2S = 1000.0;
 constexpr double MP_R3 = 1.0 / 3.0, MP_R23 = 2.0 / 3.0;
-constexpr int MP_NSCR = 12;  // scratch columns of nk+1 levels per sub-domain
+constexpr int MP_NSCR = 9;  // scratch columns of nk+1 levels per sub-domain
 
 // host-computed coefficients (oracle/gfdl_mp.py module constants; exp(-dts / tau) factors)
 struct MpConst {
@@ -318,7 +318,7 @@ __device__ __forceinline__ void mp_fallen_edges(int n, long P, double dts, CRP z
 // Lagrangian sedimentation of q (oracle lagrangian_fall_ppm + cs_profile_mono); the flux
 // out of the bottom of each layer into m1; returns m1[n-1]
 __device__ __forceinline__ double mp_lagrangian_fall(int n, long P, CRP ze, CRP zt, CRP dp, RP q, RP qm0, RP a,
-                                                     RP qe, RP gam, RP aL, RP aR, RP a6, RP qm, RP m1) {
+                                                     RP qe, RP gam, RP qm, RP m1) {
   for (int k = 0; k < n; ++k) {
     const long x = (long)k * P;
     const double m0 = q[x] * dp[x];
@@ -377,31 +377,27 @@ __device__ __forceinline__ double mp_lagrangian_fall(int n, long P, CRP ze, CRP 
       }
     }
   }
-  // monotone limiter (cs_limiters)
-  {
-    double qL = qe[0];
-    for (int k = 0; k < n; ++k) {
-      const long x = (long)k * P;
-      const double qR = qe[x + P];
-      double l = qL, r = qR, a6v;
-      const double av = a[x];
-      const double da1 = r - l;
-      if ((av - l) * (av - r) >= 0.0) {
-        l = av; r = av; a6v = 0.0;
-      } else {
-        a6v = 3.0 * (2.0 * av - (l + r));
-        if (a6v * da1 < -da1 * da1) {
-          a6v = 3.0 * (l - av);
-          r = l - a6v;
-        } else if (a6v * da1 > da1 * da1) {
-          a6v = 3.0 * (r - av);
-          l = r - a6v;
-        }
+  // monotone limiter (cs_limiters) of layer x's profile, formed where the integration
+  // needs it from the layer's edges and mean (no stored aL / aR / a6 planes: 5 column
+  // passes fewer per fall)
+  auto prof = [&](long x, double& l, double& r, double& a6v) {
+    l = qe[x];
+    r = qe[x + P];
+    const double av = a[x];
+    const double da1 = r - l;
+    if ((av - l) * (av - r) >= 0.0) {
+      l = av; r = av; a6v = 0.0;
+    } else {
+      a6v = 3.0 * (2.0 * av - (l + r));
+      if (a6v * da1 < -da1 * da1) {
+        a6v = 3.0 * (l - av);
+        r = l - a6v;
+      } else if (a6v * da1 > da1 * da1) {
+        a6v = 3.0 * (r - av);
+        l = r - a6v;
       }
-      aL[x] = l; aR[x] = r; a6[x] = a6v;
-      qL = qR;
     }
-  }
+  };
   // integrate the fallen profile over the fixed layers
   int k0 = 0;
   for (int k = 0; k < n; ++k) {
@@ -413,7 +409,8 @@ __device__ __forceinline__ double mp_lagrangian_fall(int n, long P, CRP ze, CRP 
       if (top <= ztm && top >= ztm1) {
         const double dzm = ztm - ztm1;
         const double pl = (ztm - top) / dzm;
-        const double l = aL[y], r = aR[y], a6v = a6[y];
+        double l, r, a6v;
+        prof(y, l, r, a6v);
         if (ztm1 <= bot) {
           const double pr = (ztm - bot) / dzm;
           qmk = (l + 0.5 * (a6v + r - l) * (pr + pl) - a6v * MP_R3 * (pr * (pr + pl) + pl * pl)) * (top - bot);
@@ -428,7 +425,9 @@ __device__ __forceinline__ double mp_lagrangian_fall(int n, long P, CRP ze, CRP 
             } else {
               const double dzz = zt[yy] - bot;
               const double esl = dzz / (zt[yy] - zb);
-              sm = sm + dzz * (aL[yy] + 0.5 * esl * (aR[yy] - aL[yy] + a6[yy] * (1.0 - MP_R23 * esl)));
+              double lb, rb, a6b;
+              prof(yy, lb, rb, a6b);
+              sm = sm + dzz * (lb + 0.5 * esl * (rb - lb + a6b * (1.0 - MP_R23 * esl)));
               k0 = mm;
               break;
             }
@@ -627,9 +626,8 @@ __global__ void __launch_bounds__(256) mpdrv_k(MpArgs a) {
   const double* dz = a.dz + (long)s * n * P + o;
   double* sb = a.scr + (long)s * MP_NSCR * (n + 1) * P + o;
   const long SB = (long)(n + 1) * P;
-  double *ze = sb, *zt = sb + SB, *den = sb + 2 * SB, *aa = sb + 3 * SB, *aL = sb + 4 * SB, *aR = sb + 5 * SB;
-  double *a6 = sb + 6 * SB, *gam = sb + 7 * SB, *qe = sb + 8 * SB, *vt = sb + 9 * SB, *m1 = sb + 10 * SB;
-  double* qm0 = sb + 11 * SB;
+  double *ze = sb, *zt = sb + SB, *den = sb + 2 * SB, *aa = sb + 3 * SB, *gam = sb + 4 * SB, *qe = sb + 5 * SB;
+  double *vt = sb + 6 * SB, *m1 = sb + 7 * SB, *qm0 = sb + 8 * SB;
   double* qm = vt;  // the fall speeds are consumed (fallen heights) before the remap writes qm
   {
     double z = 0.0;
@@ -652,7 +650,7 @@ __global__ void __launch_bounds__(256) mpdrv_k(MpArgs a) {
       double pfw = 0.0;
       if (mp_speeds(n, P, w, q, den, vt)) {
         mp_fallen_edges(n, P, dts, ze, vt, zt);
-        const double m = mp_lagrangian_fall(n, P, ze, zt, dp, q, qm0, aa, qe, gam, aL, aR, a6, qm, m1);
+        const double m = mp_lagrangian_fall(n, P, ze, zt, dp, q, qm0, aa, qe, gam, qm, m1);
         mp_sedi_heat(n, P, C_ICE, t, dp, dz, m1, qv, ql, qr, qi, qs, qg);
         pfw = m / GRAV;
       }
@@ -666,7 +664,7 @@ __global__ void __launch_bounds__(256) mpdrv_k(MpArgs a) {
     double pr_ = 0.0;
     if (mp_speeds(n, P, 3, qr, den, vt)) {
       mp_fallen_edges(n, P, dts, ze, vt, zt);
-      const double m = mp_lagrangian_fall(n, P, ze, zt, dp, qr, qm0, aa, qe, gam, aL, aR, a6, qm, m1);
+      const double m = mp_lagrangian_fall(n, P, ze, zt, dp, qr, qm0, aa, qe, gam, qm, m1);
       mp_sedi_heat(n, P, C_LIQ, t, dp, dz, m1, qv, ql, qr, qi, qs, qg);
       pr_ = m / GRAV;
     }
@@ -840,11 +838,16 @@ __global__ void __launch_bounds__(256) radcouple_k(RadArgs a) {
 struct AerMode {
   double n0, h, rd, sg, kap;
 };
-__constant__ AerMode c_aer_modes[3] = {{1.0e9, 2000.0, 0.02e-6, 1.6, 0.6},
-                                      {3.0e8, 2000.0, 0.08e-6, 1.8, 0.6},
-                                      {1.0e6, 1000.0, 1.00e-6, 2.0, 1.2}};
+constexpr AerMode kAerModes[3] = {{1.0e9, 2000.0, 0.02e-6, 1.6, 0.6},
+                                  {3.0e8, 2000.0, 0.08e-6, 1.8, 0.6},
+                                  {1.0e6, 1000.0, 1.00e-6, 2.0, 1.2}};
 constexpr double MW = 0.018015, MA = 0.028965, RGAS_U = 8.314462618, SURF_T = 0.0761, W_MIN = 0.1;
 
+// per-mode constants of the activation, formed on the host as the oracle forms them
+// (math.log / math.exp / math.sqrt of the mode parameters)
+struct AerModeC {
+  double n0, h, rd3, sk, ls, f, g;  // rd3 = 3 rd, sk = 2 / sqrt(kap), ls = log(sg), f, g
+};
 struct AerArgs {
   Dims d;
   int nk;
@@ -852,6 +855,7 @@ struct AerArgs {
   Tables tb;
   const double *pl, *T, *qv, *zm, *w;
   double *nactl, *nacti, *smax;
+  AerModeC mode[3];
 };
 
 __global__ void __launch_bounds__(256) aer_activation_k(AerArgs a) {
@@ -874,19 +878,31 @@ __global__ void __launch_bounds__(256) aer_activation_k(AerArgs a) {
   const double gg = 1.0 / (RHO_W * RGAS_U * t / (es * dv * MW) + HLV * RHO_W / (K_COND * t) * (HLV * MW / (RGAS_U * t) - 1.0));
   const double aw = alpha * wv / gg;
   const double zeta = 2.0 * a_k / 3.0 * sqrt(aw);
+  // x^1.5 as x sqrt(x) and x^0.75 as sqrt(x) sqrt(sqrt(x)) (within a few ulp of pow, which
+  // cost ~60 % of the kernel); the mode constants come from the host; modes with the same
+  // scale height share one exp
+  auto p15 = [](double x) { return x * sqrt(x); };
+  auto p075 = [](double x) {
+    const double r = sqrt(x);
+    return r * sqrt(r);
+  };
+  const double zp = fmax(zm, 0.0);
+  const double aw15 = p15(aw);
   double ssum = 0.0, sm[3], nn[3], ls[3];
+  double ex = 0.0;
+#pragma unroll
   for (int m = 0; m < 3; ++m) {
-    const AerMode md = c_aer_modes[m];
-    nn[m] = md.n0 * exp(-fmax(zm, 0.0) / md.h);
-    sm[m] = 2.0 / sqrt(md.kap) * pow(a_k / (3.0 * md.rd), 1.5);
-    ls[m] = log(md.sg);
-    const double eta = pow(aw, 1.5) / (2.0 * PI_ * RHO_W * gamma * nn[m]);
-    const double f = 0.5 * exp(2.5 * ls[m] * ls[m]);
-    const double g = 1.0 + 0.25 * ls[m];
-    ssum = ssum + (f * pow(zeta / eta, 1.5) + g * pow(sm[m] * sm[m] / (eta + 3.0 * zeta), 0.75)) / (sm[m] * sm[m]);
+    const AerModeC md = a.mode[m];
+    if (m == 0 || md.h != a.mode[m > 0 ? m - 1 : 0].h) ex = exp(-zp / md.h);
+    nn[m] = md.n0 * ex;
+    sm[m] = md.sk * p15(a_k / md.rd3);
+    ls[m] = md.ls;
+    const double eta = aw15 / (2.0 * PI_ * RHO_W * gamma * nn[m]);
+    ssum = ssum + (md.f * p15(zeta / eta) + md.g * p075(sm[m] * sm[m] / (eta + 3.0 * zeta))) / (sm[m] * sm[m]);
   }
   const double smax = 1.0 / sqrt(ssum);
   double nact = 0.0;
+#pragma unroll
   for (int m = 0; m < 3; ++m) {
     const double u = 2.0 * log(sm[m] / smax) / (3.0 * sqrt(2.0) * ls[m]);
     nact = nact + nn[m] * 0.5 * erfc(u);
@@ -1269,7 +1285,12 @@ void radcouple(const Ctx& c, const RadcoupleArgs& g) {
 
 void aer_activation(const Ctx& c, int nk, long qv_sub, const double* pl, const double* t, const double* qv,
                     const double* zm, const double* w, double* nactl, double* nacti, double* smax) {
-  moist::AerArgs a{c.d, nk, qv_sub > 0 ? qv_sub : nk, moist::device_tables(), pl, t, qv, zm, w, nactl, nacti, smax};
+  moist::AerArgs a{c.d, nk, qv_sub > 0 ? qv_sub : nk, moist::device_tables(), pl, t, qv, zm, w, nactl, nacti, smax, {}};
+  for (int m = 0; m < 3; ++m) {
+    const moist::AerMode& md = moist::kAerModes[m];
+    const double ls = std::log(md.sg);
+    a.mode[m] = {md.n0, md.h, 3.0 * md.rd, 2.0 / std::sqrt(md.kap), ls, 0.5 * std::exp(2.5 * ls * ls), 1.0 + 0.25 * ls};
+  }
   GT_LAUNCH(moist::aer_activation_k, moist::ptgrid(c.d, nk), dim3(BX, BY), 0, c.st, a);
   HIP_LAUNCH_CHECK();
   ktimer_bytes(8.0 * c.d.nx * c.d.ny * c.d.nsub * nk * 8.0);
