@@ -158,76 +158,114 @@ __device__ __forceinline__ void layer_coef(int l, int km, int iv, const Col& q, 
 }
 
 // constrained edge values q of the kord = 9 profile (gam: scratch column); the large-
-// scale constraint of each edge is applied as the back substitution finalises it
-__device__ void cs_edges(const Col& A, const Edges& E, int km, int iv, double qs, const Col& q, const Col& gam) {
-  auto DP = [&](int l) { return E(l + 1) - E(l); };
-  auto constrain = [&](int e, double v) {
+// scale constraint of each edge is applied as the back substitution finalises it.  The
+// columns are __restrict__ parameters and the values a level shares with the next (the
+// edge pressure, the mean, the factor just formed) are carried in registers, so the
+// forward and backward sweeps issue their loads ahead instead of waiting out a store ->
+// load round trip per level; same operations in the same order as before.
+__device__ __forceinline__ void cs_edges_r(int km, int iv, double qs, long P, int ekind,
+                                           const double* __restrict__ A, const double* __restrict__ Ea,
+                                           const double* __restrict__ Eb, double* __restrict__ q,
+                                           double* __restrict__ gam) {
+  auto E = [&](int l) -> double {
+    if (ekind == 0) return Ea[(long)l * P];
+    return l == 0 ? Ea[0] : 0.5 * (Eb[(long)l * P] + Ea[(long)l * P]);
+  };
+  auto Ak = [&](int k) { return A[(long)k * P]; };
+  auto constrain = [&](int e, double v, double am2, double am1, double a0, double ap1) {
+    // am2 .. ap1 = A[e-2] .. A[e+1] (only those in range are used)
     if (e == 1 || e == km - 1) {
-      v = fmin(v, fmax(A[e - 1], A[e]));
-      return fmax(v, fmin(A[e - 1], A[e]));
+      v = fmin(v, fmax(am1, a0));
+      return fmax(v, fmin(am1, a0));
     }
     if (e >= 2 && e <= km - 2) {
-      const double g0 = A[e - 1] - A[e - 2], g1 = A[e + 1] - A[e];
+      const double g0 = am1 - am2, g1 = ap1 - a0;
       if (g0 * g1 > 0.0) {
-        v = fmin(v, fmax(A[e - 1], A[e]));
-        v = fmax(v, fmin(A[e - 1], A[e]));
+        v = fmin(v, fmax(am1, a0));
+        v = fmax(v, fmin(am1, a0));
       } else if (g0 > 0.0) {
-        v = fmax(v, fmin(A[e - 1], A[e]));
+        v = fmax(v, fmin(am1, a0));
       } else {
-        v = fmin(v, fmax(A[e - 1], A[e]));
+        v = fmin(v, fmax(am1, a0));
         if (iv == 0) v = fmax(0.0, v);
       }
     }
     return v;
   };
+  // back substitution from edge `top` down to 0 with the A window carried downwards
+  auto back = [&](int top, double x, int gofs) {
+    // window: A[e-2], A[e-1], A[e], A[e+1] for e = top
+    double a0 = top <= km - 1 ? Ak(top) : 0.0;
+    double ap1 = top + 1 <= km - 1 ? Ak(top + 1) : 0.0;
+    double am1 = top >= 1 ? Ak(top - 1) : 0.0;
+    double am2 = top >= 2 ? Ak(top - 2) : 0.0;
+    for (int e = top; e >= 0; --e) {
+      x = q[(long)e * P] - gam[(long)(e + gofs) * P] * x;
+      q[(long)e * P] = constrain(e, x, am2, am1, a0, ap1);
+      ap1 = a0;
+      a0 = am1;
+      am1 = am2;
+      am2 = e >= 3 ? Ak(e - 3) : 0.0;
+    }
+  };
   if (iv == -2) {
-    gam[1] = 0.5;
-    double qp = 1.5 * A[0];
+    double gp = 0.5;
+    gam[P] = gp;
+    double qp = 1.5 * Ak(0);
     q[0] = qp;
-    double dprev = DP(0);
+    double el = E(1);
+    double dprev = el - E(0);
+    double aprev = Ak(0);
     for (int e = 1; e < km - 1; ++e) {
-      const double dcur = DP(e);
+      const double en = E(e + 1);
+      const double dcur = en - el;
+      const double ae = Ak(e);
       const double grat = dprev / dcur;
-      const double bet = 2.0 + grat + grat - gam[e];
-      qp = (3.0 * (A[e - 1] + A[e]) - qp) / bet;
-      q[e] = qp;
-      gam[e + 1] = grat / bet;
+      const double bet = 2.0 + grat + grat - gp;
+      qp = (3.0 * (aprev + ae) - qp) / bet;
+      q[(long)e * P] = qp;
+      gp = grat / bet;
+      gam[(long)(e + 1) * P] = gp;
       dprev = dcur;
+      el = en;
+      aprev = ae;
     }
-    const double grat = DP(km - 2) / DP(km - 1);
-    double x = (3.0 * (A[km - 2] + A[km - 1]) - grat * qs - qp) / (2.0 + grat + grat - gam[km - 1]);
-    q[km] = qs;
-    q[km - 1] = constrain(km - 1, x);
-    for (int e = km - 2; e >= 0; --e) {
-      x = q[e] - gam[e + 1] * x;
-      q[e] = constrain(e, x);
-    }
+    const double grat = (E(km - 1) - E(km - 2)) / (E(km) - E(km - 1));
+    double x = (3.0 * (Ak(km - 2) + Ak(km - 1)) - grat * qs - qp) / (2.0 + grat + grat - gp);
+    q[(long)km * P] = qs;
+    const double a_km1 = Ak(km - 1), a_km2 = Ak(km - 2), a_km3 = km >= 3 ? Ak(km - 3) : 0.0;
+    q[(long)(km - 1) * P] = constrain(km - 1, x, a_km3, a_km2, a_km1, 0.0);
+    back(km - 2, x, 1);
   } else {
-    double dprev = DP(0), dcur = DP(1);
+    double e0 = E(0), e1 = E(1);
+    double dprev = e1 - e0, dcur = E(2) - e1;
     const double grat = dcur / dprev;
     double bet = grat * (grat + 0.5);
-    double qp = ((grat + grat) * (grat + 1.0) * A[0] + A[1]) / bet;
+    double qp = ((grat + grat) * (grat + 1.0) * Ak(0) + Ak(1)) / bet;
     q[0] = qp;
     double gp = (1.0 + grat * (grat + 1.5)) / bet;
     gam[0] = gp;
     double d4 = grat;
+    double el = e1;
+    double aprev = Ak(0);
     for (int e = 1; e < km; ++e) {
-      dcur = DP(e);
+      const double en = E(e + 1);
+      dcur = en - el;
+      const double ae = Ak(e);
       d4 = dprev / dcur;
       bet = 2.0 + d4 + d4 - gp;
-      qp = (3.0 * (A[e - 1] + d4 * A[e]) - qp) / bet;
-      q[e] = qp;
+      qp = (3.0 * (aprev + d4 * ae) - qp) / bet;
+      q[(long)e * P] = qp;
       gp = d4 / bet;
-      gam[e] = gp;
+      gam[(long)e * P] = gp;
       dprev = dcur;
+      el = en;
+      aprev = ae;
     }
     const double a_bot = 1.0 + d4 * (d4 + 1.5);
-    double x = (2.0 * d4 * (d4 + 1.0) * A[km - 1] + A[km - 2] - a_bot * qp) / (d4 * (d4 + 0.5) - a_bot * gp);
-    q[km] = x;
-    for (int e = km - 1; e >= 0; --e) {
-      x = q[e] - gam[e] * x;
-      q[e] = constrain(e, x);
-    }
+    double x = (2.0 * d4 * (d4 + 1.0) * Ak(km - 1) + Ak(km - 2) - a_bot * qp) / (d4 * (d4 + 0.5) - a_bot * gp);
+    q[(long)km * P] = x;
+    back(km - 1, x, 0);
   }
 }
 
@@ -411,7 +449,7 @@ __global__ void __launch_bounds__(BLOCK) remap_job_k(RemapArgs a) {
     for (int k = 0; k < km; ++k) A[k] = f[k * P];
     OUT.p = f;
   }
-  cs_edges(A, E, km, iv, qs, q, gam);
+  cs_edges_r(km, iv, qs, P, E.kind, A.p, E.a, E.b, q.p, gam.p);
   map1(E, A, T, OUT, km, iv, q);
   if (job >= J_Q0 && a.fill) fillz_col(OUT, [&](int k) { return T(k + 1) - T(k); }, km);
 }
