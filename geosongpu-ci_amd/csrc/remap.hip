@@ -317,6 +317,124 @@ __device__ void map1(const Edges& E, const Col& A, const Targets& T, const Col& 
   }
 }
 
+// map1_ppm as ONE streaming sweep over the source layers with the target pointer dynamic
+// (the register form's walk, remap_reg_k below): per source layer the PPM coefficients from
+// a sliding window of means A[l-2 .. l+2] and edges q[l], q[l+1], then every target piece
+// inside the layer.  The loads of a layer are issued two layers ahead, independent of the
+// data-dependent walk, instead of the two-pointer search's chain of dependent HBM round
+// trips.  Same terms in the same order as map1 (bit-identical).  Returns whether a value < 0
+// was written (fillz has work only then).
+__device__ __forceinline__ bool map1_stream(int km, int iv, long P, int ekind, const double* __restrict__ Ea,
+                                            const double* __restrict__ Eb, const double* __restrict__ A,
+                                            const double* __restrict__ q, double* __restrict__ out,
+                                            const Targets& T) {
+  auto E = [&](int l) -> double {
+    if (ekind == 0) return Ea[(long)l * P];
+    return l == 0 ? Ea[0] : 0.5 * (Eb[(long)l * P] + Ea[(long)l * P]);
+  };
+  auto Ak = [&](int k) { return k < km ? A[(long)k * P] : 0.0; };
+  auto Qk = [&](int e) { return e <= km ? q[(long)e * P] : 0.0; };
+  auto Ek = [&](int e) { return e <= km ? E(e) : 0.0; };
+  double am2 = 0.0, am1 = 0.0, a0 = Ak(0), ap1 = Ak(1), ap2 = Ak(2), ap3 = Ak(3);
+  double qL = Qk(0), qR = Qk(1), qn1 = Qk(2);
+  double e0 = E(0), e1 = Ek(1), en1 = Ek(2);
+  int k = 0;
+  bool open = false, neg = false;
+  double qsum = 0.0, topk = 0.0, bot = 0.0;
+  double topv = T(0);
+  double tb1 = T(1);
+  for (int l = 0; l < km; ++l) {
+    const double ap4 = Ak(l + 4), qn2 = Qk(l + 3), en2 = Ek(l + 3);
+    // PPM coefficients of layer l (layer_coef's expressions on the window)
+    double AL = qL, AR = qR, A6;
+    {
+      const double av = a0;
+      const double g_m1 = am1 - am2, g_0 = a0 - am1, g_p1 = ap1 - a0, g_p2 = ap2 - ap1;  // gm(l-1 .. l+2)
+      if (l == 0) {
+        if (iv == 0) AL = fmax(0.0, AL);
+        else if (iv == -1 && AL * av <= 0.0) AL = 0.0;
+        A6 = 3.0 * (2.0 * av - (AL + AR));
+        lim(av, AL, AR, A6, false, 1);
+      } else if (l == 1) {
+        A6 = 3.0 * (2.0 * av - (AL + AR));
+        lim(av, AL, AR, A6, g_0 * g_p1 < 0.0, 2);
+      } else if (l < km - 2) {
+        const bool el = g_0 * g_p1 < 0.0;
+        if ((el && g_m1 * g_0 < 0.0) || (el && g_p1 * g_p2 < 0.0)) {
+          AL = av; AR = av; A6 = 0.0;
+        } else {
+          A6 = 6.0 * av - 3.0 * (AL + AR);
+          if (fabs(A6) > fabs(AL - AR)) {
+            double pmp_1 = av - 2.0 * g_p1;
+            double lac_1 = pmp_1 + 1.5 * g_p2;
+            AL = fmin(fmax(AL, fmin(fmin(av, pmp_1), lac_1)), fmax(fmax(av, pmp_1), lac_1));
+            double pmp_2 = av + 2.0 * g_0;
+            double lac_2 = pmp_2 - 1.5 * g_m1;
+            AR = fmin(fmax(AR, fmin(fmin(av, pmp_2), lac_2)), fmax(fmax(av, pmp_2), lac_2));
+            A6 = 6.0 * av - 3.0 * (AL + AR);
+          }
+        }
+        if (iv == 0) lim(av, AL, AR, A6, el, 0);
+      } else if (l == km - 2) {
+        A6 = 3.0 * (2.0 * av - (AL + AR));
+        lim(av, AL, AR, A6, g_0 * g_p1 < 0.0, 2);
+      } else {
+        if (iv == 0) AR = fmax(0.0, AR);
+        else if (iv == -1 && AR * av <= 0.0) AR = 0.0;
+        A6 = 3.0 * (2.0 * av - (AL + AR));
+        lim(av, AL, AR, A6, false, 1);
+      }
+    }
+    const double dpl = e1 - e0;
+    while (k < km) {
+      if (open) {
+        if (bot > e1) {  // whole layer
+          qsum = qsum + dpl * a0;
+          break;
+        }
+        const double dp = bot - e0;  // last (partial) piece
+        const double esl = dp / dpl;
+        qsum = qsum + dp * (AL + 0.5 * esl * (AR - AL + A6 * (1.0 - R23 * esl)));
+        const double v = qsum / (bot - topk);
+        out[(long)k * P] = v;
+        neg = neg || v < 0.0;
+        ++k;
+        tb1 = T(k + 1 <= km ? k + 1 : km);
+        open = false;
+        topv = bot;
+        continue;
+      }
+      if (!(topv >= e0 && topv <= e1)) break;
+      bot = tb1;
+      const double pl = (topv - e0) / dpl;
+      if (bot <= e1) {  // target inside this layer
+        const double pr = (bot - e0) / dpl;
+        const double v = AL + 0.5 * (A6 + AR - AL) * (pr + pl) - A6 * R3 * (pr * (pr + pl) + pl * pl);
+        out[(long)k * P] = v;
+        neg = neg || v < 0.0;
+        ++k;
+        tb1 = T(k + 1 <= km ? k + 1 : km);
+        topv = bot;
+        continue;
+      }
+      // first (partial) piece; the target continues below
+      qsum = (e1 - topv) * (AL + 0.5 * (A6 + AR - AL) * (1.0 + pl) - A6 * (R3 * (1.0 + pl * (1.0 + pl))));
+      topk = topv;
+      open = true;
+      break;
+    }
+    am2 = am1; am1 = a0; a0 = ap1; ap1 = ap2; ap2 = ap3; ap3 = ap4;
+    qL = qR; qR = qn1; qn1 = qn2;
+    e0 = e1; e1 = en1; en1 = en2;
+  }
+  if (open) {  // bottom beyond the last source edge (the walk ran out of layers)
+    const double v = qsum / (bot - topk);
+    out[(long)k * P] = v;
+    neg = neg || v < 0.0;
+  }
+  return neg;
+}
+
 template <typename DPF>
 __device__ __forceinline__ void fillz_col(const Col& q, const DPF& dp, int km) {
   if (q[0] < 0.0) {
@@ -450,8 +568,8 @@ __global__ void __launch_bounds__(BLOCK) remap_job_k(RemapArgs a) {
     OUT.p = f;
   }
   cs_edges_r(km, iv, qs, P, E.kind, A.p, E.a, E.b, q.p, gam.p);
-  map1(E, A, T, OUT, km, iv, q);
-  if (job >= J_Q0 && a.fill) fillz_col(OUT, [&](int k) { return T(k + 1) - T(k); }, km);
+  const bool neg = map1_stream(km, iv, P, E.kind, E.a, E.b, A.p, q.p, OUT.p, T);
+  if (job >= J_Q0 && a.fill && neg) fillz_col(OUT, [&](int k) { return T(k + 1) - T(k); }, km);
 }
 
 // ---------------- register-resident column form (default for the instantiated level counts) ----------------
