@@ -142,8 +142,9 @@ def parse():
     p.add_argument("--nq", type=int, default=4)
     p.add_argument("--layout", default="", help="sub-domain layout per tile, e.g. 2x2 (default: by rank count)")
     p.add_argument("--dt", type=float, default=0.0, help="dt_atmos (default 450 s x 180 / N: C180 450 s)")
-    p.add_argument("--cpu-npx", type=int, default=49,
-                   help="cpu_baseline sample grid (C48 L72, 6 tiles: ~20 s of one host core)")
+    p.add_argument("--cpu-npx", type=int, default=0,
+                   help="cpu_baseline sample grid npx (default 49: C48 L72, 6 tiles, ~20 s of one host core; "
+                        "13 with --moist, ~40 s)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--kernel-report", default="", help="write per-kernel stats JSON here")
@@ -191,11 +192,14 @@ def cpu_baseline(pkg, npx, npz, nq, dt, moist=False):
     t0 = time.perf_counter()
     out = fvd.fv_dynamics(st, ak, bk, g, nl)
     if moist:
+        from oracle import NG
         from oracle import geos_moist as gm
-        for s in range(d.nsub):
+        cd = (Ellipsis, slice(NG, NG + d.ny), slice(NG, NG + d.nx))  # the compute domain (the padded
+        for s in range(d.nsub):                                      # plane's outer cells are not state)
             q = out["q"][s]
-            sp = [q[n * npz:(n + 1) * npz] for n in range(6)]
-            gm.aquaplanet_physics(dt, out["pt"][s], *sp, out["delp"][s], out["delz"][s], out["pe"][s], out["w"][s])
+            sp = [q[n * npz:(n + 1) * npz][cd] for n in range(6)]
+            gm.aquaplanet_physics(dt, out["pt"][s][cd], *sp, out["delp"][s][cd], out["delz"][s][cd],
+                                  out["pe"][s][cd], out["w"][s][cd])
     el = time.perf_counter() - t0
     cells = 6 * d.N * d.N * npz
     d.close()
@@ -376,7 +380,9 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
-        cpu = cpu_baseline(pkg, a.cpu_npx, a.npz, nq, a.dt, a.moist)
+        # the moist oracle's column loops are ~40x slower per cell than its dycore: C12 with --moist
+        cpu_npx = a.cpu_npx if a.cpu_npx > 0 else (13 if a.moist else 49)
+        cpu = cpu_baseline(pkg, cpu_npx, a.npz, nq, a.dt, a.moist)
 
     if rank == 0:
         out = {
