@@ -377,67 +377,81 @@ __device__ __forceinline__ double mp_lagrangian_fall(int n, long P, CRP ze, CRP 
       }
     }
   }
-  // monotone limiter (cs_limiters) of layer x's profile, formed where the integration
-  // needs it from the layer's edges and mean (no stored aL / aR / a6 planes: 5 column
-  // passes fewer per fall)
-  auto prof = [&](long x, double& l, double& r, double& a6v) {
-    l = qe[x];
-    r = qe[x + P];
-    const double av = a[x];
-    const double da1 = r - l;
-    if ((av - l) * (av - r) >= 0.0) {
-      l = av; r = av; a6v = 0.0;
-    } else {
-      a6v = 3.0 * (2.0 * av - (l + r));
-      if (a6v * da1 < -da1 * da1) {
-        a6v = 3.0 * (l - av);
-        r = l - a6v;
-      } else if (a6v * da1 > da1 * da1) {
-        a6v = 3.0 * (r - av);
-        l = r - a6v;
+  // (the monotone limiter of cs_limiters is applied to each fallen layer's profile where the
+  // integration forms it: no stored aL / aR / a6 planes)
+  // integrate the fallen profile over the fixed layers: one streaming sweep over the fallen
+  // layers m with the target (fixed) layer k dynamic -- the pieces of every target in the
+  // same order and with the same expressions as the two-pointer search, whose every step
+  // was a dependent memory round trip; the fallen layer's heights, edges, mean and mass are
+  // loaded one layer ahead of their use
+  {
+    auto prof_v = [&](double l0, double r0, double av, double& l, double& r, double& a6v) {
+      l = l0;
+      r = r0;
+      const double da1 = r - l;
+      if ((av - l) * (av - r) >= 0.0) {
+        l = av; r = av; a6v = 0.0;
+      } else {
+        a6v = 3.0 * (2.0 * av - (l + r));
+        if (a6v * da1 < -da1 * da1) {
+          a6v = 3.0 * (l - av);
+          r = l - a6v;
+        } else if (a6v * da1 > da1 * da1) {
+          a6v = 3.0 * (r - av);
+          l = r - a6v;
+        }
       }
-    }
-  };
-  // integrate the fallen profile over the fixed layers
-  int k0 = 0;
-  for (int k = 0; k < n; ++k) {
-    const double top = ze[(long)k * P], bot = ze[(long)(k + 1) * P];
-    double qmk = 0.0;
-    for (int m = k0; m < n; ++m) {
-      const long y = (long)m * P;
-      const double ztm = zt[y], ztm1 = zt[y + P];
-      if (top <= ztm && top >= ztm1) {
+    };
+    int k = 0;
+    bool open = false;
+    double sm = 0.0;
+    double top = ze[0], bot = ze[P];
+    double ztm = zt[0], ztm1 = zt[P], qeL = qe[0], qeR = qe[P], am = a[0], q0m = qm0[0];
+    for (int m = 0; m < n; ++m) {
+      const long yn = (long)(m + 1) * P;
+      const bool more = m + 1 < n;
+      const double zt2 = more ? zt[yn + P] : 0.0, qe2 = more ? qe[yn + P] : 0.0;
+      const double an = more ? a[yn] : 0.0, q0n = more ? qm0[yn] : 0.0;
+      double l, r, a6v;
+      prof_v(qeL, qeR, am, l, r, a6v);
+      while (k < n) {
+        if (open) {
+          if (bot < ztm1) {  // the whole fallen layer
+            sm = sm + q0m;
+            break;
+          }
+          const double dzz = ztm - bot;  // the last (partial) piece
+          const double esl = dzz / (ztm - ztm1);
+          sm = sm + dzz * (l + 0.5 * esl * (r - l + a6v * (1.0 - MP_R23 * esl)));
+          qm[(long)k * P] = sm;
+          open = false;
+          ++k;
+          top = bot;
+          bot = k < n ? ze[(long)(k + 1) * P] : 0.0;
+          continue;
+        }
+        if (!(top <= ztm && top >= ztm1)) break;
         const double dzm = ztm - ztm1;
         const double pl = (ztm - top) / dzm;
-        double l, r, a6v;
-        prof(y, l, r, a6v);
-        if (ztm1 <= bot) {
+        if (ztm1 <= bot) {  // the target inside this fallen layer
           const double pr = (ztm - bot) / dzm;
-          qmk = (l + 0.5 * (a6v + r - l) * (pr + pl) - a6v * MP_R3 * (pr * (pr + pl) + pl * pl)) * (top - bot);
-          k0 = m;
-        } else {
-          double sm = (top - ztm1) * (l + 0.5 * (a6v + r - l) * (1.0 + pl) - a6v * (MP_R3 * (1.0 + pl * (1.0 + pl))));
-          for (int mm = m + 1; mm < n; ++mm) {
-            const long yy = (long)mm * P;
-            const double zb = zt[yy + P];
-            if (bot < zb) {
-              sm = sm + qm0[yy];
-            } else {
-              const double dzz = zt[yy] - bot;
-              const double esl = dzz / (zt[yy] - zb);
-              double lb, rb, a6b;
-              prof(yy, lb, rb, a6b);
-              sm = sm + dzz * (lb + 0.5 * esl * (rb - lb + a6b * (1.0 - MP_R23 * esl)));
-              k0 = mm;
-              break;
-            }
-          }
-          qmk = sm;
+          qm[(long)k * P] = (l + 0.5 * (a6v + r - l) * (pr + pl) - a6v * MP_R3 * (pr * (pr + pl) + pl * pl)) * (top - bot);
+          ++k;
+          top = bot;
+          bot = k < n ? ze[(long)(k + 1) * P] : 0.0;
+          continue;
         }
+        sm = (top - ztm1) * (l + 0.5 * (a6v + r - l) * (1.0 + pl) - a6v * (MP_R3 * (1.0 + pl * (1.0 + pl))));
+        open = true;
         break;
       }
+      ztm = ztm1; ztm1 = zt2; qeL = qeR; qeR = qe2; am = an; q0m = q0n;
     }
-    qm[(long)k * P] = qmk;
+    if (open) {  // the target ran past the last fallen layer: its whole-layer sum
+      qm[(long)k * P] = sm;
+      ++k;
+    }
+    for (; k < n; ++k) qm[(long)k * P] = 0.0;  // (no piece: as the search leaves them)
   }
   double acc = 0.0;
   for (int k = 0; k < n; ++k) {
