@@ -505,10 +505,17 @@ __device__ __forceinline__ void mp_revap_racc(const Tables& tb, const MpConst& k
 
 __device__ __forceinline__ void mp_revap_pass(int n, long P, const Tables& tb, const MpConst& kc, double dt, CRP den,
                                               RP t, RP qv, RP ql, RP qr, CRP qi, CRP qs, CRP qg) {
+  // software pipelined as mp_icloud_pass
+  double nt = t[0], nv = qv[0], nl = ql[0], nr = qr[0], ni = qi[0], ns = qs[0], ng = qg[0], nd = den[0];
   for (int k = 0; k < n; ++k) {
     const long x = (long)k * P;
-    double tt = t[x], v = qv[x], l = ql[x], r = qr[x];
-    mp_revap_racc(tb, kc, dt, den[x], tt, v, l, r, qi[x], qs[x], qg[x]);
+    double tt = nt, v = nv, l = nl, r = nr;
+    const double ii = ni, sn = ns, g = ng, dn = nd;
+    if (k + 1 < n) {
+      const long y = x + P;
+      nt = t[y]; nv = qv[y]; nl = ql[y]; nr = qr[y]; ni = qi[y]; ns = qs[y]; ng = qg[y]; nd = den[y];
+    }
+    mp_revap_racc(tb, kc, dt, dn, tt, v, l, r, ii, sn, g);
     t[x] = tt; qv[x] = v; ql[x] = l; qr[x] = r;
   }
 }
@@ -617,10 +624,17 @@ __device__ __forceinline__ void mp_icloud(const Tables& tb, const MpConst& kc, d
 
 __device__ __forceinline__ void mp_icloud_pass(int n, long P, const Tables& tb, const MpConst& kc, double dts,
                                                CRP den, RP t, RP qv, RP ql, RP qr, RP qi, RP qs, RP qg) {
+  // the next level's inputs are loaded while this level computes (software pipelined)
+  double nt = t[0], nv = qv[0], nl = ql[0], nr = qr[0], ni = qi[0], ns = qs[0], ng = qg[0], nd = den[0];
   for (int k = 0; k < n; ++k) {
     const long x = (long)k * P;
-    double tt = t[x], v = qv[x], l = ql[x], r = qr[x], ii = qi[x], sn = qs[x], g = qg[x];
-    mp_icloud(tb, kc, dts, den[x], tt, v, l, r, ii, sn, g);
+    double tt = nt, v = nv, l = nl, r = nr, ii = ni, sn = ns, g = ng;
+    const double dn = nd;
+    if (k + 1 < n) {
+      const long y = x + P;
+      nt = t[y]; nv = qv[y]; nl = ql[y]; nr = qr[y]; ni = qi[y]; ns = qs[y]; ng = qg[y]; nd = den[y];
+    }
+    mp_icloud(tb, kc, dts, dn, tt, v, l, r, ii, sn, g);
     t[x] = tt; qv[x] = v; ql[x] = l; qr[x] = r; qi[x] = ii; qs[x] = sn; qg[x] = g;
   }
 }
