@@ -337,11 +337,15 @@ __device__ __forceinline__ double mp_lagrangian_fall(int n, long P, CRP ze, CRP 
     qe[0] = qp;
     gam[0] = gp;
     double dzp = dz0, ap = a0, zb = z1;
+    double zn_n = z2, ak_n = a1;  // the level's loads, issued one level ahead
     for (int k = 1; k < n; ++k) {
       const long x = (long)k * P;
-      const double zn = zt[x + P];
+      const double zn = zn_n, ak = ak_n;
+      if (k + 1 < n) {
+        zn_n = zt[x + 2 * P];
+        ak_n = a[x + P];
+      }
       const double dzk = zb - zn;
-      const double ak = a[x];
       const double d4 = dzp / dzk;
       const double bt = 2.0 + d4 + d4 - gp;
       qp = (3.0 * (ap + d4 * ak) - qp) / bt;
@@ -365,11 +369,18 @@ __device__ __forceinline__ double mp_lagrangian_fall(int n, long P, CRP ze, CRP 
     double x = qe[xn];
     qe[xn] = fmax(x, 0.0);
     double anext = a[xn - P];
+    double qe_n = qe[xn - P], g_n = gam[xn - P], ap_n = n >= 2 ? a[xn - 2 * P] : 0.0;  // one level ahead
     for (int k = n - 1; k >= 0; --k) {
       const long y = (long)k * P;
-      x = qe[y] - gam[y] * x;
+      const double qek = qe_n, gk = g_n, apk = ap_n;
       if (k >= 1) {
-        const double ap = a[y - P];
+        qe_n = qe[y - P];
+        g_n = gam[y - P];
+        ap_n = k >= 2 ? a[y - 2 * P] : 0.0;
+      }
+      x = qek - gk * x;
+      if (k >= 1) {
+        const double ap = apk;
         qe[y] = fmin(fmax(x, fmin(ap, anext)), fmax(ap, anext));
         anext = ap;
       } else {
