@@ -49,8 +49,9 @@ int gtfv3_get_xyz(void* h, double* out);
 int gtfv3_get_scalars(void* h, double* out);
 
 /* host copy of the same-rank halo table of a kind (0 cell, 1 corner, 2 D-grid, 3 C-grid,
- * 4 A-grid): 6 ints per entry {dst_sub, dst_off, src_sub, src_off, comp, sign}; returns the
- * entry count (writes only when cap >= count). */
+ * 4 A-grid, 5 C-grid tile-edge sync, 6 = 5 then 3 as one exchange): 6 ints per entry
+ * {dst_sub, dst_off, src_sub, src_off, comp, sign}; returns the entry count (writes only
+ * when cap >= count). */
 int gtfv3_halo_table(void* h, int kind, int* out, int cap);
 /* cross-rank halo tables (dir 0 = pack/send, 1 = unpack/recv): entries of 6 ints
  * (sub, plane offset, component, sign, position in the peer's segment, peer rank);
@@ -58,7 +59,8 @@ int gtfv3_halo_table(void* h, int kind, int* out, int cap);
 int gtfv3_halo_remote(void* h, int kind, int dir, int* out, int cap);
 
 /* halo update, spec "name:kind,..." kind c=cell b=corner d=D-grid pair C=C-grid pair a=A-grid pair
- * (a pair lists x then y component, e.g. "u:d,v:d") */
+ * S=C-grid tile-edge sync pair X=sync and C-grid halo in one exchange (a pair lists x then y
+ * component, e.g. "u:d,v:d") */
 int gtfv3_halo_update(void* h, const char* spec);
 
 /* run one named stencil on named fields: NDSL-style `stencil(*fields, params)` */
