@@ -44,6 +44,7 @@ DEVICE_SYMBOLS = [
     "gtfv3_sync",
     "gtfv3_stream",
     "gtfv3_timers",
+    "gtfv3_step_times",
     "gtfv3_halo_remote",
     "gtfv3_kernel_timing",
     "gtfv3_kernel_timing_filter",
@@ -98,6 +99,7 @@ def lib():
         "gtfv3_sync": (I, [P]),
         "gtfv3_stream": (P, [P]),
         "gtfv3_timers": (I, [P, ctypes.c_char_p, I]),
+        "gtfv3_step_times": (I, [P, DP, I, I]),
         "gtfv3_halo_remote": (I, [P, I, I, IP, I]),
         "gtfv3_kernel_timing": (I, [P, I]),
         "gtfv3_kernel_timing_filter": (I, [P, ctypes.c_char_p]),

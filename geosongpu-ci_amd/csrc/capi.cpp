@@ -306,6 +306,17 @@ void* gtfv3_stream(void* h) {
   }
 }
 
+int gtfv3_step_times(void* h, double* out, int cap, int reset) {
+  API_TRY
+  D(h)->flush_all_timers();
+  std::vector<double>& v = D(h)->step_ms;
+  const int n = (int)v.size();
+  if (out && cap >= n) std::copy(v.begin(), v.end(), out);
+  if (reset) v.clear();
+  return n;
+  API_CATCH
+}
+
 int gtfv3_timers(void* h, char* buf, int len) {
   API_TRY
   D(h)->flush_all_timers();

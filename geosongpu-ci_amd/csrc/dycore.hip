@@ -285,6 +285,11 @@ void Dycore::tracer_2d(int nq, double /*dt*/, int fused_mode) {
       fv_tp_2d(c, a);
       std::swap(q.p, qa.p);
     }
+    // the march writes the compute domain only: give the new planes the halo ring of the
+    // last exchange (FV3's q leaves tracer_2d with those halo values, and the bridge copies
+    // q's halo back to the caller).  "q" may now live in the other allocation: device
+    // pointers taken before step() are not stable (gtfv3_device.h gtfv3_field_ptr).
+    copy_halo_ring(c, d.nsub * nq * npz, qa.p, q.p);
     return;
   }
   Field& fx = field("tr_fx", nq * npz);
@@ -669,6 +674,7 @@ void Dycore::flush_timers(int slot) {
   float tot = 0;
   HIP_CHECK(hipEventElapsedTime(&tot, ev[0], ev[4]));
   timers["fv_dynamics"] += tot;
+  step_ms.push_back(tot);
   timers["steps"] += 1;
   ev_pending[slot] = false;
 }

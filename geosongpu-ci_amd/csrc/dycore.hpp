@@ -52,6 +52,9 @@ class Dycore {
   std::vector<double> ak, bk;  // npz+1
   int ks = 0;
   std::map<std::string, double> timers;  // accumulated ms per phase (events)
+  // device time of every completed step (first to last kernel of fv_dynamics on the library
+  // stream), oldest first; the bench's median step time (report.py:152-153)
+  std::vector<double> step_ms;
   // phase events of the last two steps (the step does not wait for its own end: a step's
   // events are read two steps later, or when the timers are queried)
   hipEvent_t ev_ph[2][5] = {};

@@ -12,6 +12,8 @@ void fv_wrapup(const Ctx& c, int npz, int nq, double zvir, const double* q, cons
                const double* w, double* pt, double* omga);
 void c2l_ord4(const Ctx& c, int npz, const double* u, const double* v, double* ua, double* va);
 void held_suarez(const Ctx& c, int npz, double dt, const double* pe, double* pt, double* u, double* v);
+// copy the NG-wide halo ring of nplanes planes (every level of every sub-domain) src -> dst
+void copy_halo_ring(const Ctx& c, int nplanes, const double* src, double* dst);
 void fill_field(const Ctx& c, long n, double a, double* x);
 // y = max(y, x) elementwise
 void max_field(const Ctx& c, long n, const double* x, double* y);

@@ -143,6 +143,16 @@ __global__ void max_k(long n, const double* __restrict__ x, double* __restrict__
   for (; t < n; t += stride) y[t] = fmax(y[t], x[t]);
 }
 
+// the halo ring [-NG, n+NG) x [-NG, n+NG) minus the compute domain, src -> dst, per plane
+__global__ void __launch_bounds__(256) copy_ring_k(Dims d, const double* __restrict__ src, double* __restrict__ dst) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
+  int i, j;
+  if (!thread_point(L, i, j)) return;
+  if (i >= 0 && i < d.nx && j >= 0 && j < d.ny) return;
+  const long o = (long)blockIdx.z * d.plane + pidx(d, i, j);
+  dst[o] = src[o];
+}
+
 inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
   (void)d;
   return plane_grid(L, nz);
@@ -194,6 +204,14 @@ void held_suarez(const Ctx& c, int npz, double dt, const double* pe, double* pt,
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   gt_bytes((npz + 1) * e.C + npz * (2 * e.C + 2 * e.X + 2 * e.Y) + 2 * e.C);
+}
+
+void copy_halo_ring(const Ctx& c, int nplanes, const double* src, double* dst) {
+  const Dims& d = c.d;
+  Launch2D L{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
+  GT_LAUNCH(copy_ring_k, g2(d, L, nplanes), dim3(BX, BY), 0, c.st, d, src, dst);
+  HIP_LAUNCH_CHECK();
+  gt_bytes(2.0 * nplanes * ((d.nx + 2.0 * NG) * (d.ny + 2.0 * NG) - (double)d.nx * d.ny));
 }
 
 void fill_field(const Ctx& c, long n, double a, double* x) {

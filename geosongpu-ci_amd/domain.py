@@ -161,6 +161,18 @@ class Domain:
                 out[k] = (float(ms), int(n), float(b))
         return out
 
+    def step_times(self, reset=True):
+        """device ms of each step completed since the last reset (HIP events on the library
+        stream around fv_dynamics), oldest first"""
+        n = lib().gtfv3_step_times(self.h, None, 0, 0)
+        if n < 0:
+            raise GTFV3Error("gtfv3_step_times failed")
+        out = np.zeros(max(n, 1))
+        n2 = lib().gtfv3_step_times(self.h, dptr(out), len(out), 1 if reset else 0)
+        if n2 < 0:
+            raise GTFV3Error("gtfv3_step_times failed")
+        return out[:n2].tolist()
+
     def timers(self):
         buf = ctypes.create_string_buffer(8192)
         check(lib().gtfv3_timers(self.h, buf, 8192))

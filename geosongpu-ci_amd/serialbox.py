@@ -9,7 +9,10 @@ Serialbox 2 binary archive, restated (Serialbox 2.6, BinaryArchive + MetaDataSer
   MetaData-<prefix>.json         savepoints (name + meta-info), the fields stored at each
                                  savepoint (field -> id in that field's archive table), and
                                  the field map (type id, dims, meta-info)
-  ArchiveMetaData-<prefix>.json  per field the table of stored records [checksum, byte offset]
+  ArchiveMetaData-<prefix>.json  per field the table of stored records [byte offset, checksum]
+                                 (BinaryArchive::updateMetaData writes FileOffsetType{offset,
+                                 checksum} in that order; a [checksum, offset] record, as an
+                                 early writer of this module emitted, is recognised by type)
   <prefix>_<field>.dat           the records, raw little-endian values, column-major
                                  (the Fortran frontend's order, first dimension fastest)
 with one prefix per rank, "Generator_rank<r>" (serialbox_dat_to_netcdf.py:61-64).
@@ -42,6 +45,15 @@ def _meta_value(v):
     return v
 
 
+def _record(r):
+    """(byte offset, checksum) of one fields_table record: Serialbox's order is [offset,
+    checksum]; a [checksum, offset] pair is told apart by the element types"""
+    a, b = r
+    if isinstance(a, str) and not isinstance(b, str):
+        a, b = b, a
+    return int(a), (b or "")
+
+
 class Savepoint:
     def __init__(self, name, meta):
         self.name = name
@@ -63,7 +75,7 @@ class SerialboxReader:
             self.archive = json.load(f)
         spv = self.meta["savepoint_vector"]
         self._sps = [Savepoint(s["name"], s.get("meta_info")) for s in spv["savepoints"]]
-        self._fields = spv["fields_per_savepoint"]
+        self._fields = [f or {} for f in spv["fields_per_savepoint"]]
         self.field_map = self.meta["field_map"]
         self.global_meta_info = {k: _meta_value(v) for k, v in self.meta.get("global_meta_info", {}).items()}
 
@@ -88,11 +100,13 @@ class SerialboxReader:
         dt = TYPE_DTYPE[int(info["type_id"])]
         dims = [int(x) for x in info["dims"]]
         n = int(np.prod(dims)) if dims else 1
-        checksum, offset = self.archive["fields_table"][field][rec]
+        offset, checksum = _record(self.archive["fields_table"][field][rec])
         with open(os.path.join(self.path, f"{self.prefix}_{field}.dat"), "rb") as f:
             f.seek(int(offset))
             raw = f.read(n * dt.itemsize)
-        if verify and checksum and hashlib.sha256(raw).hexdigest() != checksum:
+        algo = str(self.archive.get("hash_algorithm", "SHA256")).lower().replace("-", "")
+        if verify and checksum and algo in ("sha256", "md5") and \
+                hashlib.new(algo, raw).hexdigest().lower() != checksum.lower():
             raise ValueError(f"{field} at {sp}: checksum mismatch")
         return np.frombuffer(raw, dtype=dt).reshape(dims, order="F").copy()
 
@@ -130,7 +144,7 @@ class SerialboxWriter:
         offset = os.path.getsize(fn) if os.path.exists(fn) else 0
         with open(fn, "ab") as f:
             f.write(raw)
-        self.table.setdefault(field, []).append([hashlib.sha256(raw).hexdigest(), offset])
+        self.table.setdefault(field, []).append([offset, hashlib.sha256(raw).hexdigest()])
         self.fields[idx][field] = len(self.table[field]) - 1
 
     def close(self):

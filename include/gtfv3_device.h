@@ -39,7 +39,9 @@ int gtfv3_field_upload(void* h, const char* name, int nk, const double* host);
 int gtfv3_field_download(void* h, const char* name, double* host);
 /* levels [k0, k0+nk) of an existing field from host (nsub, nk, nj, pitch) */
 int gtfv3_field_upload_levels(void* h, const char* name, int k0, int nk, const double* host);
-/* raw device pointer of a field (for zero-copy interop), NULL if missing */
+/* raw device pointer of a field (for zero-copy interop), NULL if missing.  Valid until the
+ * next gtfv3_step: the step ping-pongs q (tracer_2d) between two allocations, so take the
+ * pointer again after each step. */
 void* gtfv3_field_ptr(void* h, const char* name);
 
 /* metric plane(s) [nsub][plane] by name (see grid.cpp kMetricNames) */
@@ -74,6 +76,10 @@ int gtfv3_sync(void* h);
 void* gtfv3_stream(void* h);
 /* accumulated per-phase timers (ms), "name=value;..." into buf */
 int gtfv3_timers(void* h, char* buf, int len);
+/* device time (ms) of each step completed since the last reset, oldest first: HIP events on the
+ * library stream around one fv_dynamics call (first to last kernel).  Returns the count and
+ * copies when cap >= count; reset != 0 clears the record afterwards. */
+int gtfv3_step_times(void* h, double* out, int cap, int reset);
 /* per-kernel HIP-event timing (off by default); enabling resets the statistics */
 int gtfv3_kernel_timing(void* h, int on);
 /* time only this kernel family (name without template arguments, e.g. "tp_march"); NULL or "": all */

@@ -42,6 +42,52 @@ def test_archive_round_trip(sb, tmp_path):
         rd.read("u", sps[0])
 
 
+def test_reads_hand_written_upstream_layout(sb, tmp_path):
+    """A MetaData / ArchiveMetaData pair written by hand in Serialbox 2.6's own layout
+    (SavepointVector::toJSON, FieldMap::toJSON, BinaryArchive::updateMetaData: records are
+    [offset, checksum], MD5 when the library was built without OpenSSL), not by this
+    module's writer."""
+    import hashlib
+    import json
+    r = np.random.default_rng(11)
+    delp = r.standard_normal((5, 4, 2))
+    ks = np.array([7], dtype=np.int32)
+    b_delp = np.asfortranarray(delp).tobytes(order="F")
+    # two records of delp; the second one is the one the savepoint points at
+    with open(tmp_path / "Generator_rank0_delp.dat", "wb") as f:
+        f.write(b"\x00" * len(b_delp) + b_delp)
+    with open(tmp_path / "Generator_rank0_ks.dat", "wb") as f:
+        f.write(ks.tobytes())
+    meta = {
+        "serialbox_version": 20600, "prefix": "Generator_rank0",
+        "global_meta_info": {"layout": {"type_id": 2, "value": 1}},
+        "savepoint_vector": {
+            "savepoints": [{"name": "FVDynamics-In", "meta_info": {"i_call": {"type_id": 2, "value": 0}}},
+                           {"name": "Driver-In", "meta_info": {}}],
+            "fields_per_savepoint": [{"delp": 1, "ks": 0}, None]},
+        "field_map": {"delp": {"type_id": 5, "dims": [5, 4, 2], "meta_info": {}},
+                      "ks": {"type_id": 2, "dims": [1], "meta_info": {}}},
+    }
+    arch = {"serialbox_version": 20600, "archive_name": "Binary", "archive_version": 0, "hash_algorithm": "MD5",
+            "fields_table": {"delp": [[0, hashlib.md5(b"\x00" * len(b_delp)).hexdigest()],
+                                      [len(b_delp), hashlib.md5(b_delp).hexdigest().upper()]],
+                             "ks": [[0, hashlib.md5(ks.tobytes()).hexdigest()]]}}
+    (tmp_path / "MetaData-Generator_rank0.json").write_text(json.dumps(meta))
+    (tmp_path / "ArchiveMetaData-Generator_rank0.json").write_text(json.dumps(arch))
+    rd = sb.SerialboxReader(str(tmp_path), "Generator_rank0")
+    sp = rd.get_savepoint("FVDynamics-In")[0]
+    assert sp.meta_info == {"i_call": 0}
+    assert np.array_equal(rd.read("delp", sp), delp)
+    assert int(rd.read("ks", sp)[0]) == 7
+    assert rd.fields_at_savepoint(rd.get_savepoint("Driver-In")[0]) == []
+    # this module's writer emits the same record order
+    w = sb.SerialboxWriter(str(tmp_path / "w"), "p")
+    w.write("delp", "s", delp)
+    w.close()
+    rec = json.loads((tmp_path / "w" / "ArchiveMetaData-p.json").read_text())["fields_table"]["delp"][0]
+    assert isinstance(rec[0], int) and isinstance(rec[1], str)
+
+
 def test_namelist_reader(sb, tmp_path):
     p = tmp_path / "input.nml"
     p.write_text("&fv_core_nml\n  layout = 2, 3  ! comment\n  npx = 49, hydrostatic = .false.\n"
