@@ -32,6 +32,7 @@ DEVICE_SYMBOLS = [
     "gtfv3_field_upload",
     "gtfv3_field_download",
     "gtfv3_field_upload_levels",
+    "gtfv3_field_download_levels",
     "gtfv3_field_ptr",
     "gtfv3_get_metric",
     "gtfv3_get_xyz",
@@ -87,6 +88,7 @@ def lib():
         "gtfv3_field_upload": (I, [P, S, I, DP]),
         "gtfv3_field_download": (I, [P, S, DP]),
         "gtfv3_field_upload_levels": (I, [P, S, I, I, DP]),
+        "gtfv3_field_download_levels": (I, [P, S, I, I, DP]),
         "gtfv3_field_ptr": (P, [P, S]),
         "gtfv3_get_metric": (I, [P, S, DP]),
         "gtfv3_get_xyz": (I, [P, DP]),

@@ -188,6 +188,12 @@ int gtfv3_field_upload_levels(void* h, const char* name, int k0, int nk, const d
   API_CATCH
 }
 
+int gtfv3_field_download_levels(void* h, const char* name, int k0, int nk, double* host) {
+  API_TRY
+  D(h)->download_levels(name, host, k0, nk);
+  API_CATCH
+}
+
 int gtfv3_field_download(void* h, const char* name, double* host) {
   API_TRY
   D(h)->download(name, host);

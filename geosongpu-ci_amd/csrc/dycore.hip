@@ -173,6 +173,16 @@ void Dycore::upload_levels(const std::string& name, const double* host, int k0, 
   HIP_CHECK(hipStreamSynchronize(st));
 }
 
+void Dycore::download_levels(const std::string& name, double* host, int k0, int nk) {
+  Field* f = find(name);
+  if (!f) throw std::runtime_error("no field '" + name + "'");
+  if (k0 < 0 || nk < 1 || k0 + nk > f->nk) throw std::runtime_error("download_levels: level range outside the field");
+  HIP_CHECK(hipMemcpy2DAsync(host, sizeof(double) * nk * d.plane, f->p + (long)k0 * d.plane,
+                             sizeof(double) * f->nk * d.plane, sizeof(double) * nk * d.plane, d.nsub,
+                             hipMemcpyDeviceToHost, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+}
+
 void Dycore::download(const std::string& name, double* host) {
   Field* f = find(name);
   if (!f) throw std::runtime_error("no field '" + name + "'");

@@ -81,6 +81,8 @@ class Dycore {
   // host (nsub, nk, plane) into levels [k0, k0+nk) of an existing field (large tracer sets
   // are uploaded tracer by tracer)
   void upload_levels(const std::string& name, const double* host, int k0, int nk);
+  // levels [k0, k0+nk) of every sub-domain into host (nsub, nk, plane)
+  void download_levels(const std::string& name, double* host, int k0, int nk);
 
   // halo update of named fields; kinds: 'c' cell, 'b' corner, 'd' D-grid pair, 'C' C-grid pair, 'a' A-grid pair,
   // 'S' C-grid pair tile-edge synchronisation (east / north edge values from the neighbour)

@@ -153,6 +153,69 @@ __global__ void __launch_bounds__(256) copy_ring_k(Dims d, const double* __restr
   dst[o] = src[o];
 }
 
+// global tracer diagnostics (FV3 fv_diagnostics prt_mass / g_sum): one block per (sub-domain,
+// tracer, level) plane reduces sum(q * delp * area), min q, max q and the count of non-finite
+// q over the compute domain into part[(iq * nsub + s) * npz + k][4]
+__global__ void __launch_bounds__(256) tracer_stats_k(Dims d, const double* __restrict__ M, int npz, int nq,
+                                                      const double* __restrict__ q, const double* __restrict__ delp,
+                                                      double* __restrict__ part) {
+  __shared__ double red[4][256];
+  const int z = blockIdx.x;
+  const int s = z / (nq * npz), r = z - s * nq * npz, iq = r / npz, k = r - iq * npz;
+  const double* Q = q + (long)z * d.plane;
+  const double* DP = delp + ((long)s * npz + k) * d.plane;
+  const double* A = met(M, d, M_AREA, s);
+  double sm = 0.0, mn = 1.0e300, mx = -1.0e300, bad = 0.0;
+  for (int t = threadIdx.x; t < d.nx * d.ny; t += 256) {
+    const int j = t / d.nx, i = t - j * d.nx;
+    const long o = pidx(d, i, j);
+    const double v = Q[o];
+    if (!isfinite(v)) {
+      bad += 1.0;
+      continue;
+    }
+    sm += v * DP[o] * A[o];
+    mn = fmin(mn, v);
+    mx = fmax(mx, v);
+  }
+  red[0][threadIdx.x] = sm;
+  red[1][threadIdx.x] = mn;
+  red[2][threadIdx.x] = mx;
+  red[3][threadIdx.x] = bad;
+  __syncthreads();
+  for (int h = 128; h > 0; h >>= 1) {
+    if ((int)threadIdx.x < h) {
+      red[0][threadIdx.x] += red[0][threadIdx.x + h];
+      red[1][threadIdx.x] = fmin(red[1][threadIdx.x], red[1][threadIdx.x + h]);
+      red[2][threadIdx.x] = fmax(red[2][threadIdx.x], red[2][threadIdx.x + h]);
+      red[3][threadIdx.x] += red[3][threadIdx.x + h];
+    }
+    __syncthreads();
+  }
+  if (threadIdx.x < 4) {
+    const int nsub = gridDim.x / (nq * npz);
+    part[(((long)iq * nsub + s) * npz + k) * 4 + threadIdx.x] = red[threadIdx.x][0];
+  }
+}
+
+// per tracer, in a fixed order over the (sub-domain, level) partials: out[iq][4]
+__global__ void tracer_stats_fin_k(int nq, int nper, const double* __restrict__ part, double* __restrict__ out) {
+  const int iq = blockIdx.x * blockDim.x + threadIdx.x;
+  if (iq >= nq) return;
+  const double* P = part + (long)iq * nper * 4;
+  double sm = 0.0, mn = 1.0e300, mx = -1.0e300, bad = 0.0;
+  for (int n = 0; n < nper; ++n) {
+    sm += P[4 * n];
+    mn = fmin(mn, P[4 * n + 1]);
+    mx = fmax(mx, P[4 * n + 2]);
+    bad += P[4 * n + 3];
+  }
+  out[4 * iq] = sm;
+  out[4 * iq + 1] = mn;
+  out[4 * iq + 2] = mx;
+  out[4 * iq + 3] = bad;
+}
+
 inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
   (void)d;
   return plane_grid(L, nz);
@@ -212,6 +275,15 @@ void copy_halo_ring(const Ctx& c, int nplanes, const double* src, double* dst) {
   GT_LAUNCH(copy_ring_k, g2(d, L, nplanes), dim3(BX, BY), 0, c.st, d, src, dst);
   HIP_LAUNCH_CHECK();
   gt_bytes(2.0 * nplanes * ((d.nx + 2.0 * NG) * (d.ny + 2.0 * NG) - (double)d.nx * d.ny));
+}
+
+void tracer_stats(const Ctx& c, int npz, int nq, const double* q, const double* delp, double* part, double* out) {
+  const Dims& d = c.d;
+  GT_LAUNCH(tracer_stats_k, dim3((unsigned)(d.nsub * nq * npz)), dim3(256), 0, c.st, d, c.met, npz, nq, q, delp, part);
+  HIP_LAUNCH_CHECK();
+  gt_bytes((nq + 1.0) * npz * ext(d).C + ext(d).C);
+  GT_LAUNCH(tracer_stats_fin_k, dim3(cdiv(nq, 64)), dim3(64), 0, c.st, nq, d.nsub * npz, part, out);
+  HIP_LAUNCH_CHECK();
 }
 
 void fill_field(const Ctx& c, long n, double a, double* x) {

@@ -370,6 +370,19 @@ std::map<std::string, Fn>& reg() {
        [](Dycore& dy, const std::vector<std::string>&, const std::vector<double>& p) {
          dy.moist_physics(p.at(0));
        }},
+      // tracer_stats: global diagnostics of the state's q (FV3 prt_mass / g_sum) into the field
+      // "tracer_stats" (first 4 * nq values: per tracer sum(q delp area), min, max, non-finite count)
+      {"tracer_stats",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
+         need(f, 0, "tracer_stats");
+         const int npz = dy.nl.npz, nq = dy.nl.nq;
+         Field& q = dy.need("q", nq * npz);
+         Field& dp = dy.need("delp", npz);
+         const long npart = 4L * nq * dy.d.nsub * npz, per = (long)dy.d.nsub * dy.d.plane;
+         if (4L * nq > per) throw std::runtime_error("tracer_stats: too many tracers for one plane set");
+         double* part = dy.field("_tr_part", (int)((npart + per - 1) / per)).p;
+         tracer_stats(dy.ctx(), npz, nq, q.p, dp.p, part, dy.field("tracer_stats", 1).p);
+       }},
       // Held-Suarez forcing: held_suarez(pe, pt, u, v) in place, params: dt
       {"held_suarez",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {

@@ -113,7 +113,14 @@ class Domain:
         check(lib().gtfv3_field_download(self.h, name.encode(), dptr(out)))
         return out
 
+    def download_levels(self, name, k0, nk):
+        """levels k0 .. k0 + nk - 1 of a field, every sub-domain: (nsub, nk, nj, pitch)"""
+        out = np.zeros(self.shape(nk))
+        check(lib().gtfv3_field_download_levels(self.h, name.encode(), int(k0), int(nk), dptr(out)))
+        return out
+
     def device_ptr(self, name):
+        """raw device pointer; valid until the next step() (q ping-pongs between planes)"""
         return lib().gtfv3_field_ptr(self.h, name.encode())
 
     # ---- operations ----
@@ -123,6 +130,12 @@ class Domain:
     def stencil(self, name, fields, params=()):
         p = np.ascontiguousarray(params, dtype=np.float64) if len(params) else np.zeros(1)
         check(lib().gtfv3_stencil(self.h, name.encode(), ",".join(fields).encode(), dptr(p), len(params)))
+
+    def tracer_stats(self):
+        """(nq, 4) array per tracer of the device state: sum(q * delp * area) over the compute
+        domain, min q, max q, count of non-finite q (the "tracer_stats" stencil)"""
+        self.stencil("tracer_stats", [])
+        return self.download("tracer_stats")[0, 0].ravel()[:4 * self.nq].reshape(self.nq, 4)
 
     def set_vertical(self, ak, bk, ks):
         ak = np.ascontiguousarray(ak, dtype=np.float64)

@@ -39,6 +39,8 @@ int gtfv3_field_upload(void* h, const char* name, int nk, const double* host);
 int gtfv3_field_download(void* h, const char* name, double* host);
 /* levels [k0, k0+nk) of an existing field from host (nsub, nk, nj, pitch) */
 int gtfv3_field_upload_levels(void* h, const char* name, int k0, int nk, const double* host);
+/* levels [k0, k0+nk) of every sub-domain of an existing field into host (nsub, nk, nj, pitch) */
+int gtfv3_field_download_levels(void* h, const char* name, int k0, int nk, double* host);
 /* raw device pointer of a field (for zero-copy interop), NULL if missing.  Valid until the
  * next gtfv3_step: the step ping-pongs q (tracer_2d) between two allocations, so take the
  * pointer again after each step. */

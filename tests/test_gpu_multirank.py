@@ -2,7 +2,7 @@
 the loopback transport (comm.cpp), which runs the same host tables and the same
 pack / unpack kernels as the RCCL path, with device-to-device copies in place of
 ncclSend / ncclRecv.  The sub-domain layouts are exactly bench.py's for the driver's
-2, 4 and 8 GPU runs; every rank's state after a full fv_dynamics step must equal the
+2, 4 and 8 GPU runs, plus config 3's one tile per rank on 6 ranks; every rank's state after a full fv_dynamics step must equal the
 single-rank step of the same global state bit for bit."""
 import importlib
 import itertools
@@ -49,7 +49,8 @@ def _run_ranks(pkg, nranks, layout, npx=13, npz=10, nq=2):
     return doms, out
 
 
-@pytest.mark.parametrize("nranks,layout,npx", [(2, (1, 1), 13), (4, (1, 2), 13), (8, (2, 2), 13), (8, (1, 4), 25)])
+@pytest.mark.parametrize("nranks,layout,npx", [(2, (1, 1), 13), (4, (1, 2), 13), (6, (1, 1), 13), (6, (1, 1), 49), (8, (2, 2), 13),
+                                                  (8, (1, 4), 25)])
 def test_multirank_step_matches_single_rank(pkg, require_gpu, nranks, layout, npx):
     state = importlib.import_module(pkg.__name__ + ".state")
     npz = 10

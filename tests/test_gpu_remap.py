@@ -44,7 +44,7 @@ def lagrangian_state(pkg, d, npz, nq, r):
     return st, ak, bk, ks
 
 
-@pytest.mark.parametrize("npz,nq", [(72, 4), (137, 2), (10, 3)])
+@pytest.mark.parametrize("npz,nq", [(72, 4), (137, 2), (10, 3), (137, 11), (137, 19), (72, 11)])
 def test_remap_vs_oracle(pkg, require_gpu, npz, nq):
     d = pkg.Domain(npx=13, npz=npz, nq=nq)
     r = rng(300 + npz)

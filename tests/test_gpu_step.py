@@ -31,9 +31,9 @@ def comp(a, nx, ny):
     return a[..., NG:NG + ny, NG:NG + nx]
 
 
-def run_pair(pkg, npx, npz, nq, layout, nsteps=1):
+def run_pair(pkg, npx, npz, nq, layout, nsteps=1, n_split=6, ptrs=None):
     state = importlib.import_module(pkg.__name__ + ".state")
-    d = pkg.Domain(npx=npx, npz=npz, nq=nq, layout_x=layout[0], layout_y=layout[1])
+    d = pkg.Domain(npx=npx, npz=npz, nq=nq, layout_x=layout[0], layout_y=layout[1], n_split=n_split)
     ak, bk, ks = state.hybrid_levels(npz)
     st = state.jablonowski_williamson(d, ak, bk)
     d.set_vertical(ak, bk, ks)
@@ -42,13 +42,61 @@ def run_pair(pkg, npx, npz, nq, layout, nsteps=1):
     ms = metrics_of(d)
     sc = d.scalars()
     g = fvd.Grid(d.N, layout[0], layout[1], ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
-    nl = dict(NL, nq=nq)
+    nl = dict(NL, nq=nq, n_split=n_split)
     ref = st
+    if ptrs is not None:
+        ptrs["before"] = {k: d.device_ptr(k) for k in ("delp", "w", "pt", "u", "v")}
     for _ in range(nsteps):
         d.step(1)
         ref = fvd.fv_dynamics(ref, ak, bk, g, nl)
+    if ptrs is not None:
+        ptrs["after"] = {k: d.device_ptr(k) for k in ("delp", "w", "pt", "u", "v")}
     got = {k: d.download(k) for k in FIELDS}
     return d, got, ref
+
+
+def check_parity(d, got, ref):
+    nx, ny = d.nx, d.ny
+    worst = {}
+    for k in FIELDS:
+        a, b = comp(got[k], nx, ny), comp(ref[k], nx, ny)
+        assert np.all(np.isfinite(b)), f"{k}: oracle not finite"
+        assert np.all(np.isfinite(a)), f"{k}: HIP not finite"
+        worst[k] = np.abs(a - b).max() / (np.abs(b).mean() + 1e-300)
+    print("max |hip - oracle| / mean|oracle|:", {k: f"{v:.2e}" for k, v in worst.items()})
+    absbar = dict(w=1e-10, omga=1e-9)
+    for k, v in worst.items():
+        if k in absbar:
+            err = np.abs(comp(got[k], nx, ny) - comp(ref[k], nx, ny)).max()
+            assert err <= absbar[k], f"{k}: abs error {err:.3e}"
+        else:
+            assert v <= 1e-9, f"{k}: scaled error {v:.3e} (all: {worst})"
+    assert np.abs(comp(got["ps"], nx, ny) - comp(ref["ps"], nx, ny)).max() <= 1e-12 * 1e5
+
+
+@pytest.mark.parametrize("npz,nq", [(72, 4), (137, 10)])
+def test_fv_dynamics_step_parity_levels(pkg, require_gpu, npz, nq):
+    """BASELINE.json config 1's grid, C12 L72 (here with all six tiles), and the L137
+    vertical of config 5 with 10 tracers (the remap's and the tracer march's multi-tracer
+    paths past their 8-slot chunks), one step against the oracle."""
+    d, got, ref = run_pair(pkg, 13, npz, nq, (1, 1))
+    try:
+        check_parity(d, got, ref)
+    finally:
+        d.close()
+
+
+def test_fv_dynamics_odd_n_split(pkg, require_gpu):
+    """n_split = 5 (odd): the fused d_sw thermo march's ping-pong ends on the second planes
+    and is copied back (Dycore::step); parity with the oracle and delp / w / pt / u / v on
+    their original device planes after the step."""
+    ptrs = {}
+    d, got, ref = run_pair(pkg, 13, 10, 2, (1, 1), n_split=5, ptrs=ptrs)
+    try:
+        check_parity(d, got, ref)
+        assert ptrs["before"] == ptrs["after"]
+    finally:
+        d.close()
 
 
 @pytest.mark.parametrize("layout", [(1, 1), (2, 2)])
