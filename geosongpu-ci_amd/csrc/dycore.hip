@@ -234,7 +234,7 @@ void Dycore::set_vertical(const double* ak_, const double* bk_, int ks_) {
 // tracer_2d_1l (FV3 fv_tracer2d): large-time-step transport of nq tracers with
 // the mass fluxes (mfx,mfy) and Courant numbers (cx,cy) accumulated over the
 // acoustic sub-steps; dp1 = delp at the start of the step.
-void Dycore::tracer_2d(int nq, double /*dt*/, int fused_mode) {
+void Dycore::tracer_2d(int nq, double /*dt*/, int fused_mode, int nf) {
   const int npz = nl.npz;
   Ctx c = ctx();
   Field& q = field("q", nq * npz);
@@ -283,6 +283,11 @@ void Dycore::tracer_2d(int nq, double /*dt*/, int fused_mode) {
   a.crx = cx.p; a.cry = cy.p; a.xfx = xfx.p; a.yfx = yfx.p;
   a.mfx = mfx.p; a.mfy = mfy.p;
   a.ord = nl.hord_tr;
+  static const int nf_env = [] {
+    const char* e = getenv("GTFV3_TRACER_NF");
+    return e ? atoi(e) : 0;
+  }();
+  a.nf = nf != 0 ? nf : (nf_env > 0 && nq % nf_env == 0 && (fused || nf_env < 3) ? nf_env : 0);
   if (fused) {
     // each sub-step updates the tracers into a second set of planes, which then become "q"
     // (the march reads neighbouring columns' tracers as its halo: no in-place update)

@@ -92,7 +92,8 @@ class Dycore {
 
   // algorithm blocks
   // fused: 1 update inside the march, 0 flux planes + separate update, -1 GTFV3_TRACER_FUSED
-  void tracer_2d(int nq, double dt, int fused = -1);
+  // nf: tracers per march wave (1, 2, 3; 0: GTFV3_TRACER_NF, else 2 for even nq, 1 for odd)
+  void tracer_2d(int nq, double dt, int fused = -1, int nf = 0);
   void set_vertical(const double* ak_, const double* bk_, int ks_);
   void step();  // one fv_dynamics call on device-resident state
   // Aquaplanet moist column step on the state (tracers 0..5 = qv ql qr qi qs qg, nq >= 6)

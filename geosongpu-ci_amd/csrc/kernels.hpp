@@ -45,6 +45,7 @@ struct TpArgs {
   double *fx, *fy;
   int ord;
   int cfg = -1;  // tile variant (tuning); -1: default
+  int nf = 0;    // fields per wave (1, 2, 3 dividing nt; 3 only with q_out); 0: 2 for even nt, else 1
   // tracer_2d_1l update fused into the march (mfx / mfy required): the nt tracers are
   // updated into q_out (no flux planes), dp2 = dp1 + mass-flux divergence written to dp2;
   // levels with it >= nsplt[k] are copied unchanged

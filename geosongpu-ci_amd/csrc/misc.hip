@@ -1,6 +1,8 @@
 // misc.hip — pointwise pieces of fv_dynamics on gfx950: entry conversion to
 // virtual potential temperature + pkz, zh from delz, exit conversion (T, omega),
 // cubed_to_latlon (c2l_ord4) and the Held & Suarez (1994) forcing of GEOShs.
+#include <cstdlib>
+
 #include "kernels_misc.hpp"
 #include "stencil_common.hpp"
 
@@ -222,6 +224,14 @@ inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
 }
 
 }  // namespace
+
+bool xcd_order_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("GTFV3_XCD");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 void fv_prep(const Ctx& c, int npz, int nq, double zvir, const double* delp, const double* delz, const double* q, double* pt,
              double* pkz) {

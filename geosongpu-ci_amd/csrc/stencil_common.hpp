@@ -30,17 +30,34 @@ struct Launch2D {
   int ni, nj;  // extent
 };
 
+// XCD-aware block order.  Workgroups are dealt round-robin over the 8 XCDs (blocks b and
+// b + 8 share one L2; placement is a speed matter only, never correctness).  When a plane's
+// block count gridDim.x is a multiple of 8, physical block x covers logical block
+// (x % 8) * (gridDim.x / 8) + x / 8: each XCD sweeps one contiguous eighth of the plane, so
+// the j +- 1 rows a stencil reads were fetched by the same L2, and the next level's plane
+// (blockIdx.z) puts the same eighth on the same XCD, whose L2 still holds its metric terms.
+// Any other gridDim.x keeps the identity order (plane_grid pads to a multiple of 8).
+__device__ __forceinline__ unsigned xcd_block() {
+  const unsigned gx = gridDim.x, x = blockIdx.x;
+  if (gx & 7u) return x;
+  return (x & 7u) * (gx >> 3) + (x >> 3);
+}
+
 __device__ __forceinline__ bool thread_point(const Launch2D& L, int& i, int& j) {
-  const int t = (int)(blockIdx.x * (BX * BY) + threadIdx.y * BX + threadIdx.x);
+  const int t = (int)(xcd_block() * (BX * BY) + threadIdx.y * BX + threadIdx.x);
   if (t >= L.ni * L.nj) return false;
   j = t / L.ni;
   i = L.i0 + (t - j * L.ni);
   j += L.j0;
   return true;
 }
-// grid for thread_point over region L and nz planes (blockIdx.z)
+// grid for thread_point over region L and nz planes (blockIdx.z), padded to a multiple of 8
+// blocks per plane (xcd_block; GTFV3_XCD=0: one block more, which keeps the identity order)
+bool xcd_order_enabled();
 inline dim3 plane_grid(const Launch2D& L, long nz) {
-  return dim3((unsigned)(((long)L.ni * L.nj + BX * BY - 1) / (BX * BY)), 1, (unsigned)nz);
+  long gx = ((long)L.ni * L.nj + BX * BY - 1) / (BX * BY);
+  gx = xcd_order_enabled() ? (gx + 7) / 8 * 8 : (gx + 7) / 8 * 8 + 1;
+  return dim3((unsigned)gx, 1, (unsigned)nz);
 }
 
 // FV3 copy_corners source cell (global indices) for a cube-corner halo cell,

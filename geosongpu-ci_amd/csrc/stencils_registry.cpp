@@ -392,12 +392,13 @@ std::map<std::string, Fn>& reg() {
          held_suarez(dy.ctx(), pt.nk, p.at(0), F(dy, f[0]).p, pt.p, F(dy, f[2]).p, F(dy, f[3]).p);
        }},
       // tracer_2d_1l: uses state fields q, dp1, cx, cy, mfx, mfy. params: nq[, fused (1: the
-      // update inside the march, 0: flux planes and the separate update)]
+      // update inside the march, 0: flux planes and the separate update)[, tracers per march
+      // wave (1, 2, 3; 0 default)]]
       {"tracer_2d_1l",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
          (void)f;
          int nq = p.size() > 0 ? (int)p[0] : dy.nl.nq;
-         dy.tracer_2d(nq, dy.nl.dt_atmos, p.size() > 1 ? (int)p[1] : -1);
+         dy.tracer_2d(nq, dy.nl.dt_atmos, p.size() > 1 ? (int)p[1] : -1, p.size() > 2 ? (int)p[2] : 0);
        }},
   };
   return r;

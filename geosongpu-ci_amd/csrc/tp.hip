@@ -70,8 +70,8 @@ struct TpM {
   int it;
   int nt, nk, ntg;
   const double *crx, *cry, *xfx, *yfx, *mx, *my;
-  double* fxf[2];
-  double* fyf[2];
+  double* fxf[3];
+  double* fyf[3];
   int nz, nstrip, nseg, seg;
   // split launches (EXS != 0): the (sub-domain, strip) pairs of this launch's kind, as
   // s * 256 + strip; a wave's pair index runs fastest, so the four waves of a workgroup
@@ -358,12 +358,12 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
 #pragma unroll
   for (int f = 0; f < NF; ++f) {
     if (TM == 0) {
-      rFX[f] = rsrcf(a.fxf[f < 2 ? f : 0] + zo);
-      rFY[f] = rsrcf(a.fyf[f < 2 ? f : 0] + zo);
+      rFX[f] = rsrcf(a.fxf[f] + zo);
+      rFY[f] = rsrcf(a.fyf[f] + zo);
     } else if (TM == 1) {
       rFX[f] = rsrcf(a.qo[f] + fo);  // updated field f (TM = 1 groups are one field each)
     } else {
-      rFX[f] = rsrcf(a.qo[f < 2 ? f : 0] + zo);  // updated tracer f of the group
+      rFX[f] = rsrcf(a.qo[f] + zo);  // updated tracer f of the group
     }
   }
   auto bst = [&](__amdgpu_buffer_rsrc_t r, uint32_t soff, double v) {
@@ -922,7 +922,10 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
   // consecutive tracers when their count is even
   const bool pair2 = a.q2 != nullptr;
   if (pair2 && a.nt != 1) throw std::runtime_error("fv_tp_2d: a second field array needs nt = 1");
-  const int NFw = pair2 || (a.nt % 2 == 0) ? 2 : 1;
+  // fields per wave: a.nf when given (1, 2 or 3, dividing nt), else 2 for pairs / even nt
+  if (a.nf != 0 && (pair2 || a.nf < 1 || a.nf > 3 || a.nt % a.nf != 0 || (a.nf == 3 && !a.q_out)))
+    throw std::runtime_error("fv_tp_2d: nf must be 1, 2 or 3 (3 only for the tracer update) and divide nt");
+  const int NFw = a.nf != 0 ? a.nf : (pair2 || (a.nt % 2 == 0) ? 2 : 1);
   const int nfields = pair2 ? 2 : a.nt;
   {
     static const int seg_env = [] {
@@ -935,23 +938,33 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     m.M = c.met;
   m.area2 = c.area2;
     const long tstride = (long)a.nk * d.plane;  // next tracer of the same sub-domain
+    // field f of a group at slot f (the group's plane offset is added in the kernel); every
+    // slot below NFw must be set: a null or stale slot is an out-of-bounds access
     m.qf[0] = a.q;
     m.qf[1] = pair2 ? a.q2 : a.q + tstride;
+    m.qf[2] = pair2 ? nullptr : a.q + 2 * tstride;
     m.fxf[0] = a.fx;
     m.fyf[0] = a.fy;
-    m.fxf[1] = pair2 ? a.fx_2 : a.fx + tstride;
-    m.fyf[1] = pair2 ? a.fy_2 : a.fy + tstride;
+    m.fxf[1] = pair2 ? a.fx_2 : (a.fx ? a.fx + tstride : nullptr);
+    m.fyf[1] = pair2 ? a.fy_2 : (a.fy ? a.fy + tstride : nullptr);
+    m.fxf[2] = pair2 || !a.fx ? nullptr : a.fx + 2 * tstride;
+    m.fyf[2] = pair2 || !a.fy ? nullptr : a.fy + 2 * tstride;
     const bool tupd = a.q_out != nullptr;
     if (tupd) {
       if (pair2 || !a.mfx || !a.dp1 || !a.dp2 || !a.nsplt)
         throw std::runtime_error("fv_tp_2d tracer update: tracer array, mass fluxes, dp1, dp2, nsplt needed");
       m.qo[0] = a.q_out;
       m.qo[1] = a.q_out + tstride;
+      m.qo[2] = a.q_out + 2 * tstride;
       m.dp1 = a.dp1;
       m.dp2o = a.dp2;
       m.nsplt = a.nsplt;
       m.it = a.it;
     }
+    for (int f = 0; f < NFw; ++f)
+      if (!m.qf[f] || (tupd ? !m.qo[f] : (!m.fxf[f] || !m.fyf[f])))
+        throw std::runtime_error("fv_tp_2d: field slot " + std::to_string(f) + " of a " + std::to_string(NFw) +
+                                 "-field group is not set");
     m.nt = a.nt;
     m.nk = a.nk;
     m.ntg = pair2 ? 1 : a.nt / NFw;
@@ -1005,7 +1018,8 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     HIP_LAUNCH_CHECK();                                                                               \
     gt_bytes(bytes / 8.0);                                                                            \
   } while (0)
-      if (NFw == 2) { if (a.ord == 5) TQ_GO(5, 2); else TQ_GO(6, 2); }
+      if (NFw == 3) { if (a.ord == 5) TQ_GO(5, 3); else TQ_GO(6, 3); }
+      else if (NFw == 2) { if (a.ord == 5) TQ_GO(5, 2); else TQ_GO(6, 2); }
       else { if (a.ord == 5) TQ_GO(5, 1); else TQ_GO(6, 1); }
 #undef TQ_GO
     } else if (a.mfx) {

@@ -179,3 +179,23 @@ def test_tracer_update_in_march_matches_separate_update(pkg, require_gpu, npx, n
         out.append(d.download("q")[:, :, NG:NG + d.ny, NG:NG + d.nx])
     assert np.array_equal(out[0], out[1])
     d.close()
+
+
+@pytest.mark.parametrize("npx,npz,nq,cmax_amp", [(181, 2, 9, 0.45), (181, 3, 6, 1.3), (13, 6, 3, 1.2)])
+def test_tracer_march_three_fields_per_wave(pkg, require_gpu, npx, npz, nq, cmax_amp):
+    """The fused tracer march with three tracers per wave (every TpM field slot below NF set,
+    the updated tracer f written to its own slot) bit for bit against one tracer per wave and,
+    for even nq, two: C180 with an odd tracer count (nq = 9), C180 with sub-steps, C12."""
+    d = make_dom(pkg, npx, npz, nq)
+    inp = _tracer_inputs(d, npz, nq, cmax_amp, 23)
+    out = {}
+    for nf in (3, 1) + ((2,) if nq % 2 == 0 else ()):
+        for name, v in inp.items():
+            d.upload(name, v)
+        d.stencil("tracer_2d_1l", [], [nq, 1, nf])
+        out[nf] = d.download("q")[:, :, NG:NG + d.ny, NG:NG + d.nx]
+    for nf, v in out.items():
+        assert np.array_equal(v, out[1]), f"nf = {nf} differs from one tracer per wave"
+    with pytest.raises(Exception, match="nf must"):
+        d.stencil("tracer_2d_1l", [], [nq, 1, 4])
+    d.close()
