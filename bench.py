@@ -178,14 +178,8 @@ def cpu_baseline(pkg, npx, npz, nq, dt, moist=False):
     st = state.jablonowski_williamson(d, ak, bk)
     if moist:
         state.aquaplanet_tracers(d, st, ak, bk)
-    names = ["area", "rarea", "area_c", "rarea_c", "dx", "dy", "dxa", "dya", "dxc", "dyc", "rdx", "rdy",
-             "rdxa", "rdya", "rdxc", "rdyc"] + [f"sin_sg{i}" for i in range(1, 10)] + \
-        [f"cos_sg{i}" for i in range(1, 10)] + ["cosa_u", "sina_u", "rsin_u", "cosa_v", "sina_v", "rsin_v",
-                                                "cosa_s", "rsin2", "cosa", "rsina", "fC", "f0",
-                                                "a11", "a12", "a21", "a22", "lat", "lon"]
-    allm = {n: d.metric(n) for n in names}
-    ms = [{n: v[s] for n, v in allm.items()} for s in range(d.nsub)]
-    sc = d.scalars()
+    from oracle import grid as og  # the oracle's own grid (tests/test_oracle_grid.py pins grid.cpp to it)
+    ms, sc = og.domain_metrics(d.subs, d.nx, d.ny, d.N, d.pitch, d.nj)
     g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
     nl = dict(n_split=6, dt_atmos=dt, hord_mt=6, hord_vt=6, hord_tm=6, hord_dp=6, hord_tr=6, dddmp=0.2, d2_bg=0.0,
               p_fac=0.05, dz_min=2.0, fill=1, nq=nq)

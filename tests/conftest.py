@@ -36,16 +36,20 @@ def require_gpu():
 
 
 def metrics_of(dom, s=None):
-    """dict name -> plane(s) for all metrics of a Domain"""
-    names = ["area", "rarea", "area_c", "rarea_c", "dx", "dy", "dxa", "dya", "dxc", "dyc", "rdx", "rdy",
-             "rdxa", "rdya", "rdxc", "rdyc"] + [f"sin_sg{i}" for i in range(1, 10)] + \
-        [f"cos_sg{i}" for i in range(1, 10)] + ["cosa_u", "sina_u", "rsin_u", "cosa_v", "sina_v", "rsin_v",
-                                                "cosa_s", "rsin2", "cosa", "rsina", "fC", "f0",
-                                                "a11", "a12", "a21", "a22", "lat", "lon"]
-    allm = {n: dom.metric(n) for n in names}
+    """dict name -> plane(s) of the FV3 metric terms for a Domain's sub-domains, from the
+    independent oracle grid (oracle/grid.py; tests/test_oracle_grid.py compares it with the
+    product's grid.cpp), so the oracle never consumes the product's metrics"""
+    from oracle import grid as og
+    ms, _ = og.domain_metrics(dom.subs, dom.nx, dom.ny, dom.N, dom.pitch, dom.nj)
     if s is None:
-        return [{n: v[k] for n, v in allm.items()} for k in range(dom.nsub)]
-    return {n: v[s] for n, v in allm.items()}
+        return ms
+    return ms[s]
+
+
+def oracle_scalars(dom):
+    """{"corner_w", "da_min", "da_min_c"} of the oracle grid (the product's: Domain.scalars())"""
+    from oracle import grid as og
+    return og.domain_metrics(dom.subs, dom.nx, dom.ny, dom.N, dom.pitch, dom.nj)[1]
 
 
 def rng(seed=20250117):

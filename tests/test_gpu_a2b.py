@@ -6,7 +6,7 @@ of them shifted to end at the tile edge) and three row segments."""
 import numpy as np
 import pytest
 
-from conftest import metrics_of, rng
+from conftest import metrics_of, oracle_scalars, rng
 from oracle import NG
 from oracle import fv_dynamics as fvd
 from oracle import nh_core
@@ -25,7 +25,7 @@ def test_a2b_variants_and_oracle(pkg, require_gpu, npx, layout):
         out = d.download("t_qb")
         J, I = slice(NG, NG + d.ny + 1), slice(NG, NG + d.nx + 1)
         ms = metrics_of(d)
-        sc = d.scalars()
+        sc = oracle_scalars(d)
         g = fvd.Grid(d.N, layout[0], layout[1], ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
         for s in range(d.nsub):
             ref = nh_core.a2b_ord4(q[s], g.P[s], ms[s], sc["corner_w"][s])

@@ -11,7 +11,7 @@ import importlib
 import numpy as np
 import pytest
 
-from conftest import metrics_of
+from conftest import metrics_of, oracle_scalars
 from oracle import NG
 from oracle import fv_dynamics as fvd
 from oracle import geos_moist as gm
@@ -39,7 +39,7 @@ def test_aquaplanet_step_matches_oracle(pkg, require_gpu):
         got = {k: d.download(k) for k in ("pt", "q")}
         prec = sum(d.download(n)[:, 0] for n in ("prec_rain", "prec_snow", "prec_graupel", "prec_ice"))
         ms = metrics_of(d)
-        sc = d.scalars()
+        sc = oracle_scalars(d)
         g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
         ref = fvd.fv_dynamics(st, ak, bk, g, dict(NL, nq=nq))
         J, I = slice(NG, NG + d.ny), slice(NG, NG + d.nx)

@@ -147,13 +147,13 @@ def test_bridge_fp32_abi_matches_fp64(pkg, require_gpu):
 def test_bridge_adiabatic_is_dry_dynamics(pkg, require_gpu):
     """adiabatic=1 through the ABI = the oracle step with zvir = 0 (no moisture in the
     virtual temperature); adiabatic=0 differs from it wherever q != 0."""
-    from conftest import metrics_of
+    from conftest import metrics_of, oracle_scalars
     from oracle import fv_dynamics as fvd
     npx, npz, nq = 13, 10, 2
     N = npx - 1
     d, st, ak, bk, ks = _setup(pkg, npx, npz, nq)
     ms = metrics_of(d)
-    sc = d.scalars()
+    sc = oracle_scalars(d)
     g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
     nsub, nj, pitch = d.nsub, d.nj, d.pitch
     fort, shapes = _bridge_call(pkg, st, d, ak, bk, ks, npx, npz, nq, adiabatic=1)

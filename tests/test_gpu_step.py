@@ -16,7 +16,7 @@ import importlib
 import numpy as np
 import pytest
 
-from conftest import metrics_of
+from conftest import metrics_of, oracle_scalars
 from oracle import NG
 from oracle import fv_dynamics as fvd
 
@@ -40,7 +40,7 @@ def run_pair(pkg, npx, npz, nq, layout, nsteps=1, n_split=6, ptrs=None):
     for k, v in st.items():
         d.upload(k, v)
     ms = metrics_of(d)
-    sc = d.scalars()
+    sc = oracle_scalars(d)
     g = fvd.Grid(d.N, layout[0], layout[1], ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
     nl = dict(NL, nq=nq, n_split=n_split)
     ref = st

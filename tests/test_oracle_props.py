@@ -13,7 +13,7 @@ import importlib
 
 import numpy as np
 
-from conftest import metrics_of
+from conftest import metrics_of, oracle_scalars
 from oracle import NG
 from oracle import fv_dynamics as fvd
 from oracle import sw_core
@@ -29,7 +29,7 @@ def _setup(pkg, lx, ly, npz=10, npx=13):
     ak, bk, ks = state.hybrid_levels(npz)
     st = state.jablonowski_williamson(d, ak, bk)
     ms = metrics_of(d)
-    sc = d.scalars()
+    sc = oracle_scalars(d)
     g = fvd.Grid(d.N, lx, ly, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
     return d, st, ak, bk, ms, g
 

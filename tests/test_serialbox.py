@@ -161,7 +161,7 @@ def _write_archive(pkg, sb, path, nq=6):
     FVDynamics-Out from one oracle step of it, as a GEOS serialization run would write."""
     import importlib as il
     import sys
-    from conftest import metrics_of
+    from conftest import metrics_of, oracle_scalars
     from oracle import fv_dynamics as fvd
     state = il.import_module(pkg.__name__ + ".state")
     npz, npx = 10, 13
@@ -169,7 +169,7 @@ def _write_archive(pkg, sb, path, nq=6):
     ak, bk, ks = state.hybrid_levels(npz)
     st = state.jablonowski_williamson(d, ak, bk)
     ms = metrics_of(d)
-    sc = d.scalars()
+    sc = oracle_scalars(d)
     g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
     nl = dict(n_split=6, dt_atmos=900.0, hord_mt=6, hord_vt=6, hord_tm=6, hord_dp=6, hord_tr=6, dddmp=0.2,
               d2_bg=0.0, p_fac=0.05, dz_min=2.0, fill=1, nq=nq)

@@ -20,7 +20,7 @@ sys.path.insert(0, ROOT)
 sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import gtfv3_pkg  # noqa: E402
-from conftest import metrics_of  # noqa: E402
+from conftest import metrics_of, oracle_scalars  # noqa: E402
 from oracle import NG  # noqa: E402
 from oracle import fv_dynamics as fvd  # noqa: E402
 
@@ -38,7 +38,7 @@ def main():
     ak, bk, ks = state.hybrid_levels(NPZ)
     st = state.jablonowski_williamson(d, ak, bk)
     ms = metrics_of(d)
-    sc = d.scalars()
+    sc = oracle_scalars(d)
     g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
     t0 = time.time()
     ref = fvd.fv_dynamics(st, ak, bk, g, NL)

@@ -60,10 +60,10 @@ def main(argv=None):
     st = {k: np.stack([ps[k] for ps in per]) for k in per[0]}
     ks = int(scal.get("ks", 0))
     if a.engine == "oracle":
-        from conftest import metrics_of
+        from conftest import metrics_of, oracle_scalars
         from oracle import fv_dynamics as fvd
         ms = metrics_of(host)
-        sc = host.scalars()
+        sc = oracle_scalars(host)
         g = fvd.Grid(host.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], host.nj, host.pitch)
         out = fvd.fv_dynamics(st, ak, bk, g, cfg)
     else:
