@@ -126,6 +126,14 @@ def tri_lhuilier(a, b, c):
     return 4.0 * np.arctan(np.sqrt(np.maximum(t, 0.0)))
 
 
+def tri_vos(a, b, c):
+    """spherical excess by the Van Oosterom-Strackee formula (used only for the degenerate
+    cube-corner halo cells, where the product's split of the quadrilateral is the convention)"""
+    num = np.abs(_dot(a, np.cross(b, c)))
+    den = 1.0 + _dot(a, b) + _dot(b, c) + _dot(c, a)
+    return 2.0 * np.arctan2(num, den)
+
+
 def cos_at(p, q1, q2, s1=1.0, s2=1.0):
     """cosine of the angle at p between the great circles towards q1 and q2 (s = -1: the
     direction away from that point), from the normals of the two great-circle planes"""
@@ -168,11 +176,28 @@ def subdomain_metrics(tile, ioff, joff, nx, ny, N, pitch, nj):
         return _unit(t)
     exv = _unit(tang(c, e) - tang(c, w))
     eyv = _unit(tang(c, no) - tang(c, so))
+    GI, GJ = I_ + ioff, J_ + joff
+    cc_cell = ((GI < 0) | (GI >= N)) & ((GJ < 0) | (GJ >= N))
+    if cc_cell.any():  # degenerate cube-corner halo cells: the product's projected tangents
+        tproj = lambda p, q: _unit(q - _dot(p, q)[..., None] * p)
+        exv = np.where(cc_cell[..., None], _unit(tproj(c, e) - tproj(c, w)), exv)
+        eyv = np.where(cc_cell[..., None], _unit(tproj(c, no) - tproj(c, so)), eyv)
     cs[5] = _dot(exv, eyv)
     cs[6] = cos_at(p00, p10, p01)
     cs[7] = cos_at(p10, p00, p11, s1=-1.0)
     cs[8] = cos_at(p11, p01, p10, s1=-1.0, s2=-1.0)
     cs[9] = cos_at(p01, p11, p00, s2=-1.0)
+    # Cube-corner halo cells (both tile indices outside 0..N-1) are degenerate quadrilaterals of
+    # rotated halo points (fill_corners): there the values are a convention, not a geometric
+    # quantity, and the oracle adopts the product's (projected tangents, the p00-p11 diagonal)
+    if cc_cell.any():
+        tproj = lambda p, q: _unit(q - _dot(p, q)[..., None] * p)
+        tdot = lambda p, q1, q2, s1=1.0, s2=1.0: s1 * s2 * _dot(tproj(p, q1), tproj(p, q2))
+        for q_, (pp, q1, q2, a1, a2) in {6: (p00, p10, p01, 1, 1), 7: (p10, p00, p11, -1, 1),
+                                          8: (p11, p01, p10, -1, -1), 9: (p01, p11, p00, 1, -1),
+                                          1: (w, e, p01, 1, 1), 2: (so, p10, no, 1, 1),
+                                          3: (e, w, p11, -1, 1), 4: (no, p11, so, 1, -1)}.items():
+            cs[q_] = np.where(cc_cell, tdot(pp, q1, q2, a1, a2), cs[q_])
     for q in range(1, 10):
         out[f"cos_sg{q}"] = cs[q]
         out[f"sin_sg{q}"] = np.minimum(1.0, np.sqrt(np.maximum(0.0, 1.0 - cs[q] ** 2)))
@@ -182,9 +207,17 @@ def subdomain_metrics(tile, ioff, joff, nx, ny, N, pitch, nj):
     out["dya"] = R * gc(so, no)
     out["dxc"] = R * gc(Ac(-1, 0), c)
     out["dyc"] = R * gc(Ac(0, -1), c)
-    out["area"] = R * R * (tri_lhuilier(p00, p10, p01) + tri_lhuilier(p10, p11, p01))
+    out["area"] = R * R * np.where(cc_cell, tri_vos(p00, p10, p11) + tri_vos(p00, p11, p01),
+                                   tri_lhuilier(p00, p10, p01) + tri_lhuilier(p10, p11, p01))
     a_sw, a_se, a_ne, a_nw = Ac(-1, -1), Ac(0, -1), c, Ac(-1, 0)
-    area_c = R * R * (tri_lhuilier(a_sw, a_se, a_nw) + tri_lhuilier(a_se, a_ne, a_nw))
+    # a dual cell touching a cube-corner halo cell: the product's (sw-ne) diagonal, see above
+    touch = cc_cell.copy()
+    GI_l, GJ_l = GI - 1, GJ - 1
+    touch |= ((GI_l < 0) | (GI_l >= N)) & ((GJ_l < 0) | (GJ_l >= N))
+    touch |= ((GI < 0) | (GI >= N)) & ((GJ_l < 0) | (GJ_l >= N))
+    touch |= ((GI_l < 0) | (GI_l >= N)) & ((GJ < 0) | (GJ >= N))
+    area_c = R * R * np.where(touch, tri_vos(a_sw, a_se, a_ne) + tri_vos(a_sw, a_ne, a_nw),
+                              tri_lhuilier(a_sw, a_se, a_nw) + tri_lhuilier(a_se, a_ne, a_nw))
     # cube corners: the dual cell is the triangle of the three cells meeting there
     for (CI, CJ) in ((0, 0), (N, 0), (N, N), (0, N)):
         i, j = CI - ioff, CJ - joff

@@ -1,5 +1,8 @@
-"""Oracle: FV3 sw_core — c_sw (with d2a2c_vect) and d_sw (nord = 0, no vorticity
-or w damping, d_con = 0) in fp64 numpy.  TEST INFRASTRUCTURE ONLY.
+"""Oracle: FV3 sw_core — c_sw (with d2a2c_vect and, for nord > 0, divergence_corner) and
+d_sw (divergence damping nord = 0 .. 3 with the del-2 Smagorinsky-type coefficient, del-2n
+vorticity damping vtdm4 / nord_v, the d_con conversion of the damped kinetic energy into heat
+and the dissipation estimate diss_est; no w damping, no sponge-level overrides) in fp64 numpy.
+TEST INFRASTRUCTURE ONLY.
 
 Restated from the FV3 C-D grid shallow-water solver (Lin & Rood 1997; Harris &
 Lin 2013; FV3 sw_core.F90 structure).  Fortran 1-based indices f are written
@@ -432,3 +435,201 @@ def d_sw(delp, pt, u, v, w, uc, vc, ua, va, sub, m, nx, ny, dt, ords, dddmp, d2_
     v_new = np.where(P.reg(0, nx, 0, ny - 1), vdy + ke - sh(ke, 0, 1) - fxv, v)
     return dict(delp=dp_new, pt=pt_new, w=w_new, u=u_new, v=v_new, crx=crx, cry=cry, xfx=xfx, yfx=yfx,
                 fx=fx, fy=fy, ke=ke, ut=ut, vt=vt)
+
+
+# ----------------------------------------------------------------------------------
+# higher-order divergence damping, vorticity damping, d_con heating (FV3 sw_core.F90
+# d_sw / divergence_corner / del6_vt_flux and fv_grid_utils fill_corners, as described in
+# Harris et al. 2021 "A scientific description of the GFDL FV3 dynamical core" section 6
+# (damping) and restated from the FV3 module structure: literal index formulas, 0-based
+# tile-global indices g = f - 1)
+
+def divergence_corner(u, v, ua, va, sub, m, nx, ny):
+    """FV3 divergence_corner (c_sw, nord > 0): the divergence of the D-grid winds on the dual
+    cell around each compute corner (i, j in [0, n]), times rarea_c; zero elsewhere."""
+    P = Plane(sub, nx, ny, u.shape[-2], u.shape[-1])
+    N, I, J = P.N, P.I, P.J
+    s1, s2, s3, s4 = m["sin_sg1"], m["sin_sg2"], m["sin_sg3"], m["sin_sg4"]
+    c1, c2, c3, c4 = m["cos_sg1"], m["cos_sg2"], m["cos_sg3"], m["cos_sg4"]
+    # uf on x-edges (u positions), vf on y-edges (v positions)
+    sx = m["dyc"] * 0.5 * (sh(s4, 0, -1) + s2)
+    uf_gen = (u - 0.25 * (sh(va, 0, -1) + va) * (sh(c4, 0, -1) + c2)) * sx
+    uf = np.where((J == 0) | (J == N), u * sx, uf_gen)
+    sy = m["dxc"] * 0.5 * (sh(s3, -1, 0) + s1)
+    vf_gen = (v - 0.25 * (sh(ua, -1, 0) + ua) * (sh(c3, -1, 0) + c1)) * sy
+    vf = np.where((I == 0) | (I == N), v * sy, vf_gen)
+    dd = sh(vf, 0, -1) - vf + sh(uf, -1, 0) - uf
+    vS = sh(vf, 0, -1)
+    dd = np.where(P.at(0, 0) | P.at(N, 0), dd - vS, dd)
+    dd = np.where(P.at(N, N) | P.at(0, N), dd + vf, dd)
+    return np.where(P.reg(0, nx, 0, ny), m["rarea_c"] * dd, 0.0)
+
+
+def fill_corners_bgrid(q, sub, direction, nx, ny):
+    """FV3 fill_corners(q, FILL=XDir|YDir, BGRID=.true.) on a copy of a corner-point field:
+    the cube-corner halo points from the rotated ones (only corners this sub-domain holds)"""
+    out = q.copy()
+    N, io, jo = sub["N"], sub["ioff"], sub["joff"]
+
+    def slot(I, J):
+        return J - jo + NG, I - io + NG
+
+    def ok(I, J):
+        jj, ii = slot(I, J)
+        return 0 <= jj < q.shape[-2] and 0 <= ii < q.shape[-1]
+
+    def setp(I, J, Is, Js):
+        if ok(I, J) and ok(Is, Js):
+            a, b = slot(I, J)
+            c, d = slot(Is, Js)
+            out[..., a, b] = q[..., c, d]
+    own = lambda I, J: io <= I <= io + nx and jo <= J <= jo + ny
+    sw, se, ne, nw = [own(I, J) for (I, J) in ((0, 0), (N, 0), (N, N), (0, N))]
+    for j in range(1, NG + 1):
+        for i in range(1, NG + 1):
+            if direction == 1:
+                if sw: setp(-i, -j, -j, i)
+                if se: setp(N + i, -j, N + j, i)
+                if ne: setp(N + i, N + j, N + j, N - i)
+                if nw: setp(-i, N + j, -j, N - i)
+            else:
+                if sw: setp(-j, -i, i, -j)
+                if se: setp(N + j, -i, N - i, -j)
+                if ne: setp(N + j, N + i, N - i, N + j)
+                if nw: setp(-j, N + i, i, N + j)
+    return out
+
+
+def fill_corners_dgrid(x, y, sub, nx, ny, sign=-1.0):
+    """FV3 fill_corners(x, y, DGRID=.true., VECTOR=.true.) on copies: the D-grid pair's
+    cube-corner halo values (x on x-edges, y on y-edges) from the other component, the
+    south-west and north-east corners with the vector sign"""
+    xo, yo = x.copy(), y.copy()
+    N, io, jo = sub["N"], sub["ioff"], sub["joff"]
+    nj, ni = x.shape[-2:]
+
+    def slot(I, J):
+        return J - jo + NG, I - io + NG
+
+    def ok(I, J):
+        jj, ii = slot(I, J)
+        return 0 <= jj < nj and 0 <= ii < ni
+    own = lambda I, J: io <= I <= io + nx and jo <= J <= jo + ny
+    sw, se, ne, nw = [own(I, J) for (I, J) in ((0, 0), (N, 0), (N, N), (0, N))]
+
+    def cp(dst, src, I, J, Is, Js, f):
+        if ok(I, J) and ok(Is, Js):
+            a, b = slot(I, J)
+            c, d = slot(Is, Js)
+            dst[..., a, b] = f * src[..., c, d]
+    for j in range(1, NG + 1):
+        for i in range(1, NG + 1):
+            if sw: cp(xo, y, -i, -j, -j, i - 1, sign)
+            if se: cp(xo, y, N - 1 + i, -j, N + j, i - 1, 1.0)
+            if ne: cp(xo, y, N - 1 + i, N + j, N + j, N - i, sign)
+            if nw: cp(xo, y, -i, N + j, -j, N - i, 1.0)
+    for j in range(1, NG + 1):
+        for i in range(1, NG + 1):
+            if sw: cp(yo, x, -i, -j, j - 1, -i, sign)
+            if se: cp(yo, x, N + i, -j, N - j, -i, 1.0)
+            if ne: cp(yo, x, N + i, N - 1 + j, N - j, N + i, sign)
+            if nw: cp(yo, x, -i, N - 1 + j, j - 1, N + i, 1.0)
+    return xo, yo
+
+
+def _divg_u(m):
+    return m["sina_v"] * m["dyc"] / m["dx"]
+
+
+def _divg_v(m):
+    return m["sina_u"] * m["dxc"] / m["dy"]
+
+
+def _del6_u(m):
+    return m["sina_v"] * m["dx"] / m["dyc"]
+
+
+def _del6_v(m):
+    return m["sina_u"] * m["dy"] / m["dxc"]
+
+
+def divergence_damping_nord(divg_d, wk, sub, m, nx, ny, dt, nord, dddmp, d2_bg, d4_bg, da_min_c, corner_w):
+    """d_sw's nord > 0 branch: the corner damping term damp2 * delpc + dd8 * del^(2 nord) divg_d
+    (added to ke by the caller).  divg_d: the corner divergence of c_sw with its halo filled;
+    wk: the relative vorticity at cell centres (halo included) for the Smagorinsky-type del-2
+    coefficient (a2b_ord4 to the corners) when dddmp > 0."""
+    from .nh_core import a2b_ord4
+    P = Plane(sub, nx, ny, divg_d.shape[-2], divg_d.shape[-1])
+    N = P.N
+    delpc = np.where(P.reg(0, nx, 0, ny), divg_d, 0.0)
+    dgu, dgv = _divg_u(m), _divg_v(m)
+    dd = divg_d.copy()
+    corner_sub = any(P.owns(I, J) for (I, J) in ((0, 0), (N, 0), (N, N), (0, N)))
+    for n in range(1, nord + 1):
+        nt = nord - n
+        fill_c = nt != 0 and corner_sub
+        d_x = fill_corners_bgrid(dd, sub, 1, nx, ny) if fill_c else dd
+        vc = np.where(P.reg(-1 - nt, nx + nt, -nt, ny + nt), (sh(d_x, 1, 0) - d_x) * dgu, 0.0)
+        d_y = fill_corners_bgrid(dd, sub, 2, nx, ny) if fill_c else dd
+        uc = np.where(P.reg(-nt, nx + nt, -1 - nt, ny + nt), (sh(d_y, 0, 1) - d_y) * dgv, 0.0)
+        if fill_c:
+            vc, uc = fill_corners_dgrid(vc, uc, sub, nx, ny)
+        new = sh(uc, 0, -1) - uc + sh(vc, -1, 0) - vc
+        uS = sh(uc, 0, -1)
+        new = np.where(P.at(0, 0) | P.at(N, 0), new - uS, new)
+        new = np.where(P.at(N, N) | P.at(0, N), new + uc, new)
+        reg = P.reg(-nt, nx + nt, -nt, ny + nt)
+        dd = np.where(reg, new * m["rarea_c"], 0.0)
+    if dddmp < 1e-5:
+        vort = np.zeros_like(dd)
+    else:
+        vc_ = a2b_ord4(wk, P, m, corner_w)
+        vort = abs(dt) * np.sqrt(delpc ** 2 + vc_ ** 2)
+    dd8 = (da_min_c * d4_bg) ** (nord + 1)
+    damp2 = da_min_c * np.maximum(d2_bg, np.minimum(0.20, dddmp * vort))
+    return np.where(P.reg(0, nx, 0, ny), damp2 * delpc + dd8 * dd, 0.0)
+
+
+def del6_vt_flux(nord, damp, q, sub, m, nx, ny):
+    """FV3 del6_vt_flux: del-(2 nord + 2) diffusive fluxes (fx2 on y-edges, fy2 on x-edges) of
+    the cell field q (the relative vorticity) with coefficient damp"""
+    P = Plane(sub, nx, ny, q.shape[-2], q.shape[-1])
+    d6u, d6v, rarea = _del6_u(m), _del6_v(m), m["rarea"]
+    d2 = np.where(P.reg(-nord, nx - 1 + nord, -nord, ny - 1 + nord), damp * q, 0.0)
+    dx_ = copy_corners(d2, sub, 1) if nord > 0 else d2
+    fx2 = np.where(P.reg(-nord, nx + nord, -nord, ny - 1 + nord), d6v * (sh(dx_, -1, 0) - dx_), 0.0)
+    dy_ = copy_corners(d2, sub, 2) if nord > 0 else d2
+    fy2 = np.where(P.reg(-nord, nx - 1 + nord, -nord, ny + nord), d6u * (sh(dy_, 0, -1) - dy_), 0.0)
+    for n in range(1, nord + 1):
+        nt = nord - n
+        d2 = np.where(P.reg(-nt - 1, nx + nt, -nt - 1, ny + nt),
+                      (fx2 - sh(fx2, 1, 0) + fy2 - sh(fy2, 0, 1)) * rarea, 0.0)
+        dx_ = copy_corners(d2, sub, 1)
+        fx2 = np.where(P.reg(-nt, nx + nt, -nt, ny - 1 + nt), d6v * (dx_ - sh(dx_, -1, 0)), 0.0)
+        dy_ = copy_corners(d2, sub, 2)
+        fy2 = np.where(P.reg(-nt, nx - 1 + nt, -nt, ny + nt), d6u * (dy_ - sh(dy_, 0, -1)), 0.0)
+    return fx2, fy2
+
+
+def damping_heat(u, v, vd, fx2, fy2, delp, m, P, d_con):
+    """d_sw's d_con branch: the kinetic energy the divergence damping (corner term vd) and the
+    vorticity damping (fluxes fx2, fy2) remove, as a heat source delp * (-0.25 d_con ...) and
+    the dissipation estimate increment (-rsin2 ...), on compute cells.  u, v: the updated
+    D-grid winds times dx, dy before the vorticity-damping fluxes are added."""
+    nx, ny = P.nx, P.ny
+    ub = (vd - sh(vd, 1, 0) + fy2) * m["rdx"]
+    fy = u * m["rdx"]
+    gy = fy * ub
+    vb = (vd - sh(vd, 0, 1) - fx2) * m["rdy"]
+    fx = v * m["rdy"]
+    gx = fx * vb
+    u2 = fy + sh(fy, 0, 1)
+    du2 = ub + sh(ub, 0, 1)
+    v2 = fx + sh(fx, 1, 0)
+    dv2 = vb + sh(vb, 1, 0)
+    t = (ub ** 2 + sh(ub, 0, 1) ** 2 + vb ** 2 + sh(vb, 1, 0) ** 2) + 2.0 * (gy + sh(gy, 0, 1) + gx + sh(gx, 1, 0)) \
+        - m["cosa_s"] * (u2 * dv2 + v2 * du2 + du2 * dv2)
+    comp = P.reg(0, nx - 1, 0, ny - 1)
+    heat = np.where(comp, delp * (0.0 - 0.25 * d_con * m["rsin2"] * t), 0.0)
+    diss = np.where(comp, -m["rsin2"] * t, 0.0)
+    return heat, diss
