@@ -256,6 +256,15 @@ void bridge_init(void* comm, int npx, int npy, int npz, int ntiles, int is, int 
   nl.layout_x = N / nx;
   nl.layout_y = N / ny;
   nl.dt_atmos = bdt;
+  // fv_core_nml options (n_split, hord_*, kord_*, dddmp, nord, d4_bg, vtdm4, d_con, ...): the
+  // reference's Python side reads them from input.nml; here GTFV3_CONFIG carries them
+  if (const char* cfg = std::getenv("GTFV3_CONFIG")) {
+    const Namelist given = parse_config(cfg, nl);
+    if (given.npx != nl.npx || given.npz != nl.npz || given.nq != nl.nq || given.layout_x != nl.layout_x ||
+        given.layout_y != nl.layout_y)
+      throw std::runtime_error("GTFV3_CONFIG may not change the grid the init arguments define");
+    nl = given;
+  }
   if (g_tiles_per_rank == 6) {
     if (nranks != 1 || nx != N || ny != N) throw std::runtime_error("6 tiles per rank needs 1 rank and layout 1x1");
   } else if (g_tiles_per_rank != 1) {

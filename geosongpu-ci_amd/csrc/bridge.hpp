@@ -23,6 +23,11 @@ struct BridgeArgs {
       *vc, *mfx, *mfy, *cx, *cy, *diss_est;
 };
 
+struct Namelist;
+// "key=value;..." namelist items applied on top of `base` (capi.cpp; the bridge reads them from
+// GTFV3_CONFIG: the FV3 namelist options pyFV3 takes from input.nml's fv_core_nml)
+Namelist parse_config(const char* cfg, const Namelist& base);
+
 void bridge_init(void* comm, int npx, int npy, int npz, int ntiles, int is, int ie, int js, int je, int isd, int ied,
                  int jsd, int jed, float bdt, int nq_tot);
 template <typename T>

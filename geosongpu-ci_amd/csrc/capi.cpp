@@ -35,8 +35,8 @@ void set_error(const std::string& m) {
   g_err = m;
 }
 
-Namelist parse_config(const char* cfg) {
-  Namelist nl;
+Namelist parse_config(const char* cfg, const Namelist& base) {
+  Namelist nl = base;
   std::string s = cfg ? cfg : "";
   std::stringstream ss(s);
   std::string item;
@@ -66,6 +66,12 @@ Namelist parse_config(const char* cfg) {
     else if (k == "kord_tm") nl.kord_tm = ix;
     else if (k == "dddmp") nl.dddmp = x;
     else if (k == "d2_bg") nl.d2_bg = x;
+    else if (k == "nord") nl.nord = ix;
+    else if (k == "d4_bg") nl.d4_bg = x;
+    else if (k == "vtdm4") nl.vtdm4 = x;
+    else if (k == "nord_v") nl.nord_v = ix;
+    else if (k == "d_con") nl.d_con = x;
+    else if (k == "delt_max") nl.delt_max = x;
     else if (k == "p_fac") nl.p_fac = x;
     else if (k == "dz_min") nl.dz_min = x;
     else if (k == "fill") nl.fill = ix != 0;
@@ -77,6 +83,8 @@ Namelist parse_config(const char* cfg) {
   }
   for (int h : {nl.hord_mt, nl.hord_vt, nl.hord_tm, nl.hord_dp, nl.hord_tr})
     if (h != 5 && h != 6) throw std::runtime_error("hord must be 5 or 6");
+  if (nl.nord < 0 || nl.nord > 3) throw std::runtime_error("nord must be 0 .. 3");
+  if (nl.nord_v < 0 || nl.nord_v > 2) throw std::runtime_error("nord_v must be 0 .. 2");
   return nl;
 }
 
@@ -111,7 +119,7 @@ int geos_gtfv3_last_error(char* buf, int len) {
 
 void* gtfv3_create(const char* config, int rank, int nranks, const void* nccl_id) {
   try {
-    Namelist nl = parse_config(config);
+    Namelist nl = parse_config(config, Namelist());
     return new Dycore(nl, rank, nranks, nccl_id);
   } catch (const std::exception& e) {
     set_error(e.what());

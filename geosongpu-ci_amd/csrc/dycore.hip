@@ -3,11 +3,13 @@
 #include "dycore.hpp"
 
 #include <algorithm>
+#include <cmath>
 #include <cstdlib>
 #include <cstring>
 #include <stdexcept>
 
 #include "hip_util.hpp"
+#include "kernels_damp.hpp"
 #include "kernels_misc.hpp"
 #include "kernels_moist.hpp"
 #include "kernels_nh.hpp"
@@ -510,6 +512,24 @@ void Dycore::step() {
   da.fx = S("_ds_fx", npz); da.fy = S("_ds_fy", npz); da.gwx = S("_ds_gwx", npz); da.gwy = S("_ds_gwy", npz);
   da.gtx = S("_ds_gtx", npz); da.gty = S("_ds_gty", npz); da.ke = S("_ds_ke", npz); da.vort = S("_ds_vort", npz);
   da.gvx = S("_ds_gvx", npz); da.gvy = S("_ds_gvy", npz);
+  // damping beyond nord = 0 (damp.hip): off in the Held-Suarez namelist
+  da.nord = nl.nord; da.nord_v = nl.nord_v; da.d4_bg = nl.d4_bg; da.vtdm4 = nl.vtdm4; da.d_con = nl.d_con;
+  const bool dcon = nl.d_con > 1e-5, vdamp = nl.vtdm4 > 1e-5;
+  if (nl.nord > 0) {
+    da.divg = S("divgd", npz);
+    da.dd = S("_dd_dd", npz); da.dvcx = S("_dd_vcx", npz); da.ducy = S("_dd_ucy", npz);
+    da.dvort = S("_dd_vort", npz); da.dqx = S("_dd_qx", npz); da.dqy = S("_dd_qy", npz);
+  }
+  if (nl.nord > 0 || vdamp) da.wk = S("_dd_wk", npz);
+  if (vdamp) {
+    da.d2 = S("_dd_d2", npz); da.fx2 = S("_dd_fx2", npz); da.fy2 = S("_dd_fy2", npz);
+  }
+  if (dcon) {
+    // heat source and the dissipation estimate summed over this call's acoustic sub-steps
+    da.vd = S("_dd_vd", npz); da.heat = S("_dd_heat", npz); da.diss = S("diss_est", npz);
+    fill_field(c, field_elems(npz), 0.0, da.heat);
+    fill_field(c, field_elems(npz), 0.0, da.diss);
+  }
 
   UdzdArgs za{};
   za.npz = npz;
@@ -571,6 +591,8 @@ void Dycore::step() {
   for (int it = 0; it < nl.n_split; ++it) {
     const bool last = it == nl.n_split - 1;
     c_sw_transport(c, ca);
+    // nord > 0: c_sw's divergence_corner from the D-grid winds and d2a2c's ua, va
+    if (nl.nord > 0) divergence_corner(c, npz, u.p, v.p, ua, va, const_cast<double*>(da.divg));
     // c_sw's wind stage (vorticity, uc / vc) beside update_dz_c + riem_solver_c: they share
     // no field; joined before p_grad_c, which needs both
     if (fork_substep) {
@@ -592,7 +614,8 @@ void Dycore::step() {
     // the cube corners -- the corner circulation of c_sw -- and so do their mass fluxes:
     // a dry-mass drift of 3e-7 per step, 1.5e-11 with the sync); the sync and the C halo
     // as one exchange (H_CSC, bit-identical to 'S' then 'C')
-    halo_update({{"uc", 'X'}, {"vc", 'X'}});
+    if (nl.nord > 0) halo_update({{"uc", 'X'}, {"vc", 'X'}, {"divgd", 'b'}});
+    else halo_update({{"uc", 'X'}, {"vc", 'X'}});
     // fork: after the Courant numbers, the wind stage of d_sw (stream b) and update_dz_d
     // (stream c) run beside the mass / thermodynamic transport (and the wind stage on beside
     // riem_solver3 and the exchange of delp, pt, zh, ppe, w).  Default on (GTFV3_STREAMS=0: one
@@ -633,6 +656,7 @@ void Dycore::step() {
     pk3_pe_halo(c, npz, ptop, last, delp.p, pk3, pe);
     scale_field(c, field_elems(k1), Constants::grav, zh, gz);
     if (fork_substep) HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
+    if (dcon || vdamp) d_sw_post(c, da);  // the new delp and u, v: after both d_sw stages
     nh_p_grad(c, pa);
     if (!last) halo_update({{"u", 'd'}, {"v", 'd'}});
   }
@@ -641,6 +665,8 @@ void Dycore::step() {
     for (int f = 0; f < 3; ++f) copy_levels(c, field_elems(npz), cur3[f]->p, alt[f]->p);
     thermo_swap();
   }
+  // d_con: the damped kinetic energy, summed over the sub-steps, into the potential temperature
+  if (dcon) damping_heat_apply(c, npz, std::fabs(bdt * nl.delt_max), da.heat, delp.p, delz.p, pt.p);
   HIP_CHECK(hipEventRecord(ev[1], st));
 
   // ---- tracer transport with the accumulated mass fluxes, beside the remap of T_v, delz,

@@ -44,6 +44,11 @@ struct Namelist {
   int hord_mt = 6, hord_vt = 6, hord_tm = 6, hord_dp = 6, hord_tr = 6;
   int kord_mt = 9, kord_wz = 9, kord_tr = 9, kord_tm = -9;
   double dddmp = 0.2, d2_bg = 0.0;   // nord = 0 divergence damping (Smagorinsky + background)
+  // d_sw damping beyond the Held-Suarez namelist (damp.hip): del-(2 nord + 2) divergence
+  // damping with d4_bg; del-(2 nord_v + 2) vorticity damping vtdm4; d_con: the damped kinetic
+  // energy into heat (limited to delt_max * bdt K per call) and diss_est
+  int nord = 0, nord_v = 0;
+  double d4_bg = 0.0, vtdm4 = 0.0, d_con = 0.0, delt_max = 1.0;
   double p_fac = 0.05;               // SIM1 solver pressure floor factor
   double dz_min = 2.0;
   bool fill = true;                  // fillz negative tracers after remap

@@ -30,11 +30,21 @@ struct DswArgs {
   double *cx, *cy, *mfx, *mfy;        // accumulated
   double *ut, *vt, *fx, *fy, *gwx, *gwy, *gtx, *gty, *ke, *vort;  // scratch
   double *gvx, *gvy;  // vorticity fluxes (own planes: the wind stage may run beside the thermo stage)
+  // damping beyond nord = 0 (damp.hip; all off in the Held-Suarez namelist)
+  int nord = 0, nord_v = 0;
+  double d4_bg = 0.0, vtdm4 = 0.0, d_con = 0.0;
+  const double* divg = nullptr;  // nord > 0: c_sw's corner divergence, halo exchanged
+  double *wk = nullptr, *vd = nullptr;  // cell vorticity; the corner damping term (d_con)
+  double *dd = nullptr, *dvcx = nullptr, *ducy = nullptr, *dvort = nullptr, *dqx = nullptr, *dqy = nullptr;
+  double *d2 = nullptr, *fx2 = nullptr, *fy2 = nullptr;  // vorticity damping
+  double *heat = nullptr, *diss = nullptr;               // d_con: summed over the sub-steps
 };
 void d_sw(const Ctx& c, const DswArgs& a);  // the three stages in order
 void d_sw_courant(const Ctx& c, const DswArgs& a);  // ut, vt, Courant numbers and area fluxes
 void d_sw_thermo(const Ctx& c, const DswArgs& a);   // delp / w / pt transport, flux accumulation
 void d_sw_winds(const Ctx& c, const DswArgs& a);    // kinetic energy, vorticity transport, u, v
+// after both stages (needs the updated delp): d_con heat / diss_est, vorticity-damping fluxes
+void d_sw_post(const Ctx& c, const DswArgs& a);
 bool d_sw_thermo_fused(const DswArgs& a);           // delp/w/pt go to *_o (one march)
 
 }  // namespace gtfv3

@@ -8,6 +8,7 @@
 #include "dycore.hpp"
 #include "kernels.hpp"
 #include "kernels_column.hpp"
+#include "kernels_damp.hpp"
 #include "kernels_misc.hpp"
 #include "kernels_moist.hpp"
 #include "kernels_nh.hpp"
@@ -124,6 +125,58 @@ std::map<std::string, Fn>& reg() {
            copy_levels(dy.ctx(), n, a.w_o, a.w);
            copy_levels(dy.ctx(), n, a.pt_o, a.pt);
          }
+       }},
+      // divergence_corner(u, v, ua, va | divg): c_sw's corner divergence for nord > 0
+      {"divergence_corner",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {
+         need(f, 5, "divergence_corner");
+         const int npz = F(dy, f[0]).nk;
+         divergence_corner(dy.ctx(), npz, F(dy, f[0]).p, F(dy, f[1]).p, F(dy, f[2]).p, F(dy, f[3]).p,
+                           dy.field(f[4], npz).p);
+       }},
+      // d_sw_damped(the 18 d_sw fields, divg, heat, diss): d_sw (fused thermo march) with the
+      // damping options, then d_sw_post (d_con heat / diss += and the vorticity-damping
+      // fluxes).  params: dt, dddmp, d2_bg, hord_mt, hord_vt, hord_tm, hord_dp, nord, d4_bg,
+      // vtdm4, nord_v, d_con
+      {"d_sw_damped",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 21, "d_sw_damped");
+         if (p.size() < 12) throw std::runtime_error("d_sw_damped: 12 params");
+         const int npz = F(dy, f[0]).nk;
+         auto out = [&](int n) { return dy.field(f[n], npz).p; };
+         auto scr = [&](const char* n) { return dy.field(n, npz).p; };
+         DswArgs a{};
+         a.npz = npz;
+         a.dt = p[0]; a.dddmp = p[1]; a.d2_bg = p[2];
+         a.hord_mt = (int)p[3]; a.hord_vt = (int)p[4]; a.hord_tm = (int)p[5]; a.hord_dp = (int)p[6];
+         a.nord = (int)p[7]; a.d4_bg = p[8]; a.vtdm4 = p[9]; a.nord_v = (int)p[10]; a.d_con = p[11];
+         if (a.nord < 0 || a.nord > 3 || a.nord_v < 0 || a.nord_v > 2) throw std::runtime_error("d_sw_damped: nord");
+         a.delp = F(dy, f[0]).p; a.pt = F(dy, f[1]).p; a.w = F(dy, f[2]).p; a.u = F(dy, f[3]).p; a.v = F(dy, f[4]).p;
+         a.uc = F(dy, f[5]).p; a.vc = F(dy, f[6]).p; a.ua = F(dy, f[7]).p; a.va = F(dy, f[8]).p;
+         a.crx = out(9); a.cry = out(10); a.xfx = out(11); a.yfx = out(12);
+         a.cx = out(13); a.cy = out(14); a.mfx = out(15); a.mfy = out(16); a.ke = out(17);
+         a.ut = scr("_ds_ut"); a.vt = scr("_ds_vt");
+         a.fx = scr("_ds_fx"); a.fy = scr("_ds_fy"); a.gwx = scr("_ds_gwx"); a.gwy = scr("_ds_gwy");
+         a.gtx = scr("_ds_gtx"); a.gty = scr("_ds_gty"); a.vort = scr("_ds_vort");
+         a.gvx = scr("_ds_gvx"); a.gvy = scr("_ds_gvy");
+         a.divg = a.nord > 0 ? F(dy, f[18]).p : nullptr;
+         a.heat = out(19); a.diss = out(20);
+         a.wk = scr("_dd_wk"); a.vd = scr("_dd_vd");
+         a.dd = scr("_dd_dd"); a.dvcx = scr("_dd_vcx"); a.ducy = scr("_dd_ucy"); a.dvort = scr("_dd_vort");
+         a.dqx = scr("_dd_qx"); a.dqy = scr("_dd_qy");
+         a.d2 = scr("_dd_d2"); a.fx2 = scr("_dd_fx2"); a.fy2 = scr("_dd_fy2");
+         a.delp_o = scr("_ds_delp_o"); a.w_o = scr("_ds_w_o"); a.pt_o = scr("_ds_pt_o");
+         const long n = dy.field_elems(npz);
+         copy_levels(dy.ctx(), n, a.delp, a.delp_o);
+         copy_levels(dy.ctx(), n, a.w, a.w_o);
+         copy_levels(dy.ctx(), n, a.pt, a.pt_o);
+         d_sw(dy.ctx(), a);
+         if (d_sw_thermo_fused(a)) {
+           copy_levels(dy.ctx(), n, a.delp_o, a.delp);
+           copy_levels(dy.ctx(), n, a.w_o, a.w);
+           copy_levels(dy.ctx(), n, a.pt_o, a.pt);
+         }
+         d_sw_post(dy.ctx(), a);
        }},
       // riem_solver_c(delpc, ptc, wc, phis, gz | pef): gz heights in (clamped to dz_min),
       // geopotential out.  params: dt2, ptop, p_fac, dz_min[, variant (0 blocked, 1 column)]

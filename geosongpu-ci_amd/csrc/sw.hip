@@ -3,8 +3,10 @@
 // short chain of plane-parallel kernels over (i, j) x (sub, level); fv_tp_2d is
 // the shared transport operator (tp.hip).  Index conventions: stencil_common.hpp.
 // Fortran index f (1-based, npx = N+1) appears here as tile-global g = f-1.
+#include <cmath>
 #include <cstdlib>
 
+#include "kernels_damp.hpp"
 #include "kernels_sw.hpp"
 #include "stencil_common.hpp"
 
@@ -477,7 +479,8 @@ __global__ void __launch_bounds__(256) ds_ke(Dims d, const SubInfo* __restrict__
                                              const double* __restrict__ v, const double* __restrict__ uc,
                                              const double* __restrict__ vc, const double* __restrict__ ua,
                                              const double* __restrict__ va, const double* __restrict__ ut,
-                                             const double* __restrict__ vt, double* __restrict__ ke) {
+                                             const double* __restrict__ vt, double* __restrict__ ke, int nord,
+                                             double* __restrict__ vd) {
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
   KSETUP(npz)
   const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
@@ -532,6 +535,10 @@ __global__ void __launch_bounds__(256) ds_ke(Dims d, const SubInfo* __restrict__
   else if (I == 0 && J == N)
     kk = dt6 * ((AT(ut, 0, 0) + AT(ut, 0, -1)) * AT(u, 0, 0) + (AT(vt, 0, 0) + AT(vt, -1, 0)) * AT(v, 0, -1) +
                 (AT(ut, 0, -1) - AT(vt, 0, 0)) * AT(u, -1, 0));
+  if (nord > 0) {  // the higher-order damping term is added by divergence_damping (damp.hip)
+    AT(ke, 0, 0) = kk;
+    return;
+  }
   // divergence damping (nord = 0): delpc at the corner from the edge divergence terms
   auto ptc_at = [&](int di) {  // x-edge (i+di, j): u * dyc with the non-orthogonal correction
     const int Jj = J;
@@ -561,6 +568,7 @@ __global__ void __launch_bounds__(256) ds_ke(Dims d, const SubInfo* __restrict__
   dpc = MA(MT(M_RAREA_C), 0, 0) * dpc;
   double damp = da_min_c * fmax(d2_bg, fmin(0.20, dddmp * fabs(dpc * dt)));
   AT(ke, 0, 0) = kk + damp * dpc;
+  if (vd) AT(vd, 0, 0) = damp * dpc;  // the damping term on its own (d_con heat)
 }
 
 // relative vorticity (cell mean) + Coriolis -> the field transported by fv_tp_2d
@@ -735,12 +743,26 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
   const int nz = d.nsub * a.npz;
   // kinetic energy (+ divergence damping) at corners
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
+  const bool dcon = a.d_con > 1e-5, vdamp = a.vtdm4 > 1e-5;
   GT_LAUNCH(ds_ke, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.hord_mt, a.dddmp,
-                     a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke);
+                     a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke, a.nord,
+                     dcon ? a.vd : nullptr);
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   const double L = a.npz;
   gt_bytes(L * (2 * e.C + 3 * e.X + 3 * e.Y + e.K) + 17 * e.C);
+  // damping beyond nord = 0 (damp.hip), from the old winds' cell vorticity
+  if (a.nord > 0 || vdamp) vorticity_wk(c, a.npz, a.u, a.v, a.wk);
+  if (a.nord > 0) {
+    DampArgs da{};
+    da.npz = a.npz; da.nord = a.nord;
+    da.dt = a.dt; da.dddmp = a.dddmp; da.d2_bg = a.d2_bg; da.d4_bg = a.d4_bg;
+    da.divg = a.divg; da.wk = a.wk; da.ke = a.ke; da.vd = a.vd;
+    da.dd = a.dd; da.vcx = a.dvcx; da.ucy = a.ducy; da.vort = a.dvort; da.qx = a.dqx; da.qy = a.dqy;
+    divergence_damping(c, da);
+  }
+  if (vdamp) del6_vt_flux(c, a.npz, a.nord_v, std::pow(a.vtdm4 * c.da_min_c, (double)(a.nord_v + 1)), a.wk, a.d2,
+                          a.fx2, a.fy2);
   // vorticity transport
   Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
   GT_LAUNCH(ds_vort, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.vort);
@@ -754,6 +776,14 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
                      a.v);
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (e.K + 3 * e.X + 3 * e.Y) + 2 * e.C);
+}
+
+void d_sw_post(const Ctx& c, const DswArgs& a) {
+  const bool vdamp = a.vtdm4 > 1e-5;
+  if (a.d_con > 1e-5)
+    damping_heat(c, a.npz, a.d_con, a.u, a.v, a.vd, vdamp ? a.fx2 : nullptr, vdamp ? a.fy2 : nullptr, a.delp,
+                 a.heat, a.diss);
+  if (vdamp) vorticity_damping_apply(c, a.npz, a.fx2, a.fy2, a.u, a.v);
 }
 
 void d_sw(const Ctx& c, const DswArgs& a) {

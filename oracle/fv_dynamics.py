@@ -88,7 +88,9 @@ def fv_dynamics(st, ak, bk, g, nl):
     """One fv_dynamics call.  st: dict name -> array; updated and returned (new dict).
 
     Required inputs: u, v, w, delz, pt (T), delp, q (nq*npz levels, tracer 0 = sphum), phis.
-    nl: dict with n_split, dt_atmos, hord_mt/vt/tm/dp/tr, dddmp, d2_bg, p_fac, dz_min, fill, nq.
+    nl: dict with n_split, dt_atmos, hord_mt/vt/tm/dp/tr, dddmp, d2_bg, p_fac, dz_min, fill, nq;
+    optional damping keys (sw_core.d_sw): nord, d4_bg, vtdm4, nord_v, d_con, delt_max.
+    With d_con > 0 the state gains diss_est (the summed dissipation estimate of the call).
     """
     st = {k: v.copy() for k, v in st.items()}
     nsub, nx, ny = g.nsub, g.nx, g.ny
@@ -135,6 +137,14 @@ def fv_dynamics(st, ak, bk, g, nl):
             z[k] = np.where(comp[s], z[k + 1] - st["delz"][s, k], z[k])
     _halo(g, st, [("zh", "c")])
     ords = (nl["hord_mt"], nl["hord_vt"], nl["hord_tm"], nl["hord_dp"])
+    nord, d_con = int(nl.get("nord", 0)), float(nl.get("d_con", 0.0))
+    damp_kw = dict(nord=nord, d4_bg=float(nl.get("d4_bg", 0.0)), vtdm4=float(nl.get("vtdm4", 0.0)),
+                   nord_v=int(nl.get("nord_v", 0)), d_con=d_con)
+    if nord > 0:
+        st["divgd"] = np.zeros(shp)
+    if d_con > 1e-5:
+        heat = np.zeros(shp)
+        st["diss_est"] = np.zeros(shp)
     for it in range(nl["n_split"]):
         last = it == nl["n_split"] - 1
         cs = []
@@ -148,7 +158,11 @@ def fv_dynamics(st, ak, bk, g, nl):
                                              nl["p_fac"], reg)
             uc, vc = nh_core.p_grad_c(c["uc"], c["vc"], c["delpc"], pef, gzc, m, P, dt2)
             st["uc"][s], st["vc"][s], st["ua"][s], st["va"][s] = uc, vc, c["ua"], c["va"]
+            if nord > 0:  # c_sw's divergence_corner (from the old D-grid winds and d2a2c's ua, va)
+                st["divgd"][s] = sw_core.divergence_corner(st["u"][s], st["v"][s], c["ua"], c["va"], sub, m, nx, ny)
             cs.append(c)
+        if nord > 0:
+            _halo(g, st, [("divgd", "b")])
         # one value per shared tile-edge point: east / north edges take the neighbour's winds
         # (FV3 mpp_get_boundary; without it the cube-corner circulation of c_sw leaves the two
         # tiles with different winds, hence mass fluxes, next to each corner)
@@ -160,9 +174,13 @@ def fv_dynamics(st, ak, bk, g, nl):
             m, sub, P = g.ms[s], g.subs[s], g.P[s]
             r = sw_core.d_sw(st["delp"][s], st["pt"][s], st["u"][s], st["v"][s], st["w"][s], st["uc"][s],
                              st["vc"][s], st["ua"][s], st["va"][s], sub, m, nx, ny, dt, ords, nl["dddmp"],
-                             nl["d2_bg"], g.da_min_c)
+                             nl["d2_bg"], g.da_min_c, divg_d=st["divgd"][s] if nord > 0 else None,
+                             corner_w=g.corner_w[s], **damp_kw)
             for name in ("delp", "pt", "w", "u", "v"):
                 st[name][s] = r[name]
+            if d_con > 1e-5:
+                heat[s] += r["heat"]
+                st["diss_est"][s] += r["diss"]
             st["cx"][s] = np.where(P.reg(0, nx, -NG, ny + NG - 1), st["cx"][s] + r["crx"], st["cx"][s])
             st["cy"][s] = np.where(P.reg(-NG, nx + NG - 1, 0, ny), st["cy"][s] + r["cry"], st["cy"][s])
             st["mfx"][s] = np.where(P.reg(0, nx, 0, ny - 1), st["mfx"][s] + r["fx"], st["mfx"][s])
@@ -198,6 +216,24 @@ def fv_dynamics(st, ak, bk, g, nl):
                                                        st["pk3"][s], dt, ptop, P, m, g.corner_w[s])
         if not last:
             _halo(g, st, [("u", "d"), ("v", "d")])
+
+    # ---- d_con: the kinetic energy the damping removed, as heat (dyn_core after the acoustic
+    # loop): dT = heat / (cp delp), limited to delt_max * bdt per call (0.1x / 0.5x in the top
+    # two layers), added to the potential temperature through pkz ----
+    if d_con > 1e-5:
+        cp = RDGAS / KAPPA
+        k1k = KAPPA / (1.0 - KAPPA)
+        delt = abs(bdt * float(nl.get("delt_max", 1.0)))
+        lim = np.full(npz, delt)
+        lim[0] = 0.1 * delt
+        if npz > 1:
+            lim[1] = 0.5 * delt
+        lim = lim[:, None, None]
+        for s in range(nsub):
+            pkz = np.exp(k1k * np.log(rdg * st["delp"][s] / st["delz"][s] * st["pt"][s]))
+            dtmp = heat[s] / (cp * st["delp"][s])
+            st["pt"][s] = np.where(comp[s], st["pt"][s] + np.sign(dtmp) * np.minimum(lim, np.abs(dtmp)) / pkz,
+                                   st["pt"][s])
 
     # ---- tracer transport ----
     st["q"], nsplt = tp_core.tracer_2d_1l(st["q"], st["dp1"], st["mfx"], st["mfy"], st["cx"], st["cy"], g.subs,

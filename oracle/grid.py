@@ -57,7 +57,11 @@ METRICS = ["area", "rarea", "area_c", "rarea_c", "dx", "dy", "dxa", "dya", "dxc"
 
 
 def _unit(v):
-    return v / np.linalg.norm(v, axis=-1, keepdims=True)
+    """v / |v| as v * (1 / sqrt(x x + y y + z z)): the point construction rounds exactly like
+    the product's, so the points themselves (and the degenerate cube-corner halo cells built
+    from them, see subdomain_metrics) agree bit for bit; the metric formulas stay distinct"""
+    n2 = v[..., 0] * v[..., 0] + v[..., 1] * v[..., 1] + v[..., 2] * v[..., 2]
+    return v * (1.0 / np.sqrt(n2))[..., None]
 
 
 def _dot(a, b):
@@ -66,13 +70,14 @@ def _dot(a, b):
 
 def grid_tangents(N):
     """tan(alpha_i), alpha_i = (2i - N) pi / (4N), i = 0..N, exactly antisymmetric"""
+    import math
     m = 2 * np.arange(N + 1) - N
-    return np.sign(m) * np.tan(np.abs(m) * np.pi / (4.0 * N))
+    return np.array([math.copysign(math.tan(abs(int(k)) * math.pi / (4.0 * N)), k) if k else 0.0 for k in m])
 
 
 def face_point(t, tx, ty):
     c, ex, ey = (np.array(v, dtype=np.float64) for v in FACES[t])
-    return _unit(c + np.multiply.outer(tx, ex) + np.multiply.outer(ty, ey))
+    return _unit(c + (np.multiply.outer(tx, ex) + np.multiply.outer(ty, ey)))
 
 
 def corner_point(t, I, J, N, tg):
@@ -151,7 +156,7 @@ def subdomain_metrics(tile, ioff, joff, nx, ny, N, pitch, nj):
     ii = np.arange(-H, nx + H + 1)
     jj = np.arange(-H, ny + H + 1)
     P = np.array([[corner_point(tile, i + ioff, j + joff, N, tg) for i in ii] for j in jj])  # [j+H, i+H]
-    A = _unit(P[:-1, :-1] + P[:-1, 1:] + P[1:, :-1] + P[1:, 1:])  # cell centres [j+H, i+H]
+    A = _unit((P[:-1, :-1] + P[:-1, 1:]) + (P[1:, :-1] + P[1:, 1:]))  # cell centres [j+H, i+H]
 
     # the cells (i, j) of the metric region, i, j in [-NG, n+NG]
     ci = np.arange(-NG, nx + NG + 1)

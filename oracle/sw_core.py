@@ -313,10 +313,16 @@ def d_sw_ut_vt(uc, vc, P, m, dt):
     return ut, vt
 
 
-def d_sw(delp, pt, u, v, w, uc, vc, ua, va, sub, m, nx, ny, dt, ords, dddmp, d2_bg, da_min_c):
+def d_sw(delp, pt, u, v, w, uc, vc, ua, va, sub, m, nx, ny, dt, ords, dddmp, d2_bg, da_min_c, nord=0,
+         d4_bg=0.0, divg_d=None, vtdm4=0.0, nord_v=0, d_con=0.0, corner_w=None):
     """FV3 d_sw for all levels at once.  ords = (hord_mt, hord_vt, hord_tm, hord_dp).
     Returns dict: delp, pt, w (updated), u, v (times dx / dy: finished by the pressure
-    gradient), crx, cry, xfx, yfx (advective), fx, fy (mass fluxes)."""
+    gradient), crx, cry, xfx, yfx (advective), fx, fy (mass fluxes), and with d_con > 0 the
+    heat source and the dissipation-estimate increment of this call (heat, diss).
+    Damping: nord = 0 del-2 divergence damping (dddmp, d2_bg); nord = 1..3 the del-(2 nord + 2)
+    damping of the corner divergence divg_d (c_sw's, halo filled) with d4_bg plus the del-2
+    Smagorinsky-type term; vtdm4 > 0 del-(2 nord_v + 2) vorticity damping fluxes added to u, v;
+    d_con > 0 the damped kinetic energy returned as heat."""
     hord_mt, hord_vt, hord_tm, hord_dp = ords
     P = Plane(sub, nx, ny, u.shape[-2], u.shape[-1])
     N, I, J, io, jo = P.N, P.I, P.J, P.io, P.jo
@@ -402,11 +408,17 @@ def d_sw(delp, pt, u, v, w, uc, vc, ua, va, sub, m, nx, ny, dt, ords, dddmp, d2_
         put(ke, 0, N, dt6 * ((g(ut, 0, N) + g(ut, 0, N - 1)) * g(u, 0, N) + (g(vt, 0, N) + g(vt, -1, N)) * g(v, 0, N - 1)
                              + (g(ut, 0, N - 1) - g(vt, 0, N)) * g(u, -1, N)))
 
-    # relative vorticity (cell mean)
+    # relative vorticity (cell mean): the Smagorinsky coefficient and the vorticity damping
+    # use it before the transport
     udx = u * dx
     vdy = v * dy
     wk = np.where(P.reg(-NG, nx + NG - 1, -NG, ny + NG - 1), rarea * (udx - sh(udx, 0, 1) + sh(vdy, 1, 0) - vdy), z)
-
+    if nord > 0:
+        vd = divergence_damping_nord(divg_d, wk, sub, m, nx, ny, dt, nord, dddmp, d2_bg, d4_bg, da_min_c, corner_w)
+        ke = np.where(allx, ke + vd, ke)
+        return _d_sw_finish(dict(delp=dp_new, pt=pt_new, w=w_new, crx=crx, cry=cry, xfx=xfx, yfx=yfx, fx=fx, fy=fy,
+                                 ut=ut, vt=vt), ke, vd, wk, u, v, udx, vdy, dp_new, sub, m, nx, ny, crx, cry, xfx, yfx,
+                            ra_x, ra_y, hord_vt, da_min_c, vtdm4, nord_v, d_con, P)
     # divergence damping (nord = 0)
     ptc = z.copy()
     regp = P.reg(-1, nx, 0, ny)
@@ -426,15 +438,33 @@ def d_sw(delp, pt, u, v, w, uc, vc, ua, va, sub, m, nx, ny, dt, ords, dddmp, d2_
     delpc = np.where(P.at(0, N), delpc + vrt, delpc)
     delpc = m["rarea_c"] * delpc
     damp = da_min_c * np.maximum(d2_bg, np.minimum(0.20, dddmp * np.abs(delpc * dt)))
+    vd = np.where(allx, damp * delpc, z)
     ke = np.where(allx, ke + damp * delpc, ke)
+    return _d_sw_finish(dict(delp=dp_new, pt=pt_new, w=w_new, crx=crx, cry=cry, xfx=xfx, yfx=yfx, fx=fx, fy=fy,
+                             ut=ut, vt=vt), ke, vd, wk, u, v, udx, vdy, dp_new, sub, m, nx, ny, crx, cry, xfx, yfx,
+                        ra_x, ra_y, hord_vt, da_min_c, vtdm4, nord_v, d_con, P)
 
-    # vorticity transport and the final momentum update
+
+def _d_sw_finish(out, ke, vd, wk, u, v, udx, vdy, dp_new, sub, m, nx, ny, crx, cry, xfx, yfx, ra_x, ra_y, hord_vt,
+                 da_min_c, vtdm4, nord_v, d_con, P):
+    """vorticity transport and the momentum update, then the vorticity damping fluxes and the
+    d_con heat (FV3 d_sw's last part)"""
+    z = np.zeros_like(u)
     vort = np.where(P.reg(-NG, nx + NG - 1, -NG, ny + NG - 1), wk + m["f0"], z)
     fxv, fyv = fv_tp_2d(vort, crx, cry, xfx, yfx, ra_x, ra_y, sub, m, nx, ny, hord_vt)
     u_new = np.where(P.reg(0, nx - 1, 0, ny), udx + ke - sh(ke, 1, 0) + fyv, u)
     v_new = np.where(P.reg(0, nx, 0, ny - 1), vdy + ke - sh(ke, 0, 1) - fxv, v)
-    return dict(delp=dp_new, pt=pt_new, w=w_new, u=u_new, v=v_new, crx=crx, cry=cry, xfx=xfx, yfx=yfx,
-                fx=fx, fy=fy, ke=ke, ut=ut, vt=vt)
+    fx2 = fy2 = z
+    if vtdm4 > 1e-5:
+        damp4 = (vtdm4 * da_min_c) ** (nord_v + 1)
+        fx2, fy2 = del6_vt_flux(nord_v, damp4, wk, sub, m, nx, ny)
+    if d_con > 1e-5:
+        out["heat"], out["diss"] = damping_heat(u_new, v_new, vd, fx2, fy2, dp_new, m, P, d_con)
+    if vtdm4 > 1e-5:
+        u_new = np.where(P.reg(0, nx - 1, 0, ny), u_new + fy2, u_new)
+        v_new = np.where(P.reg(0, nx, 0, ny - 1), v_new - fx2, v_new)
+    out.update(u=u_new, v=v_new, ke=ke, vd=vd, wk=wk)
+    return out
 
 
 # ----------------------------------------------------------------------------------

@@ -174,10 +174,10 @@ def test_paired_last_strip_bitwise(pkg, require_gpu, monkeypatch):
 
 
 def test_d_sw_parity_c180(pkg, require_gpu):
-    """d_sw (fused thermo march) against the oracle at C180 on two levels.  Bar 1e-10 (not
-    1e-12): random inputs fill the cube-corner halo cells too, where the oracle grid's areas
-    of the degenerate corner cells match the product's only to their conditioning, and the
-    transport's halo updates carry that into a few compute-domain values (measured 3.8e-11)."""
+    """d_sw (fused thermo march) against the oracle at C180 on two levels.  Bar 1e-11: the
+    oracle's own grid differs from the product's by up to 7e-13 in the cell / dual-cell areas
+    at C180 (L'Huilier against Van Oosterom-Strackee on small triangles), which random
+    inputs carry through the transport."""
     npz = 2
     d = pkg.Domain(npx=181, npz=npz, nq=1)
     r = rng(78)
@@ -197,5 +197,5 @@ def test_d_sw_parity_c180(pkg, require_gpu):
         for o, (i0, i1, j0, j1) in dict(delp=(0, nx - 1, 0, ny - 1), pt=(0, nx - 1, 0, ny - 1),
                                         w=(0, nx - 1, 0, ny - 1), mfx=(0, nx, 0, ny - 1), mfy=(0, nx - 1, 0, ny),
                                         u=(0, nx - 1, 0, ny), v=(0, nx, 0, ny - 1)).items():
-            close(reg(got[o][s], i0, i1, j0, j1), reg(ref[o], i0, i1, j0, j1), f"sub{s} {o}", rtol=1e-10)
+            close(reg(got[o][s], i0, i1, j0, j1), reg(ref[o], i0, i1, j0, j1), f"sub{s} {o}", rtol=1e-11)
     d.close()
