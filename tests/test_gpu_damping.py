@@ -1,0 +1,188 @@
+"""GPU parity of d_sw's damping options beyond the Held-Suarez namelist (csrc/damp.hip,
+VERDICT r02 missing #1 / SURVEY §8a A6) against the oracle restatement
+(oracle/sw_core.py: divergence_corner, divergence_damping_nord with the B-grid / D-grid
+cube-corner fills, del6_vt_flux, damping_heat; oracle/fv_dynamics.py the d_con heating):
+
+  * divergence_corner (c_sw, nord > 0) at C12 and C180;
+  * d_sw at C180 on two levels, one namelist branch per case: nord = 1, 2, 3 (d4_bg, with and
+    without the Smagorinsky-type del-2 term), vtdm4 with nord_v = 0 and 2, and d_con with
+    the heat source and dissipation estimate (heat, diss_est);
+  * the full fv_dynamics step at C12 L10 with a damping namelist (nord 2, vtdm4, d_con) and
+    its diss_est;
+  * the drop-in boundary: geos_gtfv3_run_f64_c with those options through GTFV3_CONFIG
+    writes diss_est (an inout of the ABI, example_def_dycore.yaml:70) equal to the oracle's.
+
+Bar: as the undamped d_sw at C180 (tests/test_gpu_sw.py, on the product's grid checked against
+the oracle grid): 1e-12 of the field's mean magnitude; the step at 1e-9 (tests/test_gpu_step.py).
+Random inputs fill every plane point.
+Parity unpinned against FV3 itself (the numerics are external to the reference).
+"""
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+from conftest import checked_metrics, metrics_of, oracle_scalars, rng
+from oracle import NG
+from oracle import sw_core
+
+pytestmark = pytest.mark.gpu
+
+D_NAMES = ["delp", "pt", "w", "u", "v", "uc", "vc", "ua", "va", "crx", "cry", "xfx", "yfx", "cx", "cy", "mfx", "mfy",
+           "ke"]
+
+
+def close(a, b, what, rtol):
+    assert np.all(np.isfinite(b)), f"{what}: oracle not finite"
+    scale = np.abs(b).mean() + 1e-300
+    err = (np.abs(a - b) - rtol * np.abs(b)).max() / scale
+    assert err <= rtol, f"{what}: max scaled error {err:.3e}"
+
+
+def reg(a, i0, i1, j0, j1):
+    return a[..., j0 + NG:j1 + NG + 1, i0 + NG:i1 + NG + 1]
+
+
+def _inputs(d, npz, r):
+    sh = d.shape(npz)
+    return dict(delp=1000.0 + 100.0 * r.random(sh), pt=300.0 + 10.0 * r.standard_normal(sh),
+                w=r.standard_normal(sh), u=20.0 * r.standard_normal(sh), v=20.0 * r.standard_normal(sh),
+                uc=15.0 * r.standard_normal(sh), vc=15.0 * r.standard_normal(sh),
+                ua=15.0 * r.standard_normal(sh), va=15.0 * r.standard_normal(sh))
+
+
+@pytest.mark.parametrize("npx", [13, 181])
+def test_divergence_corner(pkg, require_gpu, npx):
+    npz = 2
+    d = pkg.Domain(npx=npx, npz=npz, nq=1)
+    try:
+        inp = _inputs(d, npz, rng(90))
+        for k in ("u", "v", "ua", "va"):
+            d.upload("x_" + k, inp[k])
+        d.stencil("divergence_corner", ["x_u", "x_v", "x_ua", "x_va", "x_divg"])
+        got = d.download("x_divg")
+        ms = metrics_of(d)
+        for s in range(d.nsub) if npx == 13 else (0, 2, 5):
+            ref = sw_core.divergence_corner(inp["u"][s], inp["v"][s], inp["ua"][s], inp["va"][s], d.subs[s], ms[s],
+                                            d.nx, d.ny)
+            close(reg(got[s], 0, d.nx, 0, d.ny), reg(ref, 0, d.nx, 0, d.ny), f"sub{s} divg", 1e-11)
+    finally:
+        d.close()
+
+
+CASES = {
+    "nord1": dict(nord=1, d4_bg=0.15),
+    "nord2": dict(nord=2, d4_bg=0.15),
+    "nord3_no_smag": dict(nord=3, d4_bg=0.12, dddmp=0.0),
+    "vort_del2": dict(vtdm4=0.05, nord_v=0),
+    "vort_del6": dict(vtdm4=0.05, nord_v=2),
+    "d_con": dict(nord=2, d4_bg=0.15, vtdm4=0.05, nord_v=1, d_con=1.0),
+    "d_con_nord0": dict(d_con=0.8),
+}
+
+
+@pytest.mark.parametrize("case", list(CASES))
+def test_d_sw_damping_c180(pkg, require_gpu, case):
+    """d_sw with one damping branch at C180 on two levels against the oracle"""
+    opt = dict(nord=0, d4_bg=0.0, vtdm4=0.0, nord_v=0, d_con=0.0, dddmp=0.2)
+    opt.update(CASES[case])
+    npz = 2
+    d = pkg.Domain(npx=181, npz=npz, nq=1)
+    try:
+        r = rng(91)
+        inp = _inputs(d, npz, r)
+        sh = d.shape(npz)
+        divg = 1e-5 * r.standard_normal(sh)
+        for k, v in inp.items():
+            d.upload("d_" + k, v)
+        for k in ("cx", "cy", "mfx", "mfy"):
+            d.upload("d_" + k, 0.5 * np.ones(sh))
+        d.upload("d_divg", divg)
+        for k in ("heat", "diss"):
+            d.upload("d_" + k, np.zeros(sh))
+        dt, d2_bg = 600.0, 0.0075
+        d.stencil("d_sw_damped", ["d_" + n for n in D_NAMES] + ["d_divg", "d_heat", "d_diss"],
+                  [dt, opt["dddmp"], d2_bg, 6, 6, 6, 6, opt["nord"], opt["d4_bg"], opt["vtdm4"], opt["nord_v"],
+                   opt["d_con"]])
+        got = {n: d.download("d_" + n) for n in ("delp", "pt", "w", "u", "v", "ke", "heat", "diss")}
+        nx, ny = d.nx, d.ny
+        for s in (0, 3, 5):
+            m, sc = checked_metrics(d, s)
+            ref = sw_core.d_sw(inp["delp"][s], inp["pt"][s], inp["u"][s], inp["v"][s], inp["w"][s], inp["uc"][s],
+                               inp["vc"][s], inp["ua"][s], inp["va"][s], d.subs[s], m, nx, ny, dt, (6, 6, 6, 6),
+                               opt["dddmp"], d2_bg, sc["da_min_c"], nord=opt["nord"], d4_bg=opt["d4_bg"],
+                               divg_d=divg[s], vtdm4=opt["vtdm4"], nord_v=opt["nord_v"], d_con=opt["d_con"],
+                               corner_w=sc["corner_w"])
+            regions = dict(delp=(0, nx - 1, 0, ny - 1), pt=(0, nx - 1, 0, ny - 1), w=(0, nx - 1, 0, ny - 1),
+                           u=(0, nx - 1, 0, ny), v=(0, nx, 0, ny - 1), ke=(0, nx, 0, ny))
+            if opt["d_con"] > 0:
+                regions.update(heat=(0, nx - 1, 0, ny - 1), diss=(0, nx - 1, 0, ny - 1))
+            for o, rg in regions.items():
+                close(reg(got[o][s], *rg), reg(ref[o], *rg), f"{case} sub{s} {o}", 1e-12)
+            if opt["d_con"] > 0:
+                assert np.abs(reg(ref["diss"], 0, nx - 1, 0, ny - 1)).max() > 0.0
+    finally:
+        d.close()
+
+
+DAMP_NL = dict(nord=2, d4_bg=0.15, vtdm4=0.05, nord_v=1, d_con=1.0)
+
+
+def test_step_with_damping_namelist(pkg, require_gpu):
+    """one fv_dynamics call at C12 L10 with nord 2 / vtdm4 / d_con against the oracle step,
+    diss_est included"""
+    from oracle import fv_dynamics as fvd
+    state = importlib.import_module(pkg.__name__ + ".state")
+    npz, nq = 10, 2
+    d = pkg.Domain(npx=13, npz=npz, nq=nq, **DAMP_NL)
+    try:
+        ak, bk, ks = state.hybrid_levels(npz)
+        st = state.jablonowski_williamson(d, ak, bk)
+        d.set_vertical(ak, bk, ks)
+        for k, v in st.items():
+            d.upload(k, v)
+        d.step(1)
+        ms = metrics_of(d)
+        sc = oracle_scalars(d)
+        g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
+        nl = dict(n_split=6, dt_atmos=900.0, hord_mt=6, hord_vt=6, hord_tm=6, hord_dp=6, hord_tr=6, dddmp=0.2,
+                  d2_bg=0.0, p_fac=0.05, dz_min=2.0, fill=1, nq=nq, **DAMP_NL)
+        ref = fvd.fv_dynamics(st, ak, bk, g, nl)
+        c = (Ellipsis, slice(NG, NG + d.ny), slice(NG, NG + d.nx))
+        for k in ("u", "v", "pt", "delp", "delz", "q", "ps", "diss_est"):
+            a, b = d.download(k)[c], ref[k][c]
+            err = np.abs(a - b).max() / (np.abs(b).mean() + 1e-300)
+            assert err <= 1e-9, f"{k}: scaled error {err:.2e}"
+        assert np.abs(ref["diss_est"][c]).max() > 0.0
+        err = np.abs(d.download("w")[c] - ref["w"][c]).max()
+        assert err <= 1e-10, f"w: abs error {err:.2e}"
+    finally:
+        d.close()
+
+
+def test_bridge_writes_diss_est(pkg, require_gpu, monkeypatch):
+    """geos_gtfv3_run_f64_c with the damping namelist through GTFV3_CONFIG: diss_est (an inout
+    the reference's bridge carries, example_def_dycore.yaml:70) comes back written, equal to
+    the oracle step's"""
+    import test_gpu_bridge as tb
+    from oracle import fv_dynamics as fvd
+    npx, npz, nq = 13, 10, 2
+    N = npx - 1
+    monkeypatch.setenv("GTFV3_CONFIG", ";".join(f"{k}={v}" for k, v in DAMP_NL.items()))
+    d, st, ak, bk, ks = tb._setup(pkg, npx, npz, nq)
+    ms = metrics_of(d)
+    sc = oracle_scalars(d)
+    g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
+    nsub, nj, pitch = d.nsub, d.nj, d.pitch
+    fort, shapes = tb._bridge_call(pkg, st, d, ak, bk, ks, npx, npz, nq)
+    d.close()
+    nl = dict(n_split=6, dt_atmos=900.0, hord_mt=6, hord_vt=6, hord_tm=6, hord_dp=6, hord_tr=6, dddmp=0.2,
+              d2_bg=0.0, p_fac=0.05, dz_min=2.0, fill=1, nq=nq, **DAMP_NL)
+    ref = fvd.fv_dynamics(st, ak, bk, g, nl)
+    li, hi, lj, hj, nk, kj = shapes["diss_est"]
+    got = tb.from_fortran(fort["diss_est"], nsub, nk, nj, pitch, li, hi, lj, hj, kj)[..., NG:NG + N, NG:NG + N]
+    b = ref["diss_est"][..., NG:NG + N, NG:NG + N]
+    assert np.abs(b).max() > 0.0 and np.abs(got).max() > 0.0
+    err = np.abs(got - b).max() / np.abs(b).mean()
+    assert err <= 1e-9, f"diss_est through the ABI vs oracle: {err:.2e}"

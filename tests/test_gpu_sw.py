@@ -7,7 +7,7 @@ regions FV3 defines them.  Bar: fp64, |hip - oracle| <= 1e-12 * |oracle| + 1e-12
 import numpy as np
 import pytest
 
-from conftest import metrics_of, oracle_scalars, rng
+from conftest import checked_metrics, metrics_of, oracle_scalars, rng
 from oracle import NG
 from oracle import sw_core
 
@@ -174,10 +174,8 @@ def test_paired_last_strip_bitwise(pkg, require_gpu, monkeypatch):
 
 
 def test_d_sw_parity_c180(pkg, require_gpu):
-    """d_sw (fused thermo march) against the oracle at C180 on two levels.  Bar 1e-11: the
-    oracle's own grid differs from the product's by up to 7e-13 in the cell / dual-cell areas
-    at C180 (L'Huilier against Van Oosterom-Strackee on small triangles), which random
-    inputs carry through the transport."""
+    """d_sw (fused thermo march) against the oracle at C180 on two levels, on the product's
+    grid checked against the oracle grid (conftest.checked_metrics).  Bar 1e-12."""
     npz = 2
     d = pkg.Domain(npx=181, npz=npz, nq=1)
     r = rng(78)
@@ -186,16 +184,15 @@ def test_d_sw_parity_c180(pkg, require_gpu):
     inp.update(uc=15.0 * r.standard_normal(sh), vc=15.0 * r.standard_normal(sh),
                ua=15.0 * r.standard_normal(sh), va=15.0 * r.standard_normal(sh))
     got = _d_sw_run(d, inp, npz, True, tag="o_")
-    ms = metrics_of(d)
     nx, ny = d.nx, d.ny
-    dmc = oracle_scalars(d)["da_min_c"]
     for s in (0, 3, 5):
+        m, sc = checked_metrics(d, s)
         ref = sw_core.d_sw(inp["delp"][s], inp["pt"][s], inp["u"][s], inp["v"][s], inp["w"][s], inp["uc"][s],
-                           inp["vc"][s], inp["ua"][s], inp["va"][s], d.subs[s], ms[s], nx, ny, 600.0, (6, 6, 6, 6),
-                           0.2, 0.0075, dmc)
+                           inp["vc"][s], inp["ua"][s], inp["va"][s], d.subs[s], m, nx, ny, 600.0, (6, 6, 6, 6),
+                           0.2, 0.0075, sc["da_min_c"])
         ref["mfx"], ref["mfy"] = 0.5 + ref["fx"], 0.5 + ref["fy"]
         for o, (i0, i1, j0, j1) in dict(delp=(0, nx - 1, 0, ny - 1), pt=(0, nx - 1, 0, ny - 1),
                                         w=(0, nx - 1, 0, ny - 1), mfx=(0, nx, 0, ny - 1), mfy=(0, nx - 1, 0, ny),
                                         u=(0, nx - 1, 0, ny), v=(0, nx, 0, ny - 1)).items():
-            close(reg(got[o][s], i0, i1, j0, j1), reg(ref[o], i0, i1, j0, j1), f"sub{s} {o}", rtol=1e-11)
+            close(reg(got[o][s], i0, i1, j0, j1), reg(ref[o], i0, i1, j0, j1), f"sub{s} {o}", rtol=1e-12)
     d.close()
