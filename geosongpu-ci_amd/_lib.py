@@ -20,6 +20,7 @@ BRIDGE_SYMBOLS = [
     "geos_gtfv3_last_error",
 ]
 DEVICE_SYMBOLS = [
+    "gtfv3_bridge_stats",
     "gtfv3_create",
     "gtfv3_destroy",
     "gtfv3_get_unique_id",
@@ -81,6 +82,7 @@ def lib():
         "gtfv3_get_unique_id": (I, [P]),
         "gtfv3_bootstrap_id": (I, [P, ctypes.c_char_p, IP, IP]),
         "gtfv3_bootstrap_done": (I, []),
+        "gtfv3_bridge_stats": (I, [DP]),
         "gtfv3_dims": (I, [P, IP]),
         "gtfv3_sub_info": (I, [P, I, IP]),
         "gtfv3_field_create": (I, [P, S, I]),

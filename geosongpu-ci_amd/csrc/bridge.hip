@@ -11,6 +11,7 @@
 #include <cstring>
 #include <fstream>
 #include <iterator>
+#include <map>
 #include <memory>
 #include <stdexcept>
 #include <string>
@@ -27,8 +28,6 @@ namespace {
 std::unique_ptr<Dycore> g_dy;
 int g_tiles_per_rank = 1;
 int g_is = 0, g_js = 0;
-void* g_stage = nullptr;
-size_t g_stage_bytes = 0;
 
 int env_int(const char* const* names, int dflt) {
   for (const char* const* n = names; *n; ++n) {
@@ -46,9 +45,10 @@ struct FDesc {
 
 template <typename T>
 __global__ void fort_to_dev(const T* __restrict__ f, double* __restrict__ dev, Dims d, int s, int nk_dev, FDesc fd,
-                            long n) {
-  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+                            long t0, long n) {
+  long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const long t = t0 + c;  // flat Fortran index of the element (this chunk starts at t0)
   int i = (int)(t % fd.ni), j, k;
   if (fd.order == 0) {
     j = (int)((t / fd.ni) % fd.nj);
@@ -57,14 +57,15 @@ __global__ void fort_to_dev(const T* __restrict__ f, double* __restrict__ dev, D
     k = (int)((t / fd.ni) % fd.nk);
     j = (int)(t / ((long)fd.ni * fd.nk));
   }
-  dev[((long)s * nk_dev + k) * d.plane + pidx(d, fd.ilo + i, fd.jlo + j)] = (double)f[t];
+  dev[((long)s * nk_dev + k) * d.plane + pidx(d, fd.ilo + i, fd.jlo + j)] = (double)f[c];
 }
 
 template <typename T>
 __global__ void dev_to_fort(T* __restrict__ f, const double* __restrict__ dev, Dims d, int s, int nk_dev, FDesc fd,
-                            long n) {
-  long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= n) return;
+                            long t0, long n) {
+  long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if (c >= n) return;
+  const long t = t0 + c;
   int i = (int)(t % fd.ni), j, k;
   if (fd.order == 0) {
     j = (int)((t / fd.ni) % fd.nj);
@@ -73,42 +74,162 @@ __global__ void dev_to_fort(T* __restrict__ f, const double* __restrict__ dev, D
     k = (int)((t / fd.ni) % fd.nk);
     j = (int)(t / ((long)fd.ni * fd.nk));
   }
-  f[t] = (T)dev[((long)s * nk_dev + k) * d.plane + pidx(d, fd.ilo + i, fd.jlo + j)];
+  f[c] = (T)dev[((long)s * nk_dev + k) * d.plane + pidx(d, fd.ilo + i, fd.jlo + j)];
 }
 
-void* stage(size_t bytes) {
-  if (bytes > g_stage_bytes) {
-    if (g_stage) HIP_CHECK(hipFree(g_stage));
-    HIP_CHECK(hipMalloc(&g_stage, bytes));
-    g_stage_bytes = bytes;
+// Host <-> HBM pipeline of one run call (the reference alternates two CUDA streams for its
+// uploads, data_conversion.py:42-44,113-132).  The Fortran arrays are page-locked once
+// (hipHostRegister: GEOS keeps them for the whole run), so every copy is a DMA straight from
+// or to them.  Each array travels in chunks through a ring of staging buffers: the DMA of
+// chunk n+1 on the copy stream overlaps the scatter (fort_to_dev) or gather (dev_to_fort)
+// kernel of chunk n on the compute stream, events handing each buffer back and forth.
+constexpr int kRing = 3;
+constexpr size_t kChunkBytes = size_t(32) << 20;
+// chunk of one DMA (GTFV3_BRIDGE_CHUNK_KB, at most the 32 MiB staging buffer; tests use
+// small chunks to run the ring through many wrap-arounds)
+size_t chunk_bytes() {
+  const char* e = std::getenv("GTFV3_BRIDGE_CHUNK_KB");
+  const long kb = e ? std::atol(e) : 0;
+  return kb > 0 ? std::min(kChunkBytes, (size_t)kb << 10) : kChunkBytes;
+}
+
+struct BridgeIO {
+  hipStream_t cp = nullptr;  // DMA stream
+  hipStream_t tr = nullptr;  // scatters of the tracers that upload beside the step
+  void* ring[kRing] = {};
+  hipEvent_t landed[kRing] = {}, freed[kRing] = {};
+  bool used[kRing] = {};
+  int next = 0;
+  hipEvent_t ev_t[4] = {};     // call start, state scattered, step done, last copy back
+  hipEvent_t ev_tracers = nullptr;
+  std::map<const void*, size_t> pinned;  // registered Fortran arrays (pointer -> bytes)
+  double ms[3] = {0, 0, 0};    // last call: upload (critical path), step, download
+  double bytes[2] = {0, 0};    // last call: host bytes uploaded / downloaded
+
+  void init() {
+    if (cp) return;
+    HIP_CHECK(hipStreamCreateWithFlags(&cp, hipStreamNonBlocking));
+    HIP_CHECK(hipStreamCreateWithFlags(&tr, hipStreamNonBlocking));
+    for (int b = 0; b < kRing; ++b) {
+      HIP_CHECK(hipMalloc(&ring[b], kChunkBytes));
+      HIP_CHECK(hipEventCreateWithFlags(&landed[b], hipEventDisableTiming));
+      HIP_CHECK(hipEventCreateWithFlags(&freed[b], hipEventDisableTiming));
+    }
+    for (auto& e : ev_t) HIP_CHECK(hipEventCreate(&e));
+    HIP_CHECK(hipEventCreateWithFlags(&ev_tracers, hipEventDisableTiming));
   }
-  return g_stage;
-}
+  void release() {
+    if (!cp) return;
+    (void)hipStreamSynchronize(cp);
+    (void)hipStreamSynchronize(tr);
+    unpin_except({});
+    for (int b = 0; b < kRing; ++b) {
+      (void)hipFree(ring[b]);
+      (void)hipEventDestroy(landed[b]);
+      (void)hipEventDestroy(freed[b]);
+      ring[b] = nullptr;
+      used[b] = false;
+    }
+    for (auto& e : ev_t) (void)hipEventDestroy(e);
+    (void)hipEventDestroy(ev_tracers);
+    (void)hipStreamDestroy(cp);
+    (void)hipStreamDestroy(tr);
+    cp = tr = nullptr;
+  }
+  // page-lock this call's arrays; arrays of earlier calls that are not among them are
+  // released first (a caller that reallocates between calls keeps only one set pinned)
+  void unpin_except(const std::vector<std::pair<const void*, size_t>>& keep) {
+    for (auto it = pinned.begin(); it != pinned.end();) {
+      bool k = false;
+      for (auto& p : keep) k = k || (p.first == it->first && p.second == it->second);
+      if (!k) {
+        (void)hipHostUnregister(const_cast<void*>(it->first));
+        it = pinned.erase(it);
+      } else {
+        ++it;
+      }
+    }
+  }
+  void pin(const std::vector<std::pair<const void*, size_t>>& arrays) {
+    const char* e = std::getenv("GTFV3_BRIDGE_PIN");
+    if (e && e[0] == '0') {
+      unpin_except({});
+      return;
+    }
+    unpin_except(arrays);
+    for (auto& p : arrays) {
+      if (pinned.count(p.first)) continue;
+      // a range another array already pinned (or memory HIP allocated) stays pageable here
+      if (hipHostRegister(const_cast<void*>(p.first), p.second, hipHostRegisterDefault) == hipSuccess)
+        pinned[p.first] = p.second;
+      else
+        (void)hipGetLastError();
+    }
+  }
+  // a staging buffer whose previous consumer (scatter kernel or DMA) has finished
+  int acquire(hipStream_t waiter) {
+    const int b = next;
+    next = (next + 1) % kRing;
+    if (used[b]) HIP_CHECK(hipStreamWaitEvent(waiter, freed[b], 0));
+    used[b] = true;
+    return b;
+  }
+};
 
+BridgeIO g_io;
+
+// Fortran array (all local sub-domains, tile-major) -> device field, chunked through the ring;
+// the scatter kernels run on `sst`
 template <typename T>
-void copy_in(Dycore& dy, const char* name, int nk_dev, const T* host, const FDesc& fd) {
+double copy_in(Dycore& dy, const char* name, int nk_dev, const T* host, const FDesc& fd, hipStream_t sst,
+               int s_lo = 0, int s_hi = -1, long t_lo = 0, long t_hi = -1) {
   Field& f = dy.field(name, nk_dev);
-  long n = (long)fd.ni * fd.nj * fd.nk;
-  for (int s = 0; s < g_tiles_per_rank; ++s) {
-    T* st = (T*)stage(sizeof(T) * n);
-    HIP_CHECK(hipMemcpyAsync(st, host + (size_t)s * n, sizeof(T) * n, hipMemcpyHostToDevice, dy.st));
-    GT_LAUNCH(fort_to_dev<T>, dim3(cdiv(n, 256)), dim3(256), 0, dy.st, st, f.p, dy.d, s, nk_dev, fd, n);
-    HIP_LAUNCH_CHECK();
+  const long n = (long)fd.ni * fd.nj * fd.nk;
+  const long per = (long)(chunk_bytes() / sizeof(T));
+  if (s_hi < 0) s_hi = g_tiles_per_rank;
+  if (t_hi < 0) t_hi = n;
+  double bytes = 0;
+  for (int s = s_lo; s < s_hi; ++s) {
+    for (long t0 = t_lo; t0 < t_hi; t0 += per) {
+      const long m = std::min(per, t_hi - t0);
+      const int b = g_io.acquire(g_io.cp);
+      HIP_CHECK(hipMemcpyAsync(g_io.ring[b], host + (size_t)s * n + t0, sizeof(T) * m, hipMemcpyHostToDevice,
+                               g_io.cp));
+      HIP_CHECK(hipEventRecord(g_io.landed[b], g_io.cp));
+      HIP_CHECK(hipStreamWaitEvent(sst, g_io.landed[b], 0));
+      GT_LAUNCH(fort_to_dev<T>, dim3(cdiv(m, 256)), dim3(256), 0, sst, (const T*)g_io.ring[b], f.p, dy.d, s, nk_dev,
+                fd, t0, m);
+      HIP_LAUNCH_CHECK();
+      HIP_CHECK(hipEventRecord(g_io.freed[b], sst));
+      bytes += sizeof(T) * (double)m;
+    }
   }
+  return bytes;
 }
 
 template <typename T>
-void copy_out(Dycore& dy, const char* name, T* host, const FDesc& fd) {
+double copy_out(Dycore& dy, const char* name, T* host, const FDesc& fd) {
   Field* f = dy.find(name);
   if (!f) throw std::runtime_error(std::string("bridge: missing field ") + name);
-  long n = (long)fd.ni * fd.nj * fd.nk;
+  const long n = (long)fd.ni * fd.nj * fd.nk;
+  const long per = (long)(chunk_bytes() / sizeof(T));
+  double bytes = 0;
   for (int s = 0; s < g_tiles_per_rank; ++s) {
-    T* st = (T*)stage(sizeof(T) * n);
-    GT_LAUNCH(dev_to_fort<T>, dim3(cdiv(n, 256)), dim3(256), 0, dy.st, st, f->p, dy.d, s, f->nk, fd, n);
-    HIP_LAUNCH_CHECK();
-    HIP_CHECK(hipMemcpyAsync(host + (size_t)s * n, st, sizeof(T) * n, hipMemcpyDeviceToHost, dy.st));
-    HIP_CHECK(hipStreamSynchronize(dy.st));
+    for (long t0 = 0; t0 < n; t0 += per) {
+      const long m = std::min(per, n - t0);
+      const int b = g_io.acquire(dy.st);
+      GT_LAUNCH(dev_to_fort<T>, dim3(cdiv(m, 256)), dim3(256), 0, dy.st, (T*)g_io.ring[b], f->p, dy.d, s, f->nk,
+                fd, t0, m);
+      HIP_LAUNCH_CHECK();
+      HIP_CHECK(hipEventRecord(g_io.landed[b], dy.st));
+      HIP_CHECK(hipStreamWaitEvent(g_io.cp, g_io.landed[b], 0));
+      HIP_CHECK(hipMemcpyAsync(host + (size_t)s * n + t0, g_io.ring[b], sizeof(T) * m, hipMemcpyDeviceToHost,
+                               g_io.cp));
+      HIP_CHECK(hipEventRecord(g_io.freed[b], g_io.cp));
+      bytes += sizeof(T) * (double)m;
+    }
   }
+  return bytes;
 }
 
 }  // namespace
@@ -348,35 +469,99 @@ void bridge_run(const BridgeArgs<T>& a) {
       {"cy", a.cy, D3(isd, ied, js, je + 1, npz), npz},
       {"diss_est", a.diss_est, D3(isd, ied, jsd, jed, npz), npz},
   };
-  for (auto& it : items) copy_in<T>(dy, it.name, it.nk_dev, it.p, it.fd);
-  HIP_CHECK(hipStreamSynchronize(dy.st));
-  auto t0 = std::chrono::steady_clock::now();
+  // What a call has to move.  Up: an inout the step overwrites over the whole Fortran extent
+  // before reading it needs no upload -- mfx, mfy, cx, cy (zeroed at the step's start), pkz
+  // (fv_prep writes the compute domain first), ua, va, uc, vc (d2a2c_vect writes the whole
+  // data domain each sub-step), diss_est (zeroed with d_con, else untouched) -- and q_con,
+  // which the step never touches, moves neither way (its Fortran values stay as they were, as
+  // after a copy round trip).  Down: diss_est only with d_con (phis comes back: the step
+// fills its halo).
+  // GTFV3_BRIDGE_SKIP=0 moves every array both ways.
+  const char* skip_env = std::getenv("GTFV3_BRIDGE_SKIP");
+  const bool skip = !(skip_env && skip_env[0] == '0');
+  const bool dcon = dy.nl.d_con > 1e-5;
+  auto up = [&](const std::string& n) {
+    if (!skip) return true;
+    for (const char* x : {"mfx", "mfy", "cx", "cy", "pkz", "q_con", "ua", "va", "uc", "vc", "diss_est"})
+      if (n == x) return false;
+    return true;
+  };
+  auto down = [&](const std::string& n) {
+    if (!skip) return true;
+    if (n == "q_con") return false;
+    if (n == "diss_est") return dcon;
+    return true;
+  };
+  g_io.init();
+  std::vector<std::pair<const void*, size_t>> arrays;
+  for (auto& it : items)
+    arrays.push_back({it.p, sizeof(T) * (size_t)it.fd.ni * it.fd.nj * it.fd.nk * g_tiles_per_rank});
+  g_io.pin(arrays);
+  HIP_CHECK(hipEventRecord(g_io.ev_t[0], g_io.cp));
+  double up_bytes = 0, down_bytes = 0;
+  // the state the step reads first; tracers 1.. are first read by tracer_2d, after the
+  // acoustic sub-steps, so they upload and scatter beside those (on their own stream) and
+  // the step waits for them only there
+  const long q0 = (long)(ied - isd + 1) * (jed - jsd + 1) * npz;  // tracer 0's share of a tile
+  const bool defer = nq > 1 && skip;
+  for (auto& it : items) {
+    if (!up(it.name)) continue;
+    if (defer && std::string(it.name) == "q")
+      up_bytes += copy_in<T>(dy, it.name, it.nk_dev, it.p, it.fd, dy.st, 0, -1, 0, q0);
+    else
+      up_bytes += copy_in<T>(dy, it.name, it.nk_dev, it.p, it.fd, dy.st);
+  }
+  HIP_CHECK(hipEventRecord(g_io.ev_t[1], dy.st));
+  dy.tracer_wait = nullptr;
+  if (defer) {
+    for (auto& it : items)
+      if (std::string(it.name) == "q")
+        up_bytes += copy_in<T>(dy, it.name, it.nk_dev, it.p, it.fd, g_io.tr, 0, -1, q0, -1);
+    HIP_CHECK(hipEventRecord(g_io.ev_tracers, g_io.tr));
+    dy.tracer_wait = g_io.ev_tracers;
+  }
   dy.step();
-  HIP_CHECK(hipStreamSynchronize(dy.st));
-  auto t1 = std::chrono::steady_clock::now();
-  for (auto& it : items) copy_out<T>(dy, it.name, it.p, it.fd);
+  dy.tracer_wait = nullptr;
+  HIP_CHECK(hipEventRecord(g_io.ev_t[2], dy.st));
+  for (auto& it : items)
+    if (down(it.name)) down_bytes += copy_out<T>(dy, it.name, it.p, it.fd);
+  HIP_CHECK(hipEventRecord(g_io.ev_t[3], g_io.cp));
+  HIP_CHECK(hipStreamSynchronize(g_io.cp));
+  for (int n = 0; n < 3; ++n) {
+    float ms = 0;
+    HIP_CHECK(hipEventElapsedTime(&ms, g_io.ev_t[n], g_io.ev_t[n + 1]));
+    g_io.ms[n] = ms;
+  }
+  g_io.bytes[0] = up_bytes;
+  g_io.bytes[1] = down_bytes;
   const char* lg = std::getenv("GTFV3_LOG");
   if (lg && std::atoi(lg) == 1) {
-    double sec = std::chrono::duration<double>(t1 - t0).count();
-    std::printf(" 0 , geos_gtfv3 %.6f\n", sec);
+    std::printf(" 0 , geos_gtfv3 %.6f\n", 1e-3 * g_io.ms[1]);
     std::fflush(stdout);
   }
+}
+
+void bridge_stats(double* out) {
+  for (int n = 0; n < 3; ++n) out[n] = g_io.ms[n];
+  out[3] = g_io.bytes[0];
+  out[4] = g_io.bytes[1];
+  out[5] = (double)g_io.pinned.size();
 }
 
 template void bridge_run<float>(const BridgeArgs<float>&);
 template void bridge_run<double>(const BridgeArgs<double>&);
 
-void bridge_finalize() {
-  g_dy.reset();
+void bridge_remove_id_file() {
   if (!g_id_file.empty()) {
     std::remove(g_id_file.c_str());
     g_id_file.clear();
   }
-  if (g_stage) {
-    (void)hipFree(g_stage);
-    g_stage = nullptr;
-    g_stage_bytes = 0;
-  }
+}
+
+void bridge_finalize() {
+  g_io.release();
+  g_dy.reset();
+  bridge_remove_id_file();
 }
 
 }  // namespace gtfv3

@@ -33,6 +33,11 @@ void bridge_init(void* comm, int npx, int npy, int npz, int ntiles, int is, int 
 template <typename T>
 void bridge_run(const BridgeArgs<T>& a);
 void bridge_finalize();
+// rank 0's ncclUniqueId file, if this process published one (finalize removes it too)
+void bridge_remove_id_file();
+// last run call: out[0..5] = upload ms (the part before the step), step ms, download ms,
+// host bytes uploaded, host bytes downloaded, Fortran arrays page-locked
+void bridge_stats(double* out);
 void bridge_fatal(const std::string& msg);
 // rank / size of the job: from the caller's Fortran MPI communicator when MPI is in the
 // process, else from the launcher's environment

@@ -146,7 +146,13 @@ int gtfv3_bootstrap_id(void* comm, unsigned char* id128, int* rank, int* nranks)
 
 int gtfv3_bootstrap_done(void) {
   API_TRY
-  bridge_finalize();
+  bridge_remove_id_file();
+  API_CATCH
+}
+
+int gtfv3_bridge_stats(double* out) {
+  API_TRY
+  bridge_stats(out);
   API_CATCH
 }
 

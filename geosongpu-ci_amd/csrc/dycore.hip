@@ -678,6 +678,7 @@ void Dycore::step() {
     HIP_CHECK(hipEventRecord(ev_fork, st));
     HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
     std::swap(st, st_b);  // tracer_2d enqueues (kernels, halo updates, copies) on the side stream
+    if (tracer_wait) HIP_CHECK(hipStreamWaitEvent(st, tracer_wait, 0));
     tracer_2d(nq, mdt);
     std::swap(st, st_b);
     HIP_CHECK(hipEventRecord(ev_b, st_b));
@@ -685,6 +686,7 @@ void Dycore::step() {
     lagrangian_to_eulerian(c, npz, nq, ptop, nl.fill != 0, ak_dev, bk_dev, rs1, rsc, 0, 1);
     HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
   } else {
+    if (tracer_wait) HIP_CHECK(hipStreamWaitEvent(st, tracer_wait, 0));
     tracer_2d(nq, mdt);
   }
   HIP_CHECK(hipEventRecord(ev[2], st));

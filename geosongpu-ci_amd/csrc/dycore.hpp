@@ -67,6 +67,9 @@ class Dycore {
   // memory after an event, while the first tracer sub-step already runs
   double* h_cmax = nullptr;
   hipEvent_t ev_cmax = nullptr;
+  // when set, the step's tracer transport waits for this event (the bridge uploads tracers
+  // 1.. beside the acoustic sub-steps)
+  hipEvent_t tracer_wait = nullptr;
 
   Field& field(const std::string& name, int nk);  // get or create (zeroed)
   Field* find(const std::string& name);

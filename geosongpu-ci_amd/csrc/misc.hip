@@ -14,9 +14,9 @@ constexpr double RDGAS = Constants::rdgas;
 constexpr double KAPPA = Constants::kappa;
 
 #define KSETUP3(nk_)                                                 \
-  int i, j;                                                          \
-  if (!thread_point(L, i, j)) return;                                \
-  const int z = blockIdx.z, s = z / (nk_);                           \
+  int i, j, z;                                                       \
+  if (!thread_point_lv(L, (long)d.nsub * (nk_), i, j, z)) return;    \
+  const int s = z / (nk_);                                           \
   const SubInfo sub = subs[s];                                       \
   const int N = sub.N;                                               \
   const int I = i + sub.ioff, J = j + sub.joff;                      \
@@ -222,8 +222,18 @@ inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
   (void)d;
   return plane_grid(L, nz);
 }
+// launch grid of a kernel whose setup is KSETUP3 (level-interleaved blocks)
+inline dim3 g2lv(const Launch2D& L, int nz) { return plane_grid_lv(L, nz); }
 
 }  // namespace
+
+bool level_blocks_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("GTFV3_LVB");
+    return !(e && e[0] == '0');
+  }();
+  return on;
+}
 
 bool xcd_order_enabled() {
   static const bool on = [] {
@@ -237,7 +247,7 @@ void fv_prep(const Ctx& c, int npz, int nq, double zvir, const double* delp, con
              double* pkz) {
   const Dims& d = c.d;
   Launch2D L{0, 0, d.nx, d.ny};
-  GT_LAUNCH(prep_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nq, zvir, delp, delz, q,
+  GT_LAUNCH(prep_k, g2lv(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nq, zvir, delp, delz, q,
                      pt, pkz);
   HIP_LAUNCH_CHECK();
   gt_bytes(npz * 6 * ext(d).C);
@@ -255,7 +265,7 @@ void fv_wrapup(const Ctx& c, int npz, int nq, double zvir, const double* q, cons
                const double* w, double* pt, double* omga) {
   const Dims& d = c.d;
   Launch2D L{0, 0, d.nx, d.ny};
-  GT_LAUNCH(wrapup_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nq, zvir, q, delp, delz,
+  GT_LAUNCH(wrapup_k, g2lv(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nq, zvir, q, delp, delz,
                      w, pt, omga);
   HIP_LAUNCH_CHECK();
   gt_bytes(npz * 7 * ext(d).C);
@@ -264,7 +274,7 @@ void fv_wrapup(const Ctx& c, int npz, int nq, double zvir, const double* q, cons
 void c2l_ord4(const Ctx& c, int npz, const double* u, const double* v, double* ua, double* va) {
   const Dims& d = c.d;
   Launch2D L{0, 0, d.nx, d.ny};
-  GT_LAUNCH(c2l_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, u, v, ua, va);
+  GT_LAUNCH(c2l_k, g2lv(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, u, v, ua, va);
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   gt_bytes(npz * (e.X + e.Y + 2 * e.C) + 8 * e.C);
@@ -273,7 +283,7 @@ void c2l_ord4(const Ctx& c, int npz, const double* u, const double* v, double* u
 void held_suarez(const Ctx& c, int npz, double dt, const double* pe, double* pt, double* u, double* v) {
   const Dims& d = c.d;
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  GT_LAUNCH(hs_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt, pe, pt, u, v);
+  GT_LAUNCH(hs_k, g2lv(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt, pe, pt, u, v);
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   gt_bytes((npz + 1) * e.C + npz * (2 * e.C + 2 * e.X + 2 * e.Y) + 2 * e.C);

@@ -17,9 +17,9 @@ constexpr double KAPPA = Constants::kappa;
 constexpr double R3 = 1.0 / 3.0;
 
 #define KSETUP2(nk_)                                                 \
-  int i, j;                                                          \
-  if (!thread_point(L, i, j)) return;                                \
-  const int z = blockIdx.z, s = z / (nk_);                           \
+  int i, j, z;                                                       \
+  if (!thread_point_lv(L, (long)d.nsub * (nk_), i, j, z)) return;    \
+  const int s = z / (nk_);                                           \
   const SubInfo sub = subs[s];                                       \
   const int N = sub.N;                                               \
   const int I = i + sub.ioff, J = j + sub.joff;                      \
@@ -832,6 +832,8 @@ inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
   (void)d;
   return plane_grid(L, nz);
 }
+// launch grid of a kernel whose setup is KSETUP2 (level-interleaved blocks)
+inline dim3 g2lv(const Launch2D& L, int nz) { return plane_grid_lv(L, nz); }
 
 }  // namespace
 
@@ -839,7 +841,7 @@ void update_dz_c(const Ctx& c, int npz, const double* dp0, const double* ut, con
                  double* gz_out) {
   const Dims& d = c.d;
   Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
-  GT_LAUNCH(udzc_k, g2(d, L, d.nsub * (npz + 1)), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dp0, ut, vt,
+  GT_LAUNCH(udzc_k, g2lv(L, d.nsub * (npz + 1)), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dp0, ut, vt,
                      gz, gz_out);
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
@@ -850,7 +852,7 @@ void p_grad_c(const Ctx& c, int npz, double dt2, const double* delpc, const doub
               double* vc) {
   const Dims& d = c.d;
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  GT_LAUNCH(pgradc_k, g2(d, L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt2, delpc, pkc,
+  GT_LAUNCH(pgradc_k, g2lv(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt2, delpc, pkc,
                      gz, uc, vc);
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
@@ -886,7 +888,7 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
   t.mfx = nullptr; t.mfy = nullptr; t.fx = a.fx; t.fy = a.fy; t.ord = a.hord;
   fv_tp_2d(c, t);
   Launch2D Li{0, 0, d.nx, d.ny};
-  GT_LAUNCH(zh_update_k, g2(d, Li, d.nsub * k1), dim3(BX, BY), 0, c.st, d, c.subs, c.met, k1, a.fx, a.fy,
+  GT_LAUNCH(zh_update_k, g2lv(Li, d.nsub * k1), dim3(BX, BY), 0, c.st, d, c.subs, c.met, k1, a.fx, a.fy,
                      a.xfx_e, a.yfx_e, a.zh);
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
@@ -963,7 +965,7 @@ void nh_p_grad(const Ctx& c, const NhPgArgs& a) {
   }
   const double ptk = exp(Constants::kappa * log(a.ptop));
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  GT_LAUNCH(nhpgrad_k, g2(d, L, d.nsub * a.npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, ptk,
+  GT_LAUNCH(nhpgrad_k, g2lv(L, d.nsub * a.npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, ptk,
                      a.ppb, a.gzb, a.pkb, a.wk1, a.u, a.v);
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);

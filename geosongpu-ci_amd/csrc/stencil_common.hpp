@@ -60,6 +60,47 @@ inline dim3 plane_grid(const Launch2D& L, long nz) {
   return dim3((unsigned)gx, 1, (unsigned)nz);
 }
 
+// Level-interleaved blocks (plane_grid_lv / thread_point_lv): a 256-thread block covers 64
+// consecutive points of BY = 4 consecutive planes (wave w: plane 4 * blockIdx.z + w) instead
+// of 256 points of one plane.  The four waves read the same metric-plane addresses (the 2-D
+// metric terms are shared by every level), so three of every four metric loads are served
+// by the CU's vector L1 instead of the L2 / Infinity Cache.  Used from 8 planes up (a last
+// group of fewer than 4 planes idles its spare waves; GTFV3_LVB=0: never); the kernel tells
+// the two launch shapes apart by gridDim.z (= the plane count in the one-plane form).
+bool level_blocks_enabled();
+inline dim3 plane_grid_lv(const Launch2D& L, long nz) {
+  if (!level_blocks_enabled() || nz < 2 * BY) return plane_grid(L, nz);
+  long gx = ((long)L.ni * L.nj + BX - 1) / BX;
+  gx = xcd_order_enabled() ? (gx + 7) / 8 * 8 : (gx + 7) / 8 * 8 + 1;
+  return dim3((unsigned)gx, 1, (unsigned)((nz + BY - 1) / BY));
+}
+__device__ __forceinline__ bool thread_point_lv(const Launch2D& L, long nz, int& i, int& j, int& z) {
+  if ((long)gridDim.z == nz) {
+    z = blockIdx.z;
+    return thread_point(L, i, j);
+  }
+  z = (int)(blockIdx.z * BY + threadIdx.y);
+  if (z >= nz) return false;
+  const int t = (int)(xcd_block() * BX + threadIdx.x);
+  if (t >= L.ni * L.nj) return false;
+  j = t / L.ni;
+  i = L.i0 + (t - j * L.ni);
+  j += L.j0;
+  return true;
+}
+
+// Wavefront-wide lane shifts of a double through DPP (no LDS): lane_prev(v) in lane L is v of
+// lane L-1, lane_next(v) is v of lane L+1; the lanes shifted in at the ends read 0.  Every
+// lane of the wave must execute them (no lane-divergent branch around a shift).
+template <int CTRL>
+__device__ __forceinline__ double lane_shift(double v) {
+  const int lo = __builtin_amdgcn_update_dpp(0, __double2loint(v), CTRL, 0xF, 0xF, true);
+  const int hi = __builtin_amdgcn_update_dpp(0, __double2hiint(v), CTRL, 0xF, 0xF, true);
+  return __hiloint2double(hi, lo);
+}
+__device__ __forceinline__ double lane_prev(double v) { return lane_shift<0x138>(v); }  // wave_shr:1
+__device__ __forceinline__ double lane_next(double v) { return lane_shift<0x130>(v); }  // wave_shl:1
+
 // FV3 copy_corners source cell (global indices) for a cube-corner halo cell,
 // dir = 1 (x sweep) or 2 (y sweep).  Restated from fv_grid_utils copy_corners;
 // fill_4corners / fill2_4corners are the same map restricted to the first ring.

@@ -17,9 +17,9 @@ constexpr double A1 = 0.5625, A2 = -0.0625;
 constexpr double BIG = 1.0e8;
 
 #define KSETUP(nk_)                                                  \
-  int i, j;                                                          \
-  if (!thread_point(L, i, j)) return;                                \
-  const int z = blockIdx.z, s = z / (nk_);                           \
+  int i, j, z;                                                       \
+  if (!thread_point_lv(L, (long)d.nsub * (nk_), i, j, z)) return;    \
+  const int s = z / (nk_);                                           \
   const SubInfo sub = subs[s];                                       \
   const int N = sub.N;                                               \
   const int I = i + sub.ioff, J = j + sub.joff;                      \
@@ -598,7 +598,7 @@ __global__ void __launch_bounds__(256) ds_uv(Dims d, const SubInfo* __restrict__
 
 inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
   (void)d;
-  return plane_grid(L, nz);
+  return plane_grid_lv(L, nz);
 }
 
 }  // namespace

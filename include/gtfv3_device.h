@@ -24,9 +24,13 @@ int gtfv3_get_unique_id(void* out128);
 /* The bridge's id bootstrap on its own (no GPU): rank/size from the Fortran MPI handle
  * `comm` when MPI is initialised in the process, else from the launcher environment; rank 0's
  * id128 (filled by the caller) reaches every rank by MPI_Bcast, else through the job-stamped
- * GTFV3_NCCL_ID_FILE.  gtfv3_bootstrap_done removes rank 0's id file (as finalize does). */
+ * GTFV3_NCCL_ID_FILE.  gtfv3_bootstrap_done removes rank 0's id file and nothing else (a live bridge context stays). */
 int gtfv3_bootstrap_id(void* comm, unsigned char* id128, int* rank, int* nranks);
 int gtfv3_bootstrap_done(void);
+/* the bridge's last geos_gtfv3_run call: out[0..5] = host->device ms before the step starts,
+ * step ms (incl. waiting for the tracers that upload beside it), device->host ms, host bytes
+ * uploaded, host bytes downloaded, number of page-locked Fortran arrays */
+int gtfv3_bridge_stats(double* out);
 
 /* out[0..9] = nx, ny, pitch, nj, nsub, npz, N, layout_x, layout_y, nq */
 int gtfv3_dims(void* h, int* out);

@@ -169,3 +169,62 @@ def test_bridge_adiabatic_is_dry_dynamics(pkg, require_gpu):
         err = np.abs(got - b).max() / np.abs(b).mean()
         assert err <= 1e-9, f"{name}: adiabatic bridge step vs oracle {err:.2e}"
     assert not np.array_equal(fort["pt"], moist["pt"]), "adiabatic must change the virtual-temperature step"
+
+
+# inouts the bridge does not upload (the step overwrites them over their whole Fortran
+# extent before reading them) and q_con, which moves neither way (bridge.hip bridge_run)
+SKIPPED_UP = ("mfx", "mfy", "cx", "cy", "pkz", "ua", "va", "uc", "vc", "diss_est", "q_con")
+
+
+def _garbage_call(pkg, d, st, ak, bk, ks, npx, npz, nq, env):
+    """bridge call with random values in every array the step does not read; `env` sets the
+    bridge's copy switches for this call"""
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        rng = np.random.default_rng(7)
+        st = dict(st)
+        for name in SKIPPED_UP:
+            st[name] = rng.standard_normal((d.nsub, npz, d.nj, d.pitch))
+        return _bridge_call(pkg, st, d, ak, bk, ks, npx, npz, nq)
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_bridge_copy_pipeline_equivalent(pkg, require_gpu):
+    """The pipelined copies (page-locked arrays, chunks through the staging ring, tracers
+    1.. uploaded beside the acoustic sub-steps, inouts the step overwrites not uploaded) give
+    bit for bit what moving every array both ways gives, with garbage in those inouts; q_con
+    and phis come back untouched.  Small chunks run the ring through many wrap-arounds."""
+    npx, npz, nq = 13, 10, 3
+    d, st, ak, bk, ks = _setup(pkg, npx, npz, nq)
+    full, shapes = _garbage_call(pkg, d, st, ak, bk, ks, npx, npz, nq,
+                                 {"GTFV3_BRIDGE_SKIP": "0", "GTFV3_BRIDGE_PIN": "0"})
+    piped, _ = _garbage_call(pkg, d, st, ak, bk, ks, npx, npz, nq,
+                             {"GTFV3_BRIDGE_SKIP": "1", "GTFV3_BRIDGE_PIN": "1", "GTFV3_BRIDGE_CHUNK_KB": "4"})
+    ref, _ = _garbage_call(pkg, d, st, ak, bk, ks, npx, npz, nq, {"GTFV3_BRIDGE_SKIP": "1"})
+    d.close()
+    for name in shapes:
+        if name == "q_con":
+            continue
+        assert np.array_equal(full[name], piped[name]), f"{name}: pipelined bridge differs from full copies"
+        assert np.array_equal(full[name], ref[name]), f"{name}: default chunks differ from full copies"
+    # q_con never moves: the caller's values stay
+    rng = np.random.default_rng(7)
+    for name in SKIPPED_UP:
+        g = rng.standard_normal((d.nsub, npz, d.nj, d.pitch))
+        if name == "q_con":
+            li, hi, lj, hj, nk, kj = shapes[name]
+            assert np.array_equal(piped[name], to_fortran(g, li, hi, lj, hj, kj)), "q_con must stay untouched"
+    # the bridge reports what it moved (the last call: default chunks)
+    import ctypes
+    out = (ctypes.c_double * 6)()
+    assert pkg.lib().gtfv3_bridge_stats(out) == 0
+    ms_up, ms_step, ms_down, up_b, down_b = out[0], out[1], out[2], out[3], out[4]
+    assert min(ms_up, ms_step, ms_down) > 0
+    total = sum(a.nbytes for a in ref.values())
+    assert up_b < total and down_b < total and up_b < down_b

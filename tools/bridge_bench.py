@@ -25,6 +25,8 @@ def main():
     ap.add_argument("--npz", type=int, default=72)
     ap.add_argument("--nq", type=int, default=4)
     ap.add_argument("--steps", type=int, default=3)
+    ap.add_argument("--dtype", choices=("f64", "f32"), default="f64",
+                    help="f64: geos_gtfv3_run_f64_c; f32: geos_gtfv3_run_c (float* arrays)")
     a = ap.parse_args()
     os.environ["GTFV3_BRIDGE_TILES_PER_RANK"] = "6"
     import numpy as np
@@ -35,6 +37,7 @@ def main():
     hook = importlib.import_module(pkg.__name__ + ".hook").geos_gtfv3
     state = importlib.import_module(pkg.__name__ + ".state")
     npx, npz, nq = a.npx, a.npz, a.nq
+    dt = np.float64 if a.dtype == "f64" else np.float32
     N = npx - 1
     d = pkg.Domain(npx=npx, npz=npz, nq=nq)
     ak, bk, ks = state.hybrid_levels(npz)
@@ -59,24 +62,36 @@ def main():
     fort = {}
     for name, (li, hi, lj, hj, nk, kj) in shapes.items():
         src = st[name] if name in st else np.zeros((nsub, nk, nj, pitch))
-        fort[name] = to_fortran(src, li, hi, lj, hj, kj)
+        fort[name] = to_fortran(src, li, hi, lj, hj, kj).astype(dt)
     del st
     nbytes = sum(v.nbytes for v in fort.values())
     scal = dict(comm=0, npx=npx, npy=npx, npz=npz, ntiles=6, is_=is_, ie=ie, js=js, je=je, isd=isd, ied=ied,
                 jsd=jsd, jed=jed, bdt=450.0, nq_tot=nq)
     run = dict(scal, ng=NG, ptop=float(ak[0]), ks=ks, layout_1=1, layout_2=1, adiabatic=1,
-               ak=np.asfortranarray(ak), bk=np.asfortranarray(bk))
+               ak=np.asfortranarray(ak.astype(dt)), bk=np.asfortranarray(bk.astype(dt)))
     hook.init(**scal)
     hook.run(**run, **fort)  # warm-up
+    import ctypes
+    st_out = (ctypes.c_double * 6)()
+    phases = []
     t0 = time.perf_counter()
     for _ in range(a.steps):
         hook.run(**run, **fort)
+        pkg.lib().gtfv3_bridge_stats(st_out)
+        phases.append(list(st_out))
     el = (time.perf_counter() - t0) / a.steps
     hook.finalize()
+    ph = np.median(np.array(phases), axis=0)
     cells = 6 * N * N * npz
-    print(json.dumps({"what": "geos_gtfv3_run_f64_c incl. host<->device copies", "npx": npx, "npz": npz, "nq": nq,
-                      "ms_per_call": 1e3 * el, "cell_updates_per_s": cells / el,
-                      "host_bytes_each_way": nbytes}))
+    fn = "geos_gtfv3_run_f64_c" if a.dtype == "f64" else "geos_gtfv3_run_c"
+    print(json.dumps({"what": f"{fn} incl. host<->device copies", "dtype": a.dtype, "npx": npx, "npz": npz,
+                      "nq": nq, "ms_per_call": 1e3 * el, "cell_updates_per_s": cells / el,
+                      "host_bytes_of_the_arrays": nbytes,
+                      "median_phases_ms": {"upload_before_step": ph[0], "step_incl_tracer_wait": ph[1],
+                                           "download": ph[2]},
+                      "bytes_up": ph[3], "bytes_down": ph[4],
+                      "up_GBps": ph[3] / ph[0] / 1e6, "down_GBps": ph[4] / ph[2] / 1e6,
+                      "arrays_pinned": int(ph[5])}))
 
 
 if __name__ == "__main__":
