@@ -63,9 +63,11 @@ def march_ex_fraction(nx, subs, mout=58):
     return nex / (len(subs) * nstrip)
 
 
-def manifest_step_bytes(nx, ny, nsub, npz, nq, n_split, pitch, nj, fex=0.5):
+def manifest_step_bytes(nx, ny, nsub, npz, nq, n_split, pitch, nj, fex=0.5, alternatives=False):
     """Algorithmic bytes of one step from bytes_manifest.yaml (evaluated independently of
-    the launchers' registration; tests/test_bytes_manifest.py compares the two)."""
+    the launchers' registration; tests/test_bytes_manifest.py compares the two).  Families
+    marked `alternative_to` (a fused form the benchmark step does not run by default) are
+    left out of the step unless `alternatives`."""
     import yaml
     with open(os.path.join(ROOT, "bytes_manifest.yaml")) as f:
         man = yaml.safe_load(f)["families"]
@@ -73,9 +75,23 @@ def manifest_step_bytes(nx, ny, nsub, npz, nq, n_split, pitch, nj, fex=0.5):
                L=npz, L1=npz + 1, nq=nq, ns=n_split, nsub=nsub, nx=nx, ny=ny, pitch=pitch, nj=nj, fex=fex)
     out = {}
     for fam, spec in man.items():
+        if "same_as" in spec:  # an alternative form of another family (counted once, there)
+            continue
+        if "alternative_to" in spec and not alternatives:
+            continue
         kinds = spec.get("launches") or ([spec] if "doubles" in spec else [])
         out[fam] = sum(8.0 * eval(k["n"], {}, env) * eval(k["doubles"], {}, env) for k in kinds)
     return out
+
+
+def manifest_family(fam):
+    """the manifest family whose bytes a kernel family registers (level-loop and other
+    alternative forms name the one-level form they replace with `same_as`)"""
+    import yaml
+    with open(os.path.join(ROOT, "bytes_manifest.yaml")) as f:
+        man = yaml.safe_load(f)["families"]
+    spec = man.get(fam)
+    return spec["same_as"] if isinstance(spec, dict) and "same_as" in spec else fam
 
 
 def pmc_traffic(fam, launches):

@@ -3,8 +3,11 @@
 // contravariant ut / vt scaled by dt2 * dy * sin_sg), the half-step upwind transport of
 // delp / pt / w (delpc, ptc, wc) and the cell kinetic energy ke.  It replaces the chain
 // cs_tmp -> cs_corner_fix -> cs_cgrid -> cs_transport_ke (sw.hip, kept as the checked
-// reference form, GTFV3_CSW_FUSED=0) with the same expressions in the same order, so every
-// output is bit-identical to the chain's (tests/test_gpu_sw.py compares them).
+// default form; this one with GTFV3_CSW_FUSED=1) with the same expressions in the same order,
+// so every output is bit-identical to the chain's (tests/test_gpu_sw.py compares them).
+// Measured C180 L72 on one MI355X: 5.26 ms per step against the chain's 5.25 (877 us per
+// launch, 70 % of wave cycles waiting on memory at 3 waves per SIMD): the halved field
+// passes do not pay while each row step waits out its loads, so the chain stays the default.
 //
 // One wavefront owns a strip of 64 columns (lane L: column x = a - 3 + L; the 57 output
 // columns are lanes 3 .. 59) of one (sub-domain, level) plane and marches up a segment of
@@ -27,6 +30,22 @@
 
 namespace gtfv3 {
 namespace {
+
+// debugging build (make BOUNDS=1): every plane-relative offset checked against the plane
+#ifdef GTFV3_BOUNDS
+#define CK(o) ck_plane((long)(o), d.plane, __LINE__)
+#define CKS(o) (zo + ck_plane((long)(o) - zo, d.plane, __LINE__))
+__device__ __forceinline__ long ck_plane(long o, long n, int line) {
+  if (o < 0 || o >= n) {
+    printf("csw_march line %d: offset %ld outside the plane (%ld) block %d thread %d\n", line, o, n, blockIdx.x, threadIdx.x);
+    return o < 0 ? 0 : n - 1;
+  }
+  return o;
+}
+#else
+#define CK(o) (o)
+#define CKS(o) (o)
+#endif
 
 constexpr double A1 = 0.5625, A2 = -0.0625;
 constexpr double BIG = 1.0e8;
@@ -103,19 +122,19 @@ struct Gen {
     const long o = pidx(d, i, j);
     double uy[4] = {0, 0, 0, 0}, vx[4] = {0, 0, 0, 0};
     if (f.in && (f.rows || f.two)) {
-      uy[1] = U[o];
-      uy[2] = U[o + d.pitch];
+      uy[1] = U[CK(o)];
+      uy[2] = U[CK(o + d.pitch)];
       if (f.rows) {
-        uy[0] = U[o - d.pitch];
-        uy[3] = U[o + 2 * d.pitch];
+        uy[0] = U[CK(o - d.pitch)];
+        uy[3] = U[CK(o + 2 * d.pitch)];
       }
     }
     if (f.in && (f.cols || f.two)) {
-      vx[1] = V[o];
-      vx[2] = V[o + 1];
+      vx[1] = V[CK(o)];
+      vx[2] = V[CK(o + 1)];
       if (f.cols) {
-        vx[0] = V[o - 1];
-        vx[3] = V[o + 2];
+        vx[0] = V[CK(o - 1)];
+        vx[3] = V[CK(o + 2)];
       }
     }
     tmp_eval(f, uy, vx, ut, vt);
@@ -126,7 +145,7 @@ struct Gen {
     const int i = Is - sub.ioff, j = Js - sub.joff;
     if (!uava_in(i, j, d.nx, d.ny)) return 0.0;
     const long o = pidx(d, i, j);
-    return (ut - vt * cs[o]) * r2[o];
+    return (ut - vt * cs[CK(o)]) * r2[CK(o)];
   }
   __device__ double va(int Is, int Js) const {
     double ut, vt;
@@ -134,12 +153,14 @@ struct Gen {
     const int i = Is - sub.ioff, j = Js - sub.joff;
     if (!uava_in(i, j, d.nx, d.ny)) return 0.0;
     const long o = pidx(d, i, j);
-    return (vt - ut * cs[o]) * r2[o];
+    return (vt - ut * cs[CK(o)]) * r2[CK(o)];
   }
 };
 
 __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
-  const long wid = (long)blockIdx.x * CW_WAVES + (threadIdx.x >> 6);
+  // wave index through readfirstlane: the plane, strip, segment and every pointer derived
+  // from it stay in SGPRs
+  const long wid = (long)blockIdx.x * CW_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   if (wid >= a.nwaves) return;  // whole wave; no workgroup barrier in this kernel
   const int lane = threadIdx.x & 63;
   const int strip = (int)(wid % a.nstrip);
@@ -204,17 +225,17 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
   }
   const int R_lo = j0 - 2, R_hi = j1 + 1;
 #pragma unroll
-  for (int m = 1; m < 5; ++m) uw[m] = U[ro(R_lo - 3 + m)];
+  for (int m = 1; m < 5; ++m) uw[m] = U[CK(ro(R_lo - 3 + m))];
   uw[0] = 0.0;
 
   for (int R = R_lo; R <= R_hi; ++R) {
     // ---- roll the windows, load the new rows
 #pragma unroll
     for (int m = 0; m < 4; ++m) uw[m] = uw[m + 1];
-    uw[4] = U[ro(R + 2)];
+    uw[4] = U[CK(ro(R + 2))];
     vw[0] = vw[1];
     vw[1] = vw[2];
-    vw[2] = V[ro(R)];
+    vw[2] = V[CK(ro(R))];
     const int r2 = R - 1, r3 = R - 2;
     const int J = R + jo, J2 = r2 + jo, J3 = r3 + jo;
     const long o2 = ro(r2), o3 = ro(r3);
@@ -222,11 +243,13 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
     s1w[0] = s1w[1];
     s3w[0] = s3w[1];
     s2w[0] = s2w[1];
-    s4w[1] = mS4[o2];
-    s1w[1] = mS1[o2];
-    s3w[1] = mS3[o2];
-    s2w[1] = mS2[o2];
-    // delp / pt / w: y-sweep fill of row r2 (stage 3's row r3 + 1)
+    s4w[1] = mS4[CK(o2)];
+    s1w[1] = mS1[CK(o2)];
+    s3w[1] = mS3[CK(o2)];
+    s2w[1] = mS2[CK(o2)];
+    // delp / pt / w: y-sweep fill of row r2 (stage 3's row r3 + 1).  The cube-corner remap
+    // applies to the cells' halo (i, j in [-NG, n + NG - 1]); the extra staggered column / row
+    // of the padded plane has no corner source and keeps its own (never output) value
     const bool crow2 = J2 < 0 || J2 >= N;
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
@@ -234,12 +257,12 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
       qy[f][1] = qy[f][2];
     }
     {
-      const long oq = crow2 && ccol && r2 >= -NG && r2 <= ny + NG && x >= -NG && x <= nx + NG
+      const long oq = crow2 && ccol && r2 >= -NG && r2 <= ny + NG - 1 && x >= -NG && x <= nx + NG - 1
                           ? cc_off(d, sub, x, r2, 2)
                           : o2;
-      qy[0][2] = QD[oq];
-      qy[1][2] = QP[oq];
-      qy[2][2] = QW[oq];
+      qy[0][2] = QD[CK(oq)];
+      qy[1][2] = QP[CK(oq)];
+      qy[2][2] = QW[CK(oq)];
     }
 
     // ---- stage 1, row R: utmp, vtmp and the generic ua, va
@@ -253,36 +276,45 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
       uan = van = 0.0;
       if (uava_in(x, R, nx, ny)) {
         const long o1 = ro(R);
-        const double cs = mCS[o1], r2v = mR2[o1];
+        const double cs = mCS[CK(o1)], r2v = mR2[CK(o1)];
         uan = (utn - vtn * cs) * r2v;
         van = (vtn - utn * cs) * r2v;
       }
-      // cube-corner fixes (cs_corner_fix's targets; the sources are generic values)
+      // cube-corner fixes (cs_corner_fix's targets; the sources are generic values): each
+      // output has at most one fix per lane, so the source point and sign are chosen first and
+      // the generic value is evaluated once
       if (anyown && (J <= -1 || J >= N)) {
-        if (J == -1 && own00 && I >= -3 && I <= -1) { double a_, b_; gen.tmp(-1, -I - 1, a_, b_); utn = -b_; }
-        if (J == -1 && ownN0 && I >= N && I <= N + 2) { double a_, b_; gen.tmp(N, I - N, a_, b_); utn = b_; }
-        if (J == N && ownNN && I >= N && I <= N + 2) { double a_, b_; gen.tmp(N, N - 1 - (I - N), a_, b_); utn = -b_; }
-        if (J == N && own0N && I >= -3 && I <= -1) { double a_, b_; gen.tmp(-1, N + I, a_, b_); utn = b_; }
-        if (I == -1 && own00 && J >= -3 && J <= -1) { double a_, b_; gen.tmp(-J - 1, -1, a_, b_); vtn = -a_; }
-        if (I == N && ownN0 && J >= -3 && J <= -1) { double a_, b_; gen.tmp(N + J, -1, a_, b_); vtn = a_; }
-        if (I == N && ownNN && J >= N && J <= N + 2) { double a_, b_; gen.tmp(N - (J - N) - 1, N, a_, b_); vtn = -a_; }
-        if (I == -1 && own0N && J >= N && J <= N + 2) { double a_, b_; gen.tmp(J - N, N, a_, b_); vtn = a_; }
-        if (own00 && J == -1 && I == -2) uan = -gen.va(-1, 1);
-        if (own00 && J == -1 && I == -1) uan = -gen.va(-1, 0);
-        if (own00 && I == -1 && J == -2) van = -gen.ua(1, -1);
-        if (own00 && I == -1 && J == -1) van = -gen.ua(0, -1);
-        if (ownN0 && J == -1 && I == N) uan = gen.va(N, 0);
-        if (ownN0 && J == -1 && I == N + 1) uan = gen.va(N, 1);
-        if (ownN0 && I == N && J == -1) van = gen.ua(N - 1, -1);
-        if (ownN0 && I == N && J == -2) van = gen.ua(N - 2, -1);
-        if (ownNN && J == N && I == N) uan = -gen.va(N, N - 1);
-        if (ownNN && J == N && I == N + 1) uan = -gen.va(N, N - 2);
-        if (ownNN && I == N && J == N) van = -gen.ua(N - 1, N);
-        if (ownNN && I == N && J == N + 1) van = -gen.ua(N - 2, N);
-        if (own0N && J == N && I == -2) uan = gen.va(-1, N - 2);
-        if (own0N && J == N && I == -1) uan = gen.va(-1, N - 1);
-        if (own0N && I == -1 && J == N) van = gen.ua(0, N);
-        if (own0N && I == -1 && J == N + 1) van = gen.ua(1, N);
+        int us = 0, vs = 0, as = 0, bs = 0;              // sign (0: no fix)
+        int uI = 0, uJ = 0, vI = 0, vJ = 0, aI = 0, aJ = 0, bI = 0, bJ = 0;  // source points
+        if (J == -1 && own00 && I >= -3 && I <= -1) { us = -1; uI = -1; uJ = -I - 1; }
+        if (J == -1 && ownN0 && I >= N && I <= N + 2) { us = 1; uI = N; uJ = I - N; }
+        if (J == N && ownNN && I >= N && I <= N + 2) { us = -1; uI = N; uJ = N - 1 - (I - N); }
+        if (J == N && own0N && I >= -3 && I <= -1) { us = 1; uI = -1; uJ = N + I; }
+        if (I == -1 && own00 && J >= -3 && J <= -1) { vs = -1; vI = -J - 1; vJ = -1; }
+        if (I == N && ownN0 && J >= -3 && J <= -1) { vs = 1; vI = N + J; vJ = -1; }
+        if (I == N && ownNN && J >= N && J <= N + 2) { vs = -1; vI = N - (J - N) - 1; vJ = N; }
+        if (I == -1 && own0N && J >= N && J <= N + 2) { vs = 1; vI = J - N; vJ = N; }
+        if (own00 && J == -1 && I == -2) { as = -1; aI = -1; aJ = 1; }
+        if (own00 && J == -1 && I == -1) { as = -1; aI = -1; aJ = 0; }
+        if (ownN0 && J == -1 && I == N) { as = 1; aI = N; aJ = 0; }
+        if (ownN0 && J == -1 && I == N + 1) { as = 1; aI = N; aJ = 1; }
+        if (ownNN && J == N && I == N) { as = -1; aI = N; aJ = N - 1; }
+        if (ownNN && J == N && I == N + 1) { as = -1; aI = N; aJ = N - 2; }
+        if (own0N && J == N && I == -2) { as = 1; aI = -1; aJ = N - 2; }
+        if (own0N && J == N && I == -1) { as = 1; aI = -1; aJ = N - 1; }
+        if (own00 && I == -1 && J == -2) { bs = -1; bI = 1; bJ = -1; }
+        if (own00 && I == -1 && J == -1) { bs = -1; bI = 0; bJ = -1; }
+        if (ownN0 && I == N && J == -1) { bs = 1; bI = N - 1; bJ = -1; }
+        if (ownN0 && I == N && J == -2) { bs = 1; bI = N - 2; bJ = -1; }
+        if (ownNN && I == N && J == N) { bs = -1; bI = N - 1; bJ = N; }
+        if (ownNN && I == N && J == N + 1) { bs = -1; bI = N - 2; bJ = N; }
+        if (own0N && I == -1 && J == N) { bs = 1; bI = 0; bJ = N; }
+        if (own0N && I == -1 && J == N + 1) { bs = 1; bI = 1; bJ = N; }
+        // utmp takes the source's vtmp, vtmp the source's utmp; ua the source's va, va its ua
+        if (us != 0) { double a_, b_; gen.tmp(uI, uJ, a_, b_); utn = us > 0 ? b_ : -b_; }
+        if (vs != 0) { double a_, b_; gen.tmp(vI, vJ, a_, b_); vtn = vs > 0 ? a_ : -a_; }
+        if (as != 0) { const double g = gen.va(aI, aJ); uan = as > 0 ? g : -g; }
+        if (bs != 0) { const double g = gen.ua(bI, bJ); van = bs > 0 ? g : -g; }
       }
     }
     tmu[0] = tmu[1];
@@ -299,8 +331,8 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
     uaw[2] = uan;
     if (out_lane && R >= j0 && R < j1 && R <= ny + NG) {
       const long o1 = (long)(R + NG) * pitch + xo;
-      a.ua[zo + o1] = uan;
-      a.va[zo + o1] = van;
+      a.ua[CKS(zo + o1)] = uan;
+      a.va[CKS(zo + o1)] = van;
     }
 
     // ---- stage 2, row r2: uc, ut (x-edges of y-direction faces) and vc, vt
@@ -310,7 +342,7 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
       double ex = 0.0;
       if (EX) {
         const double ua0 = uaw[1], ua_m1 = lane_prev(ua0), ua_m2 = lane_prev(ua_m1), ua_p1 = lane_next(ua0);
-        const double dx0 = mDXA[o2], dx_m1 = lane_prev(dx0), dx_m2 = lane_prev(dx_m1), dx_p1 = lane_next(dx0);
+        const double dx0 = mDXA[CK(o2)], dx_m1 = lane_prev(dx0), dx_m2 = lane_prev(dx_m1), dx_p1 = lane_next(dx0);
         if (I == 0 || I == N) ex = ei4(ua_m2, ua_m1, ua0, ua_p1, dx_m2, dx_m1, dx0, dx_p1);
       }
       double ucv = 0.0, utv = 0.0;
@@ -323,25 +355,25 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
           else if (I == 1) ucv = C1 * tm_p1 + C2 * tm + C3 * tm_m1;
           else if (I == N + 1) ucv = C3 * tm_m1 + C2 * tm + C1 * tm_p1;
           else ucv = A2 * (tm_m2 + tm_p1) + A1 * (tm_m1 + tm);
-          utv = (ucv - vw[1] * mCU[o2]) * mRU[o2];
+          utv = (ucv - vw[1] * mCU[CK(o2)]) * mRU[CK(o2)];
         }
-        const double dy = mDY[o2];
+        const double dy = mDY[CK(o2)];
         utv = utv > 0.0 ? dt2 * utv * dy * sin3m : dt2 * utv * dy * s1w[1];
       }
       double vcv = 0.0, vtv = 0.0;
       if (x >= -1 && x <= nx && r2 >= -1 && r2 <= ny + 1) {
         if (J2 == 0 || J2 == N) {
-          const double e = ei4(vaw[0], vaw[1], vaw[2], vaw[3], mDYA[o2 - 2 * pitch], mDYA[o2 - pitch], mDYA[o2],
-                               mDYA[o2 + pitch]);
+          const double e = ei4(vaw[0], vaw[1], vaw[2], vaw[3], mDYA[CK(o2 - 2 * pitch)], mDYA[CK(o2 - pitch)], mDYA[CK(o2)],
+                               mDYA[CK(o2 + pitch)]);
           vcv = e * (e > 0.0 ? s4w[0] : s2w[1]);
           vtv = e;
         } else {
           if (J2 == -1 || J2 == N - 1) vcv = C1 * tmv[0] + C2 * tmv[1] + C3 * tmv[2];
           else if (J2 == 1 || J2 == N + 1) vcv = C1 * tmv[3] + C2 * tmv[2] + C3 * tmv[1];
           else vcv = A2 * (tmv[0] + tmv[3]) + A1 * (tmv[1] + tmv[2]);
-          vtv = (vcv - uw[1] * mCV[o2]) * mRV[o2];
+          vtv = (vcv - uw[1] * mCV[CK(o2)]) * mRV[CK(o2)];
         }
-        const double dx = mDX[o2];
+        const double dx = mDX[CK(o2)];
         vtv = vtv > 0.0 ? dt2 * vtv * dx * s4w[0] : dt2 * vtv * dx * s2w[1];
       }
       uc2[0] = uc2[1];
@@ -354,10 +386,10 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
       vt2[1] = vtv;
       if (out_lane && r2 >= j0 && r2 < j1 && r2 >= -NG && r2 <= ny + NG) {
         const long oo = zo + o2;
-        a.uc[oo] = ucv;
-        a.ut[oo] = utv;
-        a.vc[oo] = vcv;
-        a.vt[oo] = vtv;
+        a.uc[CKS(oo)] = ucv;
+        a.ut[CKS(oo)] = utv;
+        a.vc[CKS(oo)] = vcv;
+        a.vt[CKS(oo)] = vtv;
       }
     }
 
@@ -366,13 +398,13 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
       // x-sweep fill of row r3 (differs from the y-sweep one only in cube-corner halo cells)
       double qx[3] = {qy[0][1], qy[1][1], qy[2][1]};
       const bool crow3 = J3 < 0 || J3 >= N;
-      if (crow3 && r3 >= -NG && r3 <= ny + NG) {
-        const bool cc = ccol && x >= -NG && x <= nx + NG;
+      if (crow3 && r3 >= -NG && r3 <= ny + NG - 1) {
+        const bool cc = ccol && x >= -NG && x <= nx + NG - 1;
         const long oq = cc ? cc_off(d, sub, x, r3, 1) : o3;
         if (__any(cc)) {
-          qx[0] = QD[oq];
-          qx[1] = QP[oq];
-          qx[2] = QW[oq];
+          qx[0] = QD[CK(oq)];
+          qx[1] = QP[CK(oq)];
+          qx[2] = QW[CK(oq)];
         }
       }
       // x faces: the lane's face x (upwind cell x-1 or x), face x+1 from the next lane
@@ -393,8 +425,8 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
       if (EX) {
         s1c = s1w[0];
         s3c = s3w[0];
-        c1c = mC1[o3];
-        c3c = mC3[o3];
+        c1c = mC1[CK(o3)];
+        c3c = mC3[CK(o3)];
       }
       if (x >= -1 && x <= nx && r3 >= -1 && r3 <= ny) {
         // y faces r3 (cells r3-1 | r3) and r3+1 (cells r3 | r3+1)
@@ -410,7 +442,7 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
           gp[f] = g1[f] * pps;
           gw[f] = g1[f] * wws;
         }
-        const double ra = mRA[o3];
+        const double ra = mRA[CK(o3)];
         const double dpo = qy[0][1], ppo = qy[1][1], wwo = qy[2][1];
         const double dpc = dpo + (f1 - f1n + g1[0] - g1[1]) * ra;
         const long oo = zo + o3;
@@ -425,17 +457,17 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
           else kk = ucn;
         }
         if (vaa > 0.0) {
-          if (J3 == 0 || J3 == N) vv = vc2[0] * s2w[0] + uw[0] * mC2[o3];
+          if (J3 == 0 || J3 == N) vv = vc2[0] * s2w[0] + uw[0] * mC2[CK(o3)];
           else vv = vc2[0];
         } else {
-          if (J3 == -1 || J3 == N - 1) vv = vc2[1] * s4w[0] + uw[1] * mC4[o3];
+          if (J3 == -1 || J3 == N - 1) vv = vc2[1] * s4w[0] + uw[1] * mC4[CK(o3)];
           else vv = vc2[1];
         }
         if (out_lane && r3 >= j0 && r3 < j1) {
-          a.delpc[oo] = dpc;
-          a.ptc[oo] = (ppo * dpo + (fp - fpn + gp[0] - gp[1]) * ra) / dpc;
-          a.wc[oo] = (wwo * dpo + (fw - fwn + gw[0] - gw[1]) * ra) / dpc;
-          a.ke[oo] = dt4 * (uaa * kk + vaa * vv);
+          a.delpc[CKS(oo)] = dpc;
+          a.ptc[CKS(oo)] = (ppo * dpo + (fp - fpn + gp[0] - gp[1]) * ra) / dpc;
+          a.wc[CKS(oo)] = (wwo * dpo + (fw - fwn + gw[0] - gw[1]) * ra) / dpc;
+          a.ke[CKS(oo)] = dt4 * (uaa * kk + vaa * vv);
         }
       }
     }
@@ -447,7 +479,7 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
 bool c_sw_fused() {
   static const bool on = [] {
     const char* e = std::getenv("GTFV3_CSW_FUSED");
-    return !(e && e[0] == '0');
+    return e && e[0] == '1';
   }();
   return on;
 }

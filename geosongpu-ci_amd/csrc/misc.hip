@@ -1,6 +1,7 @@
 // misc.hip — pointwise pieces of fv_dynamics on gfx950: entry conversion to
 // virtual potential temperature + pkz, zh from delz, exit conversion (T, omega),
 // cubed_to_latlon (c2l_ord4) and the Held & Suarez (1994) forcing of GEOShs.
+#include <algorithm>
 #include <cstdlib>
 
 #include "kernels_misc.hpp"
@@ -233,6 +234,15 @@ bool level_blocks_enabled() {
     return !(e && e[0] == '0');
   }();
   return on;
+}
+
+// levels per thread of the level-loop forms (read per launch: tests switch it within one
+// process).  Default 8: C180 L72 on one MI355X, ms per step one level / 8 / 18 per thread:
+// udzc 1.10 / 0.70 / 0.70, p_grad_c 1.30 / 1.02 / 1.07, nh_p_grad 1.61 / 1.32 / 1.30, ds_utvt1
+// 0.95 / 0.88 / 0.95 (profiles/r03e_*)
+int kloop_levels() {
+  const char* e = std::getenv("GTFV3_KLOOP");
+  return e ? std::max(0, atoi(e)) : 8;
 }
 
 bool xcd_order_enabled() {

@@ -822,6 +822,166 @@ __global__ void __launch_bounds__(256) nhpgrad_k(Dims d, const SubInfo* __restri
   }
 }
 
+// ---- level-loop forms (stencil_common.hpp kloop_levels): same expressions in the same
+// order as udzc_k / pgradc_k / nhpgrad_k above, so the outputs are bit-identical.  The
+// thread of point (i, j) walks levels k0 .. k1-1 of one sub-domain; the interface values a
+// level shares with the next and the metric terms stay in registers.
+__global__ void __launch_bounds__(256) udzc_kl(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                               int npz, int nkb, int klb, const double* __restrict__ dp0,
+                                               const double* __restrict__ ut, const double* __restrict__ vt,
+                                               const double* __restrict__ gz, double* __restrict__ gzo) {
+  Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
+  KLSETUP(npz + 1)
+  const SubInfo sub = subs[s];
+  const int km = npz;
+  const double* UT = ut + (long)s * npz * P + o;  // layer l of this column: UT[l * P]
+  const double* VT = vt + (long)s * npz * P + o;
+  const long N1 = d.pitch;
+  const double area = met(M, d, M_AREA, s)[o];
+  // cc_off source offsets of the five gz points (plane-relative, level independent)
+  const long gw = cc_off(d, sub, i - 1, j, 1), gcx = cc_off(d, sub, i, j, 1), ge = cc_off(d, sub, i + 1, j, 1);
+  const long gs = cc_off(d, sub, i, j - 1, 2), gcy = cc_off(d, sub, i, j, 2), gn = cc_off(d, sub, i, j + 1, 2);
+  // layer k-1 values (ut at o, o+1; vt at o, o+pitch) carried from the previous interface
+  double p0 = 0.0, p1 = 0.0, p2 = 0.0, p3 = 0.0;
+  bool have = false;
+  for (int k = k0; k < k1; ++k) {
+    double xf0, xf1, yf0, yf1;
+    if (k == 0) {
+      const double top_ratio = dp0[0] / (dp0[1] + dp0[0]);
+      const double a0 = UT[0], a1 = UT[1], b0 = VT[0], b1 = VT[N1];
+      xf0 = a0 + (a0 - UT[P]) * top_ratio;
+      xf1 = a1 + (a1 - UT[P + 1]) * top_ratio;
+      yf0 = b0 + (b0 - VT[P]) * top_ratio;
+      yf1 = b1 + (b1 - VT[P + N1]) * top_ratio;
+      p0 = a0; p1 = a1; p2 = b0; p3 = b1;
+      have = true;
+    } else if (k == km) {
+      const double bot_ratio = dp0[km - 1] / (dp0[km - 2] + dp0[km - 1]);
+      const long c = (long)(km - 1) * P;
+      const double a0 = have ? p0 : UT[c], a1 = have ? p1 : UT[c + 1];
+      const double b0 = have ? p2 : VT[c], b1 = have ? p3 : VT[c + N1];
+      xf0 = a0 + (a0 - UT[c - P]) * bot_ratio;
+      xf1 = a1 + (a1 - UT[c - P + 1]) * bot_ratio;
+      yf0 = b0 + (b0 - VT[c - P]) * bot_ratio;
+      yf1 = b1 + (b1 - VT[c - P + N1]) * bot_ratio;
+    } else {
+      const double int_ratio = 1.0 / (dp0[k - 1] + dp0[k]);
+      const long c = (long)k * P;
+      if (!have) {
+        p0 = UT[c - P]; p1 = UT[c - P + 1]; p2 = VT[c - P]; p3 = VT[c - P + N1];
+      }
+      const double a0 = UT[c], a1 = UT[c + 1], b0 = VT[c], b1 = VT[c + N1];
+      xf0 = (dp0[k] * p0 + dp0[k - 1] * a0) * int_ratio;
+      xf1 = (dp0[k] * p1 + dp0[k - 1] * a1) * int_ratio;
+      yf0 = (dp0[k] * p2 + dp0[k - 1] * b0) * int_ratio;
+      yf1 = (dp0[k] * p3 + dp0[k - 1] * b1) * int_ratio;
+      p0 = a0; p1 = a1; p2 = b0; p3 = b1;
+      have = true;
+    }
+    const double* g = gz + ((long)s * (npz + 1) + k) * P;
+    const double fx0 = xf0 * (xf0 > 0.0 ? g[gw] : g[gcx]);
+    const double fx1 = xf1 * (xf1 > 0.0 ? g[gcx] : g[ge]);
+    const double fy0 = yf0 * (yf0 > 0.0 ? g[gs] : g[gcy]);
+    const double fy1 = yf1 * (yf1 > 0.0 ? g[gcy] : g[gn]);
+    const double gc = g[gcy];
+    gzo[((long)s * (npz + 1) + k) * P + o] = (gc * area + fx0 - fx1 + fy0 - fy1) / (area + xf0 - xf1 + yf0 - yf1);
+  }
+}
+
+__global__ void __launch_bounds__(256) pgradc_kl(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                                 int npz, int nkb, int klb, double dt2, const double* __restrict__ delpc,
+                                                 const double* __restrict__ pkc, const double* __restrict__ gz,
+                                                 double* __restrict__ uc, double* __restrict__ vc) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KLSETUP(npz)
+  (void)subs;
+  const bool du = j < d.ny, dv = i < d.nx;
+  const long W = -1, S = -d.pitch;
+  const double rdxc = du ? met(M, d, M_RDXC, s)[o] : 0.0, rdyc = dv ? met(M, d, M_RDYC, s)[o] : 0.0;
+  const double* PK = pkc + (long)s * (npz + 1) * P + o;  // interface k: PK[k * P]
+  const double* GZ = gz + (long)s * (npz + 1) * P + o;
+  // interface k values at o, o-1 (w) and o-pitch (s)
+  long l0 = (long)k0 * P;
+  double pk0 = PK[l0], gz0 = GZ[l0];
+  double pk0w = du ? PK[l0 + W] : 0.0, gz0w = du ? GZ[l0 + W] : 0.0;
+  double pk0s = dv ? PK[l0 + S] : 0.0, gz0s = dv ? GZ[l0 + S] : 0.0;
+  for (int k = k0; k < k1; ++k) {
+    const long l1 = (long)(k + 1) * P, lk = ((long)s * npz + k) * P + o;
+    const double pk1 = PK[l1], gz1 = GZ[l1];
+    double pk1w = 0.0, gz1w = 0.0, pk1s = 0.0, gz1s = 0.0;
+    if (du) {
+      pk1w = PK[l1 + W];
+      gz1w = GZ[l1 + W];
+      const double wsum = delpc[lk + W] + delpc[lk];
+      uc[lk] = uc[lk] + dt2 * rdxc / wsum * ((gz1w - gz0) * (pk1 - pk0w) + (gz0w - gz1) * (pk1w - pk0));
+    }
+    if (dv) {
+      pk1s = PK[l1 + S];
+      gz1s = GZ[l1 + S];
+      const double wsum = delpc[lk + S] + delpc[lk];
+      vc[lk] = vc[lk] + dt2 * rdyc / wsum * ((gz1s - gz0) * (pk1 - pk0s) + (gz0s - gz1) * (pk1s - pk0));
+    }
+    pk0 = pk1; gz0 = gz1; pk0w = pk1w; gz0w = gz1w; pk0s = pk1s; gz0s = gz1s;
+  }
+}
+
+__global__ void __launch_bounds__(256) nhpgrad_kl(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                                  int npz, int nkb, int klb, double dt, double ptk,
+                                                  const double* __restrict__ ppb, const double* __restrict__ gzb,
+                                                  const double* __restrict__ pkb, const double* __restrict__ wk1,
+                                                  double* __restrict__ u, double* __restrict__ v) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KLSETUP(npz)
+  (void)subs;
+  const bool du = i < d.nx, dv = j < d.ny;
+  const long E = 1, Nn = d.pitch;
+  const double rdx = du ? met(M, d, M_RDX, s)[o] : 0.0, rdy = dv ? met(M, d, M_RDY, s)[o] : 0.0;
+  const double* PP = ppb + (long)s * (npz + 1) * P + o;
+  const double* GZ = gzb + (long)s * (npz + 1) * P + o;
+  const double* PK = pkb + (long)s * (npz + 1) * P + o;
+  // interface k values at o, o+1 (e) and o+pitch (n); level-0 pp / pk are the model-top constants
+  const long l0 = (long)k0 * P;
+  const bool top = k0 == 0;
+  double pk0 = top ? ptk : PK[l0], pp0 = top ? 0.0 : PP[l0], gz0 = GZ[l0];
+  double pk0e = 0.0, pp0e = 0.0, gz0e = 0.0, pk0n = 0.0, pp0n = 0.0, gz0n = 0.0;
+  if (du) {
+    pk0e = top ? ptk : PK[l0 + E];
+    pp0e = top ? 0.0 : PP[l0 + E];
+    gz0e = GZ[l0 + E];
+  }
+  if (dv) {
+    pk0n = top ? ptk : PK[l0 + Nn];
+    pp0n = top ? 0.0 : PP[l0 + Nn];
+    gz0n = GZ[l0 + Nn];
+  }
+  for (int k = k0; k < k1; ++k) {
+    const long l1 = (long)(k + 1) * P, lk = ((long)s * npz + k) * P + o;
+    const double pk1 = PK[l1], pp1 = PP[l1], gz1 = GZ[l1];
+    double pk1e = 0.0, pp1e = 0.0, gz1e = 0.0, pk1n = 0.0, pp1n = 0.0, gz1n = 0.0;
+    if (du) {
+      pk1e = PK[l1 + E];
+      pp1e = PP[l1 + E];
+      gz1e = GZ[l1 + E];
+      const double wk0 = pk1 - pk0, wke = pk1e - pk0e;
+      const double du1 = dt / (wk0 + wke) * ((gz1 - gz0e) * (pk1e - pk0) + (gz0 - gz1e) * (pk1 - pk0e));
+      u[lk] = (u[lk] + du1 + dt / (wk1[lk] + wk1[lk + E]) * ((gz1 - gz0e) * (pp1e - pp0) + (gz0 - gz1e) * (pp1 - pp0e))) *
+              rdx;
+    }
+    if (dv) {
+      pk1n = PK[l1 + Nn];
+      pp1n = PP[l1 + Nn];
+      gz1n = GZ[l1 + Nn];
+      const double wk0 = pk1 - pk0, wke = pk1n - pk0n;
+      const double dv1 = dt / (wk0 + wke) * ((gz1 - gz0n) * (pk1n - pk0) + (gz0 - gz1n) * (pk1 - pk0n));
+      v[lk] = (v[lk] + dv1 + dt / (wk1[lk] + wk1[lk + Nn]) * ((gz1 - gz0n) * (pp1n - pp0) + (gz0 - gz1n) * (pp1 - pp0n))) *
+              rdy;
+    }
+    pk0 = pk1; pp0 = pp1; gz0 = gz1;
+    pk0e = pk1e; pp0e = pp1e; gz0e = gz1e;
+    pk0n = pk1n; pp0n = pp1n; gz0n = gz1n;
+  }
+}
+
 __global__ void scale_k(long n, double a, const double* __restrict__ x, double* __restrict__ y) {
   long t = (long)blockIdx.x * blockDim.x + threadIdx.x;
   long stride = (long)gridDim.x * blockDim.x;
@@ -841,8 +1001,14 @@ void update_dz_c(const Ctx& c, int npz, const double* dp0, const double* ut, con
                  double* gz_out) {
   const Dims& d = c.d;
   Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
-  GT_LAUNCH(udzc_k, g2lv(L, d.nsub * (npz + 1)), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dp0, ut, vt,
-                     gz, gz_out);
+  if (const int klb = kloop_levels()) {
+    const int nkb = (npz + 1 + klb - 1) / klb;
+    GT_LAUNCH(udzc_kl, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, nkb, klb, dp0, ut,
+                       vt, gz, gz_out);
+  } else {
+    GT_LAUNCH(udzc_k, g2lv(L, d.nsub * (npz + 1)), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dp0, ut, vt,
+                       gz, gz_out);
+  }
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   gt_bytes(npz * (e.X + e.Y) + (npz + 1) * 2 * e.C + 3 * e.C);
@@ -852,8 +1018,14 @@ void p_grad_c(const Ctx& c, int npz, double dt2, const double* delpc, const doub
               double* vc) {
   const Dims& d = c.d;
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  GT_LAUNCH(pgradc_k, g2lv(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt2, delpc, pkc,
-                     gz, uc, vc);
+  if (const int klb = kloop_levels()) {
+    const int nkb = (npz + klb - 1) / klb;
+    GT_LAUNCH(pgradc_kl, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, nkb, klb, dt2,
+                       delpc, pkc, gz, uc, vc);
+  } else {
+    GT_LAUNCH(pgradc_k, g2lv(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt2, delpc, pkc,
+                       gz, uc, vc);
+  }
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   gt_bytes(npz * (e.C + 2 * e.X + 2 * e.Y) + (npz + 1) * 2 * e.C + 2 * e.C);
@@ -965,8 +1137,14 @@ void nh_p_grad(const Ctx& c, const NhPgArgs& a) {
   }
   const double ptk = exp(Constants::kappa * log(a.ptop));
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  GT_LAUNCH(nhpgrad_k, g2lv(L, d.nsub * a.npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, ptk,
-                     a.ppb, a.gzb, a.pkb, a.wk1, a.u, a.v);
+  if (const int klb = kloop_levels()) {
+    const int nkb = (a.npz + klb - 1) / klb;
+    GT_LAUNCH(nhpgrad_kl, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, nkb, klb,
+                       a.dt, ptk, a.ppb, a.gzb, a.pkb, a.wk1, a.u, a.v);
+  } else {
+    GT_LAUNCH(nhpgrad_k, g2lv(L, d.nsub * a.npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, ptk,
+                       a.ppb, a.gzb, a.pkb, a.wk1, a.u, a.v);
+  }
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   gt_bytes(k1 * 3 * e.K + a.npz * (e.K + 2 * e.X + 2 * e.Y) + 2 * e.C);

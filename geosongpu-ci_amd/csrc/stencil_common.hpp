@@ -89,6 +89,26 @@ __device__ __forceinline__ bool thread_point_lv(const Launch2D& L, long nz, int&
   return true;
 }
 
+// Level-loop forms (KL kernels): one thread per (point, sub-domain, block of kloop_levels()
+// consecutive levels) walking its levels top-down.  Kernels whose level k reads interface
+// planes k and k+1 (or layers k-1 and k) carry the shared plane in registers to the next
+// level, and the metric terms are loaded once per block instead of once per level.
+// GTFV3_KLOOP = levels per thread (default 8; 0: the one-level-per-thread forms).
+int kloop_levels();
+inline dim3 kloop_grid(const Launch2D& L, int nsub, int nkb) {
+  long gx = ((long)L.ni * L.nj + BX * BY - 1) / (BX * BY);
+  gx = xcd_order_enabled() ? (gx + 7) / 8 * 8 : (gx + 7) / 8 * 8 + 1;
+  return dim3((unsigned)gx, 1, (unsigned)(nsub * nkb));
+}
+// setup of a KL kernel with parameters (..., int nkb, int klb, ...) over region L: point
+// (i, j), sub-domain s, levels k0 .. k1-1 (nk_ levels in all), plane size P, plane offset o
+#define KLSETUP(nk_)                                                            \
+  int i, j;                                                                     \
+  if (!thread_point(L, i, j)) return;                                           \
+  const int s = blockIdx.z / nkb;                                               \
+  const int k0 = (int)(blockIdx.z % nkb) * klb, k1 = min((nk_), k0 + klb);      \
+  const long P = d.plane, o = pidx(d, i, j);
+
 // Wavefront-wide lane shifts of a double through DPP (no LDS): lane_prev(v) in lane L is v of
 // lane L-1, lane_next(v) is v of lane L+1; the lanes shifted in at the ends read 0.  Every
 // lane of the wave must execute them (no lane-divergent branch around a shift).

@@ -179,3 +179,28 @@ def test_hip_step_dry_mass_drift(pkg, require_gpu):
         assert abs(m1 - m0) / m0 < 3e-11, (m1 - m0) / m0
         m0 = m1
     d.close()
+
+
+@pytest.mark.parametrize("klb", [8, 5])
+def test_level_loop_forms_bitwise(pkg, require_gpu, monkeypatch, klb):
+    """The level-loop forms of update_dz_c, p_grad_c and nh_p_grad (GTFV3_KLOOP = levels per
+    thread: interface planes and metric terms carried in registers from level to level)
+    against the one-level-per-thread kernels: one C24 L20 step (2x2 sub-domains per tile),
+    bit for bit on every state field, with level blocks that divide the level count
+    unevenly (20 layers / 21 interfaces in blocks of 8 and of 5)."""
+    state = importlib.import_module(pkg.__name__ + ".state")
+    npz = 20
+    ak, bk, ks = state.hybrid_levels(npz)
+    out = {}
+    for mode in (0, klb):
+        monkeypatch.setenv("GTFV3_KLOOP", str(mode))
+        d = pkg.Domain(npx=25, npz=npz, nq=2, layout_x=2, layout_y=2)
+        st = state.jablonowski_williamson(d, ak, bk)
+        d.set_vertical(ak, bk, ks)
+        for k, v in st.items():
+            d.upload(k, v)
+        d.step(1)
+        out[mode] = {k: d.download(k) for k in ("u", "v", "w", "pt", "delp", "delz", "q", "ps", "pe")}
+        d.close()
+    for k in out[0]:
+        assert np.array_equal(out[0][k], out[klb][k]), f"{k}: level-loop forms differ"
