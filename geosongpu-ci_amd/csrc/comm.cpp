@@ -175,6 +175,7 @@ class NullTransport : public Transport {
   void recv(double*, size_t, int, hipStream_t) override {}
   void group_end(hipStream_t) override {}
   void allreduce_max(double*, int, hipStream_t) override {}
+  bool capturable() const override { return true; }
 };
 
 }  // namespace

@@ -22,6 +22,8 @@ class Transport {
   virtual void recv(double* buf, size_t n, int peer, hipStream_t st) = 0;
   virtual void group_end(hipStream_t st) = 0;
   virtual void allreduce_max(double* dev, int n, hipStream_t st) = 0;
+  // its enqueue makes no host wait, so a HIP graph can capture it (Dycore::step)
+  virtual bool capturable() const { return false; }
 };
 
 std::unique_ptr<Transport> make_nccl_transport(int nranks, int rank, const void* nccl_id);

@@ -82,6 +82,10 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
 }
 
 Dycore::~Dycore() {
+  if (ac_exec) {
+    if (st) (void)hipStreamSynchronize(st);
+    (void)hipGraphExecDestroy(ac_exec);
+  }
   for (auto& kv : fields) {
     if (debug_sync_launch()) {
       double* base = kv.second.p - kGuardElems;
@@ -120,6 +124,7 @@ Field& Dycore::field(const std::string& name, int nk) {
   }
   Field f;
   f.nk = nk;
+  ++field_gen;
   size_t bytes = sizeof(double) * (size_t)field_elems(nk);
   if (debug_sync_launch()) {
     // debug mode: guard zones either side of the field, checked after every launch
@@ -422,6 +427,16 @@ void Dycore::moist_physics(double dt) {
   radcouple(c, r);
 }
 
+// GTFV3_GRAPH=1: the acoustic sub-steps replayed as one captured HIP graph (read per step).
+// Off by default: measured on one MI355X, the graph saves the launch gaps of the small
+// per-rank shares (rank 0 of the 8-rank layout alone: 6.91 -> 6.66 ms per step) but loses
+// to the three-stream launches at C180 on one GPU (38.23 -> 38.60 ms), and the RCCL
+// transport of real multi-GPU runs is not captured (profiles/r03g_*)
+static bool graph_enabled() {
+  const char* e = std::getenv("GTFV3_GRAPH");
+  return e && e[0] == '1';
+}
+
 void Dycore::step() {
   if (nl.host_only) throw std::runtime_error("host-only dycore cannot step");
   if (nl.k_split != 1) throw std::runtime_error("step: only k_split = 1 is supported");
@@ -588,6 +603,7 @@ void Dycore::step() {
 
   zh_init(c, npz, phis.p, delz.p, zh);  // compute domain: reads no halo
   halo_update({{"u", 'd'}, {"v", 'd'}, {"delp", 'c'}, {"pt", 'c'}, {"w", 'c'}, {"phis", 'c'}, {"zh", 'c'}});
+  auto acoustic = [&]() {
   for (int it = 0; it < nl.n_split; ++it) {
     const bool last = it == nl.n_split - 1;
     c_sw_transport(c, ca);
@@ -660,6 +676,40 @@ void Dycore::step() {
     nh_p_grad(c, pa);
     if (!last) halo_update({{"u", 'd'}, {"v", 'd'}});
   }
+  };
+  // The n_split acoustic sub-steps (~40 launches each, on three streams, with their halo
+  // exchanges) replayed as one HIP graph (GTFV3_GRAPH=1): the per-launch gaps between
+  // dependent kernels (~9 us median at the 8-rank share, 11 % of its step) become graph edges.  Captured only
+  // where nothing in the loop waits on the host (one rank, or a capturable transport: RCCL
+  // and the loopback test transport are not), with an even n_split (the thermo ping-pong
+  // then ends on the planes it started from, so the host's pointers match the graph's), and
+  // without per-kernel timing.  The key holds everything the captured launches bake in.
+  const bool graph = graph_enabled() && nsteps > 0 && nl.n_split % 2 == 0 && !ktimer_enabled() &&
+                     !debug_sync_launch() && halo.capturable();
+  if (graph) {
+    std::vector<double> key = {(double)field_gen, dt, dt2, ptop, (double)fork_substep, (double)tfused,
+                               (double)nl.n_split, nl.dddmp, nl.d2_bg, nl.p_fac, nl.dz_min, nl.d4_bg, nl.vtdm4,
+                               nl.d_con, (double)nl.nord, (double)nl.nord_v, (double)nl.hord_mt, (double)nl.hord_vt,
+                               (double)nl.hord_tm, (double)nl.hord_dp};
+    for (const Field* f : {&u, &v, &w, &delz, &pt, &delp, &phis})
+      key.push_back((double)reinterpret_cast<uintptr_t>(f->p));
+    for (const double* p : {vert, dp_ref}) key.push_back((double)reinterpret_cast<uintptr_t>(p));
+    if (!ac_exec || key != ac_key) {
+      if (ac_exec) HIP_CHECK(hipGraphExecDestroy(ac_exec));
+      ac_exec = nullptr;
+      hipGraph_t g = nullptr;
+      HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+      acoustic();
+      HIP_CHECK(hipStreamEndCapture(st, &g));
+      HIP_CHECK(hipGraphInstantiate(&ac_exec, g, nullptr, nullptr, 0));
+      HIP_CHECK(hipGraphDestroy(g));
+      ac_key = key;
+    }
+    HIP_CHECK(hipGraphLaunch(ac_exec, st));
+  } else {
+    acoustic();
+  }
+  ++nsteps;
   // odd n_split: the fields end on the second planes; copy back to the caller's planes
   if (tfused && delp.p != orig3[0]) {
     for (int f = 0; f < 3; ++f) copy_levels(c, field_elems(npz), cur3[f]->p, alt[f]->p);

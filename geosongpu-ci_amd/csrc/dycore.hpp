@@ -70,6 +70,13 @@ class Dycore {
   // when set, the step's tracer transport waits for this event (the bridge uploads tracers
   // 1.. beside the acoustic sub-steps)
   hipEvent_t tracer_wait = nullptr;
+  // the acoustic sub-steps as one HIP graph (GTFV3_GRAPH, Dycore::step): captured on the
+  // second step (the first allocates every field and table), replayed while the key (field
+  // generation, state planes, step constants) is unchanged
+  hipGraphExec_t ac_exec = nullptr;
+  std::vector<double> ac_key;
+  long field_gen = 0;  // bumped when a field is created or freed
+  long nsteps = 0;
 
   Field& field(const std::string& name, int nk);  // get or create (zeroed)
   Field* find(const std::string& name);

@@ -50,6 +50,8 @@ class HaloExchanger {
   // remote tables (dir 0: send/pack, 1: recv/unpack) as (sub, off, comp, sign, pos_in_peer_segment, peer)
   std::vector<int> remote_table(int kind, int dir) const;
   int nranks() const { return nranks_; }
+  // an exchange enqueues without host waits (one rank, or a capturable transport)
+  bool capturable() const { return nranks_ == 1 || !tr_ || tr_->capturable(); }
 
  private:
   Dims d_{};

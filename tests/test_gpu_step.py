@@ -204,3 +204,32 @@ def test_level_loop_forms_bitwise(pkg, require_gpu, monkeypatch, klb):
         d.close()
     for k in out[0]:
         assert np.array_equal(out[0][k], out[klb][k]), f"{k}: level-loop forms differ"
+
+
+@pytest.mark.parametrize("proxy", [0, 8])
+def test_acoustic_graph_bitwise(pkg, require_gpu, monkeypatch, proxy):
+    """The acoustic sub-steps replayed as a captured HIP graph (Dycore::step, from the second
+    step on) against the same sub-steps launched one by one: three C24 L20 steps, bit for bit
+    on every state field -- one rank with all six tiles, and rank 0 of the 8-rank layout alone
+    on the null transport (bench.py --rank-proxy 8, the 1x4 bands: the exchange's pack /
+    unpack and comm-stream events inside the graph)."""
+    state = importlib.import_module(pkg.__name__ + ".state")
+    npz = 20
+    ak, bk, ks = state.hybrid_levels(npz)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GTFV3_GRAPH", mode)
+        if proxy:
+            d = pkg.Domain(0, proxy, None, npx=25, npz=npz, nq=2, layout_x=1, layout_y=4, loopback=-1)
+        else:
+            d = pkg.Domain(npx=25, npz=npz, nq=2)
+        st = state.jablonowski_williamson(d, ak, bk)
+        d.set_vertical(ak, bk, ks)
+        for k, v in st.items():
+            d.upload(k, v)
+        for _ in range(3):
+            d.step(1)
+        out[mode] = {k: d.download(k) for k in ("u", "v", "w", "pt", "delp", "delz", "q", "ps", "pe")}
+        d.close()
+    for k in out["0"]:
+        assert np.array_equal(out["0"][k], out["1"][k]), f"{k}: graph replay differs from the launches"
