@@ -79,13 +79,15 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
     halo.set_transport(comm.get());
   }
   halo.build(*cs, dc, d, max_nk, 8);
+  // the null-stream copies and memsets above complete before the non-blocking streams run
+  HIP_CHECK(hipDeviceSynchronize());
 }
 
 Dycore::~Dycore() {
-  if (ac_exec) {
-    if (st) (void)hipStreamSynchronize(st);
-    (void)hipGraphExecDestroy(ac_exec);
-  }
+  // nothing of this context may still run when its memory is released (every stream,
+  // including the halo exchanger's comm stream)
+  if (st) (void)hipDeviceSynchronize();
+  if (ac_exec) (void)hipGraphExecDestroy(ac_exec);
   for (auto& kv : fields) {
     if (debug_sync_launch()) {
       double* base = kv.second.p - kGuardElems;
