@@ -79,7 +79,9 @@ __device__ __forceinline__ bool thread_point_lv(const Launch2D& L, long nz, int&
     z = blockIdx.z;
     return thread_point(L, i, j);
   }
-  z = (int)(blockIdx.z * BY + threadIdx.y);
+  // the wave's plane through readfirstlane (threadIdx.y is one value per 64-lane wave):
+  // the sub-domain, its SubInfo and the metric-plane bases stay in SGPRs
+  z = (int)(blockIdx.z * BY + __builtin_amdgcn_readfirstlane(threadIdx.y));
   if (z >= nz) return false;
   const int t = (int)(xcd_block() * BX + threadIdx.x);
   if (t >= L.ni * L.nj) return false;
