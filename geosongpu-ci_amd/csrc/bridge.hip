@@ -393,8 +393,15 @@ void bridge_init(void* comm, int npx, int npy, int npz, int ntiles, int is, int 
   } else if (nranks != 6 * nl.layout_x * nl.layout_y) {
     throw std::runtime_error("geos_gtfv3_init: one sub-domain per rank expected (6*layout ranks)");
   }
+  // GTFV3_BRIDGE_PROXY=1 (measurement and test aid, never a numerical path): this rank alone
+  // on the null transport -- cross-rank halo messages are dropped -- so the one-sub-domain-
+  // per-rank array layout runs on a single GPU (tests/test_gpu_bridge.py compares the region
+  // the missing messages cannot reach with the six-tile run)
+  const char* const px[] = {"GTFV3_BRIDGE_PROXY", nullptr};
+  const bool proxy = nranks > 1 && env_int(px, 0) == 1;
+  if (proxy) nl.loopback = -1;
   std::vector<unsigned char> id(128, 0);
-  if (nranks > 1) {
+  if (nranks > 1 && !proxy) {
     if (rank == 0) {
       ncclUniqueId uid;
       if (ncclGetUniqueId(&uid) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
@@ -402,7 +409,7 @@ void bridge_init(void* comm, int npx, int npy, int npz, int ntiles, int is, int 
     }
     share_unique_id(comm, rank, nranks, id.data());
   }
-  g_dy = std::make_unique<Dycore>(nl, rank, nranks, nranks > 1 ? id.data() : nullptr);
+  g_dy = std::make_unique<Dycore>(nl, rank, nranks, nranks > 1 && !proxy ? id.data() : nullptr);
   // ncclCommInitRank is collective: every rank has read the id once the Dycore exists
   if (!g_id_file.empty()) {
     std::remove(g_id_file.c_str());

@@ -228,3 +228,72 @@ def test_bridge_copy_pipeline_equivalent(pkg, require_gpu):
     assert min(ms_up, ms_step, ms_down) > 0
     total = sum(a.nbytes for a in ref.values())
     assert up_b < total and down_b < total and up_b < down_b
+
+
+def _bridge_call_rank(pkg, st, ak, bk, ks, npx, npz, nq, rank):
+    """geos_gtfv3 init/run/finalize in GEOS's own topology, one sub-domain (here one tile,
+    layout 1x1) per rank with 2-D / 3-D Fortran arrays and no tile axis, as rank `rank` of 6
+    alone on the null transport (GTFV3_BRIDGE_PROXY=1)"""
+    env = dict(GTFV3_BRIDGE_TILES_PER_RANK="1", GTFV3_RANK=str(rank), GTFV3_WORLD_SIZE="6",
+               GTFV3_BRIDGE_PROXY="1", GTFV3_NONFATAL="1")
+    old = {k: os.environ.get(k) for k in env}
+    os.environ.update(env)
+    try:
+        hook = importlib.import_module(pkg.__name__ + ".hook").geos_gtfv3
+        N = npx - 1
+        shapes = _shapes(N, npz, nq)
+        fort = {}
+        for name, (li, hi, lj, hj, nk, kj) in shapes.items():
+            src = st[name][rank:rank + 1] if name in st else np.zeros((1, nk) + st["delp"].shape[2:])
+            fort[name] = np.asfortranarray(to_fortran(src, li, hi, lj, hj, kj)[..., 0])
+        scal = dict(comm=0, npx=npx, npy=npx, npz=npz, ntiles=6, is_=1, ie=N, js=1, je=N, isd=1 - NG, ied=N + NG,
+                    jsd=1 - NG, jed=N + NG, bdt=900.0, nq_tot=nq)
+        hook.init(**scal)
+        hook.run(**scal, ng=NG, ptop=float(ak[0]), ks=ks, layout_1=1, layout_2=1, adiabatic=0,
+                 ak=np.asfortranarray(ak), bk=np.asfortranarray(bk), **fort)
+        hook.finalize()
+        return fort, shapes
+    finally:
+        for k, v in old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def test_bridge_one_subdomain_per_rank(pkg, require_gpu):
+    """GEOS's rank topology through the ABI -- one sub-domain per rank (six ranks, one tile
+    each), Fortran arrays without a tile axis, the rank's (is, js) checked against the FV3
+    layout -- run as ranks 0 and 4 alone on one GPU with the null transport: the compute
+    domain the missing cross-rank halo messages cannot reach in one step (the tile minus a
+    band along its edges) equals the six-tile single-process bridge run bit for bit."""
+    npx, npz, nq = 145, 10, 2
+    N = npx - 1
+    d, st, ak, bk, ks = _setup(pkg, npx, npz, nq)
+    six, shapes = _bridge_call(pkg, st, d, ak, bk, ks, npx, npz, nq)
+    d.close()
+    band = 50  # cells along each tile edge reached by the dropped messages in one step (measured 45)
+    for rank in (0, 4):
+        one, _ = _bridge_call_rank(pkg, st, ak, bk, ks, npx, npz, nq, rank)
+        for name in ("u", "v", "w", "delz", "pt", "delp", "q", "ps", "pe", "peln", "pk", "pkz", "omga"):
+            li, hi, lj, hj, nk, kj = shapes[name]
+            a, b = one[name], six[name][..., rank]
+            # Fortran index i -> array position i - (li + 1); the central window of the tile
+            i0, i1 = band - li, N - band - li
+            j0, j1 = band - lj, N - band - lj
+            if kj:
+                wa, wb = a[i0:i1, :, j0:j1], b[i0:i1, :, j0:j1]
+            else:
+                wa, wb = a[i0:i1, j0:j1], b[i0:i1, j0:j1]
+            assert np.all(np.isfinite(wb)), f"{name}: six-tile run not finite"
+            # reach of the dropped messages: the deepest differing compute point from the edge
+            ca = a[-li:N - li, :, -lj:N - lj] if kj else a[-li:N - li, -lj:N - lj]
+            cb = b[-li:N - li, :, -lj:N - lj] if kj else b[-li:N - li, -lj:N - lj]
+            diff = np.argwhere(ca != cb)
+            if diff.size:
+                ii, jj = diff[:, 0], diff[:, 2 if kj else 1]
+                depth = np.minimum(np.minimum(ii, N - 1 - ii), np.minimum(jj, N - 1 - jj)).max()
+                print(f"rank {rank} {name}: differences reach {depth} cells from the tile edge")
+            bad = np.argwhere(wa != wb)
+            assert bad.size == 0, (f"rank {rank} {name}: {len(bad)} points of the central window differ, "
+                                   f"first at {bad[:3].tolist()}")
