@@ -227,15 +227,32 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
 #pragma unroll
   for (int m = 1; m < 5; ++m) uw[m] = U[CK(ro(R_lo - 3 + m))];
   uw[0] = 0.0;
+  // the field rows of a row step (u row R+2, v row R, delp / pt / w row R-1 with the y-sweep
+  // corner fill) are loaded one row step ahead, so a step waits on the metric loads only
+  // (L2 / Infinity-Cache hits) instead of an HBM round trip
+  auto q_off = [&](int r) -> long {
+    const int Jr = r + jo;
+    return (Jr < 0 || Jr >= N) && ccol && r >= -NG && r <= ny + NG - 1 && x >= -NG && x <= nx + NG - 1
+               ? cc_off(d, sub, x, r, 2)
+               : ro(r);
+  };
+  double nU = U[CK(ro(R_lo + 2))], nV = V[CK(ro(R_lo))];
+  double nQ[3];
+  {
+    const long oq = q_off(R_lo - 1);
+    nQ[0] = QD[CK(oq)];
+    nQ[1] = QP[CK(oq)];
+    nQ[2] = QW[CK(oq)];
+  }
 
   for (int R = R_lo; R <= R_hi; ++R) {
     // ---- roll the windows, load the new rows
 #pragma unroll
     for (int m = 0; m < 4; ++m) uw[m] = uw[m + 1];
-    uw[4] = U[CK(ro(R + 2))];
+    uw[4] = nU;
     vw[0] = vw[1];
     vw[1] = vw[2];
-    vw[2] = V[CK(ro(R))];
+    vw[2] = nV;
     const int r2 = R - 1, r3 = R - 2;
     const int J = R + jo, J2 = r2 + jo, J3 = r3 + jo;
     const long o2 = ro(r2), o3 = ro(r3);
@@ -247,22 +264,24 @@ __global__ void __launch_bounds__(64 * CW_WAVES) cs_march_k(CsM a) {
     s1w[1] = mS1[CK(o2)];
     s3w[1] = mS3[CK(o2)];
     s2w[1] = mS2[CK(o2)];
-    // delp / pt / w: y-sweep fill of row r2 (stage 3's row r3 + 1).  The cube-corner remap
-    // applies to the cells' halo (i, j in [-NG, n + NG - 1]); the extra staggered column / row
-    // of the padded plane has no corner source and keeps its own (never output) value
-    const bool crow2 = J2 < 0 || J2 >= N;
+    // delp / pt / w: y-sweep fill of row r2 (stage 3's row r3 + 1; q_off: the cube-corner
+    // remap applies to the cells' halo, i, j in [-NG, n + NG - 1]; the extra staggered column /
+    // row of the padded plane has no corner source and keeps its own, never output, value)
 #pragma unroll
     for (int f = 0; f < 3; ++f) {
       qy[f][0] = qy[f][1];
       qy[f][1] = qy[f][2];
     }
+#pragma unroll
+    for (int f = 0; f < 3; ++f) qy[f][2] = nQ[f];
+    // the next row step's field rows
+    nU = U[CK(ro(R + 3))];
+    nV = V[CK(ro(R + 1))];
     {
-      const long oq = crow2 && ccol && r2 >= -NG && r2 <= ny + NG - 1 && x >= -NG && x <= nx + NG - 1
-                          ? cc_off(d, sub, x, r2, 2)
-                          : o2;
-      qy[0][2] = QD[CK(oq)];
-      qy[1][2] = QP[CK(oq)];
-      qy[2][2] = QW[CK(oq)];
+      const long oq = q_off(R);
+      nQ[0] = QD[CK(oq)];
+      nQ[1] = QP[CK(oq)];
+      nQ[2] = QW[CK(oq)];
     }
 
     // ---- stage 1, row R: utmp, vtmp and the generic ua, va
