@@ -503,7 +503,6 @@ void Dycore::step() {
   double* pef = S("_pef", k1);
   double* ppe = S("ppe", k1);
   double* pk3 = S("_pk3", k1);
-  double* gz = S("_gz", k1);
   double* ws = S("ws", 1);
   NhScratch nsc;
   for (int n = 0; n < 14; ++n) nsc.s[n] = S(("_nh" + std::to_string(n)).c_str(), k1);
@@ -568,7 +567,10 @@ void Dycore::step() {
   NhPgArgs pa{};
   pa.npz = npz;
   pa.dt = dt; pa.ptop = ptop;
-  pa.pp = ppe; pa.pk3 = pk3; pa.gz = gz; pa.delp = delp.p;
+  pa.pp = ppe; pa.pk3 = pk3; pa.delp = delp.p;
+  // gz = grav * zh, formed as nh_p_grad's a2b_ord4 loads zh (the same product, no pass)
+  pa.gz = zh;
+  pa.gz_scale = Constants::grav;
   pa.ppb = S("_pg_pp", k1); pa.pkb = S("_pg_pk", k1); pa.gzb = S("_pg_gz", k1); pa.wk1 = S("_pg_wk", npz);
   pa.qx = S("_pg_qx", k1); pa.qy = S("_pg_qy", k1);
   pa.u = u.p; pa.v = v.p;
@@ -672,7 +674,6 @@ void Dycore::step() {
     // stage and update_dz_d do not read them), pk3_pe_halo and the next c_sw do
     halo_update({{"delp", 'c'}, {"pt", 'c'}, {"zh", 'c'}, {"ppe", 'c'}, {"w", 'c'}});
     pk3_pe_halo(c, npz, ptop, last, delp.p, pk3, pe);
-    scale_field(c, field_elems(k1), Constants::grav, zh, gz);
     if (fork_substep) HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
     if (dcon || vdamp) d_sw_post(c, da);  // the new delp and u, v: after both d_sw stages
     nh_p_grad(c, pa);

@@ -48,7 +48,9 @@ int riem_variant();
 void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* delp, double* pk3, double* pe);
 void a2b_ord4(const Ctx& c, int nk, const double* q, double* qout, double* qx, double* qy);
 // up to four fields in one launch (same result as one a2b_ord4 call per field)
-void a2b_ord4_multi(const Ctx& c, int nf, const int* nk, const double* const* q, double* const* qout);
+// scale (optional, per field): each field is multiplied by it as it is loaded
+void a2b_ord4_multi(const Ctx& c, int nf, const int* nk, const double* const* q, double* const* qout,
+                    const double* scale = nullptr);
 
 struct NhPgArgs {
   int npz;
@@ -56,6 +58,8 @@ struct NhPgArgs {
   const double *pp, *pk3, *gz, *delp;
   double *ppb, *pkb, *gzb, *wk1, *qx, *qy;
   double *u, *v;
+  // gz enters a2b_ord4 multiplied by this as it is loaded (the step passes zh and grav)
+  double gz_scale = 1.0;
 };
 void nh_p_grad(const Ctx& c, const NhPgArgs& a);
 void scale_field(const Ctx& c, long n, double a, const double* x, double* y);

@@ -383,7 +383,8 @@ struct A2bPoint {
   const double* q;   // plane of the level
   const double* dxa;
   const double* dya;
-  __device__ __forceinline__ double Q(int i, int j) const { return q[pidx(d, i, j)]; }
+  double sc;         // the field's scale, applied as it is loaded (sc * q, 1 for most fields)
+  __device__ __forceinline__ double Q(int i, int j) const { return sc * q[pidx(d, i, j)]; }
   __device__ __forceinline__ double qx(int i, int j) const {
     const int N = sub.N, io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
     const int I = i + io, J = j + jo;
@@ -474,10 +475,10 @@ struct A2bEdge {
     double acc = 0.0;
 #pragma unroll
     for (int r = 0; r < 3; ++r) {
-      const double q1 = q[pidx(P.d, kCornerA[c][r][0] * N + kCornerB[c][r][0] - io,
-                               kCornerA[c][r][1] * N + kCornerB[c][r][1] - jo)];
-      const double q2 = q[pidx(P.d, kCornerA[c][r][2] * N + kCornerB[c][r][2] - io,
-                               kCornerA[c][r][3] * N + kCornerB[c][r][3] - jo)];
+      const double q1 = P.sc * q[pidx(P.d, kCornerA[c][r][0] * N + kCornerB[c][r][0] - io,
+                                      kCornerA[c][r][1] * N + kCornerB[c][r][1] - jo)];
+      const double q2 = P.sc * q[pidx(P.d, kCornerA[c][r][2] * N + kCornerB[c][r][2] - io,
+                                      kCornerA[c][r][3] * N + kCornerB[c][r][3] - jo)];
       const double e = q1 + cw[c * 3 + r] * (q1 - q2);
       acc = r == 0 ? e : acc + e;
     }
@@ -499,16 +500,20 @@ struct A2bEdge {
 // first plane of field f (unused entries: INT_MAX).  More waves per launch overlap the
 // march kernels' row-latency chains of the four fields.
 constexpr int A2B_MAXF = 4;
+// sc[f]: a scale applied to field f as it is loaded -- nh_p_grad interpolates gz = grav * zh
+// straight from zh (the same product, so the same bits as a scaled copy, without the pass)
 struct A2bF {
   const double* q[A2B_MAXF];
   double* qo[A2B_MAXF];
   int nk[A2B_MAXF];
   int zb[A2B_MAXF + 1];
+  double sc[A2B_MAXF];
 };
 struct A2bSel {
   const double* q;
   double* qo;
   int nk, z;  // z: plane within the field
+  double sc;
 };
 __device__ __forceinline__ A2bSel a2b_select(const A2bF& F, int z) {
   const int f = (z >= F.zb[1]) + (z >= F.zb[2]) + (z >= F.zb[3]);
@@ -517,6 +522,7 @@ __device__ __forceinline__ A2bSel a2b_select(const A2bF& F, int z) {
   r.qo = f == 0 ? F.qo[0] : (f == 1 ? F.qo[1] : (f == 2 ? F.qo[2] : F.qo[3]));
   r.nk = f == 0 ? F.nk[0] : (f == 1 ? F.nk[1] : (f == 2 ? F.nk[2] : F.nk[3]));
   r.z = z - (f == 0 ? F.zb[0] : (f == 1 ? F.zb[1] : (f == 2 ? F.zb[2] : F.zb[3])));
+  r.sc = f == 0 ? F.sc[0] : (f == 1 ? F.sc[1] : (f == 2 ? F.sc[2] : F.sc[3]));
   return r;
 }
 
@@ -530,6 +536,7 @@ __global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restr
   const int z = zg - (f == 0 ? F.zb[0] : (f == 1 ? F.zb[1] : (f == 2 ? F.zb[2] : F.zb[3]))), s = z / nk;
   const double* __restrict__ q = f == 0 ? F.q[0] : (f == 1 ? F.q[1] : (f == 2 ? F.q[2] : F.q[3]));
   double* __restrict__ qout = f == 0 ? F.qo[0] : (f == 1 ? F.qo[1] : (f == 2 ? F.qo[2] : F.qo[3]));
+  const double sc = f == 0 ? F.sc[0] : (f == 1 ? F.sc[1] : (f == 2 ? F.sc[2] : F.sc[3]));
   const SubInfo sub = subs[s];
   int i, j;
   if (!edge_line_point(blockIdx.x * blockDim.x + threadIdx.x, sub, 0, d.nx, 0, d.ny, i, j)) return;
@@ -541,7 +548,7 @@ __global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restr
   (void)cw;
   double val;
   bool set = true;
-  const A2bEdge E{A2bPoint{d, sub, q + zo, met(M, d, M_DXA, s), met(M, d, M_DYA, s)}, q + zo, cw + (long)s * 12, N, io,
+  const A2bEdge E{A2bPoint{d, sub, q + zo, met(M, d, M_DXA, s), met(M, d, M_DYA, s), sc}, q + zo, cw + (long)s * 12, N, io,
                   jo};
   if ((I == 0 || I == N) && (J == 0 || J == N)) val = E.edge_or_corner(I, J);
   else if ((I == 0 && io == 0) || (I == N && io + nx == N)) {
@@ -594,7 +601,7 @@ struct A2bM {
 
 template <bool EX>
 __device__ void a2b_march_strip(const A2bM& a, const double* qf, double* qof, int nk, int z, int a0, int a1, int j0,
-                                int j1) {
+                                int j1, double sc) {
   const Dims& d = a.d;
   const int lane = threadIdx.x & (AM_W - 1);
   const int s = z / nk;
@@ -631,7 +638,7 @@ __device__ void a2b_march_strip(const A2bM& a, const double* qf, double* qof, in
   double qb[AM_B], db[AM_B], xb[AM_B], yb[AM_B], qn[AM_B], dn[AM_B], xn[AM_B], yn[AM_B];
   auto fetch = [&](int r, double& q_, double& d_, double& x_, double& y_) {
     const long o = row_of(r);
-    q_ = qq[o];
+    q_ = sc * qq[o];
     d_ = EX ? dxa[o] : 0.0;
     const int j = r - 2;  // corner row of this step
     const long oj = (long)((j > -NG ? (j < rlast ? j : rlast) : -NG) + NG) * pitch + xo;
@@ -781,8 +788,8 @@ __global__ void __launch_bounds__(AM_W * AM_WAVES) a2b_march_k(A2bM a) {
   const int A = a0 + sub.ioff;
   // x-interpolant edge forms are needed only where a lane's column reaches I <= 1 or I >= N-1
   const bool ex = !(A - 2 >= 2 && A + AM_OUT + 1 <= sub.N - 2);
-  if (ex) a2b_march_strip<true>(a, fs.q, fs.qo, fs.nk, fs.z, a0, a1, j0, j1);
-  else a2b_march_strip<false>(a, fs.q, fs.qo, fs.nk, fs.z, a0, a1, j0, j1);
+  if (ex) a2b_march_strip<true>(a, fs.q, fs.qo, fs.nk, fs.z, a0, a1, j0, j1, fs.sc);
+  else a2b_march_strip<false>(a, fs.q, fs.qo, fs.nk, fs.z, a0, a1, j0, j1, fs.sc);
 }
 
 // non-hydrostatic pressure gradient on the D-grid winds (u, v arrive x dx, dy)
@@ -1080,7 +1087,8 @@ void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* d
   gt_bytes((double)d.nsub * npz * (4.0 * (d.nx + 2) + 4.0 * d.ny) * (do_pe ? 3 : 2));  // halo ring only
 }
 
-void a2b_ord4_multi(const Ctx& c, int nf, const int* nk, const double* const* q, double* const* qout) {
+void a2b_ord4_multi(const Ctx& c, int nf, const int* nk, const double* const* q, double* const* qout,
+                    const double* scale) {
   const Dims& d = c.d;
   if (nf < 1 || nf > A2B_MAXF) throw std::runtime_error("a2b_ord4: 1..4 fields per launch");
   A2bF F{};
@@ -1092,12 +1100,14 @@ void a2b_ord4_multi(const Ctx& c, int nf, const int* nk, const double* const* q,
       F.q[f] = q[f];
       F.qo[f] = qout[f];
       F.nk[f] = nk[f];
+      F.sc[f] = scale ? scale[f] : 1.0;
       nz += (long)d.nsub * nk[f];
       lev += nk[f];
     } else {
       F.q[f] = q[0];
       F.qo[f] = qout[0];
       F.nk[f] = 1;
+      F.sc[f] = 1.0;
     }
   }
   F.zb[A2B_MAXF] = INT_MAX;
@@ -1136,7 +1146,8 @@ void nh_p_grad(const Ctx& c, const NhPgArgs& a) {
     const int nk[4] = {k1, k1, k1, a.npz};
     const double* q[4] = {a.pp, a.pk3, a.gz, a.delp};
     double* qo[4] = {a.ppb, a.pkb, a.gzb, a.wk1};
-    a2b_ord4_multi(c, 4, nk, q, qo);
+    const double sc[4] = {1.0, 1.0, a.gz_scale, 1.0};
+    a2b_ord4_multi(c, 4, nk, q, qo, sc);
   }
   const double ptk = exp(Constants::kappa * log(a.ptop));
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
