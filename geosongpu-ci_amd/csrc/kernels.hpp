@@ -54,6 +54,10 @@ struct TpArgs {
   double* dp2 = nullptr;
   const int* nsplt = nullptr;
   int it = 0;
+  // d_sw's u, v update fused into the vorticity march (nt = 1, no mass fluxes): u += ... + fy,
+  // v += ... - fx with the corner kinetic energy ke (ds_uv's expressions); no flux plane
+  const double* ke_uv = nullptr;
+  double *u_uv = nullptr, *v_uv = nullptr;
 };
 void fv_tp_2d(const Ctx& c, const TpArgs& a);
 

@@ -831,6 +831,16 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
   TpArgs t = d_sw_tp(a);
   t.mfx = nullptr; t.mfy = nullptr;
   t.q = a.vort; t.fx = a.gvx; t.fy = a.gvy; t.ord = a.hord_vt;
+  // u, v updated inside the vorticity march (tp.hip TM = 3: ds_uv's expressions on the
+  // fluxes in registers, no gvx / gvy planes); GTFV3_UV_FUSED=0: fluxes, then ds_uv
+  const char* ev = std::getenv("GTFV3_UV_FUSED");
+  if (!(ev && ev[0] == '0')) {
+    t.ke_uv = a.ke;
+    t.u_uv = a.u;
+    t.v_uv = a.v;
+    fv_tp_2d(c, t);
+    return;
+  }
   fv_tp_2d(c, t);
   GT_LAUNCH(ds_uv, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.ke, a.gvx, a.gvy, a.u,
                      a.v);

@@ -81,6 +81,9 @@ struct TpM {
   // paired last strips (split launches, pairlast set): the paired (sub-domain, strip) entries
   // follow the npair full ones
   int pairlast, npairh;
+  // TM = 3 (d_sw's ds_uv fused): corner kinetic energy; u, v updated in place
+  const double* ke;
+  double *uu, *vv;
 };
 
 // Wavefront-wide lane shifts through DPP (no LDS): dpp_prev(v) in lane L is v of lane
@@ -194,12 +197,16 @@ struct YRoll {
 // TM = 2: tracer_2d_1l's update fused (NF tracers with the mass fluxes mfx / mfy): dp2 of
 //   row r-3 is formed from the mass fluxes the march holds (tracer_dp2's expression) and the
 //   tracers are updated from their outer fluxes (tracer_update's expression) into qo.
+// TM = 3: d_sw's vorticity transport with ds_uv fused (NF = 1, no mass fluxes): u on row
+//   r-2 takes the outer y flux of that edge, v on row r-3 the outer x flux of that row, with
+//   the corner kinetic energy of rows r-3 / r-2 (ds_uv's expressions); no flux plane.
 // pair: 0 one level per wave; 1 the wave's upper half runs level k+1; 2 paired strip without
 // a level k+1 (odd level count: the upper half repeats level k and stores nothing)
 template <int ORD, bool EX, bool AHEAD2, bool MF, int NF, int TM>
 __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, int pair) {
-  static_assert(TM == 0 || (TM == 1 && NF == 3 && MF) || (TM == 2 && MF),
-                "thermo march: delp, w, pt with the accumulators as MX / MY; tracer march: mass fluxes");
+  static_assert(TM == 0 || (TM == 1 && NF == 3 && MF) || (TM == 2 && MF) || (TM == 3 && NF == 1 && !MF),
+                "thermo march: delp, w, pt with the accumulators as MX / MY; tracer march: mass fluxes; "
+                "ds_uv march: one field, no mass fluxes");
   const Dims& d = a.d;
   const int lane = threadIdx.x & (MW - 1);
   const int hl = pair ? (lane & 31) : lane;  // lane within the strip
@@ -242,6 +249,10 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
   const auto rDP1 = rsrcf(TM == 2 ? a.dp1 + fo : a.mx + fo);
   const auto rDP2 = rsrcf(TM == 2 ? a.dp2o + fo : a.mx + fo);
   const bool dp2_group = TM == 2 && tg == 0;  // one field group writes dp2
+  // TM = 3: ke, u, v (level fields), dx, dy (metric planes)
+  const auto rKE = rsrcf(TM == 3 ? a.ke + fo : a.crx + fo), rU = rsrcf(TM == 3 ? a.uu + fo : a.crx + fo);
+  const auto rV = rsrcf(TM == 3 ? a.vv + fo : a.crx + fo);
+  const auto rDX = rsrc(met(a.M, d, M_DX, s)), rDY = rsrc(met(a.M, d, M_DY, s));
   const uint32_t vx = (uint32_t)xo * 8u;  // metric planes
   const uint32_t vf = vx + (upper && pair == 1 ? (uint32_t)PBy : 0u);  // level fields
   // dxa only enters the tile-edge interface values (ppm_al at g = 0, N reads the four
@@ -349,6 +360,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
     fyo_prev[f] = 0.0;
   }
   double yfx_prev = 0.0;  // yfx at edge r-3 (the previous row step's edge r-2)
+  double ke_m = 0.0;      // TM = 3: ke of row r-3 (the previous row step's row r-2)
 
   // lane predicates (constant along the march)
   const bool l_fx2 = x >= 0 && x <= nx, l_qj = x >= 0 && x < nx;
@@ -408,6 +420,19 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
     constexpr bool GEN = decltype(gen)::value;
     if (GEN) nxt = load(r + 1);
     else load_steady(r + ahead, nxt);
+    // TM = 3: this step's ke / u / dx (row r-2) and v / dy (row r-3), issued here so their
+    // latency overlaps the step's PPM work (not prefetched: three row buffers would cost the
+    // march its third wave per SIMD)
+    double t_ke = 0.0, t_u = 0.0, t_dx = 0.0, t_v = 0.0, t_dy = 0.0;
+    if constexpr (TM == 3) {
+      const int re = r - 2 < -NG ? -NG : r - 2, rm = r - 3 < -NG ? -NG : r - 3;
+      const uint32_t se3 = (uint32_t)(re + NG) * rowb, sm3 = (uint32_t)(rm + NG) * rowb;
+      t_ke = bl(rKE, vf, se3);
+      t_u = bl(rU, vf, se3);
+      t_dx = bl(rDX, vx, se3);
+      t_v = bl(rV, vf, sm3);
+      t_dy = bl(rDY, vx, sm3);
+    }
     const long o = (long)(r + NG) * pitch + xo;
     const double rax = cur.area_r + cur.xfx - dpp_next(cur.xfx);
     // ---- row r: inner x flux fx2, q_j (per field)
@@ -512,6 +537,26 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
         }
         fyy_prev[f] = fyy;
       }
+      if constexpr (TM == 3) {
+        // ds_uv: u on edge e with this edge's outer y flux, v on row m with this row's outer
+        // x flux; ke of row m (carried from the previous step) and row e, x neighbour by DPP;
+        // ds_uv's expressions and order
+        const double ke_e1 = dpp_next(t_ke);
+        const double un = t_u * t_dx + t_ke - ke_e1 + fyo[0];
+        if (GEN) {
+          if (s_fy && e <= ny && (e < j1 || last)) bst(rU, se, un);
+        } else {
+          bstv(rU, vfy, se, un);
+        }
+        if (rowm) {
+          const double vn = t_v * t_dy + ke_m - t_ke - fxo[0];
+          if (GEN) {
+            if (s_fx && mrow < j1) bst(rV, se - rowb, vn);
+          } else {
+            bstv(rV, vfx, se - rowb, vn);
+          }
+        }
+      }
       if constexpr (TM == 1) {
         // flux capacitor (ds_accum): mfy on edge e, mfx on row m (cur.my / cur.mx hold them)
         if (GEN) {
@@ -578,6 +623,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
       }
     }
     yfx_prev = cur.yfx;
+    if constexpr (TM == 3) ke_m = t_ke;
   };
 
   // steady rows: 2 <= G <= N-2 for the y interpolant's interface G = r-1, rows r+1 (the
@@ -961,8 +1007,16 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
       m.nsplt = a.nsplt;
       m.it = a.it;
     }
+    const bool uv = a.u_uv != nullptr;
+    if (uv) {
+      if (pair2 || tupd || a.nt != 1 || a.mfx || !a.ke_uv || !a.v_uv)
+        throw std::runtime_error("fv_tp_2d with the u, v update: one field, no mass fluxes, ke, u and v needed");
+      m.ke = a.ke_uv;
+      m.uu = a.u_uv;
+      m.vv = a.v_uv;
+    }
     for (int f = 0; f < NFw; ++f)
-      if (!m.qf[f] || (tupd ? !m.qo[f] : (!m.fxf[f] || !m.fyf[f])))
+      if (!m.qf[f] || (tupd ? !m.qo[f] : (!uv && (!m.fxf[f] || !m.fyf[f]))))
         throw std::runtime_error("fv_tp_2d: field slot " + std::to_string(f) + " of a " + std::to_string(NFw) +
                                  "-field group is not set");
     m.nt = a.nt;
@@ -1011,6 +1065,15 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     HIP_LAUNCH_CHECK();                                                                            \
     gt_bytes(bytes / 8.0);                                                                         \
   } while (0)
+    if (uv) {
+      // q read; crx cry xfx yfx read; ke, u, v read, u, v written; dx, dy once
+      const double ub = 8.0 * a.nk * ((e.C + 2 * (e.X + e.Y)) + e.K + 2 * (e.X + e.Y)) + 16.0 * e.C;
+      if (a.ord == 5) GT_LAUNCH_N("tp_march_uv<5>", (tp_march<5, true, false, 1, 3>), g, b, 0, c.st, m);
+      else GT_LAUNCH_N("tp_march_uv<6>", (tp_march<6, true, false, 1, 3>), g, b, 0, c.st, m);
+      HIP_LAUNCH_CHECK();
+      gt_bytes(ub / 8.0);
+      return;
+    }
     if (tupd) {
 #define TQ_GO(O, F_)                                                                                  \
   do {                                                                                                \
