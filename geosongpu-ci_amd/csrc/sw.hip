@@ -622,6 +622,143 @@ __global__ void __launch_bounds__(256) ds_ke(Dims d, const SubInfo* __restrict__
   if (vd) AT(vd, 0, 0) = damp * dpc;  // the damping term on its own (d_con heat)
 }
 
+// ds_ke with its loads issued up front (ds_ke_ld): the same expressions in the same order
+// (bit-identical), but every value an interior corner needs -- the B-grid wind inputs, both
+// six-point PPM stencils, the Courant metric and the divergence-damping terms -- is loaded
+// unconditionally before any arithmetic, so a wave has ~45 loads in flight at once instead of
+// ~15 dependent round trips through branches (rocprof SQ counters: ds_ke waited 63 % of its
+// wave cycles).  Tile-edge inputs (vt / ut stencils, dx / dy for the edge PPM forms, sin1-4)
+// are loaded only by the waves holding such points.  hord_mt and nord = 0 are template
+// constants.
+template <int ORD, bool DAMP>
+__global__ void __launch_bounds__(256) ds_ke_ld(Dims d, const SubInfo* __restrict__ subs,
+                                                const double* __restrict__ M, int npz, double dt, double dddmp,
+                                                double d2_bg, double da_min_c, const double* __restrict__ u,
+                                                const double* __restrict__ v, const double* __restrict__ uc,
+                                                const double* __restrict__ vc, const double* __restrict__ ua,
+                                                const double* __restrict__ va, const double* __restrict__ ut,
+                                                const double* __restrict__ vt, double* __restrict__ ke,
+                                                double* __restrict__ vd) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KSETUP(npz)
+  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+  const long p = d.pitch;
+  const double dt5 = 0.5 * dt, dt4 = 0.25 * dt;
+  const int Ilo = max(1, io), Ihi = min(N - 1, io + nx), Jlo = max(1, jo), Jhi = min(N - 1, jo + ny);
+  const bool inner = I >= Ilo && I <= Ihi && J >= Jlo && J <= Jhi;
+  const bool xe = !(I - 1 >= 2 && I + 1 <= N - 2), ye = !(J - 1 >= 2 && J + 1 <= N - 2);
+  const bool xl = I == 0 || I == N, yl = J == 0 || J == N;
+  const double *U = u + zo + o, *V = v + zo + o, *UC = uc + zo + o, *VC = vc + zo + o;
+  // ---- every interior input, issued together
+  const double vcm = VC[-1], vc0 = VC[0], ucm = UC[-p], uc0 = UC[0];
+  const double cosa = MT(M_COSA)[o], rsina = MT(M_RSINA)[o];
+  double qv[6], qu[6];
+#pragma unroll
+  for (int m = 0; m < 6; ++m) {
+    qv[m] = V[(long)(m - 3) * p];
+    qu[m] = U[m - 3];
+  }
+  const double* rdy = MT(M_RDY) + o;
+  const double* rdx = MT(M_RDX) + o;
+  const double rdym = rdy[-p], rdy0 = rdy[0], rdxm = rdx[-1], rdx0 = rdx[0];
+  double dycm = 0, dyc0 = 0, vamm = 0, vam0 = 0, va0m = 0, va00 = 0, cvm = 0, cv0 = 0, svm = 0, sv0 = 0;
+  double dxcm = 0, dxc0 = 0, uamm = 0, ua0m = 0, uam0 = 0, ua00 = 0, cum = 0, cu0 = 0, sum_ = 0, su0 = 0, rac = 0;
+  if (DAMP) {
+    const double* dyc = MT(M_DYC) + o;
+    const double* dxc = MT(M_DXC) + o;
+    const double* cav = MT(M_COSA_V) + o;
+    const double* sav = MT(M_SINA_V) + o;
+    const double* cau = MT(M_COSA_U) + o;
+    const double* sau = MT(M_SINA_U) + o;
+    const double *VA = va + zo + o, *UA = ua + zo + o;
+    dycm = dyc[-1]; dyc0 = dyc[0];
+    vamm = VA[-1 - p]; vam0 = VA[-1]; va0m = VA[-p]; va00 = VA[0];
+    cvm = cav[-1]; cv0 = cav[0]; svm = sav[-1]; sv0 = sav[0];
+    dxcm = dxc[-p]; dxc0 = dxc[0];
+    uamm = UA[-1 - p]; ua0m = UA[-p]; uam0 = UA[-1]; ua00 = UA[0];
+    cum = cau[-p]; cu0 = cau[0]; sum_ = sau[-p]; su0 = sau[0];
+    rac = MT(M_RAREA_C)[o];
+  }
+  // ---- tile-edge inputs (waves with an edge point only)
+  double vts[4] = {0, 0, 0, 0}, uts[4] = {0, 0, 0, 0}, spy[6] = {0, 0, 0, 0, 0, 0}, spx[6] = {0, 0, 0, 0, 0, 0};
+  double s4m = 0, s40 = 0, s2m = 0, s20 = 0, s3m = 0, s30 = 0, s1m = 0, s10 = 0;
+  if (xe || ye) {
+    const double *VT = vt + zo + o, *UT = ut + zo + o;
+#pragma unroll
+    for (int m = 0; m < 4; ++m) {
+      vts[m] = VT[m - 2];
+      uts[m] = UT[(long)(m - 2) * p];
+    }
+    const double* dy = MT(M_DY) + o;
+    const double* dxm = MT(M_DX) + o;
+#pragma unroll
+    for (int m = 0; m < 6; ++m) {
+      spy[m] = ye ? dy[(long)(m - 3) * p] : 0.0;
+      spx[m] = xe ? dxm[m - 3] : 0.0;
+    }
+    if (DAMP) {
+      const double* s4 = MT(M_SIN4) + o;
+      const double* s2 = MT(M_SIN2) + o;
+      const double* s3 = MT(M_SIN3) + o;
+      const double* s1 = MT(M_SIN1) + o;
+      s4m = s4[-1 - p]; s40 = s4[-p]; s2m = s2[-1]; s20 = s2[0];
+      s3m = s3[-1 - p]; s30 = s3[-1]; s1m = s1[-p]; s10 = s1[0];
+    }
+  }
+  // ---- ds_ke's expressions
+  double vb = 0.0, ub = 0.0;
+  if (inner) vb = dt5 * (vcm + vc0 - (ucm + uc0) * cosa) * rsina;
+  if (xl) vb = dt4 * (-vts[0] + 3.0 * (vts[1] + vts[2]) - vts[3]);
+  else if (yl && I >= Ilo && I <= Ihi) vb = dt5 * (vts[1] + vts[2]);
+  if (inner) ub = dt5 * (ucm + uc0 - (vcm + vc0) * cosa) * rsina;
+  if (yl) ub = dt4 * (-uts[0] + 3.0 * (uts[1] + uts[2]) - uts[3]);
+  else if (xl && J >= Jlo && J <= Jhi) ub = dt5 * (uts[1] + uts[2]);
+  double cfl = vb > 0.0 ? vb * rdym : vb * rdy0;
+  const double ubf = ye ? ppm_flux<ORD>(J, N, qv, spy, cfl) : ppm_flux<ORD, false>(J, N, qv, spy, cfl);
+  double kk = vb * ubf;
+  cfl = ub > 0.0 ? ub * rdxm : ub * rdx0;
+  const double vbf = xe ? ppm_flux<ORD>(I, N, qu, spx, cfl) : ppm_flux<ORD, false>(I, N, qu, spx, cfl);
+  kk = 0.5 * (kk + ub * vbf);
+  // cube corners: u(0,0) = qu[3], u(-1,0) = qu[2], v(0,0) = qv[3], v(0,-1) = qv[2]
+  const double dt6 = dt / 6.0;
+  if (I == 0 && J == 0)
+    kk = dt6 * ((uts[2] + uts[1]) * qu[3] + (vts[2] + vts[1]) * qv[3] + (uts[2] + vts[2]) * qu[2]);
+  else if (I == N && J == 0)
+    kk = dt6 * ((uts[2] + uts[1]) * qu[2] + (vts[2] + vts[1]) * qv[3] + (uts[2] - vts[1]) * qu[3]);
+  else if (I == N && J == N)
+    kk = dt6 * ((uts[2] + uts[1]) * qu[2] + (vts[2] + vts[1]) * qv[2] + (uts[1] + vts[1]) * qu[3]);
+  else if (I == 0 && J == N)
+    kk = dt6 * ((uts[2] + uts[1]) * qu[3] + (vts[2] + vts[1]) * qv[2] + (uts[1] - vts[2]) * qu[2]);
+  if (!DAMP) {
+    AT(ke, 0, 0) = kk;
+    return;
+  }
+  // divergence damping (nord = 0), ds_ke's ptc_at / vrt_at
+  double ptm, pt0;
+  if (yl) {
+    ptm = vcm > 0.0 ? qu[2] * dycm * s4m : qu[2] * dycm * s2m;
+    pt0 = vc0 > 0.0 ? qu[3] * dyc0 * s40 : qu[3] * dyc0 * s20;
+  } else {
+    ptm = (qu[2] - 0.5 * (vamm + vam0) * cvm) * dycm * svm;
+    pt0 = (qu[3] - 0.5 * (va0m + va00) * cv0) * dyc0 * sv0;
+  }
+  double vS = 0.0, v0 = 0.0;
+  if (xl) {
+    vS = ucm > 0.0 ? qv[2] * dxcm * s3m : qv[2] * dxcm * s1m;
+    v0 = uc0 > 0.0 ? qv[3] * dxc0 * s30 : qv[3] * dxc0 * s10;
+  } else if (I >= Ilo && I <= Ihi) {
+    vS = (qv[2] - 0.5 * (uamm + ua0m) * cum) * dxcm * sum_;
+    v0 = (qv[3] - 0.5 * (uam0 + ua00) * cu0) * dxc0 * su0;
+  }
+  double dpc = vS - v0 + ptm - pt0;
+  if ((I == 0 && J == 0) || (I == N && J == 0)) dpc = dpc - vS;
+  if ((I == N && J == N) || (I == 0 && J == N)) dpc = dpc + v0;
+  dpc = rac * dpc;
+  double damp = da_min_c * fmax(d2_bg, fmin(0.20, dddmp * fabs(dpc * dt)));
+  AT(ke, 0, 0) = kk + damp * dpc;
+  if (vd) AT(vd, 0, 0) = damp * dpc;
+}
+
 // relative vorticity (cell mean) + Coriolis -> the field transported by fv_tp_2d
 __global__ void __launch_bounds__(256) ds_vort(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
                                                int npz, const double* __restrict__ u, const double* __restrict__ v,
@@ -804,9 +941,25 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
   // kinetic energy (+ divergence damping) at corners
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
   const bool dcon = a.d_con > 1e-5, vdamp = a.vtdm4 > 1e-5;
-  GT_LAUNCH(ds_ke, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.hord_mt, a.dddmp,
-                     a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke, a.nord,
-                     dcon ? a.vd : nullptr);
+  // GTFV3_KE_LD=0: the branch-ordered form (same results, bit for bit)
+  const char* kev = std::getenv("GTFV3_KE_LD");
+  if (kev && kev[0] == '0') {
+    GT_LAUNCH(ds_ke, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.hord_mt, a.dddmp,
+                       a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke, a.nord,
+                       dcon ? a.vd : nullptr);
+  } else {
+    const bool damp = a.nord == 0;
+    double* vdp = dcon ? a.vd : nullptr;
+#define KE_LD(O, D)                                                                                          \
+  GT_LAUNCH_N("ds_ke", (ds_ke_ld<O, D>), g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, \
+              a.dddmp, a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke, vdp)
+    if (a.hord_mt == 5) {
+      if (damp) KE_LD(5, true); else KE_LD(5, false);
+    } else {
+      if (damp) KE_LD(6, true); else KE_LD(6, false);
+    }
+#undef KE_LD
+  }
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   const double L = a.npz;

@@ -237,19 +237,21 @@ def test_acoustic_graph_bitwise(pkg, require_gpu, monkeypatch, proxy):
         assert np.array_equal(out["0"][k], out["1"][k], equal_nan=bool(proxy)), f"{k}: graph replay differs"
 
 
+@pytest.mark.parametrize("env", ["GTFV3_UV_FUSED", "GTFV3_KE_LD"])
 @pytest.mark.parametrize("npx,lay", [(25, 2), (49, 1)])
-def test_uv_fused_bitwise(pkg, require_gpu, monkeypatch, npx, lay):
-    """d_sw's final wind update (ds_uv) inside the vorticity march (tp.hip TM = 3: u and v
-    formed from the fluxes in registers) against the march writing the flux planes and
-    ds_uv reading them (GTFV3_UV_FUSED=0): two L20 steps, bit for bit on every state field,
-    at C24 with 2x2 sub-domains per tile (short strips: the general row steps) and at C48
-    with whole tiles (the steady row steps)."""
+def test_uv_fused_bitwise(pkg, require_gpu, monkeypatch, npx, lay, env):
+    """Two forms of d_sw's wind stage, bit for bit over two L20 steps on every state field,
+    at C24 with 2x2 sub-domains per tile (short strips, many tile-edge points) and at C48 with
+    whole tiles: GTFV3_UV_FUSED -- the final wind update (ds_uv) inside the vorticity march
+    (tp.hip TM = 3, u and v from the fluxes in registers) against the march writing flux
+    planes and ds_uv reading them; GTFV3_KE_LD -- ds_ke with every load issued before its
+    arithmetic (ds_ke_ld) against the branch-ordered ds_ke."""
     state = importlib.import_module(pkg.__name__ + ".state")
     npz = 20
     ak, bk, ks = state.hybrid_levels(npz)
     out = {}
     for mode in ("0", "1"):
-        monkeypatch.setenv("GTFV3_UV_FUSED", mode)
+        monkeypatch.setenv(env, mode)
         d = pkg.Domain(npx=npx, npz=npz, nq=2, layout_x=lay, layout_y=lay)
         st = state.jablonowski_williamson(d, ak, bk)
         d.set_vertical(ak, bk, ks)
@@ -261,4 +263,4 @@ def test_uv_fused_bitwise(pkg, require_gpu, monkeypatch, npx, lay):
         d.close()
     for k in out["0"]:
         assert np.isfinite(out["1"][k]).all(), f"{k}: non-finite"
-        assert np.array_equal(out["0"][k], out["1"][k]), f"{k}: fused wind update differs"
+        assert np.array_equal(out["0"][k], out["1"][k]), f"{k}: {env}=1 differs from {env}=0"
