@@ -240,6 +240,85 @@ __global__ void __launch_bounds__(256) cs_transport_ke(
   AT(ke, 0, 0) = dt4 * (AT(ua, 0, 0) * kk + AT(va, 0, 0) * vv);
 }
 
+// ---- loads-first forms (GTFV3_LOADS_FIRST, default on): the same expressions in the same
+// order as the kernel each replaces (bit-identical), with every input a point needs loaded
+// before any arithmetic -- addresses of the points outside the kernel's ranges clamped to an
+// interior point, tile-edge inputs loaded only by the waves holding tile-edge lines -- so a
+// wave keeps its loads in flight together instead of waiting out a chain of dependent round
+// trips through the branches (11-15 vmcnt(0) waits per wave in the branch-ordered
+// forms, rocprof SQ counters 63-65 % of wave cycles waiting).  The same form of cs_cgrid and
+// ds_courant measured slower (1.84 -> 1.87 and 1.33 -> 1.47 ms per step): loading both
+// upwind choices of their metric terms costs more than the round trips it saves.
+bool loads_first() {
+  const char* e = std::getenv("GTFV3_LOADS_FIRST");
+  return !(e && e[0] == '0');
+}
+
+// cs_transport_ke (above), loads first: the Courant numbers, the cell's own values and the
+// kinetic-energy inputs in one group, then the four upwind sources the signs select
+__global__ void __launch_bounds__(256) cs_transport_ke_ld(
+    Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M, int npz, double dt2,
+    const double* __restrict__ delp, const double* __restrict__ pt, const double* __restrict__ w,
+    const double* __restrict__ u, const double* __restrict__ v, const double* __restrict__ uc,
+    const double* __restrict__ vc, const double* __restrict__ ua, const double* __restrict__ va,
+    const double* __restrict__ ut, const double* __restrict__ vt, double* __restrict__ delpc,
+    double* __restrict__ ptc, double* __restrict__ wc, double* __restrict__ ke) {
+  Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
+  KSETUP(npz)
+  const long p = d.pitch;
+  const double* dp = delp + zo;
+  const double* pp = pt + zo;
+  const double* ww = w + zo;
+  const double c0 = ut[zo + o], c1 = ut[zo + o + 1], e0 = vt[zo + o], e1 = vt[zo + o + p];
+  const double uav = ua[zo + o], vav = va[zo + o];
+  const double uc0 = uc[zo + o], uc1 = uc[zo + o + 1], vc0 = vc[zo + o], vc1 = vc[zo + o + p];
+  const long oc = cc_off(d, sub, i, j, 2);
+  const double dpo = dp[oc], ppo = pp[oc], wwo = ww[oc];
+  const double ra = MA(MT(M_RAREA), 0, 0);
+  const bool xe = I == 0 || I == N || I == -1 || I == N - 1, ye = J == 0 || J == N || J == -1 || J == N - 1;
+  double v00 = 0, v10 = 0, s1 = 0, k1 = 0, s3 = 0, k3 = 0, u00 = 0, u01 = 0, s2 = 0, k2 = 0, s4 = 0, k4 = 0;
+  if (xe) {
+    v00 = v[zo + o]; v10 = v[zo + o + 1];
+    s1 = MT(M_SIN1)[o]; k1 = MT(M_COS1)[o]; s3 = MT(M_SIN3)[o]; k3 = MT(M_COS3)[o];
+  }
+  if (ye) {
+    u00 = u[zo + o]; u01 = u[zo + o + p];
+    s2 = MT(M_SIN2)[o]; k2 = MT(M_COS2)[o]; s4 = MT(M_SIN4)[o]; k4 = MT(M_COS4)[o];
+  }
+  const long sx0 = c0 > 0.0 ? cc_off(d, sub, i - 1, j, 1) : cc_off(d, sub, i, j, 1);
+  const long sx1 = c1 > 0.0 ? cc_off(d, sub, i, j, 1) : cc_off(d, sub, i + 1, j, 1);
+  const long sy0 = e0 > 0.0 ? cc_off(d, sub, i, j - 1, 2) : cc_off(d, sub, i, j, 2);
+  const long sy1 = e1 > 0.0 ? cc_off(d, sub, i, j, 2) : cc_off(d, sub, i, j + 1, 2);
+  const double dx0 = dp[sx0], px0 = pp[sx0], wx0 = ww[sx0], dx1 = dp[sx1], px1 = pp[sx1], wx1 = ww[sx1];
+  const double dy0 = dp[sy0], py0 = pp[sy0], wy0 = ww[sy0], dy1 = dp[sy1], py1 = pp[sy1], wy1 = ww[sy1];
+  double fx1[2], fx[2], fx2[2], fy1[2], fy[2], fy2[2];
+  fx1[0] = c0 * dx0; fx[0] = fx1[0] * px0; fx2[0] = fx1[0] * wx0;
+  fy1[0] = e0 * dy0; fy[0] = fy1[0] * py0; fy2[0] = fy1[0] * wy0;
+  fx1[1] = c1 * dx1; fx[1] = fx1[1] * px1; fx2[1] = fx1[1] * wx1;
+  fy1[1] = e1 * dy1; fy[1] = fy1[1] * py1; fy2[1] = fy1[1] * wy1;
+  const double dpc = dpo + (fx1[0] - fx1[1] + fy1[0] - fy1[1]) * ra;
+  AT(delpc, 0, 0) = dpc;
+  AT(ptc, 0, 0) = (ppo * dpo + (fx[0] - fx[1] + fy[0] - fy[1]) * ra) / dpc;
+  AT(wc, 0, 0) = (wwo * dpo + (fx2[0] - fx2[1] + fy2[0] - fy2[1]) * ra) / dpc;
+  double kk, vv;
+  if (uav > 0.0) {
+    if (I == 0 || I == N) kk = uc0 * s1 + v00 * k1;
+    else kk = uc0;
+  } else {
+    if (I == -1 || I == N - 1) kk = uc1 * s3 + v10 * k3;
+    else kk = uc1;
+  }
+  if (vav > 0.0) {
+    if (J == 0 || J == N) vv = vc0 * s2 + u00 * k2;
+    else vv = vc0;
+  } else {
+    if (J == -1 || J == N - 1) vv = vc1 * s4 + u01 * k4;
+    else vv = vc1;
+  }
+  const double dt4 = 0.5 * dt2;
+  AT(ke, 0, 0) = dt4 * (uav * kk + vav * vv);
+}
+
 // c_sw: absolute vorticity at cell corners from the C-grid circulation
 __global__ void __launch_bounds__(256) cs_vort(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
                                                int npz, const double* __restrict__ uc, const double* __restrict__ vc,
@@ -277,6 +356,34 @@ __global__ void __launch_bounds__(256) cs_update(Dims d, const SubInfo* __restri
                                     : dt2 * (AT(u, 0, 0) - AT(vc, 0, 0) * MA(MT(M_COSA_V), 0, 0)) / MA(MT(M_SINA_V), 0, 0);
     double fx = fx1 > 0.0 ? AT(vort, 0, 0) : AT(vort, 1, 0);
     AT(vc, 0, 0) = AT(vc, 0, 0) - fx1 * fx + MA(MT(M_RDYC), 0, 0) * (AT(ke, 0, -1) - AT(ke, 0, 0));
+  }
+}
+
+// cs_update (above), loads first: both upwind vorticity values are loaded (the neighbour's
+// are the same cache lines) and selected afterwards
+__global__ void __launch_bounds__(256) cs_update_ld(Dims d, const SubInfo* __restrict__ subs,
+                                                    const double* __restrict__ M, int npz, double dt2,
+                                                    const double* __restrict__ u, const double* __restrict__ v,
+                                                    const double* __restrict__ vort, const double* __restrict__ ke,
+                                                    double* __restrict__ uc, double* __restrict__ vc) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  KSETUP(npz)
+  const long p = d.pitch;
+  const double v0 = AT(v, 0, 0), u0 = AT(u, 0, 0), uc0 = AT(uc, 0, 0), vc0 = AT(vc, 0, 0);
+  const double w00 = AT(vort, 0, 0), w01 = AT(vort, 0, 1), w10 = AT(vort, 1, 0);
+  const double k00 = AT(ke, 0, 0), km0 = AT(ke, -1, 0), k0m = AT(ke, 0, -1);
+  const double cau = MT(M_COSA_U)[o], sau = MT(M_SINA_U)[o], rdxc = MT(M_RDXC)[o];
+  const double cav = MT(M_COSA_V)[o], sav = MT(M_SINA_V)[o], rdyc = MT(M_RDYC)[o];
+  (void)p;
+  if (j < d.ny) {
+    double fy1 = (I == 0 || I == N) ? dt2 * v0 : dt2 * (v0 - uc0 * cau) / sau;
+    double fy = fy1 > 0.0 ? w00 : w01;
+    AT(uc, 0, 0) = uc0 + fy1 * fy + rdxc * (km0 - k00);
+  }
+  if (i < d.nx) {
+    double fx1 = (J == 0 || J == N) ? dt2 * u0 : dt2 * (u0 - vc0 * cav) / sav;
+    double fx = fx1 > 0.0 ? w00 : w10;
+    AT(vc, 0, 0) = vc0 - fx1 * fx + rdyc * (k0m - k00);
   }
 }
 
@@ -819,8 +926,12 @@ void c_sw_transport(const Ctx& c, const CswArgs& a) {
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (3 * e.X + 3 * e.Y + 4 * e.C) + 12 * e.C);
   Launch2D Lt{-1, -1, d.nx + 2, d.ny + 2};
-  GT_LAUNCH(cs_transport_ke, g2(d, Lt, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.delp,
-                     a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke);
+  if (loads_first())
+    GT_LAUNCH_N("cs_transport_ke", cs_transport_ke_ld, g2(d, Lt, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
+                a.npz, a.dt2, a.delp, a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke);
+  else
+    GT_LAUNCH(cs_transport_ke, g2(d, Lt, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.delp,
+                       a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke);
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (9 * e.C + 3 * e.X + 3 * e.Y) + 9 * e.C);
 }
@@ -836,8 +947,12 @@ void c_sw_winds(const Ctx& c, const CswArgs& a) {
   GT_LAUNCH(cs_vort, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.vort);
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (e.X + e.Y + e.K) + 4 * e.C);
-  GT_LAUNCH(cs_update, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
-                     a.vort, a.ke, a.uc, a.vc);
+  if (loads_first())
+    GT_LAUNCH_N("cs_update", cs_update_ld, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2,
+                a.u, a.v, a.vort, a.ke, a.uc, a.vc);
+  else
+    GT_LAUNCH(cs_update, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
+                       a.vort, a.ke, a.uc, a.vc);
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (e.C + e.K + 3 * e.X + 3 * e.Y) + 6 * e.C);
 }
@@ -941,9 +1056,8 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
   // kinetic energy (+ divergence damping) at corners
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
   const bool dcon = a.d_con > 1e-5, vdamp = a.vtdm4 > 1e-5;
-  // GTFV3_KE_LD=0: the branch-ordered form (same results, bit for bit)
-  const char* kev = std::getenv("GTFV3_KE_LD");
-  if (kev && kev[0] == '0') {
+  // GTFV3_LOADS_FIRST=0: the branch-ordered form (same results, bit for bit)
+  if (!loads_first()) {
     GT_LAUNCH(ds_ke, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.hord_mt, a.dddmp,
                        a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke, a.nord,
                        dcon ? a.vd : nullptr);

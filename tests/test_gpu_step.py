@@ -237,15 +237,16 @@ def test_acoustic_graph_bitwise(pkg, require_gpu, monkeypatch, proxy):
         assert np.array_equal(out["0"][k], out["1"][k], equal_nan=bool(proxy)), f"{k}: graph replay differs"
 
 
-@pytest.mark.parametrize("env", ["GTFV3_UV_FUSED", "GTFV3_KE_LD"])
+@pytest.mark.parametrize("env", ["GTFV3_UV_FUSED", "GTFV3_LOADS_FIRST"])
 @pytest.mark.parametrize("npx,lay", [(25, 2), (49, 1)])
 def test_uv_fused_bitwise(pkg, require_gpu, monkeypatch, npx, lay, env):
     """Two forms of d_sw's wind stage, bit for bit over two L20 steps on every state field,
     at C24 with 2x2 sub-domains per tile (short strips, many tile-edge points) and at C48 with
     whole tiles: GTFV3_UV_FUSED -- the final wind update (ds_uv) inside the vorticity march
     (tp.hip TM = 3, u and v from the fluxes in registers) against the march writing flux
-    planes and ds_uv reading them; GTFV3_KE_LD -- ds_ke with every load issued before its
-    arithmetic (ds_ke_ld) against the branch-ordered ds_ke."""
+    planes and ds_uv reading them; GTFV3_LOADS_FIRST -- c_sw's cs_transport_ke / cs_update and
+    d_sw's ds_ke with every load issued before their arithmetic (the *_ld
+    kernels) against the branch-ordered kernels."""
     state = importlib.import_module(pkg.__name__ + ".state")
     npz = 20
     ak, bk, ks = state.hybrid_levels(npz)
