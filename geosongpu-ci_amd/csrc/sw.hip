@@ -319,6 +319,54 @@ __global__ void __launch_bounds__(256) cs_transport_ke_ld(
   AT(ke, 0, 0) = dt4 * (uav * kk + vav * vv);
 }
 
+// cs_tmp (above), loads first: the four u rows and four v columns of the 4th-order forms
+// (the outer two at offset 0 where the point takes no 4th-order value) and the two metric
+// terms in one group; the 4th-order / tile-edge / BIG choice made afterwards
+__global__ void __launch_bounds__(256) cs_tmp_ld(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                                 int npz, const double* __restrict__ u, const double* __restrict__ v,
+                                                 double* __restrict__ utmp, double* __restrict__ vtmp,
+                                                 double* __restrict__ ua, double* __restrict__ va) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  KSETUP(npz)
+  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+  const long p = d.pitch;
+  const bool inr = i <= nx + NG - 1 && j <= ny + NG - 1;
+  const bool rows = inr && J >= max(3, jo - 1) && J <= min(N - 4, jo + ny);
+  const bool cols = inr && I >= max(3, io - 1) && I <= min(N - 4, io + nx);
+  const double* U = u + zo + o;
+  const double* V = v + zo + o;
+  const long u1o = inr ? p : 0, umo = rows ? -p : 0, u2o = rows ? 2 * p : 0;
+  const long v1o = inr ? 1 : 0, vmo = cols ? -1 : 0, v2o = cols ? 2 : 0;
+  const double u0 = U[0], u1 = U[u1o], um = U[umo], u2 = U[u2o];
+  const double v0 = V[0], v1 = V[v1o], vm = V[vmo], v2 = V[v2o];
+  const double cs = MA(MT(M_COSA_S), 0, 0), r2 = MA(MT(M_RSIN2), 0, 0);
+  double ut = BIG, vt = BIG;
+  if (inr) {
+    if (rows) ut = A2 * (um + u2) + A1 * (u0 + u1);
+    if (cols) vt = A2 * (vm + v2) + A1 * (v0 + v1);
+    const int jsd = jo - NG, jed = jo + ny + NG - 1, isd = io - NG, ied = io + nx + NG - 1;
+    const bool mid = J >= max(3, jsd) && J <= min(N - 4, jed);
+    bool two = false;
+    if (J >= jsd && J <= 2) two = true;
+    if (J >= N - 3 && J <= jed) two = true;
+    if (mid && I >= isd && I <= 2) two = true;
+    if (mid && I >= N - 3 && I <= ied) two = true;
+    if (two) {
+      ut = 0.5 * (u0 + u1);
+      vt = 0.5 * (v0 + v1);
+    }
+  }
+  AT(utmp, 0, 0) = ut;
+  AT(vtmp, 0, 0) = vt;
+  double a = 0.0, b = 0.0;
+  if (i >= -2 && i <= nx + 1 && j >= -2 && j <= ny + 1) {
+    a = (ut - vt * cs) * r2;
+    b = (vt - ut * cs) * r2;
+  }
+  AT(ua, 0, 0) = a;
+  AT(va, 0, 0) = b;
+}
+
 // c_sw: absolute vorticity at cell corners from the C-grid circulation
 __global__ void __launch_bounds__(256) cs_vort(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
                                                int npz, const double* __restrict__ uc, const double* __restrict__ vc,
@@ -913,8 +961,12 @@ void c_sw_transport(const Ctx& c, const CswArgs& a) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  GT_LAUNCH(cs_tmp, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.utmp,
-                     a.vtmp, a.ua, a.va);
+  if (loads_first())
+    GT_LAUNCH_N("cs_tmp", cs_tmp_ld, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v,
+                a.utmp, a.vtmp, a.ua, a.va);
+  else
+    GT_LAUNCH(cs_tmp, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.utmp,
+                       a.vtmp, a.ua, a.va);
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   const double L = a.npz;

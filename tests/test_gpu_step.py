@@ -244,7 +244,7 @@ def test_uv_fused_bitwise(pkg, require_gpu, monkeypatch, npx, lay, env):
     at C24 with 2x2 sub-domains per tile (short strips, many tile-edge points) and at C48 with
     whole tiles: GTFV3_UV_FUSED -- the final wind update (ds_uv) inside the vorticity march
     (tp.hip TM = 3, u and v from the fluxes in registers) against the march writing flux
-    planes and ds_uv reading them; GTFV3_LOADS_FIRST -- c_sw's cs_transport_ke / cs_update and
+    planes and ds_uv reading them; GTFV3_LOADS_FIRST -- c_sw's cs_tmp / cs_transport_ke / cs_update and
     d_sw's ds_ke with every load issued before their arithmetic (the *_ld
     kernels) against the branch-ordered kernels."""
     state = importlib.import_module(pkg.__name__ + ".state")
