@@ -596,6 +596,7 @@ __global__ void __launch_bounds__(256) ds_courant(Dims d, const SubInfo* __restr
 // the point are loaded once for its block of levels (which of them a point needs is fixed by
 // its position), then the same expressions per level as above.  (The same form of
 // ds_courant and ds_ke measured slower: 1.56 -> 1.68 and 2.65 -> 3.37 ms per step)
+template <bool LF>
 __global__ void __launch_bounds__(256) ds_utvt1_kl(Dims d, const SubInfo* __restrict__ subs,
                                                    const double* __restrict__ M, int npz, int nkb, int klb,
                                                    double dt, const double* __restrict__ uc,
@@ -622,6 +623,27 @@ __global__ void __launch_bounds__(256) ds_utvt1_kl(Dims d, const SubInfo* __rest
     } else if (j >= -1 && j <= ny + 1) {
       my = 2; ay = met(M, d, M_COSA_V, s)[o]; by = met(M, d, M_RSIN_V, s)[o];
     }
+  }
+  if (LF) {
+    // loads first (GTFV3_LOADS_FIRST): the point's uc / vc and the four neighbours of each
+    // generic form in one group per level (offset 0 where the form is not taken), then the
+    // same expressions as below
+    const long xw = mx == 2 ? -1 : 0, xn = mx == 2 ? pt : 0;
+    const long ys = my == 2 ? -pt : 0, ye = my == 2 ? 1 : 0;
+    for (int k = k0; k < k1; ++k) {
+      const long lk = ((long)s * npz + k) * P + o;
+      const double u0 = uc[lk], v0 = vc[lk];
+      const double vw = vc[lk + xw], vwn = vc[lk + xw + xn], vn = vc[lk + xn];
+      const double us = uc[lk + ys], use = uc[lk + ye + ys], ue = uc[lk + ye];
+      double a = 0.0, b = 0.0;
+      if (mx == 1) a = u0 * dt > 0.0 ? u0 / ax : u0 / bx;
+      else if (mx == 2) a = (u0 - 0.25 * ax * (vw + v0 + vwn + vn)) * bx;
+      if (my == 1) b = v0 * dt > 0.0 ? v0 / ay : v0 / by;
+      else if (my == 2) b = (v0 - 0.25 * ay * (us + use + u0 + ue)) * by;
+      ut[lk] = a;
+      vt[lk] = b;
+    }
+    return;
   }
   for (int k = k0; k < k1; ++k) {
     const long lk = ((long)s * npz + k) * P + o;
@@ -1029,10 +1051,14 @@ void d_sw_courant(const Ctx& c, const DswArgs& a) {
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   const int klb = kloop_levels(), nkb = klb ? (a.npz + klb - 1) / klb : 0;
-  if (klb)
-    GT_LAUNCH(ds_utvt1_kl, kloop_grid(full, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, nkb, klb,
-                         a.dt, a.uc, a.vc, a.ut, a.vt);
-  else
+  if (klb) {
+    if (loads_first())
+      GT_LAUNCH_N("ds_utvt1_kl", ds_utvt1_kl<true>, kloop_grid(full, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs,
+                  c.met, a.npz, nkb, klb, a.dt, a.uc, a.vc, a.ut, a.vt);
+    else
+      GT_LAUNCH_N("ds_utvt1_kl", ds_utvt1_kl<false>, kloop_grid(full, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs,
+                  c.met, a.npz, nkb, klb, a.dt, a.uc, a.vc, a.ut, a.vt);
+  } else
     GT_LAUNCH(ds_utvt1, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.uc, a.vc,
                        a.ut, a.vt);
   HIP_LAUNCH_CHECK();
