@@ -4,6 +4,7 @@
 // Column kernels put one (i,j) column per lane: a wavefront covers 64 consecutive
 // i, so every k-plane access is coalesced; per-column work arrays are planes of
 // scratch fields (same [sub][k][plane] layout).
+#include <cstdlib>
 #include <algorithm>
 #include <climits>
 
@@ -836,6 +837,10 @@ __global__ void __launch_bounds__(256) nhpgrad_k(Dims d, const SubInfo* __restri
 // order as udzc_k / pgradc_k / nhpgrad_k above, so the outputs are bit-identical.  The
 // thread of point (i, j) walks levels k0 .. k1-1 of one sub-domain; the interface values a
 // level shares with the next and the metric terms stay in registers.
+// LF (GTFV3_LOADS_FIRST, default on): the six gz points both upwind picks choose among are
+// loaded with the level's ut / vt, before the fluxes whose signs select them (the same
+// values and expressions: bit-identical); otherwise each pick's load waits for its flux
+template <bool LF>
 __global__ void __launch_bounds__(256) udzc_kl(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
                                                int npz, int nkb, int klb, const double* __restrict__ dp0,
                                                const double* __restrict__ ut, const double* __restrict__ vt,
@@ -856,6 +861,11 @@ __global__ void __launch_bounds__(256) udzc_kl(Dims d, const SubInfo* __restrict
   bool have = false;
   for (int k = k0; k < k1; ++k) {
     double xf0, xf1, yf0, yf1;
+    const double* g = gz + ((long)s * (npz + 1) + k) * P;
+    double gW = 0.0, gCX = 0.0, gE = 0.0, gS = 0.0, gCY = 0.0, gN = 0.0;
+    if (LF) {
+      gW = g[gw]; gCX = g[gcx]; gE = g[ge]; gS = g[gs]; gCY = g[gcy]; gN = g[gn];
+    }
     if (k == 0) {
       const double top_ratio = dp0[0] / (dp0[1] + dp0[0]);
       const double a0 = UT[0], a1 = UT[1], b0 = VT[0], b1 = VT[N1];
@@ -888,16 +898,20 @@ __global__ void __launch_bounds__(256) udzc_kl(Dims d, const SubInfo* __restrict
       p0 = a0; p1 = a1; p2 = b0; p3 = b1;
       have = true;
     }
-    const double* g = gz + ((long)s * (npz + 1) + k) * P;
-    const double fx0 = xf0 * (xf0 > 0.0 ? g[gw] : g[gcx]);
-    const double fx1 = xf1 * (xf1 > 0.0 ? g[gcx] : g[ge]);
-    const double fy0 = yf0 * (yf0 > 0.0 ? g[gs] : g[gcy]);
-    const double fy1 = yf1 * (yf1 > 0.0 ? g[gcy] : g[gn]);
-    const double gc = g[gcy];
+    if (!LF) {
+      gW = xf0 > 0.0 ? g[gw] : 0.0; gCX = g[gcx]; gE = xf1 > 0.0 ? 0.0 : g[ge];
+      gS = yf0 > 0.0 ? g[gs] : 0.0; gCY = g[gcy]; gN = yf1 > 0.0 ? 0.0 : g[gn];
+    }
+    const double fx0 = xf0 * (xf0 > 0.0 ? gW : gCX);
+    const double fx1 = xf1 * (xf1 > 0.0 ? gCX : gE);
+    const double fy0 = yf0 * (yf0 > 0.0 ? gS : gCY);
+    const double fy1 = yf1 * (yf1 > 0.0 ? gCY : gN);
+    const double gc = gCY;
     gzo[((long)s * (npz + 1) + k) * P + o] = (gc * area + fx0 - fx1 + fy0 - fy1) / (area + xf0 - xf1 + yf0 - yf1);
   }
 }
 
+template <bool LF>
 __global__ void __launch_bounds__(256) pgradc_kl(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
                                                  int npz, int nkb, int klb, double dt2, const double* __restrict__ delpc,
                                                  const double* __restrict__ pkc, const double* __restrict__ gz,
@@ -915,6 +929,28 @@ __global__ void __launch_bounds__(256) pgradc_kl(Dims d, const SubInfo* __restri
   double pk0 = PK[l0], gz0 = GZ[l0];
   double pk0w = du ? PK[l0 + W] : 0.0, gz0w = du ? GZ[l0 + W] : 0.0;
   double pk0s = dv ? PK[l0 + S] : 0.0, gz0s = dv ? GZ[l0 + S] : 0.0;
+  if (LF) {
+    // loads first (GTFV3_LOADS_FIRST): both directions' inputs of a level in one group (the
+    // west / south offsets 0 on the row / column that takes no update), then the same
+    // expressions as below
+    const long Wd = du ? W : 0, Sd = dv ? S : 0;
+    for (int k = k0; k < k1; ++k) {
+      const long l1 = (long)(k + 1) * P, lk = ((long)s * npz + k) * P + o;
+      const double pk1 = PK[l1], gz1 = GZ[l1];
+      const double pk1w = PK[l1 + Wd], gz1w = GZ[l1 + Wd], pk1s = PK[l1 + Sd], gz1s = GZ[l1 + Sd];
+      const double dcw = delpc[lk + Wd], dc = delpc[lk], dcs = delpc[lk + Sd], u0 = uc[lk], v0 = vc[lk];
+      if (du) {
+        const double wsum = dcw + dc;
+        uc[lk] = u0 + dt2 * rdxc / wsum * ((gz1w - gz0) * (pk1 - pk0w) + (gz0w - gz1) * (pk1w - pk0));
+      }
+      if (dv) {
+        const double wsum = dcs + dc;
+        vc[lk] = v0 + dt2 * rdyc / wsum * ((gz1s - gz0) * (pk1 - pk0s) + (gz0s - gz1) * (pk1s - pk0));
+      }
+      pk0 = pk1; gz0 = gz1; pk0w = pk1w; gz0w = gz1w; pk0s = pk1s; gz0s = gz1s;
+    }
+    return;
+  }
   for (int k = k0; k < k1; ++k) {
     const long l1 = (long)(k + 1) * P, lk = ((long)s * npz + k) * P + o;
     const double pk1 = PK[l1], gz1 = GZ[l1];
@@ -1013,8 +1049,13 @@ void update_dz_c(const Ctx& c, int npz, const double* dp0, const double* ut, con
   Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
   if (const int klb = kloop_levels()) {
     const int nkb = (npz + 1 + klb - 1) / klb;
-    GT_LAUNCH(udzc_kl, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, nkb, klb, dp0, ut,
-                       vt, gz, gz_out);
+    const char* lf = std::getenv("GTFV3_LOADS_FIRST");
+    if (!(lf && lf[0] == '0'))
+      GT_LAUNCH_N("udzc_kl", udzc_kl<true>, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz,
+                  nkb, klb, dp0, ut, vt, gz, gz_out);
+    else
+      GT_LAUNCH_N("udzc_kl", udzc_kl<false>, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
+                  npz, nkb, klb, dp0, ut, vt, gz, gz_out);
   } else {
     GT_LAUNCH(udzc_k, g2lv(L, d.nsub * (npz + 1)), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dp0, ut, vt,
                        gz, gz_out);
@@ -1030,8 +1071,13 @@ void p_grad_c(const Ctx& c, int npz, double dt2, const double* delpc, const doub
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
   if (const int klb = kloop_levels()) {
     const int nkb = (npz + klb - 1) / klb;
-    GT_LAUNCH(pgradc_kl, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, nkb, klb, dt2,
-                       delpc, pkc, gz, uc, vc);
+    const char* lf = std::getenv("GTFV3_LOADS_FIRST");
+    if (!(lf && lf[0] == '0'))
+      GT_LAUNCH_N("pgradc_kl", pgradc_kl<true>, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
+                  npz, nkb, klb, dt2, delpc, pkc, gz, uc, vc);
+    else
+      GT_LAUNCH_N("pgradc_kl", pgradc_kl<false>, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
+                  npz, nkb, klb, dt2, delpc, pkc, gz, uc, vc);
   } else {
     GT_LAUNCH(pgradc_k, g2lv(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt2, delpc, pkc,
                        gz, uc, vc);
