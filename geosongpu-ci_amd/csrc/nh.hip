@@ -971,6 +971,7 @@ __global__ void __launch_bounds__(256) pgradc_kl(Dims d, const SubInfo* __restri
   }
 }
 
+template <bool LF>
 __global__ void __launch_bounds__(256) nhpgrad_kl(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
                                                   int npz, int nkb, int klb, double dt, double ptk,
                                                   const double* __restrict__ ppb, const double* __restrict__ gzb,
@@ -999,6 +1000,33 @@ __global__ void __launch_bounds__(256) nhpgrad_kl(Dims d, const SubInfo* __restr
     pk0n = top ? ptk : PK[l0 + Nn];
     pp0n = top ? 0.0 : PP[l0 + Nn];
     gz0n = GZ[l0 + Nn];
+  }
+  if (LF) {
+    // loads first (GTFV3_LOADS_FIRST): both directions' inputs of a level in one group (the
+    // east / north offsets 0 on the column / row that takes no update), then the same
+    // expressions as below
+    const long Ed = du ? E : 0, Nd = dv ? Nn : 0;
+    for (int k = k0; k < k1; ++k) {
+      const long l1 = (long)(k + 1) * P, lk = ((long)s * npz + k) * P + o;
+      const double pk1 = PK[l1], pp1 = PP[l1], gz1 = GZ[l1];
+      const double pk1e = PK[l1 + Ed], pp1e = PP[l1 + Ed], gz1e = GZ[l1 + Ed];
+      const double pk1n = PK[l1 + Nd], pp1n = PP[l1 + Nd], gz1n = GZ[l1 + Nd];
+      const double u0 = u[lk], v0 = v[lk], w0 = wk1[lk], we = wk1[lk + Ed], wn = wk1[lk + Nd];
+      if (du) {
+        const double wk0 = pk1 - pk0, wke = pk1e - pk0e;
+        const double du1 = dt / (wk0 + wke) * ((gz1 - gz0e) * (pk1e - pk0) + (gz0 - gz1e) * (pk1 - pk0e));
+        u[lk] = (u0 + du1 + dt / (w0 + we) * ((gz1 - gz0e) * (pp1e - pp0) + (gz0 - gz1e) * (pp1 - pp0e))) * rdx;
+      }
+      if (dv) {
+        const double wk0 = pk1 - pk0, wke = pk1n - pk0n;
+        const double dv1 = dt / (wk0 + wke) * ((gz1 - gz0n) * (pk1n - pk0) + (gz0 - gz1n) * (pk1 - pk0n));
+        v[lk] = (v0 + dv1 + dt / (w0 + wn) * ((gz1 - gz0n) * (pp1n - pp0) + (gz0 - gz1n) * (pp1 - pp0n))) * rdy;
+      }
+      pk0 = pk1; pp0 = pp1; gz0 = gz1;
+      pk0e = pk1e; pp0e = pp1e; gz0e = gz1e;
+      pk0n = pk1n; pp0n = pp1n; gz0n = gz1n;
+    }
+    return;
   }
   for (int k = k0; k < k1; ++k) {
     const long l1 = (long)(k + 1) * P, lk = ((long)s * npz + k) * P + o;
@@ -1199,8 +1227,13 @@ void nh_p_grad(const Ctx& c, const NhPgArgs& a) {
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
   if (const int klb = kloop_levels()) {
     const int nkb = (a.npz + klb - 1) / klb;
-    GT_LAUNCH(nhpgrad_kl, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, nkb, klb,
-                       a.dt, ptk, a.ppb, a.gzb, a.pkb, a.wk1, a.u, a.v);
+    const char* lf = std::getenv("GTFV3_LOADS_FIRST");
+    if (!(lf && lf[0] == '0'))
+      GT_LAUNCH_N("nhpgrad_kl", nhpgrad_kl<true>, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs,
+                  c.met, a.npz, nkb, klb, a.dt, ptk, a.ppb, a.gzb, a.pkb, a.wk1, a.u, a.v);
+    else
+      GT_LAUNCH_N("nhpgrad_kl", nhpgrad_kl<false>, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs,
+                  c.met, a.npz, nkb, klb, a.dt, ptk, a.ppb, a.gzb, a.pkb, a.wk1, a.u, a.v);
   } else {
     GT_LAUNCH(nhpgrad_k, g2lv(L, d.nsub * a.npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, ptk,
                        a.ppb, a.gzb, a.pkb, a.wk1, a.u, a.v);

@@ -245,7 +245,7 @@ def test_uv_fused_bitwise(pkg, require_gpu, monkeypatch, npx, lay, env):
     whole tiles: GTFV3_UV_FUSED -- the final wind update (ds_uv) inside the vorticity march
     (tp.hip TM = 3, u and v from the fluxes in registers) against the march writing flux
     planes and ds_uv reading them; GTFV3_LOADS_FIRST -- c_sw's cs_tmp / cs_transport_ke / cs_update and
-    d_sw's ds_ke / ds_utvt1_kl and the C-grid udzc_kl / pgradc_kl with every load issued before their arithmetic (the *_ld
+    d_sw's ds_ke / ds_utvt1_kl and udzc_kl / pgradc_kl / nhpgrad_kl with every load issued before their arithmetic (the *_ld
     kernels) against the branch-ordered kernels."""
     state = importlib.import_module(pkg.__name__ + ".state")
     npz = 20
