@@ -521,6 +521,10 @@ void bridge_run(const BridgeArgs<T>& a) {
   HIP_CHECK(hipEventRecord(g_io.ev_t[1], dy.st));
   dy.tracer_wait = nullptr;
   if (defer) {
+    // the deferred scatters write into q, which the first call allocates and zeroes on dy.st:
+    // the tracer stream starts behind everything queued on dy.st so far (the step itself starts
+    // at ev_t[1] as well, so this costs no overlap)
+    HIP_CHECK(hipStreamWaitEvent(g_io.tr, g_io.ev_t[1], 0));
     for (auto& it : items)
       if (std::string(it.name) == "q")
         up_bytes += copy_in<T>(dy, it.name, it.nk_dev, it.p, it.fd, g_io.tr, 0, -1, q0, -1);

@@ -35,18 +35,42 @@ void set_error(const std::string& m) {
   g_err = m;
 }
 
+// GTFV3_CONFIG: `key=value` items separated by ',' or ';' (whitespace around items, keys
+// and values ignored).  A value must be a number consumed whole (integer keys: an integer);
+// anything else is an error, never a silently truncated option.
 Namelist parse_config(const char* cfg, const Namelist& base) {
   Namelist nl = base;
   std::string s = cfg ? cfg : "";
+  for (char& ch : s)
+    if (ch == ';') ch = ',';
+  auto trim = [](std::string t) {
+    const auto a = t.find_first_not_of(" \t\n\r"), b = t.find_last_not_of(" \t\n\r");
+    return a == std::string::npos ? std::string() : t.substr(a, b - a + 1);
+  };
   std::stringstream ss(s);
   std::string item;
-  while (std::getline(ss, item, ';')) {
+  bool nord_v_given = false;
+  while (std::getline(ss, item, ',')) {
+    item = trim(item);
     if (item.empty()) continue;
     auto eq = item.find('=');
     if (eq == std::string::npos) throw std::runtime_error("config item without '=': " + item);
-    std::string k = item.substr(0, eq), v = item.substr(eq + 1);
-    double x = std::stod(v);
+    std::string k = trim(item.substr(0, eq)), v = trim(item.substr(eq + 1));
+    size_t used = 0;
+    double x = 0.0;
+    try {
+      x = std::stod(v, &used);
+    } catch (const std::exception&) {
+      used = 0;
+    }
+    if (v.empty() || used != v.size()) throw std::runtime_error("config value of " + k + " is not a number: '" + v + "'");
     int ix = (int)x;
+    static const char* real_keys[] = {"dt", "dddmp", "d2_bg", "d4_bg", "vtdm4", "d_con", "delt_max", "p_fac",
+                                      "dz_min", "ptop"};
+    bool is_real = false;
+    for (const char* rk : real_keys) is_real = is_real || k == rk;
+    if (!is_real && (double)ix != x) throw std::runtime_error("config value of " + k + " must be an integer: '" + v + "'");
+    if (k == "nord_v") nord_v_given = true;
     if (k == "npx") nl.npx = nl.npy = ix;
     else if (k == "npz") nl.npz = ix;
     else if (k == "nq") nl.nq = ix;
@@ -79,8 +103,13 @@ Namelist parse_config(const char* cfg, const Namelist& base) {
     else if (k == "ptop") nl.ptop = x;
     else if (k == "host_only") nl.host_only = ix != 0;
     else if (k == "loopback") nl.loopback = ix;
+    else if (k == "do_vort_damp") nl.do_vort_damp = ix != 0;
     else throw std::runtime_error("unknown config key: " + k);
   }
+  // fv_core_nml semantics: the vorticity damping order follows nord (FV3 dyn_core:
+  // nord_v = min(2, nord)) unless given, and vtdm4 acts only with do_vort_damp
+  if (!nord_v_given) nl.nord_v = nl.nord < 2 ? nl.nord : 2;
+  if (!nl.do_vort_damp) nl.vtdm4 = 0.0;
   for (int h : {nl.hord_mt, nl.hord_vt, nl.hord_tm, nl.hord_dp, nl.hord_tr})
     if (h != 5 && h != 6) throw std::runtime_error("hord must be 5 or 6");
   if (nl.nord < 0 || nl.nord > 3) throw std::runtime_error("nord must be 0 .. 3");

@@ -164,10 +164,11 @@ class LoopbackTransport : public Transport {
 };
 
 // ---- null (measurement only) ----
-// One rank of a multi-rank layout alone on a device: cross-rank messages are dropped (the
-// remote halo points keep their values), so the rank's kernels run exactly the work of its
-// share of the layout -- the per-GPU compute time of an N-GPU run without the exchange
-// (bench.py --rank-proxy).  Never a numerical path.
+// One rank of a multi-rank layout alone on a device: cross-rank messages are dropped and
+// not unpacked (the remote halo points keep their values -- the initial state's, so the
+// rank's state stays physical, only stale near its cross-rank edges), so the rank's kernels
+// run exactly the work of its share of the layout -- the per-GPU compute time of an N-GPU
+// run without the exchange (bench.py --rank-proxy).  Never a numerical path.
 class NullTransport : public Transport {
  public:
   void group_start() override {}
@@ -176,6 +177,7 @@ class NullTransport : public Transport {
   void group_end(hipStream_t) override {}
   void allreduce_max(double*, int, hipStream_t) override {}
   bool capturable() const override { return true; }
+  bool delivers() const override { return false; }
 };
 
 }  // namespace

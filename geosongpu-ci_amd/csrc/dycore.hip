@@ -693,7 +693,10 @@ void Dycore::step() {
     std::vector<double> key = {(double)field_gen, dt, dt2, ptop, (double)fork_substep, (double)tfused,
                                (double)nl.n_split, nl.dddmp, nl.d2_bg, nl.p_fac, nl.dz_min, nl.d4_bg, nl.vtdm4,
                                nl.d_con, (double)nl.nord, (double)nl.nord_v, (double)nl.hord_mt, (double)nl.hord_vt,
-                               (double)nl.hord_tm, (double)nl.hord_dp};
+                               (double)nl.hord_tm, (double)nl.hord_dp,
+                               // launch-shape switches read at every launch (tests flip them in-process)
+                               (double)kloop_levels(), (double)loads_first(), (double)c_sw_fused(),
+                               (double)riem_variant()};
     for (const Field* f : {&u, &v, &w, &delz, &pt, &delp, &phis})
       key.push_back((double)reinterpret_cast<uintptr_t>(f->p));
     for (const double* p : {vert, dp_ref}) key.push_back((double)reinterpret_cast<uintptr_t>(p));

@@ -47,8 +47,11 @@ struct Namelist {
   // d_sw damping beyond the Held-Suarez namelist (damp.hip): del-(2 nord + 2) divergence
   // damping with d4_bg; del-(2 nord_v + 2) vorticity damping vtdm4; d_con: the damped kinetic
   // energy into heat (limited to delt_max * bdt K per call) and diss_est
+  // (GTFV3_CONFIG follows fv_core_nml: nord_v defaults to min(2, nord) and vtdm4 acts only
+  // with do_vort_damp, capi.cpp parse_config)
   int nord = 0, nord_v = 0;
   double d4_bg = 0.0, vtdm4 = 0.0, d_con = 0.0, delt_max = 1.0;
+  bool do_vort_damp = false;
   double p_fac = 0.05;               // SIM1 solver pressure floor factor
   double dz_min = 2.0;
   bool fill = true;                  // fillz negative tracers after remap

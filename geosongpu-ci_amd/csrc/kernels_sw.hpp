@@ -20,6 +20,8 @@ void c_sw(const Ctx& c, const CswArgs& a);            // the two stages in order
 void c_sw_transport(const Ctx& c, const CswArgs& a);  // d2a2c_vect, delpc / ptc / wc, ke
 void c_sw_winds(const Ctx& c, const CswArgs& a);      // vorticity, uc / vc update
 bool c_sw_fused();                                           // GTFV3_CSW_FUSED=1 (default off)
+bool loads_first();                                          // GTFV3_LOADS_FIRST (default on)
+int kloop_levels();                                          // GTFV3_KLOOP (stencil_common.hpp)
 void c_sw_transport_march(const Ctx& c, const CswArgs& a);  // the first stage as one march
 
 struct DswArgs {

@@ -12,6 +12,7 @@
 // Everything else (dm, pm, dz, pl, g_rat, bb, dd, aa) is recomputed on the fly with
 // the same expressions as the oracle (oracle/nh_core.py sim1_solver), so results are
 // bit-identical to the previous scratch-plane version.
+#include "blockscan.hpp"
 #include "kernels_nh.hpp"
 #include "stencil_common.hpp"
 
@@ -24,11 +25,11 @@ constexpr double KAPPA = Constants::kappa;
 constexpr double R3 = 1.0 / 3.0;
 constexpr int BLOCK = 256;
 
-int g_riem_variant = 0;
+int g_riem_variant = -1;  // -1: not set, GTFV3_RIEM decides
 
 struct RiemArgs {
   Dims d;
-  int npz, ring, last_call, cgrid, dump;
+  int npz, ring, last_call, cgrid;
   double dt, ptop, p_fac, dz_min;
   const double *delp, *pt, *w_in, *phis;
   double* G;       // zh (heights, D-grid) or gz (heights in -> geopotential out, C-grid); L+1
@@ -38,7 +39,11 @@ struct RiemArgs {
   double *pk3, *pe, *peln, *pk;  // D-grid only (pe/peln/pk on the last call)
   double* ws_out;  // D-grid: surface w for the remap (may be null)
   double *gam, *pp, *w2;  // scratch, L+1 planes each
+  double* dbg = nullptr;   // debug: intermediates of column dbg_col of sub-domain 0 (scan form)
+  int dbg_col = -1;
 };
+double* g_riem_dbg = nullptr;
+int g_riem_dbg_col = -1;
 
 // The column body takes every array as a distinct __restrict__ pointer: the arrays never
 // alias, and saying so lets the compiler hoist the loads of an unrolled group of levels
@@ -287,193 +292,177 @@ __global__ void __launch_bounds__(BLOCK) riem_col_k(RiemArgs a) {
               at(a.delz, bk));
 }
 
-// ---------------- register-resident form (default) ----------------
+// ---------------- level-block scan form (default) ----------------
 //
-// One wavefront owns 16 columns; its 64 lanes are 4 level blocks x 16 columns
-// (lane = 16 b + column), block b holding layers [b M, b M + M) and interfaces
-// b M .. b M + M of its column in registers (M = 18 at L72).  Every output is written
-// once; inputs the registers cannot hold across all sweeps (DP, PT, W1, G) are re-read
-// from cache where a later sweep needs them, and the clamped heights and interface
-// pressures are recomputed there (nothing is parked in HBM and read back).
+// One wavefront owns NC = 64 / NB columns; lane = NB * column + b, block b holding layers
+// [b M, b M + M) and interfaces b M .. b M + M of its column in registers (L72: M = 9, NB = 8,
+// eight columns a wave; L137: M = 9, NB = 16 with a partial last block).  A column's blocks sit
+// in consecutive lanes of one 16-lane DPP row, so every hand-over between neighbouring blocks
+// is a DPP row shift (no LDS, no ds_bpermute).
 //
-//   * pointwise work (the transcendentals of pm, pl, pk3, dz2; aa, the numerators) runs
-//     on all 64 lanes at once;
-//   * each recurrence (pem and pe prefixes, both Thomas eliminations and back
-//     substitutions, the p1 recurrence, the height sums) runs block after block with its
-//     carry handed to the next block by a lane shuffle (lane +- 16), so every value is
-//     formed by the same operations in the same order as in riem_column: the results
-//     are bit-identical to the column form (tests/test_gpu_riem.py compares them);
-//   * the dz_min clamp (bottom-up max recurrence) runs on all blocks at once from the
-//     unclamped interface below each block, then repeats only if a block's lower
-//     neighbour changed that interface (exact; the clamp is rarely active).
-// Two per-layer arrays that live from the first sweep to the last (pm, g_rat) are
-// kept in LDS, the rest in VGPRs.
-//
-// A column whose level count is not a multiple of M (L137 = 7 x 18 + 11) runs as eight
-// blocks of eight columns with a partial last block (PARTIAL, MV < M real layers, a template
-// constant): its lanes' loads past the surface are masked to zero and their stores dropped,
-// and every recurrence starts or stops at the real bottom MV instead of M.
-constexpr int RB_WAVES = 4;
+// Every sweep runs on all 64 lanes at once:
+//   * pointwise work: the logs / exps of pln, pk3, pl and dz2, the layer quantities;
+//   * prefix sums (pem, pe, the heights): each block sums its layers, a Kogge-Stone scan of the
+//     block totals over the NB lanes (log2 NB DPP shifts) gives each block its carry-in, and the
+//     block runs its recurrence from that carry;
+//   * the two tridiagonal solves (pp, then w) as a partitioned Thomas algorithm (tri_solve):
+//     the pivots bet_k = d_k - a_k c_{k-1} / bet_{k-1} are a Möbius recurrence, a product of 2x2
+//     matrices [[d_k, -a_k c_{k-1}], [1, 0]]: each block multiplies its M, a scan multiplies the
+//     block products, block b reads its incoming pivot off the product of blocks 0..b-1 and
+//     eliminates from it; the forward-substituted right-hand side y_k = (r_k - a_k y_{k-1}) / bet_k
+//     and the back substitution x_k = y_k - gam_{k+1} x_{k+1} are affine recurrences, each run as
+//     a block pass with a zero carry (giving the block's affine map), a scan of the maps and a
+//     second block pass from the true carry;
+//   * the p1 recurrence (bottom-up affine) and the dz_min clamp (bottom-up max recurrence,
+//     speculative per block, repeated only where a block below changed its bottom interface).
+// The w system is nearly singular (the acoustic coupling aa ~ 1e8 against layer masses ~ 1e2):
+// its incoming pivots carry the cancellation of the matrix products (~1e-13 relative), so its
+// solve takes one step of iterative refinement (residual from the DPP-neighbour values, the
+// same factors), which brings the error back to the sequential sweep's (~3e-14 of the mean
+// |w| in a numpy model of the solve, against 1e-14 for the column sweep).
+// Sums and products are associated differently from the column sweep (riem_col_k): the
+// results agree with it and with the oracle to rounding (tests/test_gpu_riem.py), not bit for
+// bit.  Transcendentals and divisions come from fastmath.hpp (~1 ulp; a third of ocml's log).
+// Each input is read once (G, DP, PT, W1, phis) and each output written once.
+constexpr int RS_WAVES = 4;
 typedef unsigned int RbU2 __attribute__((ext_vector_type(2)));
-// The pointwise loops are long straight-line runs of independent transcendentals; left
-// alone the scheduler interleaves all M of them and runs out of registers.  A fence per
-// level keeps one or two in flight (two waves per SIMD hide the latency instead).
-#define RB_SCHED_FENCE() __builtin_amdgcn_sched_barrier(0)
 
-template <int NC>
-__device__ __forceinline__ double rb_below(double v, int lane) { return __shfl(v, (lane + NC) & 63); }
-template <int NC>
-__device__ __forceinline__ double rb_above(double v, int lane) { return __shfl(v, (lane - NC) & 63); }
-
-template <int M, bool CG, int NB = 4, int MV = M>
-__global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
-  constexpr int RB_NB = NB, RB_NC = 64 / NB;
-  constexpr bool PARTIAL = MV < M;  // the last block holds MV < M layers (km = (nblk - 1) M + MV)
-  auto from_below = [](double v, int ln) { return rb_below<RB_NC>(v, ln); };
-  auto from_above = [](double v, int ln) { return rb_above<RB_NC>(v, ln); };
-  __shared__ double lds_pm[RB_WAVES][M][64];
-  __shared__ double lds_g[RB_WAVES][M][64];
-  constexpr bool cg = CG;
+template <int M, int NB, bool PART, bool CG>
+__global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
+  constexpr int NC = 64 / NB;
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  const int b = lane / RB_NC;
+  const int b = lane & (NB - 1);
+  const bool last = b == NB - 1;
   const Dims& d = a.d;
-  const int km = a.npz;
-  const int nblk = (km + M - 1) / M;  // launch_riem: nblk <= NB, km = (nblk - 1) M + MV
+  const int km = a.npz;  // launch_riem: km = (NB - 1) M + nv_last, 1 <= nv_last <= M
+  const int nv = PART && last ? km - (NB - 1) * M : M;  // real layers of this block
+  auto real = [&](int m) { return !PART || m < nv; };
+  auto isbot = [&](int m) { return last && m == nv - 1; };
   const int ni = d.nx + 2 * a.ring, nj = d.ny + 2 * a.ring;
   const int ncol = ni * nj;
   const int s = blockIdx.y;
-  const int c0 = (blockIdx.x * RB_WAVES + wv) * RB_NC;
+  const int c0 = (blockIdx.x * RS_WAVES + wv) * NC;
   if (c0 >= ncol) return;  // whole wavefront; no workgroup barrier in this kernel
-  int c = c0 + (lane & (RB_NC - 1));
-  const bool act = b < nblk;                // lanes of blocks past the column idle
-  const bool valid = c < ncol && act;       // writes
-  if (c >= ncol) c = ncol - 1;
+  int c = c0 + lane / NB;
+  const bool valid = c < ncol;  // writes
+  if (!valid) c = ncol - 1;
   const int i = c % ni - a.ring, j = c / ni - a.ring;
   const long P = d.plane;
   const long o = pidx(d, i, j);
-  const int kb0 = act ? b * M : 0;
-  const bool lastblk = b == nblk - 1;
-  double(&spm)[M][64] = lds_pm[wv];
-  double(&sg)[M][64] = lds_g[wv];
-  const double dt = a.dt;
+  // debug build only (-DGTFV3_RIEM_DEBUG, tools/dbg_riem_replay.py): one column's intermediates
+#ifdef GTFV3_RIEM_DEBUG
+  const bool dbg = a.dbg && s == 0 && c0 + lane / NB == a.dbg_col;
+  auto dump = [&](int phase, int m, double v) {
+    if (dbg) a.dbg[(phase * NB + b) * M + m] = v;
+  };
+#else
+  auto dump = [](int, int, double) {};
+#endif
+  const double dt = a.dt, rdt = 1.0 / dt;
   const double gama = 1.0 / (1.0 - KAPPA);
   const double t1g = gama * 2.0 * dt * dt;
-  const double rdt = 1.0 / dt;
   const double capa1 = KAPPA - 1.0;
 
   // Memory: one buffer descriptor per array and sub-domain (wave-uniform SGPRs), a 32-bit
-  // per-lane byte offset (the block's first level) and the level as the scalar offset.
+  // per-lane byte offset (the block's first level) and the level as the scalar offset.  Levels
+  // past the bottom (a partial block's) fall outside the descriptor's range: their loads read
+  // zero and their stores are dropped by the hardware range check.
   const uint32_t PB = (uint32_t)P * 8u;
-  const uint32_t lo = (uint32_t)((o + (long)kb0 * P) * 8);
-  const int li = (km + 1) * (int)PB, ll = km * (int)PB;  // bytes of a sub-domain's field
+  const uint32_t lo = (uint32_t)((o + (long)(b * M) * P) * 8);
+  const uint32_t o8 = (uint32_t)o * 8u;
+  const int li = (km + 1) * (int)PB, ll = km * (int)PB;
   auto rs = [&](const double* p, bool itf) {
     const long so = (long)s * (itf ? km + 1 : km) * P;
     return __builtin_amdgcn_make_buffer_rsrc((void*)(p + so), 0, itf ? li : ll, 0x00020000);
   };
-  // itf: an interface field (levels 0 .. km).  In a partial block the levels past the surface
-  // (static m >= MV, or > MV for interface fields) exist only for the other blocks' lanes: the
-  // last block's lanes read zero there and store nothing (masked, no access).
-  auto past = [&](int m, bool itf) { return PARTIAL && m >= MV + (itf ? 1 : 0); };
-  auto ld = [&](__amdgpu_buffer_rsrc_t r, int m, bool itf = false) {
-    if (past(m, itf)) {
-      double v = 0.0;
-      if (!lastblk) v = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lo, (uint32_t)m * PB, 0));
-      return v;
-    }
+  auto ld = [&](__amdgpu_buffer_rsrc_t r, int m) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lo, (uint32_t)m * PB, 0));
   };
-  auto st = [&](__amdgpu_buffer_rsrc_t r, int m, double v, bool itf = false) {
-    if (past(m, itf) && lastblk) return;
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), r, lo, (uint32_t)m * PB, 0);
+  auto st = [&](__amdgpu_buffer_rsrc_t r, int m, double v) {
+    if (valid) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), r, lo, (uint32_t)m * PB, 0);
+  };
+  // the column's bottom interface (level km), written by the last block
+  auto st_bot = [&](__amdgpu_buffer_rsrc_t r, double v) {
+    if (valid && last) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), r, o8, (uint32_t)km * PB, 0);
   };
   const auto rG = rs(a.G, true), rPO = rs(a.pout, true);
   const auto rDP = rs(a.delp, false), rPT = rs(a.pt, false), rW1 = rs(a.w_in, false);
 
-  // ---- loads
-  double gr[M + 1], DP[M];
+  // ---- loads (W1 after the pp solve)
+  double G[M + 1], DP[M], PT[M];
 #pragma unroll
-  for (int m = 0; m <= M; ++m) gr[m] = ld(rG, m, true);
+  for (int m = 0; m <= M; ++m) G[m] = ld(rG, m);
 #pragma unroll
   for (int m = 0; m < M; ++m) DP[m] = ld(rDP, m);
-  // surface values (re-read where used instead of held in registers)
-  const uint32_t o8 = (uint32_t)o * 8u;
-  const auto rPH = __builtin_amdgcn_make_buffer_rsrc((void*)(a.phis + (long)s * P), 0, (int)PB, 0x00020000);
-  auto surf = [&](double& hs, double& zs, double& ws) {
-    hs = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rPH, o8, 0, 0));
-    zs = hs * (1.0 / GRAV);
-    const double gbot = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rG, o8, (uint32_t)km * PB, 0));
-    ws = (zs - gbot) * (1.0 / dt);
-  };
-  if (a.ws_out && valid && b == 0) {
-    double hs, zs, ws;
-    surf(hs, zs, ws);
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, ws),
+#pragma unroll
+  for (int m = 0; m < M; ++m) PT[m] = ld(rPT, m);
+  const double hs = __builtin_bit_cast(
+      double, __builtin_amdgcn_raw_buffer_load_b64(
+                  __builtin_amdgcn_make_buffer_rsrc((void*)(a.phis + (long)s * P), 0, (int)PB, 0x00020000), o8, 0, 0));
+  const double gsurf = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rG, o8, (uint32_t)km * PB, 0));
+  const double zs = hs * (1.0 / GRAV);
+  const double ws = (zs - gsurf) * (1.0 / dt);
+  if (a.ws_out && valid && b == 0)
+    __builtin_amdgcn_raw_buffer_store_b64(
+        __builtin_bit_cast(RbU2, ws),
         __builtin_amdgcn_make_buffer_rsrc((void*)(a.ws_out + (long)s * P), 0, (int)PB, 0x00020000), o8, 0, 0);
-  }
 
-  // dz_min clamp of the heights g (bottom-up), speculative per block: each block clamps from
-  // the unclamped interface below it, and repeats only if the block below changed it
-  auto clamp = [&](const double (&g)[M + 1], double (&gl)[M + 1]) {
-    double gin = g[M];  // unclamped interface kb1
-    if (PARTIAL && lastblk) gin = ld(rG, MV, true);  // the partial block's is the surface at MV
-    for (int it = 0; it <= RB_NB; ++it) {
+  // ---- S0: dz_min clamp (bottom-up max recurrence): each block clamps from the unclamped
+  // interface below it and repeats only if the block below changed that interface (exact)
+  double gl[M + 1];
+  {
+    double gin = PART && last ? gsurf : G[M];
+    for (int it = 0; it <= NB; ++it) {
       gl[M] = gin;
 #pragma unroll
-      for (int m = M - 1; m >= 0; --m)
-        gl[m] = PARTIAL && lastblk && m >= MV ? gin : fmax(g[m], gl[m + 1] + a.dz_min);
-      const double gn = from_below(gl[0], lane);
-      const double want = lastblk || !act ? gin : gn;
+      for (int m = M - 1; m >= 0; --m) gl[m] = real(m) ? fmax(G[m], gl[m + 1] + a.dz_min) : gin;
+      const double gn = blk_next(gl[0]);
+      const double want = last ? gin : gn;
       if (!__any(want != gin)) break;
       gin = want;
     }
-  };
-  // interface pressures pem = ptop + prefix sums of DP (top-down, block after block)
-  auto prefix = [&](const double (&dpv)[M], double (&pe_)[M + 1]) {
-#pragma unroll
-    for (int m = 0; m <= M; ++m) pe_[m] = 0.0;
-    double carry = a.ptop;
-#pragma unroll 1
-    for (int r = 0; r < nblk; ++r) {
-      if (b == r) {
-        pe_[0] = carry;
-#pragma unroll
-        for (int m = 0; m < M; ++m) pe_[m + 1] = pe_[m] + dpv[m];
-      }
-      carry = from_above(pe_[M], lane);
-    }
-  };
-  // The clamped heights and pem are recomputed where S3 / S6 need them again (same
-  // operations, same values) instead of being parked in HBM between the sweeps: the parked
-  // copies cost a write and one or two re-reads per level (riem traffic was 2.4-3x its
-  // algorithmic bytes).
-  RB_SCHED_FENCE();
-  // ---- S0: dz_min clamp
-  double gl[M + 1];
-  clamp(gr, gl);
+  }
 
-  RB_SCHED_FENCE();
-  // ---- S1a: pem prefix
+  // ---- S1: pem (ptop + prefix sums of DP)
   double pem[M + 1];
-  prefix(DP, pem);
+  {
+    double tot = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) tot += DP[m];
+    const double ex = blk_prev(scan_sum<NB, true>(tot, b));
+    pem[0] = b == 0 ? a.ptop : a.ptop + ex;  // ex: shifted above, outside the ?: (blockscan.hpp)
+#pragma unroll
+    for (int m = 0; m < M; ++m) pem[m + 1] = pem[m] + DP[m];
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) { dump(0, m, pem[m]); dump(13, m, gl[m]); dump(14, m, G[m]); }
 
-  RB_SCHED_FENCE();
-  // ---- S1b: pointwise layer quantities
-  double pl[M], dm[M];
+  // ---- S1b: pointwise layer quantities (and pk3 / pe / peln / pk on the D grid)
+  // per-layer values that live from the first sweep to the last, in LDS: pm, q = dm RDGAS pt
+  // (dz2's factor) and g_rat
+  __shared__ double lds_rs[3][RS_WAVES][M][64];
+  double(&Spm)[M][64] = lds_rs[0][wv];
+  double(&Sq)[M][64] = lds_rs[1][wv];
+  double(&Sg)[M][64] = lds_rs[2][wv];
+  double dm[M], dz[M], pl[M];
   {
     double pln[M + 1];
-    if (!cg) {
+    if constexpr (!CG) {
+      const double lpt = fm_log(a.ptop);
+#pragma unroll
+      for (int m = 1; m <= M; ++m) pln[m] = fm_log(pem[m]);
+      const double plu = blk_prev(pln[M]);
+      pln[0] = b == 0 ? lpt : plu;
       const auto rK3 = rs(a.pk3, true);
 #pragma unroll
       for (int m = 0; m <= M; ++m) {
-        pln[m] = log(pem[m]);  // slot 0 of block 0: log(ptop)
-        if (valid && (m < M || lastblk)) {
-          RB_SCHED_FENCE();
-          const double pkk = exp(KAPPA * pln[m]);
-          st(rK3, m, pkk, true);
+        if (m > 0 || b == 0) {  // interface 0 of block b > 0 is written by block b - 1
+          const double pkk = fm_exp(KAPPA * pln[m]);
+          st(rK3, m, pkk);
           if (a.last_call) {
-            st(rs(a.pe, true), m, pem[m], true);
-            st(rs(a.peln, true), m, pln[m], true);
-            st(rs(a.pk, true), m, pkk, true);
+            st(rs(a.pe, true), m, pem[m]);
+            st(rs(a.peln, true), m, pln[m]);
+            st(rs(a.pk, true), m, pkk);
           }
         }
       }
@@ -481,335 +470,228 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) riem_blk_k(RiemArgs a) {
 #pragma unroll
     for (int m = 0; m < M; ++m) {
       dm[m] = DP[m] * (1.0 / GRAV);
-      const double dz = gl[m + 1] - gl[m];
-      const double pm = cg ? DP[m] / log(pem[m + 1] / pem[m]) : DP[m] / (pln[m + 1] - pln[m]);
-      spm[m][lane] = pm;
-      pl[m] = exp(gama * log(-dm[m] / dz * RDGAS * ld(rPT, m))) - pm;
-      RB_SCHED_FENCE();
-    }
-  }
-  // g_rat and the right-hand side of the pp system
-  double dd[M], gprev;
-  {
-    const double dm_nb = from_below(dm[0], lane), pl_nb = from_below(pl[0], lane);
-#pragma unroll
-    for (int m = 0; m < M; ++m) {
-      const bool bot = lastblk && m == MV - 1;
-      const double dmn = m + 1 < M ? dm[m + 1 < M ? m + 1 : 0] : dm_nb;
-      const double pln_ = m + 1 < M ? pl[m + 1 < M ? m + 1 : 0] : pl_nb;
-      const double g = bot ? 0.0 : dm[m] / dmn;
-      sg[m][lane] = g;
-      dd[m] = bot ? 3.0 * pl[m] : 3.0 * (pl[m] + g * pln_);
-    }
-    gprev = from_above(sg[M - 1][lane], lane);  // g_rat of layer kb0-1
-  }
-
-  RB_SCHED_FENCE();
-  // ---- S1c: forward elimination for pp (top-down, block after block)
-  double pp[M + 1], gam[M];
-#pragma unroll
-  for (int m = 0; m <= M; ++m) pp[m] = 0.0;
-#pragma unroll
-  for (int m = 0; m < M; ++m) gam[m] = 0.0;
-  {
-    double cbet = 0.0, cpp = 0.0;
-#pragma unroll 1
-    for (int r = 0; r < nblk; ++r) {
-      double bet_o = 0.0;
-      if (b == r) {
-        double bet = cbet, ppk = cpp;
-        pp[0] = cpp;
-#pragma unroll
-        for (int m = 0; m < M; ++m) {
-          const bool bot = lastblk && m == MV - 1;
-          const double g = sg[m][lane];
-          const double bbk = bot ? 2.0 : 2.0 * (1.0 + g);
-          double ppn;
-          if (m == 0 && b == 0) {
-            bet = bbk;
-            ppn = dd[m] / bet;
-          } else {
-            const double gm = (m == 0 ? gprev : sg[m > 0 ? m - 1 : 0][lane]) / bet;
-            gam[m] = gm;
-            bet = bbk - gm;
-            ppn = (dd[m] - ppk) / bet;
-          }
-          if (PARTIAL && lastblk && m >= MV) ppn = ppk;  // past the surface: pp[M] = pp[MV] for S2 and S3
-          pp[m + 1] = ppn;
-          ppk = ppn;
-        }
-        bet_o = bet;
-      }
-      cbet = from_above(bet_o, lane);
-      cpp = from_above(pp[M], lane);
-    }
-  }
-  RB_SCHED_FENCE();
-  // ---- S2: back substitution for pp (bottom-up)
-  {
-    double cx = 0.0;
-#pragma unroll 1
-    for (int r = nblk - 1; r >= 0; --r) {
-      if (b == r) {
-        if (!lastblk) pp[M] = cx;
-        double x = pp[M];
-#pragma unroll
-        for (int m = M - 1; m >= 0; --m) {
-          if ((m > 0 || b > 0) && !(PARTIAL && lastblk && m >= MV)) {
-            x = pp[m] - gam[m] * x;
-            pp[m] = x;
-          }
-        }
-      }
-      cx = from_below(pp[0], lane);
+      dz[m] = gl[m + 1] - gl[m];
+      double pmv;
+      if constexpr (CG) pmv = fm_div(DP[m], fm_log(fm_div(pem[m + 1], pem[m])));
+      else pmv = fm_div(DP[m], pln[m + 1] - pln[m]);
+      const double plv = fm_exp(gama * fm_log(fm_div(-dm[m], dz[m]) * RDGAS * PT[m])) - pmv;
+      Spm[m][lane] = real(m) ? pmv : 0.0;
+      Sq[m][lane] = dm[m] * RDGAS * PT[m];
+      pl[m] = real(m) ? plv : 0.0;
+      dump(1, m, dz[m]); dump(2, m, pmv); dump(3, m, pl[m]);
     }
   }
 
-  RB_SCHED_FENCE();
-  // ---- S3: forward elimination for w (top-down)
-  double aat[M], num[M], aab_last;
+  // ---- S1c/S2: the pp system (rows: interfaces 1..km), g_rat
+  double pp[M];  // pp[m] = pp at interface b M + m + 1
   {
-    double pemr[M + 1], glr[M + 1], dz[M];
-    {
-      double dpv[M], g0[M + 1];
-#pragma unroll
-      for (int m = 0; m < M; ++m) dpv[m] = ld(rDP, m);
-#pragma unroll
-      for (int m = 0; m <= M; ++m) g0[m] = ld(rG, m, true);  // the unclamped heights (G is written in S6)
-      prefix(dpv, pemr);
-      clamp(g0, glr);
-#pragma unroll
-      for (int m = 0; m < M; ++m) dm[m] = dpv[m] * (1.0 / GRAV);
-    }
-#pragma unroll
-    for (int m = 0; m < M; ++m) dz[m] = glr[m + 1] - glr[m];
-    const double dz_ab = from_above(dz[M - 1], lane);
+    const double dmn_b = blk_next(dm[0]), pln_b = blk_next(pl[0]);
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      const double dzu = m == 0 ? dz_ab : dz[m > 0 ? m - 1 : 0];
-      aat[m] = t1g / (dzu + dz[m]) * (pemr[m] + pp[m]);  // aa at interface kb0+m (unused at 0)
-      num[m] = dm[m] * ld(rW1, m) + dt * (pp[m + 1] - pp[m]);
+      const double dmn = m + 1 < M ? dm[m + 1 < M ? m + 1 : 0] : dmn_b;
+      const double pn = m + 1 < M ? pl[m + 1 < M ? m + 1 : 0] : pln_b;
+      const bool bt = isbot(m);
+      const double gv = bt || !real(m) ? 0.0 : fm_div(dm[m], dmn);
+      Sg[m][lane] = gv;
+      // (rows past a partial block's bottom: 0 by a select -- pn there is the next column's
+      // value, and 0 * NaN would carry a garbage column's NaN into this one)
+      pp[m] = !real(m) ? 0.0 : (bt ? 3.0 * pl[m] : 3.0 * (pl[m] + gv * pn));
     }
-    // aa below the block's last layer: the next block's first aa, or p1 for the bottom
-    const double aab_nb = from_below(aat[0], lane);
-    double hs, zs, ws;
-    surf(hs, zs, ws);
-    double dzb = dz[M - 1];
-    if (PARTIAL && lastblk) {  // the bottom layer MV-1 of the partial block, clamped as in clamp()
-      const double gs = ld(rG, MV, true);
-      dzb = gs - fmax(ld(rG, MV - 1, true), gs + a.dz_min);
-    }
-    const double p1 = t1g / dzb * (pemr[M] + pp[M]);  // pemr, pp constant past the surface
+    double dd[M];
 #pragma unroll
-    for (int m = 0; m < M; ++m)
-      if (lastblk && m == MV - 1) num[m] = num[m] - p1 * ws;
-    aab_last = lastblk ? p1 : aab_nb;
+    for (int m = 0; m < M; ++m) dd[m] = pp[m];
+    auto row = [&](int m, double& am, double& dg, double& cm) {
+      am = (b == 0 && m == 0) || !real(m) ? 0.0 : 1.0;
+      const double gv = Sg[m][lane];
+      dg = !real(m) ? 1.0 : (isbot(m) ? 2.0 : 2.0 * (1.0 + gv));
+      cm = gv;
+    };
+    tri_solve<M, NB, true>(row, [&](int m) { return dd[m]; }, pp, b, last);
+#pragma unroll
+    for (int m = 0; m < M; ++m) { dump(4, m, Sg[m][lane]); dump(5, m, pp[m]); dump(15, m, dd[m]); }
   }
+
+  // ---- S3/S4: the w system
+  double W1[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) W1[m] = ld(rW1, m);
   double w2[M];
-#pragma unroll
-  for (int m = 0; m < M; ++m) w2[m] = 0.0;
   {
-    double cbet = 0.0, cw = 0.0;
-#pragma unroll 1
-    for (int r = 0; r < nblk; ++r) {
-      double bet_o = 0.0, w_o = 0.0;
-      if (b == r) {
-        double bet = cbet, wp = cw;
+    // pp and dz at the block's interfaces / layers above
+    const double ppu = blk_prev(pp[M - 1]);
+    const double pp_up = b == 0 ? 0.0 : ppu;  // pp at interface b M
+    const double dz_up = blk_prev(dz[M - 1]);
+    auto ppi = [&](int m) { return m > 0 ? pp[m > 0 ? m - 1 : 0] : pp_up; };  // pp at interface m
+    double aat[M];  // aa at interface b M + m (0 at the column's top)
 #pragma unroll
-        for (int m = 0; m < M; ++m) {
-          const double aab = m + 1 < M && !(PARTIAL && lastblk && m == MV - 1) ? aat[m + 1 < M ? m + 1 : 0] : aab_last;
-          if (m == 0 && b == 0) {
-            bet = dm[m] - aab;
-            wp = num[m] / bet;
-          } else {
-            const double gm = aat[m] / bet;
-            gam[m] = gm;
-            bet = dm[m] - (aat[m] + aab + aat[m] * gm);
-            wp = (num[m] - aat[m] * wp) / bet;
-          }
-          w2[m] = wp;
-        }
-        bet_o = bet;
-        w_o = wp;
-      }
-      cbet = from_above(bet_o, lane);
-      cw = from_above(w_o, lane);
+    for (int m = 0; m < M; ++m) {
+      const double dzu = m > 0 ? dz[m > 0 ? m - 1 : 0] : dz_up;
+      const double v = fm_div(t1g, dzu + dz[m]) * (pem[m] + ppi(m));
+      aat[m] = (b == 0 && m == 0) || !real(m) ? 0.0 : v;
     }
-  }
-  RB_SCHED_FENCE();
-  // ---- S4: back substitution for w (bottom-up)
-  {
-    const double gam_nb = from_below(gam[0], lane);
-    double cx = 0.0;
-#pragma unroll 1
-    for (int r = nblk - 1; r >= 0; --r) {
-      if (b == r) {
-        double x = cx;
+    // aa below the block's last real layer: the next block's first, or p1 at the surface
+    const double aab_nb = blk_next(aat[0]);
+    double p1 = 0.0;
+    if (last) {
+      double dzb = dz[M - 1], pemb = pem[M], ppb = pp[M - 1];
+      if constexpr (PART) {
 #pragma unroll
-        for (int m = M - 1; m >= 0; --m) {
-          if (lastblk && m == MV - 1) {
-            x = w2[m];
-          } else if (!(PARTIAL && lastblk && m >= MV)) {
-            x = w2[m] - (m + 1 < M ? gam[m + 1 < M ? m + 1 : 0] : gam_nb) * x;
-            w2[m] = x;
+        for (int m = 0; m < M; ++m)
+          if (m == nv - 1) {
+            dzb = dz[m];
+            pemb = pem[m + 1];
+            ppb = pp[m];
           }
-        }
       }
-      cx = from_below(w2[0], lane);
+      p1 = fm_div(t1g, dzb) * (pemb + ppb);
     }
+    auto aab = [&](int m) { return isbot(m) ? p1 : (m + 1 < M ? aat[m + 1 < M ? m + 1 : 0] : aab_nb); };
+    auto row = [&](int m, double& am, double& dg, double& cm) {
+      am = aat[m];
+      const double ab = aab(m);
+      dg = real(m) ? dm[m] - (aat[m] + ab) : 1.0;
+      cm = isbot(m) || !real(m) ? 0.0 : ab;
+    };
+    auto rhs = [&](int m) {
+      const double v = dm[m] * W1[m] + dt * (pp[m] - ppi(m));
+      return isbot(m) ? v - p1 * ws : (real(m) ? v : 0.0);
+    };
+#pragma unroll
+    for (int m = 0; m < M; ++m) { dump(6, m, aat[m]); dump(16, m, rhs(m)); }
+    dump(17, 0, p1);
+    tri_solve<M, NB, false>(row, rhs, w2, b, last);
+#pragma unroll
+    for (int m = 0; m < M; ++m) dump(7, m, w2[m]);
   }
 
-  RB_SCHED_FENCE();
   // ---- S5: pe prefix (top-down); w out
-#pragma unroll
-  for (int m = 0; m < M; ++m) num[m] = ld(rDP, m) * (1.0 / GRAV) * (w2[m] - ld(rW1, m)) * rdt;
-  if (a.w_out && valid) {
-    const auto rW = rs(a.w_out, false);
-#pragma unroll
-    for (int m = 0; m < M; ++m) st(rW, m, w2[m]);
-  }
-  if (a.dump && valid) {  // debug: w2 and the final pp into the column kernel's scratch planes
-    const auto rw = rs(a.w2, true), rg = rs(a.gam, true);
+  double pe[M + 1];  // pe at interfaces b M .. b M + M
+  {
+    double num[M], tot = 0.0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      st(rw, m, w2[m], true);
-      st(rg, m, gam[m], true);
+      num[m] = dm[m] * (w2[m] - W1[m]) * rdt;
+      tot += num[m];
     }
-  }
-  auto& pe = pp;  // pe replaces pp
-  {
-    double carry = 0.0;
-#pragma unroll 1
-    for (int r = 0; r < nblk; ++r) {
-      if (b == r) {
-        pe[0] = carry;
+    const double ex = blk_prev(scan_sum<NB, true>(tot, b));
+    pe[0] = b == 0 ? 0.0 : ex;
 #pragma unroll
-        for (int m = 0; m < M; ++m) pe[m + 1] = pe[m] + num[m];
-      }
-      carry = from_above(pe[M], lane);
+    for (int m = 0; m < M; ++m) pe[m + 1] = pe[m] + num[m];
+#pragma unroll
+    for (int m = 0; m < M; ++m) dump(8, m, pe[m]);
+    if (a.w_out) {
+      const auto rW = rs(a.w_out, false);
+#pragma unroll
+      for (int m = 0; m < M; ++m) st(rW, m, w2[m]);
     }
   }
 
-  if (a.dump && valid) {
-    const auto rp = rs(a.pp, true);
-#pragma unroll
-    for (int m = 0; m < M; ++m) st(rp, m, pe[m], true);
-  }
-  RB_SCHED_FENCE();
-  // ---- S6: p1 recurrence, dz2, heights (bottom-up)
+  // ---- S6: p1 recurrence (bottom-up affine), dz2, heights
   {
-    const double pe2_nb = from_below(pe[1], lane);  // pe at interface kb1+1
-    double t[M];
+    const double pe2_nb = blk_next(pe[1]);  // pe at interface b M + M + 1
+    double p1v[M];
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      const double g = sg[m][lane];
       const double pe2 = m + 2 <= M ? pe[m + 2 <= M ? m + 2 : 0] : pe2_nb;
-      if (lastblk && m == MV - 1) t[m] = (pe[m] + 2.0 * pe[m + 1]) * R3;
-      else t[m] = (pe[m] + 2.0 * (1.0 + g) * pe[m + 1] + g * pe2) * R3;
+      const double gv = Sg[m][lane];
+      const double t = isbot(m) ? (pe[m] + 2.0 * pe[m + 1]) * R3 : (pe[m] + 2.0 * (1.0 + gv) * pe[m + 1] + gv * pe2) * R3;
+      p1v[m] = real(m) ? t : 0.0;
     }
-    double cp = 0.0;
-#pragma unroll 1
-    for (int r = nblk - 1; r >= 0; --r) {
-      if (b == r) {
-        double p1 = cp;
+    // p1_k = t_k - g_k p1_{k+1}: block pass with a zero carry, scan of the maps, second pass
+    double ph = 0.0, Cc = 1.0;
 #pragma unroll
-        for (int m = M - 1; m >= 0; --m) {
-          if (PARTIAL && lastblk && m >= MV) continue;
-          if (lastblk && m == MV - 1) p1 = t[m];
-          else p1 = t[m] - sg[m][lane] * p1;
-          t[m] = p1;
-        }
-      }
-      cp = from_below(t[0], lane);
+    for (int m = M - 1; m >= 0; --m) {
+      const double gv = Sg[m][lane];
+      ph = __builtin_fma(-gv, ph, p1v[m]);
+      Cc = -gv * Cc;
     }
-    // dz2 (pointwise), then the height sums
-    double dz2[M];
+    const Aff H = scan_aff<NB, false>(Aff{Cc, ph}, b);
+    const double pnd = blk_next(H.B);
+    double pin = last ? 0.0 : pnd;
+#pragma unroll
+    for (int m = M - 1; m >= 0; --m) {
+      pin = __builtin_fma(-Sg[m][lane], pin, p1v[m]);
+      p1v[m] = pin;
+    }
+    double dz2[M], tot = 0.0;
 #pragma unroll
     for (int m = 0; m < M; ++m) {
-      const double pmk = spm[m][lane];
-      dz2[m] = -(ld(rDP, m) * (1.0 / GRAV)) * RDGAS * ld(rPT, m) *
-               exp(capa1 * log(fmax(a.p_fac * pmk, t[m] + pmk)));
-      RB_SCHED_FENCE();
+      const double pmk = Spm[m][lane];
+      const double v = -Sq[m][lane] * fm_exp(capa1 * fm_log(fmax(a.p_fac * pmk, p1v[m] + pmk)));
+      dz2[m] = real(m) ? v : 0.0;
+      dump(9, m, p1v[m]); dump(10, m, dz2[m]);
+      tot += CG ? dz2[m] * GRAV : dz2[m];
     }
-    double gz[M + 1];
+    // heights bottom-up from the surface
+    const double incl = scan_sum<NB, false>(tot, b);
+    const double base = CG ? hs : zs;
+    const double incl_d = blk_next(incl);
+    double gz = last ? base : base - incl_d;
+    double gzo[M];
 #pragma unroll
-    for (int m = 0; m <= M; ++m) gz[m] = 0.0;
-    double hs, zs, ws;
-    surf(hs, zs, ws);
-    double cg_in = cg ? hs : zs;
-#pragma unroll 1
-    for (int r = nblk - 1; r >= 0; --r) {
-      if (b == r) {
-        double go = cg_in;
-        gz[M] = go;
+    for (int m = M - 1; m >= 0; --m) {
+      gz = CG ? gz - dz2[m] * GRAV : gz - dz2[m];
+      gzo[m] = gz;
+      dump(11, m, gz);
+    }
 #pragma unroll
-        for (int m = M - 1; m >= 0; --m) {
-          if (!(PARTIAL && lastblk && m >= MV)) go = cg ? go - dz2[m] * GRAV : go - dz2[m];
-          gz[m] = go;  // the partial block: the surface up to MV
-        }
+    for (int m = 0; m < M; ++m) st(rG, m, gzo[m]);
+    st_bot(rG, base);
+    if constexpr (CG) {
+#pragma unroll
+      for (int m = 0; m < M; ++m) st(rPO, m, b == 0 && m == 0 ? a.ptop : pe[m] + pem[m]);
+      double peb = pe[M] + pem[M];
+      if constexpr (PART) {
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+          if (m == nv - 1) peb = pe[m + 1] + pem[m + 1];
       }
-      cg_in = from_below(gz[0], lane);
-    }
-    // C grid: pem again for the full pressure (outside the divergent branch: the prefix
-    // hands its carry between lanes)
-    double pemr[M + 1];
-    if (cg) {
-      double dpv[M];
-#pragma unroll
-      for (int m = 0; m < M; ++m) dpv[m] = ld(rDP, m);
-      prefix(dpv, pemr);
+      st_bot(rPO, peb);
     } else {
-#pragma unroll
-      for (int m = 0; m <= M; ++m) pemr[m] = 0.0;
-    }
-    if (valid) {
       const auto rDZ = rs(a.delz, false);
 #pragma unroll
       for (int m = 0; m < M; ++m) {
-        st(rG, m, gz[m], true);
-        if (cg) {
-          st(rPO, m, m == 0 && b == 0 ? a.ptop : pe[m] + pemr[m], true);
-        } else {
-          st(rDZ, m, dz2[m]);
-          st(rPO, m, pe[m], true);
-        }
+        st(rDZ, m, dz2[m]);
+        st(rPO, m, pe[m]);
       }
-      if (lastblk) {
-        st(rG, M, cg ? hs : zs, true);
-        st(rPO, M, cg ? pe[M] + pemr[M] : pe[M], true);
+      double peb = pe[M];
+      if constexpr (PART) {
+#pragma unroll
+        for (int m = 0; m < M; ++m)
+          if (m == nv - 1) peb = pe[m + 1];
       }
+      st_bot(rPO, peb);
     }
   }
 }
-
 
 void launch_riem(const Ctx& c, const RiemArgs& a) {
   if (a.npz < 2) throw std::runtime_error("riem: npz >= 2 required");
   const int km = a.npz;
   const int ncol = (c.d.nx + 2 * a.ring) * (c.d.ny + 2 * a.ring);
-  const dim3 gb(cdiv(cdiv(ncol, 16), RB_WAVES), c.d.nsub);
-  const dim3 gb8(cdiv(cdiv(ncol, 8), RB_WAVES), c.d.nsub);
-  const dim3 tb(64 * RB_WAVES);
-  // blocked form when the column splits into at most four blocks of an instantiated size
-  // (16 columns a wave), or into up to eight blocks of 18 with a partial last one (8 columns)
-  auto fits = [&](int m) { return km % m == 0 && km / m <= 4; };
-  const bool blk = riem_variant() != 1;
-  const bool part = blk && km == 7 * 18 + 11;  // L137
-  if (blk && fits(3)) {
-    if (a.cgrid) GT_LAUNCH((riem_blk_k<3, true>), gb, tb, 0, c.st, a);
-    else GT_LAUNCH((riem_blk_k<3, false>), gb, tb, 0, c.st, a);
-  } else if (blk && fits(5)) {
-    if (a.cgrid) GT_LAUNCH((riem_blk_k<5, true>), gb, tb, 0, c.st, a);
-    else GT_LAUNCH((riem_blk_k<5, false>), gb, tb, 0, c.st, a);
-  } else if (blk && fits(18)) {
-    if (a.cgrid) GT_LAUNCH((riem_blk_k<18, true>), gb, tb, 0, c.st, a);
-    else GT_LAUNCH((riem_blk_k<18, false>), gb, tb, 0, c.st, a);
-  } else if (part) {
-    if (a.cgrid) GT_LAUNCH((riem_blk_k<18, true, 8, 11>), gb8, tb, 0, c.st, a);
-    else GT_LAUNCH((riem_blk_k<18, false, 8, 11>), gb8, tb, 0, c.st, a);
-  } else {
-    GT_LAUNCH(riem_col_k, dim3(cdiv(ncol, BLOCK), c.d.nsub), dim3(BLOCK), 0, c.st, a);
-  }
+  const dim3 tb(64 * RS_WAVES);
+  // scan form when the column splits into NB blocks of an instantiated M (all but the last
+  // block full): (NB - 1) M < km <= NB M
+  auto fits = [&](int m, int nb) { return (nb - 1) * m < km && km <= nb * m; };
+  auto grid = [&](int nb) { return dim3(cdiv(cdiv(ncol, 64 / nb), RS_WAVES), c.d.nsub); };
+  const bool scan = riem_variant() != 1;
+  RiemArgs& am = const_cast<RiemArgs&>(a);
+  am.dbg = g_riem_dbg;
+  am.dbg_col = g_riem_dbg_col;
+#define RIEM_SCAN(M_, NB_, PART_)                                                                   \
+  do {                                                                                              \
+    if (a.cgrid) GT_LAUNCH((riem_scan_k<M_, NB_, PART_, true>), grid(NB_), tb, 0, c.st, a);        \
+    else GT_LAUNCH((riem_scan_k<M_, NB_, PART_, false>), grid(NB_), tb, 0, c.st, a);               \
+  } while (0)
+  if (scan && km == 72) RIEM_SCAN(9, 8, false);
+  else if (scan && fits(9, 8)) RIEM_SCAN(9, 8, true);
+  else if (scan && fits(9, 16)) RIEM_SCAN(9, 16, true);
+  else if (scan && fits(6, 16)) RIEM_SCAN(6, 16, true);
+  else if (scan && fits(5, 4)) RIEM_SCAN(5, 4, true);
+  else if (scan && fits(3, 4)) RIEM_SCAN(3, 4, true);
+  else if (scan && fits(2, 4)) RIEM_SCAN(2, 4, true);
+  else GT_LAUNCH(riem_col_k, dim3(cdiv(ncol, BLOCK), c.d.nsub), dim3(BLOCK), 0, c.st, a);
+#undef RIEM_SCAN
   HIP_LAUNCH_CHECK();
   // algorithmic bytes per column: C grid reads delpc ptc wc (L) gz (L+1) phis, writes gz pef (L+1);
   // D grid reads zh (L+1) delp pt w (L) phis, writes w delz (L) zh ppe pk3 (L+1) ws (+ pe peln pk)
@@ -821,7 +703,19 @@ void launch_riem(const Ctx& c, const RiemArgs& a) {
 }  // namespace
 
 void set_riem_variant(int v) { g_riem_variant = v; }
-int riem_variant() { return g_riem_variant; }
+void riem_debug(double* buf, int col) {
+  g_riem_dbg = buf;
+  g_riem_dbg_col = col;
+}
+// GTFV3_RIEM=1: the column sweeps on the step (A/B and fault isolation); the stencil
+// interface's explicit variant parameter overrides it
+int riem_variant() {
+  static const int env = [] {
+    const char* e = std::getenv("GTFV3_RIEM");
+    return e ? std::atoi(e) : 0;
+  }();
+  return g_riem_variant >= 0 ? g_riem_variant : env;
+}
 
 void riem_solver_c(const Ctx& c, int npz, double dt2, double ptop, double p_fac, double dz_min, const double* delpc,
                    const double* ptc, const double* wc, const double* phis, double* gz, double* pef,
@@ -844,7 +738,6 @@ void riem_solver_c(const Ctx& c, int npz, double dt2, double ptop, double p_fac,
   a.gam = sc.s[5];
   a.pp = sc.s[6];
   a.w2 = sc.s[13];
-  a.dump = riem_variant() == 2;
   launch_riem(c, a);
 }
 

@@ -249,7 +249,7 @@ __global__ void __launch_bounds__(256) cs_transport_ke(
 // forms, rocprof SQ counters 63-65 % of wave cycles waiting).  The same form of cs_cgrid and
 // ds_courant measured slower (1.84 -> 1.87 and 1.33 -> 1.47 ms per step): loading both
 // upwind choices of their metric terms costs more than the round trips it saves.
-bool loads_first() {
+bool loads_first_env() {
   const char* e = std::getenv("GTFV3_LOADS_FIRST");
   return !(e && e[0] == '0');
 }
@@ -968,6 +968,8 @@ inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
 
 }  // namespace
 
+bool loads_first() { return loads_first_env(); }
+
 void c_sw(const Ctx& c, const CswArgs& a) {
   c_sw_transport(c, a);
   c_sw_winds(c, a);
@@ -983,7 +985,7 @@ void c_sw_transport(const Ctx& c, const CswArgs& a) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  if (loads_first())
+  if (loads_first_env())
     GT_LAUNCH_N("cs_tmp", cs_tmp_ld, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v,
                 a.utmp, a.vtmp, a.ua, a.va);
   else
@@ -1000,7 +1002,7 @@ void c_sw_transport(const Ctx& c, const CswArgs& a) {
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (3 * e.X + 3 * e.Y + 4 * e.C) + 12 * e.C);
   Launch2D Lt{-1, -1, d.nx + 2, d.ny + 2};
-  if (loads_first())
+  if (loads_first_env())
     GT_LAUNCH_N("cs_transport_ke", cs_transport_ke_ld, g2(d, Lt, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
                 a.npz, a.dt2, a.delp, a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke);
   else
@@ -1021,7 +1023,7 @@ void c_sw_winds(const Ctx& c, const CswArgs& a) {
   GT_LAUNCH(cs_vort, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.vort);
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (e.X + e.Y + e.K) + 4 * e.C);
-  if (loads_first())
+  if (loads_first_env())
     GT_LAUNCH_N("cs_update", cs_update_ld, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2,
                 a.u, a.v, a.vort, a.ke, a.uc, a.vc);
   else
@@ -1052,7 +1054,7 @@ void d_sw_courant(const Ctx& c, const DswArgs& a) {
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   const int klb = kloop_levels(), nkb = klb ? (a.npz + klb - 1) / klb : 0;
   if (klb) {
-    if (loads_first())
+    if (loads_first_env())
       GT_LAUNCH_N("ds_utvt1_kl", ds_utvt1_kl<true>, kloop_grid(full, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs,
                   c.met, a.npz, nkb, klb, a.dt, a.uc, a.vc, a.ut, a.vt);
     else
@@ -1135,7 +1137,7 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
   const bool dcon = a.d_con > 1e-5, vdamp = a.vtdm4 > 1e-5;
   // GTFV3_LOADS_FIRST=0: the branch-ordered form (same results, bit for bit)
-  if (!loads_first()) {
+  if (!loads_first_env()) {
     GT_LAUNCH(ds_ke, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.hord_mt, a.dddmp,
                        a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke, a.nord,
                        dcon ? a.vd : nullptr);

@@ -138,8 +138,10 @@ def fv_dynamics(st, ak, bk, g, nl):
     _halo(g, st, [("zh", "c")])
     ords = (nl["hord_mt"], nl["hord_vt"], nl["hord_tm"], nl["hord_dp"])
     nord, d_con = int(nl.get("nord", 0)), float(nl.get("d_con", 0.0))
-    damp_kw = dict(nord=nord, d4_bg=float(nl.get("d4_bg", 0.0)), vtdm4=float(nl.get("vtdm4", 0.0)),
-                   nord_v=int(nl.get("nord_v", 0)), d_con=d_con)
+    # fv_core_nml: nord_v = min(2, nord) unless given; vtdm4 only with do_vort_damp
+    vtdm4 = float(nl.get("vtdm4", 0.0)) if nl.get("do_vort_damp", 0) else 0.0
+    damp_kw = dict(nord=nord, d4_bg=float(nl.get("d4_bg", 0.0)), vtdm4=vtdm4,
+                   nord_v=int(nl.get("nord_v", min(2, nord))), d_con=d_con)
     if nord > 0:
         st["divgd"] = np.zeros(shp)
     if d_con > 1e-5:

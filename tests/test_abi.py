@@ -97,3 +97,20 @@ def test_no_kernel_uses_scratch(pkg, tmp_path):
                     bad.append(name)
     assert nkern > 20
     assert not bad, f"kernels using scratch memory: {bad}"
+
+
+def test_config_separators_and_malformed_values(pkg):
+    """GTFV3_CONFIG items split on ',' or ';' (INTEGRATION.md's comma form); a value that is
+    not a whole number (or not an integer for an integer key) is an error, never truncated"""
+    lib = pkg.lib()
+    buf = ctypes.create_string_buffer(256)
+    ok = lib.gtfv3_create(b"npx=13, npz=3; nq=1,host_only=1,n_split=5 ,hord_mt=5", 0, 1, None)
+    assert ok
+    lib.gtfv3_destroy(ok)
+    for bad, what in ((b"npx=13,npz=3,nq=1,host_only=1,n_split=6x", b"n_split"),
+                      (b"npx=13,npz=3,nq=1,host_only=1,n_split=6.5", b"n_split"),
+                      (b"npx=13,npz=3,nq=1,host_only=1,d4_bg=", b"d4_bg"),
+                      (b"npx=13,npz=3,nq=1,host_only=1,nord=2,d4_bg=0.15,vtdm4=0.05x", b"vtdm4")):
+        h = lib.gtfv3_create(bad, 0, 1, None)
+        assert not h, bad
+        assert lib.geos_gtfv3_last_error(buf, 256) > 0 and what in buf.value, buf.value

@@ -206,3 +206,55 @@ def test_c360_l137_54_tracers_step_properties(pkg, require_gpu):
         print(f"C360 L137 x 54: total {time.time() - t0:.0f} s")
     finally:
         d.close()
+
+
+def test_c720_l137_54_rank_proxy8_step_properties(pkg, require_gpu):
+    """Config 5 at its own geometry, as one GPU's share of the 8-GPU run: C720 L137 x 54
+    tracers, layout 1x4 (bench.py's 8-GPU layout: bands of 720 x 180, three per rank), rank 0
+    of 8 alone on the GPU with the null transport (anchor: held_suarez.py:320 for L137).  The
+    cross-rank messages are dropped and not unpacked, so the remote halo points keep the
+    initial state's values: the rank's state stays physical, stale only within reach of its
+    cross-rank edges.  After one step: every field finite and bounded over the rank's whole
+    compute domain, no negative tracer after fill and no tracer above its initial maximum by
+    more than 1e-9 of it (the stale halo values lie within the initial ranges too).  Set-up
+    uploads the tracers one at a time (the host never holds all 54 at this size)."""
+    import time
+    state = importlib.import_module(pkg.__name__ + ".state")
+    npx, npz, nq, dt = 721, 137, 54, 112.5
+    t0 = time.time()
+    d = pkg.Domain(0, 8, None, npx=npx, npz=npz, nq=nq, layout_x=1, layout_y=4, dt=dt, loopback=-1)
+    try:
+        assert (d.nsub, d.nx, d.ny) == (3, 720, 180)
+        ak, bk, ks = state.hybrid_levels(npz)
+        st = state.jablonowski_williamson(d, ak, bk, tracers=1)
+        d.set_vertical(ak, bk, ks)
+        for k, v in st.items():
+            if k != "q":
+                d.upload(k, v)
+        d.create("q", nq * npz)
+        d.upload_levels("q", 0, st["q"])
+        for iq in range(1, nq):
+            d.upload_levels("q", iq * npz, state.tracer_planes(d, iq))
+        del st
+        s0 = d.tracer_stats()
+        print(f"C720 L137 x 54 rank proxy 8: set-up {time.time() - t0:.0f} s", flush=True)
+        d.step(1)
+        s1 = d.tracer_stats()
+        assert np.all(s1[:, 3] == 0), "non-finite tracer values"
+        print("min q", f"{s1[:, 1].min():.2e}", "max overshoot", f"{(s1[:, 2] / s0[:, 2] - 1).max():.2e}",
+              "mass change", f"{(np.abs(s1[:, 0] - s0[:, 0]) / s0[:, 0]).max():.2e}", flush=True)
+        assert np.all(s1[:, 1] >= 0.0), s1[:, 1]
+        assert np.all(s1[:, 2] <= (1.0 + 1e-9) * s0[:, 2]), s1[:, 2] / s0[:, 2]
+        c = (Ellipsis, slice(NG, NG + d.ny), slice(NG, NG + d.nx))
+        for k in ("u", "v", "w", "pt", "delp", "delz", "ps"):
+            a = d.download(k)[c]
+            assert np.all(np.isfinite(a)), k
+            if k == "pt":
+                assert 150.0 < a.min() and a.max() < 400.0
+            if k in ("u", "v"):
+                assert np.abs(a).max() < 150.0
+            if k == "ps":
+                assert 9.0e4 < a.min() and a.max() < 1.1e5
+        print(f"C720 L137 x 54 rank proxy 8: total {time.time() - t0:.0f} s")
+    finally:
+        d.close()

@@ -126,7 +126,7 @@ def test_d_sw_damping_c180(pkg, require_gpu, case):
         d.close()
 
 
-DAMP_NL = dict(nord=2, d4_bg=0.15, vtdm4=0.05, nord_v=1, d_con=1.0)
+DAMP_NL = dict(nord=2, d4_bg=0.15, vtdm4=0.05, do_vort_damp=1, nord_v=1, d_con=1.0)
 
 
 def test_step_with_damping_namelist(pkg, require_gpu):

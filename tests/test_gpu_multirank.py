@@ -49,11 +49,13 @@ def _run_ranks(pkg, nranks, layout, npx=13, npz=10, nq=2):
     return doms, out
 
 
-@pytest.mark.parametrize("nranks,layout,npx", [(2, (1, 1), 13), (4, (1, 2), 13), (6, (1, 1), 13), (6, (1, 1), 49), (8, (2, 2), 13),
-                                                  (8, (1, 4), 25)])
-def test_multirank_step_matches_single_rank(pkg, require_gpu, nranks, layout, npx):
+@pytest.mark.parametrize("nranks,layout,npx,npz", [(2, (1, 1), 13, 10), (4, (1, 2), 13, 10), (6, (1, 1), 13, 10),
+                                                      (6, (1, 1), 49, 10), (8, (2, 2), 13, 10), (8, (1, 4), 25, 10),
+                                                      (6, (1, 1), 181, 72)])
+def test_multirank_step_matches_single_rank(pkg, require_gpu, nranks, layout, npx, npz):
+    """(6, 1x1, C180 L72): BASELINE.json config 3's layout (one tile per rank, held_suarez.py:149-151)
+    at its own size"""
     state = importlib.import_module(pkg.__name__ + ".state")
-    npz = 10
     ak, bk, ks = state.hybrid_levels(npz)
     ref = pkg.Domain(npx=npx, npz=npz, nq=2, layout_x=layout[0], layout_y=layout[1])
     st = state.jablonowski_williamson(ref, ak, bk)
