@@ -18,8 +18,9 @@ Prints ONE JSON line on rank 0 (contract in DESIGN.md §Measurement):
                    step_bytes (every kernel's algorithmic bytes, bytes_manifest.yaml, as
                    registered by the launchers on the probe step) / ms_per_step -> step_frac
   cpu_baseline     the numpy oracle (oracle/fv_dynamics.py) timed for one step on a
-                   bounded sample (C48 L72, 6 tiles, ~20 s of one core) on the host, rank 0
-                   only; the host's CPU count and this process's affinity are recorded
+                   bounded sample (C48 L72, 6 tiles, ~20 s per core) on the host, rank 0
+                   only, as --cpu-procs concurrent single-threaded replicas (one per core);
+                   the host's CPU count and this process's affinity are recorded
 """
 import argparse
 import json
@@ -161,6 +162,8 @@ def parse():
     p.add_argument("--cpu-npx", type=int, default=0,
                    help="cpu_baseline sample grid npx (default 49: C48 L72, 6 tiles, ~20 s of one host core; "
                         "13 with --moist, ~40 s)")
+    p.add_argument("--cpu-procs", type=int, default=8,
+                   help="cpu_baseline: concurrent single-threaded oracle replicas (= host cores used)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timing", action="store_true")
     p.add_argument("--kernel-report", default="", help="write per-kernel stats JSON here")
@@ -182,12 +185,36 @@ def parse():
     return p.parse_args()
 
 
-def cpu_baseline(pkg, npx, npz, nq, dt, moist=False):
-    """One oracle fv_dynamics step (+ the oracle moist column step with --moist) of a
-    bounded sample, single host core."""
-    import importlib
-
+def _cpu_replica(args):
+    """one oracle step in a child process (numpy only: the child never loads the HIP library)"""
+    st, ak, bk, grid, nl, moist, cd_info, barrier = args
     from oracle import fv_dynamics as fvd
+    g = fvd.Grid(*grid)
+    barrier.wait()
+    t0 = time.perf_counter()
+    out = fvd.fv_dynamics(st, ak, bk, g, nl)
+    if moist:
+        from oracle import NG
+        from oracle import geos_moist as gm
+        nsub, ny, nx, npz, dt = cd_info
+        cd = (Ellipsis, slice(NG, NG + ny), slice(NG, NG + nx))  # the compute domain (the padded
+        for s in range(nsub):                                    # plane's outer cells are not state)
+            q = out["q"][s]
+            sp = [q[n * npz:(n + 1) * npz][cd] for n in range(6)]
+            gm.aquaplanet_physics(dt, out["pt"][s][cd], *sp, out["delp"][s][cd], out["delz"][s][cd],
+                                  out["pe"][s][cd], out["w"][s][cd])
+    return time.perf_counter() - t0
+
+
+def cpu_baseline(pkg, npx, npz, nq, dt, moist=False, procs=8):
+    """The oracle fv_dynamics step (+ the oracle moist column step with --moist) of a bounded
+    sample, timed on the host: `procs` single-threaded processes each run the same step at
+    once (the oracle's tiles exchange halos every acoustic sub-step inside one process, so
+    a step does not split over processes; concurrent replicas measure what `procs` host
+    cores sustain).  value = sum over replicas of cells / own step time."""
+    import importlib
+    import multiprocessing as mp
+
     state = importlib.import_module(pkg.__name__ + ".state")
     d = pkg.Domain(npx=npx, npz=npz, nq=nq, host_only=1, dt=dt)
     ak, bk, ks = state.hybrid_levels(npz)
@@ -196,33 +223,38 @@ def cpu_baseline(pkg, npx, npz, nq, dt, moist=False):
         state.aquaplanet_tracers(d, st, ak, bk)
     from oracle import grid as og  # the oracle's own grid (tests/test_oracle_grid.py pins grid.cpp to it)
     ms, sc = og.domain_metrics(d.subs, d.nx, d.ny, d.N, d.pitch, d.nj)
-    g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
+    grid = (d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
     nl = dict(n_split=6, dt_atmos=dt, hord_mt=6, hord_vt=6, hord_tm=6, hord_dp=6, hord_tr=6, dddmp=0.2, d2_bg=0.0,
               p_fac=0.05, dz_min=2.0, fill=1, nq=nq)
-    t0 = time.perf_counter()
-    out = fvd.fv_dynamics(st, ak, bk, g, nl)
-    if moist:
-        from oracle import NG
-        from oracle import geos_moist as gm
-        cd = (Ellipsis, slice(NG, NG + d.ny), slice(NG, NG + d.nx))  # the compute domain (the padded
-        for s in range(d.nsub):                                      # plane's outer cells are not state)
-            q = out["q"][s]
-            sp = [q[n * npz:(n + 1) * npz][cd] for n in range(6)]
-            gm.aquaplanet_physics(dt, out["pt"][s][cd], *sp, out["delp"][s][cd], out["delz"][s][cd],
-                                  out["pe"][s][cd], out["w"][s][cd])
-    el = time.perf_counter() - t0
+    cd_info = (d.nsub, d.ny, d.nx, npz, dt)
     cells = 6 * d.N * d.N * npz
+    N = d.N
     d.close()
+    env = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS", "MKL_NUM_THREADS")}
+    for k in env:
+        os.environ[k] = "1"  # one core per replica; the spawned children inherit this
+    try:
+        ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's GPU state
+        with ctx.Manager() as man:
+            bar = man.Barrier(procs)
+            with ctx.Pool(procs) as pool:
+                els = pool.map(_cpu_replica, [(st, ak, bk, grid, nl, moist, cd_info, bar)] * procs)
+    finally:
+        for k, v in env.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
     try:
         aff = sorted(os.sched_getaffinity(0))
     except AttributeError:
         aff = []
-    return dict(value=cells / el, unit="grid-cell-updates/s", cores=1, kind="port",
+    return dict(value=sum(cells / e for e in els), unit="grid-cell-updates/s", cores=procs, kind="port",
                 host_cpus=os.cpu_count(), affinity=f"{len(aff)} cpus ({aff[0]}-{aff[-1]})" if aff else None,
-                sample=f"one fv_dynamics step{' + moist physics' if moist else ''}, C{d.N} L{npz} nq={nq}, "
-                       f"6 tiles, numpy fp64 oracle "
-                       f"(oracle/fv_dynamics.py), {el:.1f} s on 1 host core (numpy single-threaded; the "
-                       f"process may run on any of the affinity set)")
+                per_core=cells / float(np.median(els)),
+                sample=f"one fv_dynamics step{' + moist physics' if moist else ''}, C{N} L{npz} nq={nq}, "
+                       f"6 tiles, numpy fp64 oracle (oracle/fv_dynamics.py), {procs} concurrent single-threaded "
+                       f"replicas (one per core), step times {min(els):.1f}-{max(els):.1f} s")
 
 
 def main():
@@ -405,7 +437,7 @@ def main():
     if rank == 0 and world == 1 and not a.no_cpu_baseline:
         # the moist oracle's column loops are ~40x slower per cell than its dycore: C12 with --moist
         cpu_npx = a.cpu_npx if a.cpu_npx > 0 else (13 if a.moist else 49)
-        cpu = cpu_baseline(pkg, cpu_npx, a.npz, nq, a.dt, a.moist)
+        cpu = cpu_baseline(pkg, cpu_npx, a.npz, nq, a.dt, a.moist, max(1, a.cpu_procs))
 
     if rank == 0:
         out = {

@@ -695,7 +695,7 @@ void Dycore::step() {
                                nl.d_con, (double)nl.nord, (double)nl.nord_v, (double)nl.hord_mt, (double)nl.hord_vt,
                                (double)nl.hord_tm, (double)nl.hord_dp,
                                // launch-shape switches read at every launch (tests flip them in-process)
-                               (double)kloop_levels(), (double)loads_first(), (double)c_sw_fused(),
+                               (double)kloop_levels(), (double)loads_first(),
                                (double)riem_variant()};
     for (const Field* f : {&u, &v, &w, &delz, &pt, &delp, &phis})
       key.push_back((double)reinterpret_cast<uintptr_t>(f->p));

@@ -12,17 +12,12 @@ struct CswArgs {
   double *uc, *vc, *ua, *va, *ut, *vt;  // outputs (ut, vt: dt2 * area fluxes)
   double *delpc, *ptc, *wc;
   double *utmp, *vtmp, *ke, *vort;  // scratch
-  // first stage as one column march (csw_march.hip; utmp / vtmp unused) or the kernel chain
-  // (sw.hip); -1: c_sw_fused()
-  int march = -1;
 };
 void c_sw(const Ctx& c, const CswArgs& a);            // the two stages in order
 void c_sw_transport(const Ctx& c, const CswArgs& a);  // d2a2c_vect, delpc / ptc / wc, ke
 void c_sw_winds(const Ctx& c, const CswArgs& a);      // vorticity, uc / vc update
-bool c_sw_fused();                                           // GTFV3_CSW_FUSED=1 (default off)
 bool loads_first();                                          // GTFV3_LOADS_FIRST (default on)
 int kloop_levels();                                          // GTFV3_KLOOP (stencil_common.hpp)
-void c_sw_transport_march(const Ctx& c, const CswArgs& a);  // the first stage as one march
 
 struct DswArgs {
   int npz;

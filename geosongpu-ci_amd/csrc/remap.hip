@@ -16,6 +16,7 @@
 #include <type_traits>
 #include <utility>
 
+#include "blockscan.hpp"
 #include "kernels_nh.hpp"
 #include "stencil_common.hpp"
 
@@ -950,6 +951,352 @@ __global__ void __launch_bounds__(64) remap_reg_k(RemapArgs a) {
   }
 }
 
+// ---------------- level-block form (default where instantiated) ----------------
+//
+// A job's column split into NB level blocks on NB consecutive lanes of one 16-lane DPP row
+// (lane = NB * column + b; block b: source layers / edges b M .. b M + M - 1), as the SIM1
+// solver's scan form (riem.hip, blockscan.hpp).  Every stage runs on all lanes:
+//   * the kord = 9 edge values: cs_profile's tridiagonal system (the bottom edge eliminated
+//     into the last real row, so the km unknowns fill the blocks), solved by tri_solve with
+//     Möbius-scan pivots (strongly diagonally dominant rows [1, 2 + 2 d4, d4]), then the
+//     large-scale constraints pointwise -- the neighbouring blocks' means by DPP;
+//   * the PPM coefficients of each layer (cs_limiters) pointwise;
+//   * map1_ppm through the mass function Q(p) = integral of the profile from the top to p:
+//     each block forms its layers' running mass, a scan of the block totals gives each block
+//     its offset, each block evaluates Q at the target interfaces inside its source range
+//     (the profile's partial integral in the layer holding the interface) into LDS, and each
+//     target layer's mean is (Q(bottom) - Q(top)) / dp -- taken from block-local values when
+//     both interfaces lie in one block, so the column's mass above does not cancel there.
+// The same expressions as cs_profile / map1_ppm, associated differently (sums through the
+// scan, a target's pieces as a difference of running integrals): agreement with the oracle and
+// the column forms to rounding (tests/test_gpu_remap.py), not bit for bit.  No scratch planes;
+// each job's source column and output field move once, the source edges once per job.
+constexpr int RB_WAVES = 4;
+typedef unsigned int RbU2 __attribute__((ext_vector_type(2)));
+template <int M, int NB, bool PART, int JK>
+__global__ void __launch_bounds__(64 * RB_WAVES) remap_blk_k(RemapArgs a) {
+  constexpr int NC = 64 / NB, KX = NB * M;  // KX: the largest level count of this shape
+  __shared__ double lab[2 * (KX + 1)];                 // ak | bk
+  __shared__ double lq[RB_WAVES][NC][KX + 1];          // block-local Q at target interface k
+  __shared__ double lt[RB_WAVES][NC][KX + 1];          // target interface k
+  __shared__ int lown[RB_WAVES][NC][KX + 1];           // the block holding target interface k
+  __shared__ double loff[RB_WAVES][NC][NB];            // Q at each block's top edge
+  const int km = a.npz;  // launcher: (NB - 1) M < km <= NB M
+  for (int k = threadIdx.x; k <= km; k += 64 * RB_WAVES) {
+    lab[k] = a.ak[k];
+    lab[KX + 1 + k] = a.bk[k];
+  }
+  __syncthreads();
+  const Dims d = a.d;
+  const double ptop = a.ptop;
+  const int fill = a.fill;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = lane & (NB - 1), cl = lane / NB;
+  const bool last = b == NB - 1;
+  const int nv = PART && last ? km - (NB - 1) * M : M;  // real layers of this block
+  auto real = [&](int m) { return !PART || m < nv; };
+  const int job = JK == JK_PT ? J_PT : JK == JK_DZ ? J_DZ : JK == JK_W ? J_W
+                : JK == JK_UV ? J_U + (int)blockIdx.y : J_Q0 + (int)blockIdx.y;
+  const int s = blockIdx.z;
+  // the job's columns: cells nx x ny, u edges nx x (ny + 1), v edges (nx + 1) x ny
+  const int ni = job == J_V ? d.nx + 1 : d.nx, nj = job == J_U ? d.ny + 1 : d.ny;
+  const int ncol = ni * nj;
+  const int c0 = (blockIdx.x * RB_WAVES + wv) * NC;
+  if (c0 >= ncol) return;  // whole wavefront (no barrier follows)
+  int c = c0 + cl;
+  const bool valid = c < ncol;
+  if (!valid) c = ncol - 1;
+  const int i = c % ni, j = c / ni;
+  const long P = d.plane, o = pidx(d, i, j);
+  const uint32_t PB = (uint32_t)P * 8u, vo = (uint32_t)o * 8u;
+  const uint32_t vb = vo + (uint32_t)(b * M) * PB;  // the block's first level
+  auto rsrc = [&](const double* base, int nk) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(nk * PB), 0x00020000);
+  };
+  auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t v, int lev) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, v, (uint32_t)lev * PB, 0));
+  };
+  const double* pe_s = a.S.pe + (long)s * (km + 1) * P;
+  const auto rPE = rsrc(pe_s, km + 1);
+  auto rEA = rPE;
+  uint32_t vob = vo;
+  constexpr bool ewind = JK == JK_UV;
+  constexpr int tkind = JK == JK_PT ? 1 : (JK == JK_UV ? 2 : 0);
+  constexpr int iv = JK == JK_W ? -2 : (JK == JK_UV ? -1 : (JK == JK_Q ? 0 : 1));
+  const double ps = ld(rPE, vo, km);
+  double lntop = 0.0, lnbot = 0.0, pb = 0.0, qs = 0.0;
+  const double* src;
+  double* out;
+  const long slot = ((long)s * a.nslot + job) * (km + 1) * P;
+  if (JK == JK_PT) {
+    rEA = rsrc(a.S.peln + (long)s * (km + 1) * P, km + 1);
+    lntop = ld(rEA, vo, 0);
+    lnbot = ld(rEA, vo, km);
+    src = a.src + slot;
+    out = a.S.pt + (long)s * km * P;
+  } else if (JK == JK_DZ) {
+    src = a.src + slot;
+    out = a.S.delz + (long)s * km * P;
+  } else {
+    double* f;
+    if (JK == JK_W) {
+      f = a.S.w + (long)s * km * P;
+      qs = a.S.ws[(long)s * P + o];
+    } else if (JK == JK_UV) {
+      f = (job == J_U ? a.S.u : a.S.v) + (long)s * km * P;
+      const long w = job == J_U ? -d.pitch : -1;
+      vob = (uint32_t)(o + w) * 8u;
+      pb = ld(rPE, vob, km) + ps;
+    } else {
+      f = a.S.q + ((long)s * a.nq + (job - J_Q0)) * km * P;
+    }
+    src = f;
+    out = f;
+  }
+  const auto rSRC = rsrc(src, km), rOUT = rsrc(out, km);
+  // source edge of the block's local interface m (levels past the bottom read 0 -> replaced)
+  auto Eloc = [&](int m) -> double {
+    const int lev = b * M + m;
+    if (!ewind) return ld(rEA, vb, m);
+    const double x0 = ld(rEA, vb, m);
+    const double x1 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rEA, vob + (uint32_t)(b * M) * PB,
+                                                                                       (uint32_t)m * PB, 0));
+    return lev == 0 ? x0 : 0.5 * (x1 + x0);
+  };
+  auto T = [&](int k) -> double {
+    if (tkind == 0) return k == 0 ? ptop : (k == km ? ps : lab[k] + lab[KX + 1 + k] * ps);
+    if (tkind == 1) return k == 0 ? lntop : (k == km ? lnbot : fm_log(lab[k] + lab[KX + 1 + k] * ps));
+    return lab[k] + 0.5 * lab[KX + 1 + k] * pb;
+  };
+
+  // ---- loads: means and edges of the block (a partial block's virtual layers: A = 0, edges
+  // held at its bottom edge, so their thickness is 0)
+  double A[M], Ev[M + 1];
+#pragma unroll
+  for (int m = 0; m < M; ++m) A[m] = ld(rSRC, vb, m);
+#pragma unroll
+  for (int m = 0; m <= M; ++m) Ev[m] = Eloc(m);
+  if constexpr (PART) {
+    double eb = Ev[M];
+#pragma unroll
+    for (int m = 0; m <= M; ++m)
+      if (m == nv) eb = Ev[m];
+#pragma unroll
+    for (int m = 0; m <= M; ++m) Ev[m] = m > nv ? eb : Ev[m];
+  }
+  double dp[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) dp[m] = Ev[m + 1] - Ev[m];
+  // neighbouring blocks' means and thicknesses (shifted outside any select; blockscan.hpp)
+  const double am1_ = blk_prev(A[M - 1]), am2_ = blk_prev(A[M - 2 >= 0 ? M - 2 : 0]), dpm1_ = blk_prev(dp[M - 1]);
+  const double ap1_ = blk_next(A[0]), ap2_ = blk_next(A[M > 1 ? 1 : 0]);
+  const double am1 = b == 0 ? 0.0 : am1_, am2 = b == 0 ? 0.0 : am2_, dpm1 = b == 0 ? 1.0 : dpm1_;
+  const double ap1 = last ? 0.0 : ap1_, ap2 = last ? 0.0 : ap2_;
+  // mean of local layer m in [-2, M + 1]
+  auto Aw = [&](int m) -> double {
+    return m == -2 ? am2 : m == -1 ? am1 : m == M ? ap1 : m == M + 1 ? ap2 : A[m < 0 ? 0 : (m > M - 1 ? M - 1 : m)];
+  };
+  auto dpw = [&](int m) -> double { return m < 0 ? dpm1 : dp[m]; };
+  auto glob = [&](int m) { return b * M + m; };
+
+  // ---- edge values: rows e = 0 .. km - 1 (cs_profile's system with q[km] eliminated from the
+  // last row; iv = -2: q[km] = qs given)
+  double abot = 0.0, dbot = 1.0, rbot = 0.0;  // the bottom edge's row (iv != -2), last block
+  if constexpr (iv != -2) {
+    double d4b = 0.0, a1 = 0.0, a2 = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (m == nv - 1) {  // the column's last layer (last block)
+        d4b = dpw(m - 1) / dp[m];
+        a1 = A[m];
+        a2 = Aw(m - 1);
+      }
+    abot = 1.0 + d4b * (d4b + 1.5);
+    dbot = d4b * (d4b + 0.5);
+    rbot = 2.0 * d4b * (d4b + 1.0) * a1 + a2;
+  }
+  auto row = [&](int m, double& am, double& dg, double& cm) {
+    const int e = glob(m);
+    const bool bt = last && m == nv - 1;  // row km - 1
+    if (!real(m)) {
+      am = 0.0; dg = 1.0; cm = 0.0;
+      return;
+    }
+    if (e == 0) {
+      am = 0.0;
+      if (iv == -2) {
+        dg = 1.0; cm = 0.5;
+      } else {
+        const double grat = dp[1 < M ? 1 : 0] / dp[0];
+        dg = grat * (grat + 0.5);
+        cm = 1.0 + grat * (grat + 1.5);
+      }
+      return;
+    }
+    const double d4 = dpw(m - 1) / dp[m];
+    am = 1.0;
+    dg = 2.0 + d4 + d4;
+    cm = d4;
+    if (bt) {
+      if (iv == -2) cm = 0.0;
+      else {
+        dg = dg - cm * abot / dbot;
+        cm = 0.0;
+      }
+    }
+  };
+  auto rhs = [&](int m) -> double {
+    const int e = glob(m);
+    const bool bt = last && m == nv - 1;
+    if (!real(m)) return 0.0;
+    if (e == 0) {
+      if (iv == -2) return 1.5 * A[0];
+      const double grat = dp[1 < M ? 1 : 0] / dp[0];
+      return (grat + grat) * (grat + 1.0) * A[0] + A[1 < M ? 1 : 0];
+    }
+    const double d4 = dpw(m - 1) / dp[m];
+    double r = iv == -2 ? 3.0 * (Aw(m - 1) + A[m]) : 3.0 * (Aw(m - 1) + d4 * A[m]);
+    if (bt) r = iv == -2 ? r - d4 * qs : r - d4 * rbot / dbot;
+    return r;
+  };
+  double qe[M];
+  tri_solve<M, NB, true>(row, rhs, qe, b, last);
+  // the bottom edge q[km] (last block)
+  double qlast = qe[M - 1];
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+    if (m == nv - 1) qlast = qe[m];
+  const double qbot = iv == -2 ? qs : (rbot - abot * qlast) / dbot;
+  // large-scale constraints of edges 1 .. km - 1
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int e = glob(m);
+    double v = qe[m];
+    const double a0 = Aw(m - 1), a1 = A[m];
+    if (e == 1 || e == km - 1) {
+      v = fmin(v, fmax(a0, a1));
+      v = fmax(v, fmin(a0, a1));
+    } else if (e >= 2 && e <= km - 2) {
+      const double g0 = a0 - Aw(m - 2), g1 = Aw(m + 1) - a1;
+      if (g0 * g1 > 0.0) {
+        v = fmin(v, fmax(a0, a1));
+        v = fmax(v, fmin(a0, a1));
+      } else if (g0 > 0.0) {
+        v = fmax(v, fmin(a0, a1));
+      } else {
+        v = fmin(v, fmax(a0, a1));
+        if (iv == 0) v = fmax(0.0, v);
+      }
+    }
+    qe[m] = real(m) ? v : 0.0;
+  }
+  const double qn_ = blk_next(qe[0]);
+  // edge at local interface m + 1 of layer m
+  auto qr = [&](int m) -> double {
+    if (m + 1 < M) return (last && m == nv - 1) ? qbot : qe[m + 1 < M ? m + 1 : 0];
+    return last ? qbot : qn_;
+  };
+
+  // ---- running mass of the block, block offsets
+  double C[M + 1];
+  C[0] = 0.0;
+#pragma unroll
+  for (int m = 0; m < M; ++m) C[m + 1] = C[m] + A[m] * dp[m];
+  const double offx = blk_prev(scan_sum<NB, true>(C[M], b));
+  const double off = b == 0 ? 0.0 : offx;
+  loff[wv][cl][b] = off;
+  // the target interfaces in the block's source range [Ev[0], Ev[M]) (the last block's
+  // last real layer takes every remaining one, k = km included)
+  int k = b * M < km ? b * M : km;
+  if (b == 0) {
+    k = 0;
+  } else {
+    while (k > 0 && T(k - 1) >= Ev[0]) --k;
+    while (k <= km && T(k) < Ev[0]) ++k;
+  }
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    if (!real(m)) continue;
+    // PPM coefficients of layer l (kord = 9 cs_profile + cs_limiters)
+    const int l = glob(m);
+    auto gm = [&](int mm) { return Aw(mm) - Aw(mm - 1); };
+    auto extm = [&](int mm) { return gm(mm) * gm(mm + 1) < 0.0; };
+    const double av = A[m];
+    double AL = qe[m], AR = qr(m), A6;
+    if (l == 0) {
+      if (iv == 0) AL = fmax(0.0, AL);
+      else if (iv == -1 && AL * av <= 0.0) AL = 0.0;
+      A6 = 3.0 * (2.0 * av - (AL + AR));
+      lim(av, AL, AR, A6, false, 1);
+    } else if (l == 1) {
+      A6 = 3.0 * (2.0 * av - (AL + AR));
+      lim(av, AL, AR, A6, extm(m), 2);
+    } else if (l < km - 2) {
+      const bool el = extm(m);
+      if ((el && extm(m - 1)) || (el && extm(m + 1))) {
+        AL = av; AR = av; A6 = 0.0;
+      } else {
+        A6 = 6.0 * av - 3.0 * (AL + AR);
+        if (fabs(A6) > fabs(AL - AR)) {
+          double pmp_1 = av - 2.0 * gm(m + 1);
+          double lac_1 = pmp_1 + 1.5 * gm(m + 2);
+          AL = fmin(fmax(AL, fmin(fmin(av, pmp_1), lac_1)), fmax(fmax(av, pmp_1), lac_1));
+          double pmp_2 = av + 2.0 * gm(m);
+          double lac_2 = pmp_2 - 1.5 * gm(m - 1);
+          AR = fmin(fmax(AR, fmin(fmin(av, pmp_2), lac_2)), fmax(fmax(av, pmp_2), lac_2));
+          A6 = 6.0 * av - 3.0 * (AL + AR);
+        }
+      }
+      if (iv == 0) lim(av, AL, AR, A6, el, 0);
+    } else if (l == km - 2) {
+      A6 = 3.0 * (2.0 * av - (AL + AR));
+      lim(av, AL, AR, A6, extm(m), 2);
+    } else {
+      if (iv == 0) AR = fmax(0.0, AR);
+      else if (iv == -1 && AR * av <= 0.0) AR = 0.0;
+      A6 = 3.0 * (2.0 * av - (AL + AR));
+      lim(av, AL, AR, A6, false, 1);
+    }
+    // Q at the target interfaces inside layer l: C + the profile's integral from its top
+    const bool lastlayer = last && m == nv - 1;
+    const double e0 = Ev[m], e1 = Ev[m + 1], rdp = 1.0 / dp[m];
+    while (k <= km) {
+      const double t = T(k);
+      if (!lastlayer && t >= e1) break;
+      const double y = t - e0, x = y * rdp;
+      lq[wv][cl][k] = C[m] + y * (AL + 0.5 * x * (AR - AL + A6 * (1.0 - R23 * x)));
+      lt[wv][cl][k] = t;
+      lown[wv][cl][k] = b;
+      ++k;
+    }
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  // ---- target layer means for levels b M .. b M + M - 1
+  bool neg = false;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const int kk = glob(m);
+    if (kk >= km) break;
+    const int o0 = lown[wv][cl][kk], o1 = lown[wv][cl][kk + 1];
+    const double q0 = lq[wv][cl][kk], q1 = lq[wv][cl][kk + 1];
+    const double num = o0 == o1 ? q1 - q0 : (loff[wv][cl][o1] - loff[wv][cl][o0]) + (q1 - q0);
+    const double v = num / (lt[wv][cl][kk + 1] - lt[wv][cl][kk]);
+    if (valid)
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), rOUT, vb, (uint32_t)m * PB, 0);
+    neg = neg || v < 0.0;
+  }
+  if constexpr (JK == JK_Q) {
+    // fillz: one lane of a column with a negative value walks the column (rare)
+    const unsigned long long any = __ballot(neg);
+    const bool col_neg = ((any >> (cl * NB)) & ((NB == 64 ? ~0ull : (1ull << NB) - 1))) != 0;
+    if (fill && col_neg && b == 0 && valid) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      fillz_col(Col{out + o, P}, [&](int k2) { return lt[wv][cl][k2 + 1] - lt[wv][cl][k2]; }, km);
+    }
+  }
+}
+
 // Eulerian state from the remapped fields, one lane per (column, interface k = 0 .. km): the
 // top interface of layer k is ptop (k = 0) or ak + bk ps, its log the stored peln (k = 0, km)
 // or the log of that -- the same values a top-down walk carries from layer to layer
@@ -1032,10 +1379,46 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
     HIP_LAUNCH_CHECK();
     gt_bytes(L * 5 * e.C);  // delp delz pt read, T_v and -delz/delp source columns written
   }
-  // register-resident columns for the instantiated level counts (L72 of the benchmark and
-  // the L10 / L12 / L20 test configurations), the scratch-column jobs otherwise (L137)
-  const bool reg = variant != 1 && (npz == 72 || npz == 10 || npz == 12 || npz == 20);
-  if (reg) {
+  // variant 0: the level-block form where a shape is instantiated ((NB - 1) M < npz <= NB M);
+  // 2: the register-resident columns (L10 / 12 / 20 / 72); 1 (or no shape): the scratch-column jobs
+  auto fits = [&](int m, int nb) { return (nb - 1) * m < npz && npz <= nb * m; };
+  auto blk = [&](auto Mc, auto NBc, auto PARTc) {
+    constexpr int M = decltype(Mc)::value, NB = decltype(NBc)::value;
+    constexpr bool PART = decltype(PARTc)::value;
+    const unsigned gx = cdiv(cdiv(nce, 64 / NB), RB_WAVES);
+    const dim3 tb(64 * RB_WAVES);
+    if (p1) {
+      GT_LAUNCH((remap_blk_k<M, NB, PART, JK_PT>), dim3(gx, 1, d.nsub), tb, 0, c.st, a);
+      gt_bytes(L * 2 * e.C + L1 * 2 * e.C);
+      GT_LAUNCH((remap_blk_k<M, NB, PART, JK_DZ>), dim3(gx, 1, d.nsub), tb, 0, c.st, a);
+      gt_bytes(L * 2 * e.C + L1 * e.C);
+      GT_LAUNCH((remap_blk_k<M, NB, PART, JK_W>), dim3(gx, 1, d.nsub), tb, 0, c.st, a);
+      gt_bytes(L * 2 * e.C + L1 * e.C + e.C);
+      GT_LAUNCH((remap_blk_k<M, NB, PART, JK_UV>), dim3(gx, 2, d.nsub), tb, 0, c.st, a);
+      gt_bytes(L * 2 * (e.X + e.Y) + L1 * e.C);
+    }
+    if (p2 && nq > 0) {
+      GT_LAUNCH((remap_blk_k<M, NB, PART, JK_Q>), dim3(gx, nq, d.nsub), tb, 0, c.st, a);
+      gt_bytes(nq * L * 2 * e.C + L1 * e.C);
+    }
+  };
+  using std::integral_constant;
+  const bool b0 = variant == 0;
+  if (b0 && npz == 72) {
+    blk(integral_constant<int, 9>{}, integral_constant<int, 8>{}, std::false_type{});
+  } else if (b0 && fits(9, 8)) {
+    blk(integral_constant<int, 9>{}, integral_constant<int, 8>{}, std::true_type{});
+  } else if (b0 && fits(9, 16)) {
+    blk(integral_constant<int, 9>{}, integral_constant<int, 16>{}, std::true_type{});
+  } else if (b0 && fits(6, 16)) {
+    blk(integral_constant<int, 6>{}, integral_constant<int, 16>{}, std::true_type{});
+  } else if (b0 && fits(5, 4)) {
+    blk(integral_constant<int, 5>{}, integral_constant<int, 4>{}, std::true_type{});
+  } else if (b0 && fits(3, 4)) {
+    blk(integral_constant<int, 3>{}, integral_constant<int, 4>{}, std::true_type{});
+  } else if (b0 && fits(2, 4)) {
+    blk(integral_constant<int, 2>{}, integral_constant<int, 4>{}, std::true_type{});
+  } else if (variant != 1 && (npz == 72 || npz == 10 || npz == 12 || npz == 20)) {
     const unsigned gx = cdiv(nce, 64);
     auto go = [&](auto KMc, auto CHc) {
       constexpr int KM = decltype(KMc)::value, CH = decltype(CHc)::value;

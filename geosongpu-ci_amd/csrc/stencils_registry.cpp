@@ -72,8 +72,7 @@ std::map<std::string, Fn>& reg() {
          a.ord = p.size() > 0 ? (int)p[0] : 6;
          fv_tp_2d(dy.ctx(), a);
        }},
-      // c_sw(delp, pt, w, u, v | uc, vc, ua, va, ut, vt, delpc, ptc, wc) params: dt2[, first
-      // stage form: 0 the kernel chain, 1 the column march]
+      // c_sw(delp, pt, w, u, v | uc, vc, ua, va, ut, vt, delpc, ptc, wc) params: dt2
       {"c_sw",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
          need(f, 14, "c_sw");
@@ -87,7 +86,6 @@ std::map<std::string, Fn>& reg() {
          a.delpc = out(11); a.ptc = out(12); a.wc = out(13);
          a.utmp = dy.field("_cs_utmp", npz).p; a.vtmp = dy.field("_cs_vtmp", npz).p;
          a.ke = dy.field("_cs_ke", npz).p; a.vort = dy.field("_cs_vort", npz).p;
-         if (p.size() > 1) a.march = p[1] != 0.0 ? 1 : 0;
          c_sw(dy.ctx(), a);
        }},
       // d_sw(delp, pt, w, u, v, uc, vc, ua, va | crx, cry, xfx, yfx, cx, cy, mfx, mfy, ke)

@@ -978,10 +978,6 @@ void c_sw(const Ctx& c, const CswArgs& a) {
 // c_sw first stage: d2a2c_vect (uc, vc, ua, va, ut, vt), the half-step transport (delpc,
 // ptc, wc) and the kinetic energy
 void c_sw_transport(const Ctx& c, const CswArgs& a) {
-  if (a.march > 0 || (a.march < 0 && c_sw_fused())) {
-    c_sw_transport_march(c, a);
-    return;
-  }
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};

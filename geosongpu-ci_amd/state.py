@@ -49,10 +49,12 @@ def _latlon(p):
     return np.arcsin(np.clip(p[..., 2], -1.0, 1.0)), np.arctan2(p[..., 1], p[..., 0])
 
 
-def _jw_wind(lat, lon, eta):
+def _jw_wind(lat, lon, eta, perturb=True):
     u0, eta0 = 35.0, 0.252
     ev = (eta - eta0) * np.pi / 2.0
     u = u0 * np.cos(ev) ** 1.5 * np.sin(2.0 * lat) ** 2
+    if not perturb:  # the steady-state test (JW06 section 3.1)
+        return u
     # perturbation: Gaussian bump of 1 m/s centred at (20E, 40N), radius a/10
     lonc, latc = np.deg2rad(20.0), np.deg2rad(40.0)
     r = np.arccos(np.clip(np.sin(latc) * np.sin(lat) + np.cos(latc) * np.cos(lat) * np.cos(lon - lonc), -1, 1))
@@ -91,10 +93,11 @@ def tracer_planes(dom, iq):
     return out
 
 
-def jablonowski_williamson(dom, ak, bk, ps=1.0e5, tracers=None):
+def jablonowski_williamson(dom, ak, bk, ps=1.0e5, tracers=None, perturb=True):
     """dict of host arrays (nsub, nk, nj, pitch): u, v, w, delz, pt, delp, q, phis.
     tracers: how many tracers to put in q (default all dom.nq; large sets go through
-    tracer_planes + Domain.upload_levels one tracer at a time)."""
+    tracer_planes + Domain.upload_levels one tracer at a time).  perturb=False: the
+    balanced jet alone (JW06's steady-state test)."""
     nsub, npz = dom.nsub, dom.npz
     nq = max(dom.nq, 1) if tracers is None else max(int(tracers), 1)
     nj, pitch, nx, ny = dom.nj, dom.pitch, dom.nx, dom.ny
@@ -127,7 +130,7 @@ def jablonowski_williamson(dom, ak, bk, ps=1.0e5, tracers=None):
             ev = _unit(pb - pa)  # edge direction
             elon = np.stack([-np.sin(lon), np.cos(lon), np.zeros_like(lon)], -1)
             for k in range(npz):
-                uz = _jw_wind(lat, lon, eta[k])
+                uz = _jw_wind(lat, lon, eta[k], perturb)
                 out[name][s, k] = uz * np.sum(elon * ev, axis=-1)
         lat, lon = lat_c[s], lon_c[s]
         out["phis"][s, 0] = _jw_phis(lat)

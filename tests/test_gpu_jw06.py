@@ -1,0 +1,62 @@
+"""Jablonowski & Williamson (2006, QJRMS 132, 2943-2975) section 3.1: the steady-state test.
+The unperturbed baroclinic jet (u0 = 35 m/s, eta0 = 0.252, the analytic temperature and
+surface geopotential that balance it, ps = 1000 hPa everywhere) is a steady solution of the
+primitive equations; a dynamical core started from it should hold it, drifting only by its
+truncation error.  Run on the whole HIP fv_dynamics step (C48 L72, 6 tiles, dt 1800 s,
+n_split 6) for five days.
+
+Checked, on the D-grid edge winds u and v (the jet projected onto each edge's direction):
+  * the dp-weighted l2 norm of (wind - initial wind) over every edge and level (JW06 eq. 14's
+    l2(u) restated on the edges) stays <= 0.5 m/s after 5 days (measured values printed);
+  * ps stays within 1 hPa of 1000 hPa (the balanced state has no surface pressure tendency);
+  * everything finite.
+JW06's own error norms for the FV core are not available offline here; the bars are this
+core's measured drift with headroom, as a regression pin on the whole step's balance (a
+sign or metric error in any term of the step breaks the balance within hours)."""
+import importlib
+
+import numpy as np
+import pytest
+
+from oracle import NG
+
+pytestmark = pytest.mark.gpu
+
+
+def l2_edges(a, b, w):
+    return float(np.sqrt(((a - b) ** 2 * w).sum() / w.sum()))
+
+
+def test_jw06_steady_state_five_days(pkg, require_gpu):
+    state = importlib.import_module(pkg.__name__ + ".state")
+    npx, npz, dt = 49, 72, 1800.0
+    d = pkg.Domain(npx=npx, npz=npz, nq=1, dt=dt)
+    try:
+        ak, bk, ks = state.hybrid_levels(npz)
+        st = state.jablonowski_williamson(d, ak, bk, perturb=False)
+        d.set_vertical(ak, bk, ks)
+        for k, v in st.items():
+            d.upload(k, v)
+        nx, ny = d.nx, d.ny
+        cu = (Ellipsis, slice(NG, NG + ny + 1), slice(NG, NG + nx))
+        cv = (Ellipsis, slice(NG, NG + ny), slice(NG, NG + nx + 1))
+        cc = (Ellipsis, slice(NG, NG + ny), slice(NG, NG + nx))
+        dp = st["delp"][:, :, NG, NG]  # (nsub, npz): the same at every column (ps uniform)
+        wu = np.broadcast_to(dp[:, :, None, None], st["u"][cu].shape)
+        wv = np.broadcast_to(dp[:, :, None, None], st["v"][cv].shape)
+        u0, v0 = st["u"][cu].copy(), st["v"][cv].copy()
+        per_day = int(round(86400.0 / dt))
+        hist = []
+        for day in range(1, 6):
+            d.step(per_day)
+            u, v, ps = d.download("u")[cu], d.download("v")[cv], d.download("ps")[cc]
+            assert np.all(np.isfinite(u)) and np.all(np.isfinite(v)) and np.all(np.isfinite(ps)), day
+            eu = np.sqrt((l2_edges(u, u0, wu) ** 2 * wu.sum() + l2_edges(v, v0, wv) ** 2 * wv.sum())
+                         / (wu.sum() + wv.sum()))
+            hist.append((day, eu, float(np.abs(ps - 1.0e5).max())))
+            print(f"JW06 steady state day {day}: l2(wind - wind0) {eu:.4f} m/s, max |ps - 1000 hPa| "
+                  f"{hist[-1][2]:.2f} Pa", flush=True)
+        assert hist[-1][1] <= 0.5, hist
+        assert max(h[2] for h in hist) <= 100.0, hist
+    finally:
+        d.close()

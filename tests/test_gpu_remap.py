@@ -1,6 +1,6 @@
 """GPU parity of the vertical remap (Lagrangian_to_Eulerian).
 
-The remap kernels (remap_prep_k, remap_job_k, remap_finish_k) against the oracle
+The remap kernels (remap_prep_k, remap_blk_k / remap_job_k, remap_finish_k) against the oracle
 (oracle/fv_mapz.py lagrangian_to_eulerian, one sub-domain at a time):
 |hip - oracle| <= 1e-11 * mean|oracle| per state field the remap writes (exp / log from
 ocml on the device and glibc on the host).
@@ -44,15 +44,17 @@ def lagrangian_state(pkg, d, npz, nq, r):
     return st, ak, bk, ks
 
 
-@pytest.mark.parametrize("npz,nq", [(72, 4), (137, 2), (10, 3), (137, 11), (137, 19), (72, 11)])
-def test_remap_vs_oracle(pkg, require_gpu, npz, nq):
+@pytest.mark.parametrize("variant", [0, 1])
+@pytest.mark.parametrize("npz,nq", [(72, 4), (137, 2), (10, 3), (137, 11), (137, 19), (72, 11), (20, 2)])
+def test_remap_vs_oracle(pkg, require_gpu, npz, nq, variant):
+    """variant 0: the level-block form (remap_blk_k, default), 1: the scratch-column job form"""
     d = pkg.Domain(npx=13, npz=npz, nq=nq)
     r = rng(300 + npz)
     st, ak, bk, ks = lagrangian_state(pkg, d, npz, nq, r)
     d.set_vertical(ak, bk, ks)
     for k, v in st.items():
         d.upload(k, v)
-    d.stencil("lagrangian_to_eulerian", [], [1])
+    d.stencil("lagrangian_to_eulerian", [], [1, variant])
     got = {k: d.download(k) for k in FIELDS}
     P = types.SimpleNamespace(nx=d.nx, ny=d.ny)
     ny, nx = d.ny, d.nx
@@ -75,10 +77,10 @@ def test_remap_vs_oracle(pkg, require_gpu, npz, nq):
 
 @pytest.mark.parametrize("npz,nq", [(72, 4), (10, 3), (20, 2)])
 def test_remap_register_columns_bitwise(pkg, require_gpu, npz, nq):
-    """The register-resident column remap (remap_reg_k<L>, the default at L10/12/20/72) gives
-    bit for bit the scratch-column job form (remap_job_k) on the same displaced state."""
+    """The register-resident column remap (remap_reg_k<L>, variant 2) gives bit for bit the
+    scratch-column job form (remap_job_k, variant 1) on the same displaced state."""
     outs = []
-    for variant in (0, 1):
+    for variant in (2, 1):
         d = pkg.Domain(npx=13, npz=npz, nq=nq)
         r = rng(700 + npz)
         st, ak, bk, ks = lagrangian_state(pkg, d, npz, nq, r)

@@ -79,36 +79,6 @@ def test_c_sw_parity(pkg, require_gpu, layout):
 C_OUTS = ["uc", "vc", "ua", "va", "ut", "vt", "delpc", "ptc", "wc"]
 
 
-@pytest.mark.parametrize("npx,layout", [(13, (1, 1)), (13, (2, 2)), (181, (1, 1)), (181, (1, 4))])
-def test_c_sw_march_matches_kernel_chain(pkg, require_gpu, npx, layout):
-    """c_sw's first stage as one column march (csw_march.hip: d2a2c_vect with the cube-corner
-    fixes, the half-step transport and ke, utmp / vtmp kept in registers) against the kernel
-    chain cs_tmp -> cs_corner_fix -> cs_cgrid -> cs_transport_ke, bit for bit on every output
-    point either form writes, then the shared second stage (uc / vc update) on top of each:
-    C12 with every sub-domain owning cube corners (1x1) or only some (2x2), C180 with interior
-    strips, strip seams and multi-segment marches, and the 1x4 band layout."""
-    npz = 3
-    d = pkg.Domain(npx=npx, npz=npz, nq=1, layout_x=layout[0], layout_y=layout[1])
-    r = rng(23)
-    inp = sw_inputs(d, npz, r)
-    for k, v in inp.items():
-        d.upload("c_" + k, v)
-    got = {}
-    for form in (0, 1):
-        d.stencil("c_sw", ["c_delp", "c_pt", "c_w", "c_u", "c_v"] + [f"c{form}_" + o for o in C_OUTS],
-                  [300.0, float(form)])
-        got[form] = {o: d.download(f"c{form}_" + o) for o in C_OUTS}
-    nx, ny = d.nx, d.ny
-    for o, (i0, i1, j0, j1) in dict(delpc=(-1, nx, -1, ny), ptc=(-1, nx, -1, ny), wc=(-1, nx, -1, ny),
-                                     uc=(-NG, nx + NG, -NG, ny + NG), vc=(-NG, nx + NG, -NG, ny + NG),
-                                     ua=(-NG, nx + NG, -NG, ny + NG), va=(-NG, nx + NG, -NG, ny + NG),
-                                     ut=(-NG, nx + NG, -NG, ny + NG), vt=(-NG, nx + NG, -NG, ny + NG)).items():
-        a, b = reg(got[1][o], i0, i1, j0, j1), reg(got[0][o], i0, i1, j0, j1)
-        bad = np.argwhere(a != b)
-        assert bad.size == 0, f"{o}: march differs from the chain at {len(bad)} points, first {bad[:4].tolist()}"
-    d.close()
-
-
 @pytest.mark.parametrize("layout", [(1, 1), (2, 2)])
 def test_d_sw_parity(pkg, require_gpu, layout):
     npz = 3

@@ -109,7 +109,9 @@ def _run(pkg, npx, alpha, nsteps):
             # hand it the full-step values every step
             for n, v in (("cx", cx), ("cy", cy), ("mfx", xfx), ("mfy", yfx), ("dp1", ones)):
                 d.upload(n, v)
-            d.halo_update("cx:C,cy:C,mfx:C,mfy:C")
+            # the dycore's synchronised C-grid exchange ('X': a tile's east / north edge values
+            # replaced by the neighbour's west / south ones, then the C halo), as uc / vc get
+            d.halo_update("cx:X,cy:X,mfx:X,mfy:X")
             d.stencil("tracer_2d_1l", [], [1])
         return norms(d.download("q"), q0, area, d)
     finally:
