@@ -56,12 +56,13 @@ def families(kstats):
 
 
 def march_ex_fraction(nx, subs, mout=58):
-    """share of (sub-domain, strip) pairs of the column marches whose 64-column strip reaches
-    a tile edge (tp.hip ex_fraction: the tile-edge kernel's part of each march)"""
+    """share of the column marches' output columns in strips that reach a tile edge (tp.hip
+    ex_fraction: the tile-edge kernel's part of each march, strips weighted by their outputs)"""
     nstrip = (nx + 1 + mout - 1) // mout
-    nex = sum(1 for s in subs for st in range(nstrip)
+    outs = [min(mout, nx + 1 - st * mout) for st in range(nstrip)]
+    nex = sum(outs[st] for s in subs for st in range(nstrip)
               if not (st * mout + s["ioff"] - 1 >= 2 and st * mout + s["ioff"] + mout + 1 <= s["N"] - 2))
-    return nex / (len(subs) * nstrip)
+    return nex / (len(subs) * sum(outs))
 
 
 def manifest_step_bytes(nx, ny, nsub, npz, nq, n_split, pitch, nj, fex=0.5, alternatives=False):

@@ -115,11 +115,12 @@ __device__ __forceinline__ Mob scan_mob(Mob v, int b) {
 // x_k = y_k - gam_{k+1} x_{k+1} are affine recurrences: a block pass with a zero carry gives
 // the block's map, a scan composes the maps, a second pass runs from the true carry (as
 // accurate as the sequential sweep: ~1e-14 of the mean |x| on both systems in a numpy model).
-template <int M, int NB, bool MOBIUS, class Row, class Rhs>
-__device__ __forceinline__ void tri_solve(Row row, Rhs rhs, double (&x)[M], int b, bool last) {
-  double gam[M], rbs[M];
+// The pivots depend on the rows only: tri_factor forms them (gam_k = c_{k-1} / bet_{k-1}, rbs_k
+// = 1 / bet_k) once, tri_apply solves for a right-hand side -- several right-hand sides of one
+// system (remap_blk_k's tracers) share one factorisation.
+template <int M, int NB, bool MOBIUS, class Row>
+__device__ __forceinline__ void tri_factor(Row row, double (&gam)[M], double (&rbs)[M], int b) {
   auto cof = [&](int m, double& a_, double& d_, double& c_) { row(m, a_, d_, c_); };
-  auto a_of = [&](int m) { double a_, d_, c_; cof(m, a_, d_, c_); return a_; };
   auto c_of = [&](int m) { double a_, d_, c_; cof(m, a_, d_, c_); return c_; };
   const double cprev_ = blk_prev(c_of(M - 1));
   const double cprev = b == 0 ? 0.0 : cprev_;  // c of the row above the block
@@ -158,6 +159,12 @@ __device__ __forceinline__ void tri_solve(Row row, Rhs rhs, double (&x)[M], int 
       rb_in = b == r + 1 ? nx : rb_in;
     }
   }
+}
+
+template <int M, int NB, class Row, class Rhs>
+__device__ __forceinline__ void tri_apply(Row row, Rhs rhs, const double (&gam)[M], const double (&rbs)[M],
+                                          double (&x)[M], int b, bool last) {
+  auto a_of = [&](int m) { double a_, d_, c_; row(m, a_, d_, c_); return a_; };
   // y with a zero carry, and its coefficient on the carry
   double yh = 0.0, A = 1.0;
 #pragma unroll
@@ -190,6 +197,13 @@ __device__ __forceinline__ void tri_solve(Row row, Rhs rhs, double (&x)[M], int 
     xi = __builtin_fma(-gnext(m), xi, x[m]);
     x[m] = xi;
   }
+}
+
+template <int M, int NB, bool MOBIUS, class Row, class Rhs>
+__device__ __forceinline__ void tri_solve(Row row, Rhs rhs, double (&x)[M], int b, bool last) {
+  double gam[M], rbs[M];
+  tri_factor<M, NB, MOBIUS>(row, gam, rbs, b);
+  tri_apply<M, NB>(row, rhs, gam, rbs, x, b, last);
 }
 
 }  // namespace gtfv3

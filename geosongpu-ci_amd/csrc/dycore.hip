@@ -696,7 +696,7 @@ void Dycore::step() {
                                (double)nl.hord_tm, (double)nl.hord_dp,
                                // launch-shape switches read at every launch (tests flip them in-process)
                                (double)kloop_levels(), (double)loads_first(),
-                               (double)riem_variant()};
+                               (double)riem_variant(), (double)remap_variant()};
     for (const Field* f : {&u, &v, &w, &delz, &pt, &delp, &phis})
       key.push_back((double)reinterpret_cast<uintptr_t>(f->p));
     for (const double* p : {vert, dp_ref}) key.push_back((double)reinterpret_cast<uintptr_t>(p));
@@ -739,7 +739,7 @@ void Dycore::step() {
     std::swap(st, st_b);
     HIP_CHECK(hipEventRecord(ev_b, st_b));
     RemapState rs1{pe, peln, pk, pkz, delp.p, delz.p, pt.p, w.p, q.p, u.p, v.p, ps, ws};
-    lagrangian_to_eulerian(c, npz, nq, ptop, nl.fill != 0, ak_dev, bk_dev, rs1, rsc, 0, 1);
+    lagrangian_to_eulerian(c, npz, nq, ptop, nl.fill != 0, ak_dev, bk_dev, rs1, rsc, remap_variant(), 1);
     HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
   } else {
     if (tracer_wait) HIP_CHECK(hipStreamWaitEvent(st, tracer_wait, 0));
@@ -749,7 +749,7 @@ void Dycore::step() {
 
   // ---- vertical remap to the hybrid Eulerian coordinate ----
   RemapState rs{pe, peln, pk, pkz, delp.p, delz.p, pt.p, w.p, q.p, u.p, v.p, ps, ws};
-  lagrangian_to_eulerian(c, npz, nq, ptop, nl.fill != 0, ak_dev, bk_dev, rs, rsc, 0, fork_substep ? 2 : 0);
+  lagrangian_to_eulerian(c, npz, nq, ptop, nl.fill != 0, ak_dev, bk_dev, rs, rsc, remap_variant(), fork_substep ? 2 : 0);
   HIP_CHECK(hipEventRecord(ev[3], st));
 
   // ---- exit: T, omega, A-grid winds ----

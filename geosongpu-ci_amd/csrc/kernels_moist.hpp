@@ -20,6 +20,7 @@ struct Gfdl1mArgs {
   const double *dp, *dz;                   // delp (Pa), delz (m, < 0)
   double* scr;                             // gfdl_mp_scratch_levels(nk) planes per sub-domain
   double *pr, *ps, *pg, *pi;               // surface rain / snow / graupel / ice (kg m-2 per step)
+  int variant = 0;                         // 0: the level-block form where instantiated, 1: the column driver
 };
 int gfdl_mp_scratch_levels(int nk);
 void gfdl_1m(const Ctx& c, const Gfdl1mArgs& a);

@@ -73,8 +73,10 @@ struct RemapScratch {
 };
 int remap_jobs(int nq);
 int remap_scratch_slots(int nq);  // scratch column sets (jobs run in chunks of this many)
-// variant: 0 = register-resident columns where instantiated (L10/12/20/72), else the
-// scratch-column jobs; 1 = force the scratch-column jobs (remap_job_k, the bitwise reference)
+// variant: 0 = the level-block form (remap_blk_k) where a shape is instantiated, else the
+// register-resident columns (L10/12/20/72) or the scratch-column jobs; 2 = the register
+// columns; 1 = the scratch-column jobs (remap_job_k)
+int remap_variant();  // GTFV3_REMAP (default 0: the level-block form where instantiated)
 void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fill, const double* ak_dev,
                             const double* bk_dev, const RemapState& S, const RemapScratch& R, int variant = 0,
                             int phase = 0);  // 1: prep + T_v/delz/w/winds, 2: tracers + finish

@@ -20,6 +20,7 @@
 #include <mutex>
 #include <vector>
 
+#include "blockscan.hpp"
 #include "kernels_moist.hpp"
 #include "stencil_common.hpp"
 
@@ -181,6 +182,13 @@ __device__ __forceinline__ double lhi_(double t) { return LI00 + DC_ICE * t; }
 __device__ __forceinline__ double cvm_(double qv, double ql, double qr, double qi, double qs, double qg) {
   return CV_AIR + qv * CV_VAP + (qr + ql) * C_LIQ + (qi + qs + qg) * C_ICE;
 }
+// exp / log of the processes: ocml (the column driver) or fastmath.hpp's (~1 ulp; the
+// level-block form)
+template <bool FM>
+__device__ __forceinline__ double mexp(double x) { return FM ? fm_exp(x) : exp(x); }
+template <bool FM>
+__device__ __forceinline__ double mlog(double x) { return FM ? fm_log(x) : log(x); }
+
 // density-form saturation mixing ratio and its T derivative (oracle wqs2 / iqs2)
 __device__ __forceinline__ void qs2(const Tables& tb, bool ice, double t, double den, double& q, double& dq) {
   double es, des;
@@ -490,6 +498,7 @@ __device__ __forceinline__ void mp_sedi_heat(int n, long P, double cw, RP t, CRP
   }
 }
 
+template <bool FM = false>
 __device__ __forceinline__ void mp_revap_racc(const Tables& tb, const MpConst& kc, double dt, double den, double& t, double& qv,
                               double& ql, double& qr, double qi, double qs, double qg) {
   const double cvm = cvm_(qv, ql, qr, qi, qs, qg);
@@ -499,7 +508,7 @@ __device__ __forceinline__ void mp_revap_racc(const Tables& tb, const MpConst& k
   const double dqv = qsat - qv;
   const double qden = fmax(qr, QRMIN) * den;
   const double t2 = t * t;
-  const double ev = kc.crevp[0] * t2 * dqv * (kc.crevp[1] * sqrt(qden) + kc.crevp[2] * exp(0.725 * log(qden))) /
+  const double ev = kc.crevp[0] * t2 * dqv * (kc.crevp[1] * sqrt(qden) + kc.crevp[2] * mexp<FM>(0.725 * mlog<FM>(qden))) /
                     (kc.crevp[3] * t2 + kc.crevp[4] * qsat * den);
   double evap = fmin(fmin(qr, dt * ev), dqv / (1.0 + lcpk * dqsdt));
   if (!(dqv > QVMIN && qr > QRMIN)) evap = 0.0;
@@ -507,7 +516,7 @@ __device__ __forceinline__ void mp_revap_racc(const Tables& tb, const MpConst& k
   qv = qv + evap;
   t = t - evap * lcpk;
   const double denfac = sqrt(SFCRHO / den);
-  double sink = dt * denfac * kc.cracw * exp(0.95 * log(fmax(qr, QRMIN) * den));
+  double sink = dt * denfac * kc.cracw * mexp<FM>(0.95 * mlog<FM>(fmax(qr, QRMIN) * den));
   sink = sink / (1.0 + sink) * ql;
   if (!(qr > QRMIN && ql > QCMIN)) sink = 0.0;
   ql = ql - sink;
@@ -543,6 +552,7 @@ __device__ __forceinline__ void mp_autoconv(int n, long P, double dts, RP ql, RP
   }
 }
 
+template <bool FM = false>
 __device__ __forceinline__ void mp_icloud(const Tables& tb, const MpConst& kc, double dts, double den, double& t, double& qv,
                           double& ql, double& qr, double& qi, double& qs, double& qg) {
   const double denfac = sqrt(SFCRHO / den);
@@ -561,7 +571,7 @@ __device__ __forceinline__ void mp_icloud(const Tables& tb, const MpConst& kc, d
   tc = t - T_ICE;
   const bool cold = tc < 0.0;
   {  // psacw
-    const double fac = dts * denfac * kc.csacw * exp(0.8125 * log(fmax(qs, QCMIN) * den));
+    const double fac = dts * denfac * kc.csacw * mexp<FM>(0.8125 * mlog<FM>(fmax(qs, QCMIN) * den));
     const double psacw = (qs > QCMIN && ql > QCMIN) ? fac / (1.0 + fac) * ql : 0.0;
     ql = ql - psacw;
     const double icpk = lhi_(t) / cvm_(qv, ql, qr, qi, qs, qg);
@@ -571,21 +581,21 @@ __device__ __forceinline__ void mp_icloud(const Tables& tb, const MpConst& kc, d
   }
   {  // psaut
     const double qim = QI0_CRIT / den;
-    const double aut = (cold && qi > qim) ? (1.0 - exp(-dts * exp(0.025 * tc) / TAU_I2S)) * (qi - qim) : 0.0;
+    const double aut = (cold && qi > qim) ? (1.0 - mexp<FM>(-dts * mexp<FM>(0.025 * tc) / TAU_I2S)) * (qi - qim) : 0.0;
     qi = qi - aut; qs = qs + aut;
   }
   {  // psaci
-    const double fac = dts * denfac * kc.csacw * C_PSACI * exp(0.05 * tc + 0.8125 * log(fmax(qs, QCMIN) * den));
+    const double fac = dts * denfac * kc.csacw * C_PSACI * mexp<FM>(0.05 * tc + 0.8125 * mlog<FM>(fmax(qs, QCMIN) * den));
     const double saci = (cold && qs > QCMIN && qi > QCMIN) ? fac / (1.0 + fac) * qi : 0.0;
     qi = qi - saci; qs = qs + saci;
   }
   {  // pgaut
-    double gaut = (cold && qs > QS0_CRIT) ? dts * 1.0e-3 * exp(0.09 * tc) * (qs - QS0_CRIT) : 0.0;
+    double gaut = (cold && qs > QS0_CRIT) ? dts * 1.0e-3 * mexp<FM>(0.09 * tc) * (qs - QS0_CRIT) : 0.0;
     gaut = fmin(gaut, fmax(qs, 0.0));
     qs = qs - gaut; qg = qg + gaut;
   }
   {  // pgacw
-    const double fac = dts * kc.cgacw * exp(0.875 * log(fmax(qg, QCMIN) * den)) * denfac;
+    const double fac = dts * kc.cgacw * mexp<FM>(0.875 * mlog<FM>(fmax(qg, QCMIN) * den)) * denfac;
     const double gacw = (qg > QCMIN && ql > QCMIN) ? fac / (1.0 + fac) * ql : 0.0;
     ql = ql - gacw;
     const double icpk = lhi_(t) / cvm_(qv, ql, qr, qi, qs, qg);
@@ -723,6 +733,506 @@ __global__ void __launch_bounds__(256) mpdrv_k(MpArgs a) {
 }
 #undef RP
 #undef CRP
+
+// ---- GFDL cloud microphysics, level-block form (default where a shape is instantiated) ----
+//
+// The column driver above keeps one lane per column and its nine working columns in HBM:
+// ~3000 waves at C180, every pass a chain of dependent memory round trips (9.2 ms per C180
+// step, 0.026 of the HBM roofline).  Here a column's levels sit in NB blocks of M on NB
+// consecutive lanes of one DPP row (blockscan.hpp, as riem_scan_k / remap_blk_k), the whole
+// state (T, six species, dp, dz) in registers for all ntimes sub-steps, read and written
+// once; every lane works on every process:
+//   * the pointwise processes (neg_adj's phase borrowing, melting, revap_racc, autoconversion,
+//     icloud + subgrid_z_proc) per level, the same scalar functions as the column driver;
+//   * neg_adj's vapour borrowing and fallen_edges' monotone fix are serial chains that
+//     almost never act: each block runs its chain from the incoming value its upper
+//     neighbour hands down by DPP, and the hand-over repeats until no incoming value changes
+//     (one round when no block's chain reaches its bottom; results identical to the serial
+//     walk);
+//   * the Lagrangian sedimentation: fallen heights and layer densities pointwise, cs_profile's
+//     edge system (the bottom edge eliminated into the last row, as remap_blk_k) by
+//     tri_solve with Moebius-scan pivots, the edge bounds and the monotone limiter pointwise,
+//     and the integration over the fixed layers through the mass function Q(z) (the fallen
+//     column's mass above height z: block running sums + scanned offsets, each fixed
+//     interface's Q evaluated by the block whose fallen range holds it, into LDS; a layer's
+//     mass is Q(bottom) - Q(top), from block-local values when both lie in one block);
+//     the fluxes m1 by a block scan and sedi_heat as an affine recurrence (scan_aff).
+// The same expressions as the column driver, associated differently in the sums and the
+// recurrences: agreement with the oracle to rounding (tests/test_gpu_moist.py bars), not bit
+// for bit.  Shapes: NB M >= nk with the column's last two levels in one block.
+constexpr int MB_WAVES = 4;
+typedef unsigned int MbU2 __attribute__((ext_vector_type(2)));
+template <int M, int NB>
+__global__ void __launch_bounds__(64 * MB_WAVES) mpdrv_blk_k(MpArgs a) {
+  constexpr int NC = 64 / NB, KX = NB * M;
+  __shared__ double lze[MB_WAVES][NC][KX + 1];  // fixed interface heights (surface 0)
+  __shared__ double lq[MB_WAVES][NC][KX + 1];   // block-local Q at fixed interface k
+  __shared__ int lown[MB_WAVES][NC][KX + 1];    // the block whose fallen range holds interface k
+  __shared__ double loff[MB_WAVES][NC][NB];     // Q at each block's top
+  const Dims d = a.d;
+  const int n = a.nk;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = lane & (NB - 1), cl = lane / NB;
+  const int ncol = d.nx * d.ny;
+  const int c0 = (blockIdx.x * MB_WAVES + wv) * NC;
+  if (c0 >= ncol) return;  // whole wavefront (no barrier follows)
+  int c = c0 + cl;
+  const bool valid = c < ncol;
+  if (!valid) c = ncol - 1;
+  const int s = blockIdx.z;
+  const long P = d.plane, o = pidx(d, c % d.nx, c / d.nx);
+  const int g0 = b * M;
+  const int nv = min(max(n - g0, 0), M);  // real levels of this block
+  const bool lastb = b == (n - 1) / M;     // holds levels n - 2 and n - 1 (launcher)
+  const double dts = a.dts;
+  const MpConst& kc = a.k;
+  const unsigned long long cmask = NB == 64 ? ~0ull : ((1ull << NB) - 1) << (cl * NB);
+  // buffer resources per field (the sub-domain's nk planes), one VGPR offset per lane (the
+  // lane's column at its block's first level), the level in the scalar offset
+  const uint32_t PB = (uint32_t)P * 8u;
+  const uint32_t vb = (uint32_t)(o + (long)g0 * P) * 8u;
+  auto rsrc = [&](const double* base) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(n * PB), 0x00020000);
+  };
+  const long qo = (long)s * a.qsub * P;
+  const auto rT = rsrc(a.T + (long)s * n * P), rV = rsrc(a.qv + qo), rL = rsrc(a.ql + qo), rR = rsrc(a.qr + qo);
+  const auto rI = rsrc(a.qi + qo), rS = rsrc(a.qs + qo), rG = rsrc(a.qg + qo);
+  const auto rP = rsrc(a.dp + (long)s * n * P), rZ = rsrc(a.dz + (long)s * n * P);
+  auto ld = [&](__amdgpu_buffer_rsrc_t r, int m) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vb, (uint32_t)m * PB, 0));
+  };
+  auto st = [&](__amdgpu_buffer_rsrc_t r, int m, double v) {
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(MbU2, v), r, vb, (uint32_t)m * PB, 0);
+  };
+  double t[M], qv[M], ql[M], qr[M], qi[M], qs[M], qg[M], dp[M], dz[M], den[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    const bool r = m < nv;
+    t[m] = r ? ld(rT, m) : T_ICE;
+    qv[m] = r ? ld(rV, m) : 0.0;
+    ql[m] = r ? ld(rL, m) : 0.0;
+    qr[m] = r ? ld(rR, m) : 0.0;
+    qi[m] = r ? ld(rI, m) : 0.0;
+    qs[m] = r ? ld(rS, m) : 0.0;
+    qg[m] = r ? ld(rG, m) : 0.0;
+    dp[m] = r ? ld(rP, m) : 1.0;
+    dz[m] = r ? ld(rZ, m) : -1.0;
+    den[m] = -dp[m] / (GRAV * dz[m]);
+  }
+  // fixed interface heights: the block's own sums from its bottom, the blocks below by a scan
+  {
+    double zl[M], z = 0.0;
+#pragma unroll
+    for (int m = M - 1; m >= 0; --m) {
+      z = m < nv ? z - dz[m] : z;
+      zl[m] = z;
+    }
+    const double incl = scan_sum<NB, false>(z, b);
+    const double below_ = blk_next(incl);
+    const double below = b == NB - 1 ? 0.0 : below_;
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (m < nv) lze[wv][cl][g0 + m] = below + zl[m];
+    if (lastb) lze[wv][cl][n] = 0.0;
+  }
+  __builtin_amdgcn_wave_barrier();
+  asm volatile("" ::: "memory");
+  auto zeF = [&](int k) { return lze[wv][cl][k]; };
+
+  // one Lagrangian fall of species q (w: 0 ice, 1 snow, 2 graupel, 3 rain) with sedi_heat;
+  // returns the flux out of the column's bottom (in the lane holding level n - 1)
+  auto fall = [&](double (&q)[M], int w, double cw) -> double {
+    const double thr = w == 3 ? QRMIN : QCMIN;
+    double vt[M];
+    bool lany = false;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const double dn = den[m], qq = q[m];
+      const double rhof = sqrt(fmin(10.0, SFCRHO / dn));
+      double v;
+      if (w == 3) {
+        const double q_ = fmax(qq, QRMIN);
+        v = qq > QRMIN ? fmin(VR_MAX, fmax(VR_MIN, VCONR * rhof * fm_exp(0.2 * fm_log(q_ * dn / NORMR)))) : 0.0;
+      } else if (w == 0) {
+        const double q_ = fmax(qq, QCMIN);
+        v = qq > QCMIN ? fmin(VI_MAX, 3.29 * fm_exp(0.16 * fm_log(q_ * dn))) : 0.0;
+      } else if (w == 1) {
+        const double q_ = fmax(qq, QCMIN);
+        v = qq > QCMIN ? fmin(VS_MAX, VCONS * rhof * fm_exp(0.0625 * fm_log(q_ * dn / NORMS))) : 0.0;
+      } else {
+        const double q_ = fmax(qq, QCMIN);
+        v = qq > QCMIN ? fmin(VG_MAX, VCONG * rhof * sqrt(sqrt(sqrt(q_ * dn / NORMG)))) : 0.0;
+      }
+      vt[m] = v;
+      lany = lany || (m < nv && qq > thr);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const bool cany = (__ballot(lany) & cmask) != 0;  // the column holds this species
+    if (__ballot(cany) == 0) return 0.0;               // (wave-uniform)
+    // fallen interface heights, raw: interface g0 + m is the top of local layer m
+    const double vpv_ = blk_prev(vt[M - 1]);
+    const double vpv = b == 0 ? 0.0 : vpv_;
+    double zr[M], zbr = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int g = g0 + m;
+      const double vp = m == 0 ? vpv : vt[m > 0 ? m - 1 : 0];
+      const double ze = m < nv ? zeF(g) : 0.0;
+      zr[m] = g == 0 ? ze : ze - 0.5 * dts * (vp + vt[m]);
+      if (lastb && m == nv - 1) zbr = zeF(n) - dts * vt[m];
+    }
+    // monotone fix (each interface strictly below the one above), as a chain from the
+    // incoming fixed height of interface g0 - 1
+    double zf[M], zfb = 0.0;
+    auto chain = [&](double zin) {
+      double zp = zin;
+#pragma unroll
+      for (int m = 0; m < M; ++m) {
+        double z = zr[m];
+        if (g0 + m > 0 && m < nv && z >= zp) z = zp - DZ_MIN_FALL;
+        zf[m] = z;
+        zp = m < nv ? z : zp;
+      }
+      double z = zbr;
+      if (z >= zp) z = zp - DZ_MIN_FALL;
+      zfb = z;
+    };
+    const double zin0_ = blk_prev(zr[M - 1]);
+    double zin = b == 0 ? 0.0 : zin0_;
+    chain(zin);
+#pragma unroll 1
+    for (int r = 0; r < NB; ++r) {
+      const double zn_ = blk_prev(zf[M - 1]);
+      const double zn = b == 0 ? 0.0 : zn_;
+      const bool ch = zn != zin;
+      if (__ballot(ch) == 0) break;
+      zin = zn;
+      chain(zin);
+    }
+    // fallen thicknesses and densities per height
+    const double zfn_ = blk_next(zf[0]);
+    double dzf[M], qm0[M], aa[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const double zlo = m + 1 < M ? zf[m + 1 < M ? m + 1 : 0] : zfn_;
+      const double zb = (lastb && m == nv - 1) ? zfb : zlo;
+      dzf[m] = m < nv ? zf[m] - zb : 1.0;
+      qm0[m] = q[m] * dp[m];
+      aa[m] = qm0[m] / dzf[m];
+    }
+    const double am1_ = blk_prev(aa[M - 1]), dzm1_ = blk_prev(dzf[M - 1]);
+    const double am1 = b == 0 ? 0.0 : am1_, dzm1 = b == 0 ? 1.0 : dzm1_;
+    auto Aw = [&](int m) { return m < 0 ? am1 : aa[m]; };
+    auto Dw = [&](int m) { return m < 0 ? dzm1 : dzf[m]; };
+    // the bottom edge's row (last block; levels n - 2, n - 1 both in it)
+    double abot = 1.0, dbot = 1.0, rbot = 0.0, d4b = 0.0;
+#pragma unroll
+    for (int m = 1; m < M; ++m)
+      if (m == nv - 1) {
+        d4b = dzf[m - 1] / dzf[m];
+        abot = 1.0 + d4b * (d4b + 1.5);
+        dbot = d4b * (d4b + 0.5);
+        rbot = 2.0 * d4b * (d4b + 1.0) * aa[m] + aa[m - 1];
+      }
+    auto row = [&](int m, double& am, double& dg, double& cm) {
+      const int e = g0 + m;
+      if (m >= nv) {
+        am = 0.0; dg = 1.0; cm = 0.0;
+        return;
+      }
+      if (e == 0) {
+        const double grat = dzf[1 < M ? 1 : 0] / dzf[0];
+        am = 0.0;
+        dg = grat * (grat + 0.5);
+        cm = 1.0 + grat * (grat + 1.5);
+        return;
+      }
+      const double d4 = Dw(m - 1) / dzf[m];
+      am = 1.0;
+      dg = 2.0 + d4 + d4;
+      cm = d4;
+      if (lastb && m == nv - 1) {
+        dg = dg - cm * abot / dbot;
+        cm = 0.0;
+      }
+    };
+    auto rhs = [&](int m) -> double {
+      const int e = g0 + m;
+      if (m >= nv) return 0.0;
+      if (e == 0) {
+        const double grat = dzf[1 < M ? 1 : 0] / dzf[0];
+        return (grat + grat) * (grat + 1.0) * aa[0] + aa[1 < M ? 1 : 0];
+      }
+      const double d4 = Dw(m - 1) / dzf[m];
+      double r = 3.0 * (Aw(m - 1) + d4 * aa[m]);
+      if (lastb && m == nv - 1) r = r - d4 * rbot / dbot;
+      return r;
+    };
+    double qe[M];
+    tri_solve<M, NB, true>(row, rhs, qe, b, b == NB - 1);
+    double qlast = qe[0];
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (m == nv - 1) qlast = qe[m];
+    const double qbot = fmax((rbot - abot * qlast) / dbot, 0.0);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const double a0 = Aw(m - 1), a1 = aa[m];
+      qe[m] = g0 + m == 0 ? fmax(qe[m], 0.0) : fmin(fmax(qe[m], fmin(a0, a1)), fmax(a0, a1));
+    }
+    const double qen_ = blk_next(qe[0]);
+    // running mass of the fallen block, block offsets
+    double C[M + 1];
+    C[0] = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) C[m + 1] = C[m] + (m < nv ? qm0[m] : 0.0);
+    const double offx = blk_prev(scan_sum<NB, true>(C[M], b));
+    loff[wv][cl][b] = b == 0 ? 0.0 : offx;
+    // fixed interfaces in the block's fallen range (the last real layer takes the rest)
+    int k = g0 < n ? g0 : n;
+    if (b == 0) k = 0;
+    else
+      while (k <= n && zeF(k) > zf[0]) ++k;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (m >= nv) continue;
+      // the monotone profile of fallen layer m (cs_limiters, mono)
+      const double av = aa[m];
+      double l = qe[m];
+      double r = m + 1 < M ? qe[m + 1 < M ? m + 1 : 0] : qen_;
+      if (lastb && m == nv - 1) r = qbot;
+      double a6v;
+      const double da1 = r - l;
+      if ((av - l) * (av - r) >= 0.0) {
+        l = av; r = av; a6v = 0.0;
+      } else {
+        a6v = 3.0 * (2.0 * av - (l + r));
+        if (a6v * da1 < -da1 * da1) {
+          a6v = 3.0 * (l - av);
+          r = l - a6v;
+        } else if (a6v * da1 > da1 * da1) {
+          a6v = 3.0 * (r - av);
+          l = r - a6v;
+        }
+      }
+      const bool lastlayer = lastb && m == nv - 1;
+      const double ztop = zf[m];
+      const double zlow = m + 1 < M ? zf[m + 1 < M ? m + 1 : 0] : zfn_;
+      const double rdz = 1.0 / dzf[m];
+      while (k <= n) {
+        const double z = zeF(k);
+        if (!lastlayer && z <= zlow) break;
+        const double y = ztop - z, x = y * rdz;
+        lq[wv][cl][k] = C[m] + y * (l + 0.5 * (a6v + r - l) * x - a6v * MP_R3 * x * x);
+        lown[wv][cl][k] = b;
+        ++k;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    // fixed layer masses, fluxes through their bottoms, new mixing ratios
+    double qm[M], f[M], racc = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int kk = g0 + m;
+      double v = 0.0;
+      if (m < nv) {
+        const int o0 = lown[wv][cl][kk], o1 = lown[wv][cl][kk + 1];
+        const double q0 = lq[wv][cl][kk], q1 = lq[wv][cl][kk + 1];
+        v = o0 == o1 ? q1 - q0 : (loff[wv][cl][o1] - loff[wv][cl][o0]) + (q1 - q0);
+      }
+      qm[m] = v;
+      racc = racc + (m < nv ? qm0[m] - v : 0.0);
+      f[m] = racc;
+    }
+    const double m1x = blk_prev(scan_sum<NB, true>(racc, b));
+    const double m1o = b == 0 ? 0.0 : m1x;
+#pragma unroll
+    for (int m = 0; m < M; ++m) f[m] = m1o + f[m];
+    // sedi_heat: t_k = (cv0 t_k + m1_{k-1} (cw t'_{k-1} + dgz)) / (cv0 + cw m1_{k-1}), affine
+    // in t'_{k-1}
+    const double m1p_ = blk_prev(f[M - 1]);
+    double qn[M], A[M], B[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) qn[m] = m < nv ? qm[m] / dp[m] : 0.0;
+    Aff blk{1.0, 0.0};
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int g = g0 + m;
+      const double mp = m == 0 ? m1p_ : f[m > 0 ? m - 1 : 0];
+      double qvv = qv[m], qll = ql[m], qrr = qr[m], qii = qi[m], qss = qs[m], qgg = qg[m];
+      if (w == 0) qii = qn[m];
+      else if (w == 1) qss = qn[m];
+      else if (w == 2) qgg = qn[m];
+      else qrr = qn[m];
+      const double dgz = -0.5 * GRAV * dz[m];
+      const double cv0 = dp[m] * cvm_(qvv, qll, qrr, qii, qss, qgg) + cw * (f[m] - mp);
+      const double dd = cv0 + cw * mp;
+      double Am = cw * mp / dd, Bm = (cv0 * t[m] + mp * dgz) / dd;
+      if (g == 0) { Am = 0.0; Bm = t[m]; }
+      if (m >= nv) { Am = 1.0; Bm = 0.0; }
+      A[m] = Am;
+      B[m] = Bm;
+      blk = Aff{Am * blk.A, __builtin_fma(Am, blk.B, Bm)};
+    }
+    const Aff F = scan_aff<NB, true>(blk, b);
+    const double tin_ = blk_prev(F.B);
+    double tc = b == 0 ? 0.0 : tin_;
+    double bottom = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      tc = __builtin_fma(A[m], tc, B[m]);
+      if (cany && m < nv) {
+        t[m] = tc;
+        q[m] = qn[m];
+      }
+      if (m == nv - 1) bottom = f[m];
+    }
+    return cany && lastb ? bottom : 0.0;
+  };
+
+  double prr = 0.0, prs = 0.0, prg = 0.0, pri = 0.0;
+#pragma unroll 1
+  for (int it = 0; it < a.ntimes; ++it) {
+    // ---- neg_adj: phase borrowing per level, then negative vapour borrows from below
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      double tt = t[m], v = qv[m], l = ql[m], r = qr[m], ii = qi[m], sn = qs[m], g = qg[m];
+      const double cvm = cvm_(v, l, r, ii, sn, g);
+      const double lcpk = lhl_(tt) / cvm, icpk = lhi_(tt) / cvm;
+      if (ii < 0.0) { sn = sn + ii; ii = 0.0; }
+      if (sn < 0.0) { g = g + sn; sn = 0.0; }
+      {
+        const double dq = g < 0.0 ? g : 0.0;
+        v = v + dq;
+        tt = tt - dq * (lcpk + icpk);
+        if (g < 0.0) g = 0.0;
+      }
+      if (r < 0.0) { l = l + r; r = 0.0; }
+      {
+        const double dq = l < 0.0 ? l : 0.0;
+        v = v + dq;
+        tt = tt - dq * lcpk;
+        if (l < 0.0) l = 0.0;
+      }
+      t[m] = tt; qv[m] = v; ql[m] = l; qr[m] = r; qi[m] = ii; qs[m] = sn; qg[m] = g;
+    }
+    {
+      double vq[M], cout = 0.0;
+      const double dpin_ = blk_prev(dp[M - 1]);
+      const double dpin = b == 0 ? 1.0 : dpin_;
+      // the block's chain from the incoming value of level g0 - 1 (after its own borrow)
+      auto chain = [&](double cin) {
+        double cur = cin, dprev = dpin;
+#pragma unroll
+        for (int m = 0; m < M; ++m) {
+          const int g = g0 + m;
+          double v = qv[m];
+          if (g >= 1 && m < nv && cur < 0.0) v = v + cur * dprev / dp[m];
+          vq[m] = v;
+          cur = m < nv ? v : cur;
+          dprev = dp[m];
+        }
+        cout = cur;
+      };
+      double cin = 0.0;
+      chain(cin);
+#pragma unroll 1
+      for (int r = 0; r < NB; ++r) {
+        const double cn_ = blk_prev(cout);
+        const double cn = b == 0 ? 0.0 : cn_;
+        const bool ch = (cn < 0.0 || cin < 0.0) && cn != cin;
+        if (__ballot(ch) == 0) break;
+        cin = cn;
+        chain(cin);
+      }
+      // levels 0 .. n - 2 that went negative passed their vapour down
+#pragma unroll
+      for (int m = 0; m < M; ++m) qv[m] = (g0 + m <= n - 2 && vq[m] < 0.0) ? 0.0 : vq[m];
+      // bottom: the last level borrows from the one above
+#pragma unroll
+      for (int m = 1; m < M; ++m)
+        if (lastb && m == nv - 1) {
+          const double qb = qv[m], qa = qv[m - 1];
+          double dq = fmin(-qb * dp[m], qa * dp[m - 1]);
+          if (!(qb < 0.0 && qa > 0.0)) dq = 0.0;
+          qv[m - 1] = qa - dq / dp[m - 1];
+          qv[m] = qb + dq / dp[m];
+        }
+    }
+    // ---- terminal_fall: melting of the falling ice species, then ice, snow, graupel
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      double tt = t[m];
+      if (!(tt > T_ICE)) continue;
+      double v = qv[m], l = ql[m], r = qr[m], ii = qi[m], sn = qs[m], g = qg[m];
+#pragma unroll
+      for (int w = 0; w < 3; ++w) {
+        double& q = w == 0 ? ii : (w == 1 ? sn : g);
+        const double fq = w == 0 ? kc.e_imlt : (w == 1 ? kc.e_smlt : kc.e_gmlt);
+        const double icpk = lhi_(tt) / cvm_(v, l, r, ii, sn, g);
+        const double mlt = fmin(fq * q, (tt - T_ICE) / icpk);
+        if (mlt > 0.0) {
+          q = q - mlt;
+          if (w == 0) l = l + mlt;
+          else r = r + mlt;
+          tt = tt - mlt * icpk;
+        }
+      }
+      t[m] = tt; ql[m] = l; qr[m] = r; qi[m] = ii; qs[m] = sn; qg[m] = g;
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    const double pf0 = fall(qi, 0, C_ICE);
+    const double pf1 = fall(qs, 1, C_ICE);
+    const double pf2 = fall(qg, 2, C_ICE);
+    // ---- warm_rain
+    const double dt5 = 0.5 * dts;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      mp_revap_racc<true>(a.tb, kc, dt5, den[m], t[m], qv[m], ql[m], qr[m], qi[m], qs[m], qg[m]);
+      __builtin_amdgcn_sched_barrier(0);  // one level at a time (register pressure)
+    }
+    const double pr_ = fall(qr, 3, C_LIQ);
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      mp_revap_racc<true>(a.tb, kc, dt5, den[m], t[m], qv[m], ql[m], qr[m], qi[m], qs[m], qg[m]);
+      __builtin_amdgcn_sched_barrier(0);  // one level at a time (register pressure)
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const double l = ql[m];
+      const double dq = l - QL0_AUT;
+      double aut = dts * C_PAUT * 1.0e-3 * dq * dq / (dq + 1.0e-3);
+      aut = dq > 0.0 ? fmin(aut, dq) : 0.0;
+      ql[m] = l - aut;
+      qr[m] = qr[m] + aut;
+    }
+    prr = prr + pr_ / GRAV;
+    prs = prs + pf1 / GRAV;
+    prg = prg + pf2 / GRAV;
+    pri = pri + pf0 / GRAV;
+    // ---- icloud
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      mp_icloud<true>(a.tb, kc, dts, den[m], t[m], qv[m], ql[m], qr[m], qi[m], qs[m], qg[m]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  }
+  if (!valid) return;
+#pragma unroll
+  for (int m = 0; m < M; ++m) {
+    if (m >= nv) continue;
+    st(rT, m, t[m]); st(rV, m, qv[m]); st(rL, m, ql[m]); st(rR, m, qr[m]);
+    st(rI, m, qi[m]); st(rS, m, qs[m]); st(rG, m, qg[m]);
+  }
+  if (lastb) {
+    const long p2 = (long)s * P + o;
+    a.pr[p2] = prr;
+    a.ps[p2] = prs;
+    a.pg[p2] = prg;
+    a.pi[p2] = pri;
+  }
+}
 
 // ---- GEOS pieces around the microphysics (oracle/geos_moist.py), pointwise ----
 constexpr double RHO_W = 1000.0, RHO_I = 917.0;
@@ -1295,7 +1805,23 @@ void gfdl_1m(const Ctx& c, const Gfdl1mArgs& g) {
   const double dts = g.dt / ntimes;
   moist::MpArgs a{c.d, g.nk, g.qsub > 0 ? g.qsub : g.nk, ntimes, dts, moist::device_tables(), moist::mp_const(dts),
                   g.T, g.qv, g.ql, g.qr, g.qi, g.qs, g.qg, g.dp, g.dz, g.scr, g.pr, g.ps, g.pg, g.pi};
-  GT_LAUNCH(moist::mpdrv_k, moist::colgrid(c.d), dim3(BX, BY), 0, c.st, a);
+  // the level-block form where a shape holds the column with its last two levels in one block
+  // (NB M >= nk, nk mod M != 1); else (or variant 1) the column driver
+  const int nk = g.nk, ncol = c.d.nx * c.d.ny;
+  auto blk = [&](auto Mc, auto NBc) {
+    constexpr int M = decltype(Mc)::value, NB = decltype(NBc)::value;
+    if (g.variant == 1 || NB * M < nk || (NB - 1) * M >= nk + M || nk % M == 1) return false;
+    const dim3 grid(cdiv(cdiv(ncol, 64 / NB), moist::MB_WAVES), 1, c.d.nsub);
+    GT_LAUNCH((moist::mpdrv_blk_k<M, NB>), grid, dim3(64 * moist::MB_WAVES), 0, c.st, a);
+    return true;
+  };
+  using std::integral_constant;
+  const bool done = blk(integral_constant<int, 2>{}, integral_constant<int, 8>{}) ||
+                    blk(integral_constant<int, 2>{}, integral_constant<int, 16>{}) ||
+                    blk(integral_constant<int, 3>{}, integral_constant<int, 16>{}) ||
+                    blk(integral_constant<int, 4>{}, integral_constant<int, 16>{}) ||
+                    blk(integral_constant<int, 5>{}, integral_constant<int, 16>{});
+  if (!done) GT_LAUNCH(moist::mpdrv_k, moist::colgrid(c.d), dim3(BX, BY), 0, c.st, a);
   HIP_LAUNCH_CHECK();
   // algorithmic bytes: T + 6 species read and written, dp dz read (L each), 4 surface fields
   ktimer_bytes(8.0 * c.d.nx * c.d.ny * c.d.nsub * (16.0 * g.nk + 4.0));

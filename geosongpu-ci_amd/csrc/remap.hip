@@ -972,6 +972,7 @@ __global__ void __launch_bounds__(64) remap_reg_k(RemapArgs a) {
 // the column forms to rounding (tests/test_gpu_remap.py), not bit for bit.  No scratch planes;
 // each job's source column and output field move once, the source edges once per job.
 constexpr int RB_WAVES = 4;
+constexpr int RB_NT = 4;  // tracers per wave of remap_blkq_k
 typedef unsigned int RbU2 __attribute__((ext_vector_type(2)));
 template <int M, int NB, bool PART, int JK>
 __global__ void __launch_bounds__(64 * RB_WAVES) remap_blk_k(RemapArgs a) {
@@ -1297,6 +1298,289 @@ __global__ void __launch_bounds__(64 * RB_WAVES) remap_blk_k(RemapArgs a) {
   }
 }
 
+// The tracer jobs of the level-block form, NT tracers per wave: everything that depends on
+// the pressures only -- the layer thicknesses, the cs_profile pivots (tri_factor, the Moebius
+// scan: the row coefficients [1, 2 + 2 d4, d4] and the eliminated bottom row involve dp
+// alone), the target interfaces and which block / layer holds each -- is formed once per
+// column and shared by the NT tracers; per tracer only the right-hand side, tri_apply, the
+// constraints, the PPM coefficients and the mass-function pieces run.  Same expressions per
+// tracer as remap_blk_k<.., JK_Q> (bit-identical to it).
+template <int M, int NB, bool PART, int NT>
+__global__ void __launch_bounds__(64 * RB_WAVES, 2) remap_blkq_k(RemapArgs a) {
+  constexpr int NC = 64 / NB, KX = NB * M;
+  __shared__ double lab[2 * (KX + 1)];
+  __shared__ double lq[RB_WAVES][NC][KX + 1];
+  __shared__ double lt[RB_WAVES][NC][KX + 1];
+  __shared__ int lown[RB_WAVES][NC][KX + 1];
+  __shared__ double loff[RB_WAVES][NC][NB];
+  const int km = a.npz;
+  for (int k = threadIdx.x; k <= km; k += 64 * RB_WAVES) {
+    lab[k] = a.ak[k];
+    lab[KX + 1 + k] = a.bk[k];
+  }
+  __syncthreads();
+  const Dims d = a.d;
+  const double ptop = a.ptop;
+  const int fill = a.fill;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int b = lane & (NB - 1), cl = lane / NB;
+  const bool last = b == NB - 1;
+  const int nv = PART && last ? km - (NB - 1) * M : M;
+  auto real = [&](int m) { return !PART || m < nv; };
+  const int s = blockIdx.z;
+  const int ncol = d.nx * d.ny;
+  const int c0 = (blockIdx.x * RB_WAVES + wv) * NC;
+  if (c0 >= ncol) return;  // whole wavefront (no barrier follows)
+  int c = c0 + cl;
+  const bool valid = c < ncol;
+  if (!valid) c = ncol - 1;
+  const long P = d.plane, o = pidx(d, c % d.nx, c / d.nx);
+  const uint32_t PB = (uint32_t)P * 8u, vo = (uint32_t)o * 8u;
+  const uint32_t vb = vo + (uint32_t)(b * M) * PB;
+  auto rsrc = [&](const double* base, int nk) {
+    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(nk * PB), 0x00020000);
+  };
+  auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t v, int lev) {
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, v, (uint32_t)lev * PB, 0));
+  };
+  const auto rPE = rsrc(a.S.pe + (long)s * (km + 1) * P, km + 1);
+  const double ps = ld(rPE, vo, km);
+  auto T = [&](int k) -> double { return k == 0 ? ptop : (k == km ? ps : lab[k] + lab[KX + 1 + k] * ps); };
+  auto glob = [&](int m) { return b * M + m; };
+
+  // ---- the pressure part, once: edges, thicknesses, pivots, target ownership
+  double Ev[M + 1];
+#pragma unroll
+  for (int m = 0; m <= M; ++m) Ev[m] = ld(rPE, vb, m);
+  if constexpr (PART) {
+    double eb = Ev[M];
+#pragma unroll
+    for (int m = 0; m <= M; ++m)
+      if (m == nv) eb = Ev[m];
+#pragma unroll
+    for (int m = 0; m <= M; ++m) Ev[m] = m > nv ? eb : Ev[m];
+  }
+  double dp[M];
+#pragma unroll
+  for (int m = 0; m < M; ++m) dp[m] = Ev[m + 1] - Ev[m];
+  const double dpm1_ = blk_prev(dp[M - 1]);
+  const double dpm1 = b == 0 ? 1.0 : dpm1_;
+  auto dpw = [&](int m) -> double { return m < 0 ? dpm1 : dp[m]; };
+  double abot = 0.0, dbot = 1.0, d4b = 0.0;
+#pragma unroll
+  for (int m = 0; m < M; ++m)
+    if (m == nv - 1) {
+      d4b = dpw(m - 1) / dp[m];
+    }
+  abot = 1.0 + d4b * (d4b + 1.5);
+  dbot = d4b * (d4b + 0.5);
+  auto row = [&](int m, double& am, double& dg, double& cm) {
+    const int e = glob(m);
+    const bool bt = last && m == nv - 1;
+    if (!real(m)) {
+      am = 0.0; dg = 1.0; cm = 0.0;
+      return;
+    }
+    if (e == 0) {
+      const double grat = dp[1 < M ? 1 : 0] / dp[0];
+      am = 0.0;
+      dg = grat * (grat + 0.5);
+      cm = 1.0 + grat * (grat + 1.5);
+      return;
+    }
+    const double d4 = dpw(m - 1) / dp[m];
+    am = 1.0;
+    dg = 2.0 + d4 + d4;
+    cm = d4;
+    if (bt) {
+      dg = dg - cm * abot / dbot;
+      cm = 0.0;
+    }
+  };
+  double gam[M], rbs[M];
+  tri_factor<M, NB, true>(row, gam, rbs, b);
+  // target interfaces of each source layer: kb[m] .. kb[m + 1] - 1
+  int kb[M + 1];
+  {
+    int k = b * M < km ? b * M : km;
+    if (b == 0) {
+      k = 0;
+    } else {
+      while (k > 0 && T(k - 1) >= Ev[0]) --k;
+      while (k <= km && T(k) < Ev[0]) ++k;
+    }
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      kb[m] = k;
+      if (!real(m)) continue;
+      const bool lastlayer = last && m == nv - 1;
+      while (k <= km) {
+        const double t = T(k);
+        if (!lastlayer && t >= Ev[m + 1]) break;
+        lt[wv][cl][k] = t;
+        lown[wv][cl][k] = b;
+        ++k;
+      }
+    }
+    kb[M] = k;
+  }
+
+  // ---- per tracer
+  const int q0 = blockIdx.y * NT;
+#pragma unroll 1
+  for (int tq = 0; tq < NT; ++tq) {
+    const int iq = q0 + tq;
+    if (iq >= a.nq) break;  // (wave-uniform)
+    asm volatile("" ::: "memory");
+    double* const out = a.S.q + ((long)s * a.nq + iq) * km * P;
+    const auto rQ = rsrc(out, km);
+    double A[M];
+#pragma unroll
+    for (int m = 0; m < M; ++m) A[m] = ld(rQ, vb, m);
+    const double am1_ = blk_prev(A[M - 1]), am2_ = blk_prev(A[M - 2 >= 0 ? M - 2 : 0]);
+    const double ap1_ = blk_next(A[0]), ap2_ = blk_next(A[M > 1 ? 1 : 0]);
+    const double am1 = b == 0 ? 0.0 : am1_, am2 = b == 0 ? 0.0 : am2_;
+    const double ap1 = last ? 0.0 : ap1_, ap2 = last ? 0.0 : ap2_;
+    auto Aw = [&](int m) -> double {
+      return m == -2 ? am2 : m == -1 ? am1 : m == M ? ap1 : m == M + 1 ? ap2 : A[m < 0 ? 0 : (m > M - 1 ? M - 1 : m)];
+    };
+    double rbot = 0.0;
+    {
+      double a1 = 0.0, a2 = 0.0;
+#pragma unroll
+      for (int m = 0; m < M; ++m)
+        if (m == nv - 1) {
+          a1 = A[m];
+          a2 = Aw(m - 1);
+        }
+      rbot = 2.0 * d4b * (d4b + 1.0) * a1 + a2;
+    }
+    auto rhs = [&](int m) -> double {
+      const int e = glob(m);
+      const bool bt = last && m == nv - 1;
+      if (!real(m)) return 0.0;
+      if (e == 0) {
+        const double grat = dp[1 < M ? 1 : 0] / dp[0];
+        return (grat + grat) * (grat + 1.0) * A[0] + A[1 < M ? 1 : 0];
+      }
+      const double d4 = dpw(m - 1) / dp[m];
+      double r = 3.0 * (Aw(m - 1) + d4 * A[m]);
+      if (bt) r = r - d4 * rbot / dbot;
+      return r;
+    };
+    double qe[M];
+    tri_apply<M, NB>(row, rhs, gam, rbs, qe, b, last);
+    double qlast = qe[M - 1];
+#pragma unroll
+    for (int m = 0; m < M; ++m)
+      if (m == nv - 1) qlast = qe[m];
+    const double qbot = (rbot - abot * qlast) / dbot;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int e = glob(m);
+      double v = qe[m];
+      const double a0 = Aw(m - 1), a1 = A[m];
+      if (e == 1 || e == km - 1) {
+        v = fmin(v, fmax(a0, a1));
+        v = fmax(v, fmin(a0, a1));
+      } else if (e >= 2 && e <= km - 2) {
+        const double g0 = a0 - Aw(m - 2), g1 = Aw(m + 1) - a1;
+        if (g0 * g1 > 0.0) {
+          v = fmin(v, fmax(a0, a1));
+          v = fmax(v, fmin(a0, a1));
+        } else if (g0 > 0.0) {
+          v = fmax(v, fmin(a0, a1));
+        } else {
+          v = fmin(v, fmax(a0, a1));
+          v = fmax(0.0, v);
+        }
+      }
+      qe[m] = real(m) ? v : 0.0;
+    }
+    const double qn_ = blk_next(qe[0]);
+    auto qr = [&](int m) -> double {
+      if (m + 1 < M) return (last && m == nv - 1) ? qbot : qe[m + 1 < M ? m + 1 : 0];
+      return last ? qbot : qn_;
+    };
+    double C[M + 1];
+    C[0] = 0.0;
+#pragma unroll
+    for (int m = 0; m < M; ++m) C[m + 1] = C[m] + A[m] * dp[m];
+    const double offx = blk_prev(scan_sum<NB, true>(C[M], b));
+    loff[wv][cl][b] = b == 0 ? 0.0 : offx;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      if (!real(m)) continue;
+      const int l = glob(m);
+      auto gm = [&](int mm) { return Aw(mm) - Aw(mm - 1); };
+      auto extm = [&](int mm) { return gm(mm) * gm(mm + 1) < 0.0; };
+      const double av = A[m];
+      double AL = qe[m], AR = qr(m), A6;
+      if (l == 0) {
+        AL = fmax(0.0, AL);
+        A6 = 3.0 * (2.0 * av - (AL + AR));
+        lim(av, AL, AR, A6, false, 1);
+      } else if (l == 1) {
+        A6 = 3.0 * (2.0 * av - (AL + AR));
+        lim(av, AL, AR, A6, extm(m), 2);
+      } else if (l < km - 2) {
+        const bool el = extm(m);
+        if ((el && extm(m - 1)) || (el && extm(m + 1))) {
+          AL = av; AR = av; A6 = 0.0;
+        } else {
+          A6 = 6.0 * av - 3.0 * (AL + AR);
+          if (fabs(A6) > fabs(AL - AR)) {
+            double pmp_1 = av - 2.0 * gm(m + 1);
+            double lac_1 = pmp_1 + 1.5 * gm(m + 2);
+            AL = fmin(fmax(AL, fmin(fmin(av, pmp_1), lac_1)), fmax(fmax(av, pmp_1), lac_1));
+            double pmp_2 = av + 2.0 * gm(m);
+            double lac_2 = pmp_2 - 1.5 * gm(m - 1);
+            AR = fmin(fmax(AR, fmin(fmin(av, pmp_2), lac_2)), fmax(fmax(av, pmp_2), lac_2));
+            A6 = 6.0 * av - 3.0 * (AL + AR);
+          }
+        }
+        lim(av, AL, AR, A6, el, 0);
+      } else if (l == km - 2) {
+        A6 = 3.0 * (2.0 * av - (AL + AR));
+        lim(av, AL, AR, A6, extm(m), 2);
+      } else {
+        AR = fmax(0.0, AR);
+        A6 = 3.0 * (2.0 * av - (AL + AR));
+        lim(av, AL, AR, A6, false, 1);
+      }
+      const double e0 = Ev[m], rdp = 1.0 / dp[m];
+      for (int k = kb[m]; k < kb[m + 1]; ++k) {
+        const double y = lt[wv][cl][k] - e0, x = y * rdp;
+        lq[wv][cl][k] = C[m] + y * (AL + 0.5 * x * (AR - AL + A6 * (1.0 - R23 * x)));
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+    asm volatile("" ::: "memory");
+    bool neg = false;
+#pragma unroll
+    for (int m = 0; m < M; ++m) {
+      const int kk = glob(m);
+      if (kk < km) {
+        const int o0 = lown[wv][cl][kk], o1 = lown[wv][cl][kk + 1];
+        const double q0v = lq[wv][cl][kk], q1v = lq[wv][cl][kk + 1];
+        const double num = o0 == o1 ? q1v - q0v : (loff[wv][cl][o1] - loff[wv][cl][o0]) + (q1v - q0v);
+        const double v = num / (lt[wv][cl][kk + 1] - lt[wv][cl][kk]);
+        if (valid)
+          __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), rQ, vb, (uint32_t)m * PB, 0);
+        neg = neg || v < 0.0;
+      }
+    }
+    const unsigned long long any = __ballot(neg);
+    const bool col_neg = ((any >> (cl * NB)) & ((NB == 64 ? ~0ull : (1ull << NB) - 1))) != 0;
+    if (fill && col_neg && b == 0 && valid) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      fillz_col(Col{out + o, P}, [&](int k2) { return lt[wv][cl][k2 + 1] - lt[wv][cl][k2]; }, km);
+    }
+    // the next tracer rewrites lq / loff: this one's reads (and fillz's) come first
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+  }
+}
+
 // Eulerian state from the remapped fields, one lane per (column, interface k = 0 .. km): the
 // top interface of layer k is ptop (k = 0) or ak + bk ps, its log the stored peln (k = 0, km)
 // or the log of that -- the same values a top-down walk carries from layer to layer
@@ -1342,6 +1626,16 @@ __global__ void __launch_bounds__(BLOCK) remap_finish_k(RemapArgs a) {
 
 int remap_jobs(int nq) { return nq + J_Q0; }
 
+// the step's remap form: GTFV3_REMAP (0 the level-block form, 2 the register columns, 1 the
+// scratch-column jobs; see lagrangian_to_eulerian)
+int remap_variant() {
+  static const int env = [] {
+    const char* e = std::getenv("GTFV3_REMAP");
+    return e ? std::atoi(e) : 0;
+  }();
+  return env;
+}
+
 // The column-job form keeps three scratch columns (edge values, factors, source copy) per
 // job: at most RM_CHUNK jobs share one set of scratch planes (jobs launched in chunks), so
 // L137 with 54 tracers needs 3 x 8 x 138 planes per sub-domain, not 3 x 59 x 138.
@@ -1379,7 +1673,8 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
     HIP_LAUNCH_CHECK();
     gt_bytes(L * 5 * e.C);  // delp delz pt read, T_v and -delz/delp source columns written
   }
-  // variant 0: the level-block form where a shape is instantiated ((NB - 1) M < npz <= NB M);
+  // variant 0: the level-block form where a shape is instantiated ((NB - 1) M < npz <= NB M),
+  // tracers RB_NT per wave (remap_blkq_k); 3: the same with one tracer per wave (remap_blk_k);
   // 2: the register-resident columns (L10 / 12 / 20 / 72); 1 (or no shape): the scratch-column jobs
   auto fits = [&](int m, int nb) { return (nb - 1) * m < npz && npz <= nb * m; };
   auto blk = [&](auto Mc, auto NBc, auto PARTc) {
@@ -1398,12 +1693,17 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
       gt_bytes(L * 2 * (e.X + e.Y) + L1 * e.C);
     }
     if (p2 && nq > 0) {
-      GT_LAUNCH((remap_blk_k<M, NB, PART, JK_Q>), dim3(gx, nq, d.nsub), tb, 0, c.st, a);
+      // tracers: RB_NT per wave sharing the pressure part (remap_blkq_k), or one per wave
+      if (variant == 3) {
+        GT_LAUNCH((remap_blk_k<M, NB, PART, JK_Q>), dim3(gx, nq, d.nsub), tb, 0, c.st, a);
+      } else {
+        GT_LAUNCH((remap_blkq_k<M, NB, PART, RB_NT>), dim3(gx, cdiv(nq, RB_NT), d.nsub), tb, 0, c.st, a);
+      }
       gt_bytes(nq * L * 2 * e.C + L1 * e.C);
     }
   };
   using std::integral_constant;
-  const bool b0 = variant == 0;
+  const bool b0 = variant == 0 || variant == 3;
   if (b0 && npz == 72) {
     blk(integral_constant<int, 9>{}, integral_constant<int, 8>{}, std::false_type{});
   } else if (b0 && fits(9, 8)) {

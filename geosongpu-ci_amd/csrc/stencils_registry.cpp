@@ -320,8 +320,9 @@ std::map<std::string, Fn>& reg() {
          Field& q = F(dy, f[0]);
          fillq2zero(dy.ctx(), q.nk, q.p, F(dy, f[1]).p, dy.field(f[2], 1).p);
        }},
-      // gfdl_1m(T, qv, ql, qr, qi, qs, qg, delp, delz | prec_r, prec_s, prec_g, prec_i) params: dt;
-      // the GFDL cloud microphysics column driver; the first seven fields are updated in place
+      // gfdl_1m(T, qv, ql, qr, qi, qs, qg, delp, delz | prec_r, prec_s, prec_g, prec_i) params: dt[,
+      // variant: 0 the level-block form where instantiated, 1 the column driver]; the GFDL cloud
+      // microphysics; the first seven fields are updated in place
       {"gfdl_1m",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
          need(f, 13, "gfdl_1m");
@@ -338,6 +339,7 @@ std::map<std::string, Fn>& reg() {
          a.scr = dy.field("_mp_scr", gfdl_mp_scratch_levels(t.nk)).p;
          a.pr = dy.field(f[9], 1).p; a.ps = dy.field(f[10], 1).p; a.pg = dy.field(f[11], 1).p;
          a.pi = dy.field(f[12], 1).p;
+         a.variant = p.size() > 1 ? (int)p[1] : 0;
          gfdl_1m(dy.ctx(), a);
        }},
       // evap_subl_pdf(T, qv, qlls, qils, qlcn, qicn, clls, clcn, pl, nactl, nacti) params: dt;

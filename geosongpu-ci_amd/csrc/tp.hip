@@ -711,10 +711,15 @@ __global__ void __launch_bounds__(MW * MWAVES, OCC ? OCC : (AHEAD2 ? 1 : 4)) tp_
     return (s_ * a.nk + k) * a.ntg + tg;
   };
   if constexpr (EXS == 0) {
-    strip = (int)(w % (unsigned)a.nstrip);
-    const unsigned t = w / (unsigned)a.nstrip;
+    // field group fastest: the groups of one (strip, segment, level) are neighbouring waves
+    // of one workgroup, so the Courant / flux rows they all read come from HBM once (one
+    // CU's L1, one XCD's L2) instead of once per group on different XCDs
+    const unsigned tg = w % (unsigned)a.ntg;
+    unsigned t = w / (unsigned)a.ntg;
+    strip = (int)(t % (unsigned)a.nstrip);
+    t = t / (unsigned)a.nstrip;
     seg = (int)(t % (unsigned)a.nseg);
-    z = (int)(t / (unsigned)a.nseg);
+    z = (int)((t / (unsigned)a.nseg) * (unsigned)a.ntg + tg);
     if (z >= a.nz) return;  // whole wavefront leaves; no workgroup barrier follows
   } else {
     // pair p = (sub-domain, strip) of this kind; then segment; then (field group, level);
@@ -777,17 +782,21 @@ bool pair_last_strip(const Dims& d, int nstrip) {
 // Fraction of the (sub-domain, strip) pairs of a launch whose strip reaches a tile edge
 // (same test as the kernel): the EX kernel's share of the launch's algorithmic bytes.
 // `pex` / `pin` receive the (sub-domain, strip) pairs of each kind (s * 256 + strip).
+// Weighted by the strips' output columns (the last strip of a row is short: C180 has strips
+// of 58, 58, 58 and 7 edges), so each kernel is charged the bytes of the columns it writes.
 double ex_fraction(const Ctx& c, int nstrip, std::vector<int>* pex = nullptr, std::vector<int>* pin = nullptr) {
-  int nex = 0;
+  long nex = 0, nall = 0;
   for (int s = 0; s < c.d.nsub; ++s)
     for (int st = 0; st < nstrip; ++st) {
       const int A = st * MOUT + c.hsubs[s].ioff;
       const bool ex = !(A - 1 >= 2 && A + MOUT + 1 <= c.hsubs[s].N - 2);
-      nex += ex ? 1 : 0;
+      const int outs = std::min(MOUT, c.d.nx + 1 - st * MOUT);
+      nex += ex ? outs : 0;
+      nall += outs;
       std::vector<int>* v = ex ? pex : pin;
       if (v) v->push_back(s * 256 + st);
     }
-  return (double)nex / ((double)c.d.nsub * nstrip);
+  return (double)nex / (double)nall;
 }
 
 // One march as two kernels: the tile-edge strips (EX forms, AHEAD2, their register count)

@@ -80,13 +80,15 @@ def close(got, ref, what, floor=1e-300):
     np.testing.assert_allclose(got, ref, rtol=1e-4, atol=1e-9 * scale, err_msg=what)
 
 
-def test_gfdl_mp_matches_oracle(dom, require_gpu):
+@pytest.mark.parametrize("variant", [0, 1])
+def test_gfdl_mp_matches_oracle(dom, require_gpu, variant):
+    """variant 0: the level-block form (mpdrv_blk_k<2, 16> at 30 levels), 1: the column driver"""
     st = moist_state(dom.shape(NK), seed=13)
     upload_state(dom, st)
     dt = 450.0
     names = ["m_T", "m_qv", "m_ql", "m_qr", "m_qi", "m_qs", "m_qg", "m_delp", "m_delz",
              "m_pr", "m_ps", "m_pg", "m_pi"]
-    dom.stencil("gfdl_1m", names, [dt])
+    dom.stencil("gfdl_1m", names, [dt, variant])
     got = {n: dom.download(n) for n in names[:7] + names[9:]}
     for s, rows in SAMPLE:
         c = {k: cols_of(dom, st[k], s, rows) for k in ("T", "delp", "delz", "qv", "ql", "qr", "qi", "qs", "qg")}

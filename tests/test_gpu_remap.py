@@ -92,3 +92,22 @@ def test_remap_register_columns_bitwise(pkg, require_gpu, npz, nq):
         d.close()
     for k in FIELDS:
         assert np.array_equal(outs[0][k], outs[1][k]), f"{k}: register columns differ from the job form"
+
+
+@pytest.mark.parametrize("npz,nq", [(72, 11), (137, 5), (10, 3)])
+def test_remap_shared_tracer_pivots_bitwise(pkg, require_gpu, npz, nq):
+    """The tracer jobs with the pressure part shared by four tracers per wave (remap_blkq_k,
+    variant 0; nq = 11 and 5 leave a partial last group) give bit for bit the one-tracer-per-
+    wave level-block form (remap_blk_k, variant 3)."""
+    outs = []
+    for variant in (0, 3):
+        d = pkg.Domain(npx=13, npz=npz, nq=nq)
+        r = rng(900 + npz)
+        st, ak, bk, ks = lagrangian_state(pkg, d, npz, nq, r)
+        d.set_vertical(ak, bk, ks)
+        for k, v in st.items():
+            d.upload(k, v)
+        d.stencil("lagrangian_to_eulerian", [], [1, variant])
+        outs.append(d.download("q"))
+        d.close()
+    assert np.array_equal(outs[0], outs[1]), "shared-pivot tracer remap differs from the per-tracer form"

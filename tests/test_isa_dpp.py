@@ -95,6 +95,7 @@ def masked_dpp(asm, kernel_re, allowed=1):
 @pytest.mark.skipif(not os.path.exists(HIPCC), reason="hipcc not available")
 @pytest.mark.parametrize("src,kre,allowed", [(os.path.join(CSRC, "riem.hip"), r"_Z\S*riem_scan_k\S*", 1),
                                              (os.path.join(CSRC, "remap.hip"), r"_Z\S*remap_blk_k\S*", 1),
+                                             (os.path.join(CSRC, "moist.hip"), r"_Z\S*mpdrv_blk_k\S*", 1),
                                              (os.path.join(ROOT, "tests", "native", "blockscan_probe.hip"),
                                               r"_Z5k_tri\S*", 0)])
 def test_no_dpp_under_divergent_exec(tmp_path, src, kre, allowed):
