@@ -173,8 +173,9 @@ def parse():
                         "transport beside the main chain; 1: everything on one stream)")
     p.add_argument("--rank-proxy", type=int, default=0,
                    help="measurement aid, one GPU: run rank 0 of an N-rank layout alone with the null "
-                        "transport (cross-rank messages dropped) -- the per-GPU compute time of an N-GPU "
-                        "run without the exchange; not a numerical result")
+                        "transport (each cross-rank receive answered by the rank's own send, as device copies) -- "
+                        "the per-GPU compute time of an N-GPU run without the xGMI transfers; not a "
+                        "numerical result")
     p.add_argument("--roofline-steps", type=int, default=3,
                    help="steps of the single-stream roofline pass after the timed region")
     p.add_argument("--moist", action="store_true",

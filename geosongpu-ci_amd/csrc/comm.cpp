@@ -164,20 +164,49 @@ class LoopbackTransport : public Transport {
 };
 
 // ---- null (measurement only) ----
-// One rank of a multi-rank layout alone on a device: cross-rank messages are dropped and
-// not unpacked (the remote halo points keep their values -- the initial state's, so the
-// rank's state stays physical, only stale near its cross-rank edges), so the rank's kernels
-// run exactly the work of its share of the layout -- the per-GPU compute time of an N-GPU
-// run without the exchange (bench.py --rank-proxy).  Never a numerical path.
+// One rank of a multi-rank layout alone on a device (bench.py --rank-proxy, the bridge's
+// proxy topology): no peer exists, so each message from a peer is answered by this rank's own
+// message to that peer -- the k-th receive from rank R gets a device copy of the k-th send to
+// R (the same halo depth both ways, so the sizes match; a shorter one is copied as far as it
+// goes).  The remote halo points then hold values of this rank's own rows next to that edge
+// (a reflection, in the peer's point order): finite and of the field's own magnitude at that
+// level, so the state stays physical away from the cross-rank edges, and the pack, copy and
+// unpack launches are those of the real exchange.  The rank's kernels run exactly the work of
+// its share of the layout.  Never a numerical path: values within reach of a cross-rank edge
+// are not the multi-rank run's.
 class NullTransport : public Transport {
  public:
-  void group_start() override {}
-  void send(const double*, size_t, int, hipStream_t) override {}
-  void recv(double*, size_t, int, hipStream_t) override {}
-  void group_end(hipStream_t) override {}
+  void group_start() override {
+    sends_.clear();
+    recvs_.clear();
+  }
+  void send(const double* buf, size_t n, int peer, hipStream_t) override { sends_.push_back({peer, buf, n}); }
+  void recv(double* buf, size_t n, int peer, hipStream_t) override { recvs_.push_back({peer, buf, n}); }
+  void group_end(hipStream_t st) override {
+    std::vector<bool> used(sends_.size(), false);
+    for (auto& r : recvs_) {
+      for (size_t i = 0; i < sends_.size(); ++i) {
+        if (used[i] || sends_[i].peer != r.peer) continue;
+        used[i] = true;
+        const size_t n = std::min(r.n, sends_[i].n);
+        if (n) HIP_CHECK(hipMemcpyAsync(const_cast<double*>(r.p), sends_[i].p, sizeof(double) * n,
+                                        hipMemcpyDeviceToDevice, st));
+        break;
+      }
+    }
+    sends_.clear();
+    recvs_.clear();
+  }
   void allreduce_max(double*, int, hipStream_t) override {}
   bool capturable() const override { return true; }
-  bool delivers() const override { return false; }
+
+ private:
+  struct Pending {
+    int peer;
+    const double* p;
+    size_t n;
+  };
+  std::vector<Pending> sends_, recvs_;
 };
 
 }  // namespace

@@ -24,13 +24,11 @@ class Transport {
   virtual void allreduce_max(double* dev, int n, hipStream_t st) = 0;
   // its enqueue makes no host wait, so a HIP graph can capture it (Dycore::step)
   virtual bool capturable() const { return false; }
-  // messages arrive (false: the null transport -- the exchanger then skips the unpack, so
-  // the remote halo points keep their values instead of the never-received buffer's)
-  virtual bool delivers() const { return true; }
 };
 
 std::unique_ptr<Transport> make_nccl_transport(int nranks, int rank, const void* nccl_id);
-// group < 0: the null transport (one rank alone, messages dropped: measurement only)
+// group < 0: the null transport (one rank alone, each receive answered by its own send to
+// that peer: measurement only)
 std::unique_ptr<Transport> make_loopback_transport(int group, int nranks, int rank);
 
 }  // namespace gtfv3

@@ -235,8 +235,7 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
   if (buf_elems_) {
     HIP_CHECK(hipMalloc(&sendbuf_, sizeof(double) * buf_elems_));
     HIP_CHECK(hipMalloc(&recvbuf_, sizeof(double) * buf_elems_));
-    // zeroed (deterministic contents; with the null transport nothing is received and
-    // nothing is unpacked)
+    // zeroed (deterministic contents before the first message)
     HIP_CHECK(hipMemset(sendbuf_, 0, sizeof(double) * buf_elems_));
     HIP_CHECK(hipMemset(recvbuf_, 0, sizeof(double) * buf_elems_));
   }
@@ -424,7 +423,7 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
   launch(0);
   if (remote) {
     HIP_CHECK(hipStreamWaitEvent(stream, ev_recvd_, 0));
-    if (tr_->delivers()) launch(2);
+    launch(2);
   }
 }
 

@@ -8,6 +8,7 @@
 #include <algorithm>
 #include <climits>
 
+#include "fastmath.hpp"
 #include "kernels_nh.hpp"
 #include "stencil_common.hpp"
 
@@ -362,7 +363,7 @@ __global__ void __launch_bounds__(64) pk3_pe_halo_k(Dims d, int npz, double ptop
     if (k0 + u < k1e) {
       pei = pei + v[u];
       const long x = b1 + (long)(k0 + u + 1) * P;
-      pk3[x] = exp(KAPPA * log(pei));
+      pk3[x] = fm_exp(KAPPA * fm_log(pei));  // as riem_scan_k forms pk3 in the compute domain
       if (do_pe && ring1) pe[x] = pei;
     }
   }

@@ -1310,7 +1310,11 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) remap_blkq_k(RemapArgs a) {
   constexpr int NC = 64 / NB, KX = NB * M;
   __shared__ double lab[2 * (KX + 1)];
   __shared__ double lq[RB_WAVES][NC][KX + 1];
-  __shared__ double lt[RB_WAVES][NC][KX + 1];
+  // per target interface k, formed once from the pressures: its offset y from the top edge of
+  // the source layer holding it and y / dp of that layer (the source edges and 1 / dp then
+  // hold no registers across the tracers; the target thicknesses are T(k + 1) - T(k))
+  __shared__ double ly[RB_WAVES][NC][KX + 1];
+  __shared__ double lx[RB_WAVES][NC][KX + 1];
   __shared__ int lown[RB_WAVES][NC][KX + 1];
   __shared__ double loff[RB_WAVES][NC][NB];
   const int km = a.npz;
@@ -1414,10 +1418,13 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) remap_blkq_k(RemapArgs a) {
       kb[m] = k;
       if (!real(m)) continue;
       const bool lastlayer = last && m == nv - 1;
+      const double e0 = Ev[m], rdp = 1.0 / dp[m];
       while (k <= km) {
         const double t = T(k);
         if (!lastlayer && t >= Ev[m + 1]) break;
-        lt[wv][cl][k] = t;
+        const double y = t - e0;
+        ly[wv][cl][k] = y;
+        lx[wv][cl][k] = y * rdp;
         lown[wv][cl][k] = b;
         ++k;
       }
@@ -1548,9 +1555,8 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) remap_blkq_k(RemapArgs a) {
         A6 = 3.0 * (2.0 * av - (AL + AR));
         lim(av, AL, AR, A6, false, 1);
       }
-      const double e0 = Ev[m], rdp = 1.0 / dp[m];
       for (int k = kb[m]; k < kb[m + 1]; ++k) {
-        const double y = lt[wv][cl][k] - e0, x = y * rdp;
+        const double y = ly[wv][cl][k], x = lx[wv][cl][k];
         lq[wv][cl][k] = C[m] + y * (AL + 0.5 * x * (AR - AL + A6 * (1.0 - R23 * x)));
       }
     }
@@ -1564,7 +1570,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) remap_blkq_k(RemapArgs a) {
         const int o0 = lown[wv][cl][kk], o1 = lown[wv][cl][kk + 1];
         const double q0v = lq[wv][cl][kk], q1v = lq[wv][cl][kk + 1];
         const double num = o0 == o1 ? q1v - q0v : (loff[wv][cl][o1] - loff[wv][cl][o0]) + (q1v - q0v);
-        const double v = num / (lt[wv][cl][kk + 1] - lt[wv][cl][kk]);
+        const double v = num / (T(kk + 1) - T(kk));
         if (valid)
           __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), rQ, vb, (uint32_t)m * PB, 0);
         neg = neg || v < 0.0;
@@ -1574,7 +1580,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) remap_blkq_k(RemapArgs a) {
     const bool col_neg = ((any >> (cl * NB)) & ((NB == 64 ? ~0ull : (1ull << NB) - 1))) != 0;
     if (fill && col_neg && b == 0 && valid) {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      fillz_col(Col{out + o, P}, [&](int k2) { return lt[wv][cl][k2 + 1] - lt[wv][cl][k2]; }, km);
+      fillz_col(Col{out + o, P}, [&](int k2) { return T(k2 + 1) - T(k2); }, km);
     }
     // the next tracer rewrites lq / loff: this one's reads (and fillz's) come first
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");

@@ -423,16 +423,23 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
     }
   }
 
-  // ---- S1: pem (ptop + prefix sums of DP)
+  // ---- S1: pem = ptop + DP[0] + DP[1] + ... summed top-down in level order, block after
+  // block (the carry handed down by DPP): bit for bit the sum pk3_pe_halo forms for the halo
+  // columns, so pk3 / pe agree across a sub-domain edge (the step is then the same on 1x1 and
+  // 2x2 / 1x4 sub-domains); M dependent adds per block, NB blocks in turn
   double pem[M + 1];
   {
-    double tot = 0.0;
+    double carry = a.ptop;
+#pragma unroll 1
+    for (int r = 0; r < NB; ++r) {
+      if (b == r) {
+        pem[0] = carry;
 #pragma unroll
-    for (int m = 0; m < M; ++m) tot += DP[m];
-    const double ex = blk_prev(scan_sum<NB, true>(tot, b));
-    pem[0] = b == 0 ? a.ptop : a.ptop + ex;  // ex: shifted above, outside the ?: (blockscan.hpp)
-#pragma unroll
-    for (int m = 0; m < M; ++m) pem[m + 1] = pem[m] + DP[m];
+        for (int m = 0; m < M; ++m) pem[m + 1] = pem[m] + DP[m];
+      }
+      const double nx = blk_prev(pem[M]);  // all lanes, outside the branch (blockscan.hpp)
+      carry = b == r + 1 ? nx : carry;
+    }
   }
 #pragma unroll
   for (int m = 0; m < M; ++m) { dump(0, m, pem[m]); dump(13, m, gl[m]); dump(14, m, G[m]); }

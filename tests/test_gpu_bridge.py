@@ -272,7 +272,7 @@ def test_bridge_one_subdomain_per_rank(pkg, require_gpu):
     d, st, ak, bk, ks = _setup(pkg, npx, npz, nq)
     six, shapes = _bridge_call(pkg, st, d, ak, bk, ks, npx, npz, nq)
     d.close()
-    band = 50  # cells along each tile edge reached by the dropped messages in one step (measured 45)
+    band = 50  # cells along each tile edge reached by the missing messages in one step (measured 45)
     for rank in (0, 4):
         one, _ = _bridge_call_rank(pkg, st, ak, bk, ks, npx, npz, nq, rank)
         for name in ("u", "v", "w", "delz", "pt", "delp", "q", "ps", "pe", "peln", "pk", "pkz", "omga"):
@@ -286,7 +286,7 @@ def test_bridge_one_subdomain_per_rank(pkg, require_gpu):
             else:
                 wa, wb = a[i0:i1, j0:j1], b[i0:i1, j0:j1]
             assert np.all(np.isfinite(wb)), f"{name}: six-tile run not finite"
-            # reach of the dropped messages: the deepest differing compute point from the edge
+            # reach of the missing messages: the deepest differing compute point from the edge
             ca = a[-li:N - li, :, -lj:N - lj] if kj else a[-li:N - li, -lj:N - lj]
             cb = b[-li:N - li, :, -lj:N - lj] if kj else b[-li:N - li, -lj:N - lj]
             diff = np.argwhere(ca != cb)

@@ -211,10 +211,10 @@ def test_c360_l137_54_tracers_step_properties(pkg, require_gpu):
 def test_c720_l137_54_rank_proxy8_step_properties(pkg, require_gpu):
     """Config 5 at its own geometry, as one GPU's share of the 8-GPU run: C720 L137 x 54
     tracers, layout 1x4 (bench.py's 8-GPU layout: bands of 720 x 180, three per rank), rank 0
-    of 8 alone on the GPU with the null transport (anchor: held_suarez.py:320 for L137).  The
-    cross-rank messages are dropped and not unpacked, so the remote halo points keep the
-    initial state's values: the rank's state stays physical, stale only within reach of its
-    cross-rank edges.  After one step: every field finite and bounded over the rank's whole
+    of 8 alone on the GPU with the null transport (anchor: held_suarez.py:320 for L137).  Each
+    cross-rank message is answered by the rank's own message to that peer (comm.cpp
+    NullTransport): the remote halo points hold the rank's own edge rows, so its state stays
+    physical, wrong only within reach of its cross-rank edges.  After one step: every field finite and bounded over the rank's whole
     compute domain, no negative tracer after fill and no tracer above its initial maximum by
     more than 1e-9 of it (the stale halo values lie within the initial ranges too).  Set-up
     uploads the tracers one at a time (the host never holds all 54 at this size)."""

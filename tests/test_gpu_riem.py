@@ -302,3 +302,38 @@ def test_riem_on_step_inputs(pkg, require_gpu, monkeypatch, npz, n_split):
             # column form (ocml exp / log against glibc) is 2.4e-9 from the oracle here
             closef(region(got["ppe"][s], 0, d.nx, d.ny), region(o["ppe"], 0, d.nx, d.ny), f"{t} ppe", rtol=1e-8)
     d.close()
+
+
+@pytest.mark.parametrize("npz", [10, 72, 137])
+@pytest.mark.parametrize("cgrid", [True, False])
+@pytest.mark.parametrize("shift", [1, 5])
+def test_riem_column_position_invariant(pkg, require_gpu, npz, cgrid, shift):
+    """Each column's result depends on that column's data only, not on which lanes (or which
+    neighbours in its wave) it lands on: the inputs rolled by `shift` columns along x give
+    the outputs rolled by the same amount, bit for bit (the step's 1x1 vs 2x2 and 1x1 vs
+    1x4 identity rests on this)"""
+    d = pkg.Domain(npx=13, npz=npz, nq=1)
+    col = columns(d, npz, rng(500 + npz), True)
+    ring = 1 if cgrid else 0
+    got = []
+    for sh in (0, shift):
+        for k in ("delp", "pt", "phis", "w", "zh"):
+            d.upload("rp_" + k, np.roll(col[k], sh, axis=-1))
+        if cgrid:
+            d.stencil("riem_solver_c", ["rp_delp", "rp_pt", "rp_w", "rp_phis", "rp_zh", "rp_pef"],
+                      [225.0, PTOP, P_FAC, DZ_MIN, 0])
+            outs = ("rp_zh", "rp_pef")
+        else:
+            for k in ("rp_pe", "rp_peln", "rp_pk"):
+                d.upload(k, np.zeros(d.shape(npz + 1)))
+            d.stencil("riem_solver3", ["rp_delp", "rp_pt", "rp_w", "rp_phis", "rp_zh", "rp_delz", "rp_ppe",
+                                       "rp_pk3", "rp_pe", "rp_peln", "rp_pk", "rp_ws"],
+                      [450.0, PTOP, P_FAC, DZ_MIN, 1, 0])
+            outs = ("rp_w", "rp_zh", "rp_delz", "rp_ppe", "rp_pk3")
+        got.append({k: d.download(k) for k in outs})
+    lo, hi = NG - ring, NG + d.nx + ring  # computed columns; compare where both runs computed
+    for k in got[0]:
+        a = got[0][k][..., NG - ring:NG + d.ny + ring, lo:hi - shift]
+        b = got[1][k][..., NG - ring:NG + d.ny + ring, lo + shift:hi]
+        nbad = int((a != b).sum())
+        assert nbad == 0, f"{k}: {nbad} values depend on the column's position (max diff {np.abs(a - b).max():.3e})"

@@ -212,9 +212,8 @@ def test_acoustic_graph_bitwise(pkg, require_gpu, monkeypatch, proxy):
     step on) against the same sub-steps launched one by one: three C24 L20 steps, bit for bit
     on every state field -- one rank with all six tiles, and rank 0 of the 8-rank layout alone
     on the null transport (bench.py --rank-proxy 8, the 1x4 bands: the exchange's pack /
-    unpack and comm-stream events inside the graph).  The proxy's remote halo points are never
-    received (zeros from the unpack), so its state is not physical and turns non-finite: there
-    the comparison counts NaN equal to NaN."""
+    unpack and comm-stream events inside the graph).  The proxy's remote halo points hold its
+    own reflected edge rows (comm.cpp NullTransport); NaN would count equal to NaN."""
     state = importlib.import_module(pkg.__name__ + ".state")
     npz = 20
     ak, bk, ks = state.hybrid_levels(npz)
