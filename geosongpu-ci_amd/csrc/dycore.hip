@@ -527,7 +527,6 @@ void Dycore::step() {
   da.ut = S("_ds_ut", npz); da.vt = S("_ds_vt", npz);
   da.fx = S("_ds_fx", npz); da.fy = S("_ds_fy", npz); da.gwx = S("_ds_gwx", npz); da.gwy = S("_ds_gwy", npz);
   da.gtx = S("_ds_gtx", npz); da.gty = S("_ds_gty", npz); da.ke = S("_ds_ke", npz); da.vort = S("_ds_vort", npz);
-  da.gvx = S("_ds_gvx", npz); da.gvy = S("_ds_gvy", npz);
   // damping beyond nord = 0 (damp.hip): off in the Held-Suarez namelist
   da.nord = nl.nord; da.nord_v = nl.nord_v; da.d4_bg = nl.d4_bg; da.vtdm4 = nl.vtdm4; da.d_con = nl.d_con;
   const bool dcon = nl.d_con > 1e-5, vdamp = nl.vtdm4 > 1e-5;
@@ -695,7 +694,7 @@ void Dycore::step() {
                                nl.d_con, (double)nl.nord, (double)nl.nord_v, (double)nl.hord_mt, (double)nl.hord_vt,
                                (double)nl.hord_tm, (double)nl.hord_dp,
                                // launch-shape switches read at every launch (tests flip them in-process)
-                               (double)kloop_levels(), (double)loads_first(),
+                               (double)kloop_levels(),
                                (double)riem_variant(), (double)remap_variant()};
     for (const Field* f : {&u, &v, &w, &delz, &pt, &delp, &phis})
       key.push_back((double)reinterpret_cast<uintptr_t>(f->p));

@@ -16,7 +16,6 @@ struct CswArgs {
 void c_sw(const Ctx& c, const CswArgs& a);            // the two stages in order
 void c_sw_transport(const Ctx& c, const CswArgs& a);  // d2a2c_vect, delpc / ptc / wc, ke
 void c_sw_winds(const Ctx& c, const CswArgs& a);      // vorticity, uc / vc update
-bool loads_first();                                          // GTFV3_LOADS_FIRST (default on)
 int kloop_levels();                                          // GTFV3_KLOOP (stencil_common.hpp)
 
 struct DswArgs {

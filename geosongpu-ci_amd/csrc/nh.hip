@@ -838,10 +838,9 @@ __global__ void __launch_bounds__(256) nhpgrad_k(Dims d, const SubInfo* __restri
 // order as udzc_k / pgradc_k / nhpgrad_k above, so the outputs are bit-identical.  The
 // thread of point (i, j) walks levels k0 .. k1-1 of one sub-domain; the interface values a
 // level shares with the next and the metric terms stay in registers.
-// LF (GTFV3_LOADS_FIRST, default on): the six gz points both upwind picks choose among are
-// loaded with the level's ut / vt, before the fluxes whose signs select them (the same
-// values and expressions: bit-identical); otherwise each pick's load waits for its flux
-template <bool LF>
+// Loads first: the six gz points both upwind picks choose among are loaded with the level's
+// ut / vt, before the fluxes whose signs select them (the branch-ordered twin, each pick's
+// load waiting for its flux, was bit-identical and is deleted in round 4)
 __global__ void __launch_bounds__(256) udzc_kl(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
                                                int npz, int nkb, int klb, const double* __restrict__ dp0,
                                                const double* __restrict__ ut, const double* __restrict__ vt,
@@ -863,10 +862,7 @@ __global__ void __launch_bounds__(256) udzc_kl(Dims d, const SubInfo* __restrict
   for (int k = k0; k < k1; ++k) {
     double xf0, xf1, yf0, yf1;
     const double* g = gz + ((long)s * (npz + 1) + k) * P;
-    double gW = 0.0, gCX = 0.0, gE = 0.0, gS = 0.0, gCY = 0.0, gN = 0.0;
-    if (LF) {
-      gW = g[gw]; gCX = g[gcx]; gE = g[ge]; gS = g[gs]; gCY = g[gcy]; gN = g[gn];
-    }
+    const double gW = g[gw], gCX = g[gcx], gE = g[ge], gS = g[gs], gCY = g[gcy], gN = g[gn];
     if (k == 0) {
       const double top_ratio = dp0[0] / (dp0[1] + dp0[0]);
       const double a0 = UT[0], a1 = UT[1], b0 = VT[0], b1 = VT[N1];
@@ -899,10 +895,6 @@ __global__ void __launch_bounds__(256) udzc_kl(Dims d, const SubInfo* __restrict
       p0 = a0; p1 = a1; p2 = b0; p3 = b1;
       have = true;
     }
-    if (!LF) {
-      gW = xf0 > 0.0 ? g[gw] : 0.0; gCX = g[gcx]; gE = xf1 > 0.0 ? 0.0 : g[ge];
-      gS = yf0 > 0.0 ? g[gs] : 0.0; gCY = g[gcy]; gN = yf1 > 0.0 ? 0.0 : g[gn];
-    }
     const double fx0 = xf0 * (xf0 > 0.0 ? gW : gCX);
     const double fx1 = xf1 * (xf1 > 0.0 ? gCX : gE);
     const double fy0 = yf0 * (yf0 > 0.0 ? gS : gCY);
@@ -912,7 +904,6 @@ __global__ void __launch_bounds__(256) udzc_kl(Dims d, const SubInfo* __restrict
   }
 }
 
-template <bool LF>
 __global__ void __launch_bounds__(256) pgradc_kl(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
                                                  int npz, int nkb, int klb, double dt2, const double* __restrict__ delpc,
                                                  const double* __restrict__ pkc, const double* __restrict__ gz,
@@ -930,49 +921,26 @@ __global__ void __launch_bounds__(256) pgradc_kl(Dims d, const SubInfo* __restri
   double pk0 = PK[l0], gz0 = GZ[l0];
   double pk0w = du ? PK[l0 + W] : 0.0, gz0w = du ? GZ[l0 + W] : 0.0;
   double pk0s = dv ? PK[l0 + S] : 0.0, gz0s = dv ? GZ[l0 + S] : 0.0;
-  if (LF) {
-    // loads first (GTFV3_LOADS_FIRST): both directions' inputs of a level in one group (the
-    // west / south offsets 0 on the row / column that takes no update), then the same
-    // expressions as below
-    const long Wd = du ? W : 0, Sd = dv ? S : 0;
-    for (int k = k0; k < k1; ++k) {
-      const long l1 = (long)(k + 1) * P, lk = ((long)s * npz + k) * P + o;
-      const double pk1 = PK[l1], gz1 = GZ[l1];
-      const double pk1w = PK[l1 + Wd], gz1w = GZ[l1 + Wd], pk1s = PK[l1 + Sd], gz1s = GZ[l1 + Sd];
-      const double dcw = delpc[lk + Wd], dc = delpc[lk], dcs = delpc[lk + Sd], u0 = uc[lk], v0 = vc[lk];
-      if (du) {
-        const double wsum = dcw + dc;
-        uc[lk] = u0 + dt2 * rdxc / wsum * ((gz1w - gz0) * (pk1 - pk0w) + (gz0w - gz1) * (pk1w - pk0));
-      }
-      if (dv) {
-        const double wsum = dcs + dc;
-        vc[lk] = v0 + dt2 * rdyc / wsum * ((gz1s - gz0) * (pk1 - pk0s) + (gz0s - gz1) * (pk1s - pk0));
-      }
-      pk0 = pk1; gz0 = gz1; pk0w = pk1w; gz0w = gz1w; pk0s = pk1s; gz0s = gz1s;
-    }
-    return;
-  }
+  // loads first: both directions' inputs of a level in one group (the west / south offsets 0
+  // on the row / column that takes no update)
+  const long Wd = du ? W : 0, Sd = dv ? S : 0;
   for (int k = k0; k < k1; ++k) {
     const long l1 = (long)(k + 1) * P, lk = ((long)s * npz + k) * P + o;
     const double pk1 = PK[l1], gz1 = GZ[l1];
-    double pk1w = 0.0, gz1w = 0.0, pk1s = 0.0, gz1s = 0.0;
+    const double pk1w = PK[l1 + Wd], gz1w = GZ[l1 + Wd], pk1s = PK[l1 + Sd], gz1s = GZ[l1 + Sd];
+    const double dcw = delpc[lk + Wd], dc = delpc[lk], dcs = delpc[lk + Sd], u0 = uc[lk], v0 = vc[lk];
     if (du) {
-      pk1w = PK[l1 + W];
-      gz1w = GZ[l1 + W];
-      const double wsum = delpc[lk + W] + delpc[lk];
-      uc[lk] = uc[lk] + dt2 * rdxc / wsum * ((gz1w - gz0) * (pk1 - pk0w) + (gz0w - gz1) * (pk1w - pk0));
+      const double wsum = dcw + dc;
+      uc[lk] = u0 + dt2 * rdxc / wsum * ((gz1w - gz0) * (pk1 - pk0w) + (gz0w - gz1) * (pk1w - pk0));
     }
     if (dv) {
-      pk1s = PK[l1 + S];
-      gz1s = GZ[l1 + S];
-      const double wsum = delpc[lk + S] + delpc[lk];
-      vc[lk] = vc[lk] + dt2 * rdyc / wsum * ((gz1s - gz0) * (pk1 - pk0s) + (gz0s - gz1) * (pk1s - pk0));
+      const double wsum = dcs + dc;
+      vc[lk] = v0 + dt2 * rdyc / wsum * ((gz1s - gz0) * (pk1 - pk0s) + (gz0s - gz1) * (pk1s - pk0));
     }
     pk0 = pk1; gz0 = gz1; pk0w = pk1w; gz0w = gz1w; pk0s = pk1s; gz0s = gz1s;
   }
 }
 
-template <bool LF>
 __global__ void __launch_bounds__(256) nhpgrad_kl(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
                                                   int npz, int nkb, int klb, double dt, double ptk,
                                                   const double* __restrict__ ppb, const double* __restrict__ gzb,
@@ -1002,54 +970,24 @@ __global__ void __launch_bounds__(256) nhpgrad_kl(Dims d, const SubInfo* __restr
     pp0n = top ? 0.0 : PP[l0 + Nn];
     gz0n = GZ[l0 + Nn];
   }
-  if (LF) {
-    // loads first (GTFV3_LOADS_FIRST): both directions' inputs of a level in one group (the
-    // east / north offsets 0 on the column / row that takes no update), then the same
-    // expressions as below
-    const long Ed = du ? E : 0, Nd = dv ? Nn : 0;
-    for (int k = k0; k < k1; ++k) {
-      const long l1 = (long)(k + 1) * P, lk = ((long)s * npz + k) * P + o;
-      const double pk1 = PK[l1], pp1 = PP[l1], gz1 = GZ[l1];
-      const double pk1e = PK[l1 + Ed], pp1e = PP[l1 + Ed], gz1e = GZ[l1 + Ed];
-      const double pk1n = PK[l1 + Nd], pp1n = PP[l1 + Nd], gz1n = GZ[l1 + Nd];
-      const double u0 = u[lk], v0 = v[lk], w0 = wk1[lk], we = wk1[lk + Ed], wn = wk1[lk + Nd];
-      if (du) {
-        const double wk0 = pk1 - pk0, wke = pk1e - pk0e;
-        const double du1 = dt / (wk0 + wke) * ((gz1 - gz0e) * (pk1e - pk0) + (gz0 - gz1e) * (pk1 - pk0e));
-        u[lk] = (u0 + du1 + dt / (w0 + we) * ((gz1 - gz0e) * (pp1e - pp0) + (gz0 - gz1e) * (pp1 - pp0e))) * rdx;
-      }
-      if (dv) {
-        const double wk0 = pk1 - pk0, wke = pk1n - pk0n;
-        const double dv1 = dt / (wk0 + wke) * ((gz1 - gz0n) * (pk1n - pk0) + (gz0 - gz1n) * (pk1 - pk0n));
-        v[lk] = (v0 + dv1 + dt / (w0 + wn) * ((gz1 - gz0n) * (pp1n - pp0) + (gz0 - gz1n) * (pp1 - pp0n))) * rdy;
-      }
-      pk0 = pk1; pp0 = pp1; gz0 = gz1;
-      pk0e = pk1e; pp0e = pp1e; gz0e = gz1e;
-      pk0n = pk1n; pp0n = pp1n; gz0n = gz1n;
-    }
-    return;
-  }
+  // loads first: both directions' inputs of a level in one group (the east / north offsets 0
+  // on the column / row that takes no update)
+  const long Ed = du ? E : 0, Nd = dv ? Nn : 0;
   for (int k = k0; k < k1; ++k) {
     const long l1 = (long)(k + 1) * P, lk = ((long)s * npz + k) * P + o;
     const double pk1 = PK[l1], pp1 = PP[l1], gz1 = GZ[l1];
-    double pk1e = 0.0, pp1e = 0.0, gz1e = 0.0, pk1n = 0.0, pp1n = 0.0, gz1n = 0.0;
+    const double pk1e = PK[l1 + Ed], pp1e = PP[l1 + Ed], gz1e = GZ[l1 + Ed];
+    const double pk1n = PK[l1 + Nd], pp1n = PP[l1 + Nd], gz1n = GZ[l1 + Nd];
+    const double u0 = u[lk], v0 = v[lk], w0 = wk1[lk], we = wk1[lk + Ed], wn = wk1[lk + Nd];
     if (du) {
-      pk1e = PK[l1 + E];
-      pp1e = PP[l1 + E];
-      gz1e = GZ[l1 + E];
       const double wk0 = pk1 - pk0, wke = pk1e - pk0e;
       const double du1 = dt / (wk0 + wke) * ((gz1 - gz0e) * (pk1e - pk0) + (gz0 - gz1e) * (pk1 - pk0e));
-      u[lk] = (u[lk] + du1 + dt / (wk1[lk] + wk1[lk + E]) * ((gz1 - gz0e) * (pp1e - pp0) + (gz0 - gz1e) * (pp1 - pp0e))) *
-              rdx;
+      u[lk] = (u0 + du1 + dt / (w0 + we) * ((gz1 - gz0e) * (pp1e - pp0) + (gz0 - gz1e) * (pp1 - pp0e))) * rdx;
     }
     if (dv) {
-      pk1n = PK[l1 + Nn];
-      pp1n = PP[l1 + Nn];
-      gz1n = GZ[l1 + Nn];
       const double wk0 = pk1 - pk0, wke = pk1n - pk0n;
       const double dv1 = dt / (wk0 + wke) * ((gz1 - gz0n) * (pk1n - pk0) + (gz0 - gz1n) * (pk1 - pk0n));
-      v[lk] = (v[lk] + dv1 + dt / (wk1[lk] + wk1[lk + Nn]) * ((gz1 - gz0n) * (pp1n - pp0) + (gz0 - gz1n) * (pp1 - pp0n))) *
-              rdy;
+      v[lk] = (v0 + dv1 + dt / (w0 + wn) * ((gz1 - gz0n) * (pp1n - pp0) + (gz0 - gz1n) * (pp1 - pp0n))) * rdy;
     }
     pk0 = pk1; pp0 = pp1; gz0 = gz1;
     pk0e = pk1e; pp0e = pp1e; gz0e = gz1e;
@@ -1078,13 +1016,8 @@ void update_dz_c(const Ctx& c, int npz, const double* dp0, const double* ut, con
   Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
   if (const int klb = kloop_levels()) {
     const int nkb = (npz + 1 + klb - 1) / klb;
-    const char* lf = std::getenv("GTFV3_LOADS_FIRST");
-    if (!(lf && lf[0] == '0'))
-      GT_LAUNCH_N("udzc_kl", udzc_kl<true>, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz,
+    GT_LAUNCH_N("udzc_kl", udzc_kl, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz,
                   nkb, klb, dp0, ut, vt, gz, gz_out);
-    else
-      GT_LAUNCH_N("udzc_kl", udzc_kl<false>, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
-                  npz, nkb, klb, dp0, ut, vt, gz, gz_out);
   } else {
     GT_LAUNCH(udzc_k, g2lv(L, d.nsub * (npz + 1)), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dp0, ut, vt,
                        gz, gz_out);
@@ -1100,12 +1033,7 @@ void p_grad_c(const Ctx& c, int npz, double dt2, const double* delpc, const doub
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
   if (const int klb = kloop_levels()) {
     const int nkb = (npz + klb - 1) / klb;
-    const char* lf = std::getenv("GTFV3_LOADS_FIRST");
-    if (!(lf && lf[0] == '0'))
-      GT_LAUNCH_N("pgradc_kl", pgradc_kl<true>, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
-                  npz, nkb, klb, dt2, delpc, pkc, gz, uc, vc);
-    else
-      GT_LAUNCH_N("pgradc_kl", pgradc_kl<false>, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
+    GT_LAUNCH_N("pgradc_kl", pgradc_kl, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
                   npz, nkb, klb, dt2, delpc, pkc, gz, uc, vc);
   } else {
     GT_LAUNCH(pgradc_k, g2lv(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, dt2, delpc, pkc,
@@ -1228,12 +1156,7 @@ void nh_p_grad(const Ctx& c, const NhPgArgs& a) {
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
   if (const int klb = kloop_levels()) {
     const int nkb = (a.npz + klb - 1) / klb;
-    const char* lf = std::getenv("GTFV3_LOADS_FIRST");
-    if (!(lf && lf[0] == '0'))
-      GT_LAUNCH_N("nhpgrad_kl", nhpgrad_kl<true>, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs,
-                  c.met, a.npz, nkb, klb, a.dt, ptk, a.ppb, a.gzb, a.pkb, a.wk1, a.u, a.v);
-    else
-      GT_LAUNCH_N("nhpgrad_kl", nhpgrad_kl<false>, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs,
+    GT_LAUNCH_N("nhpgrad_kl", nhpgrad_kl, kloop_grid(L, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs,
                   c.met, a.npz, nkb, klb, a.dt, ptk, a.ppb, a.gzb, a.pkb, a.wk1, a.u, a.v);
   } else {
     GT_LAUNCH(nhpgrad_k, g2lv(L, d.nsub * a.npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, ptk,

@@ -39,45 +39,6 @@ __device__ __forceinline__ double ei4(double u0, double u1, double u2, double u3
 
 // ---------------- c_sw ----------------
 
-// d2a2c_vect part 1: utmp, vtmp (4th order interior / 2nd order near tile edges) and generic ua, va
-__global__ void __launch_bounds__(256) cs_tmp(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
-                                              int npz, const double* __restrict__ u, const double* __restrict__ v,
-                                              double* __restrict__ utmp, double* __restrict__ vtmp,
-                                              double* __restrict__ ua, double* __restrict__ va) {
-  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  KSETUP(npz)
-  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
-  double ut = BIG, vt = BIG;
-  if (i <= nx + NG - 1 && j <= ny + NG - 1) {
-    const bool rows = J >= max(3, jo - 1) && J <= min(N - 4, jo + ny);
-    const bool cols = I >= max(3, io - 1) && I <= min(N - 4, io + nx);
-    if (rows) ut = A2 * (AT(u, 0, -1) + AT(u, 0, 2)) + A1 * (AT(u, 0, 0) + AT(u, 0, 1));
-    if (cols) vt = A2 * (AT(v, -1, 0) + AT(v, 2, 0)) + A1 * (AT(v, 0, 0) + AT(v, 1, 0));
-    // tile-edge zones (npt = 4: three cells, the halo width) wherever the halo reaches them
-    const int jsd = jo - NG, jed = jo + ny + NG - 1, isd = io - NG, ied = io + nx + NG - 1;
-    const bool mid = J >= max(3, jsd) && J <= min(N - 4, jed);
-    bool two = false;
-    if (J >= jsd && J <= 2) two = true;
-    if (J >= N - 3 && J <= jed) two = true;
-    if (mid && I >= isd && I <= 2) two = true;
-    if (mid && I >= N - 3 && I <= ied) two = true;
-    if (two) {
-      ut = 0.5 * (AT(u, 0, 0) + AT(u, 0, 1));
-      vt = 0.5 * (AT(v, 0, 0) + AT(v, 1, 0));
-    }
-  }
-  AT(utmp, 0, 0) = ut;
-  AT(vtmp, 0, 0) = vt;
-  double a = 0.0, b = 0.0;
-  if (i >= -2 && i <= nx + 1 && j >= -2 && j <= ny + 1) {
-    const double cs = MA(MT(M_COSA_S), 0, 0), r2 = MA(MT(M_RSIN2), 0, 0);
-    a = (ut - vt * cs) * r2;
-    b = (vt - ut * cs) * r2;
-  }
-  AT(ua, 0, 0) = a;
-  AT(va, 0, 0) = b;
-}
-
 // d2a2c_vect cube-corner fixes of utmp/vtmp/ua/va (reads generic values at non-corner points only)
 __global__ void cs_corner_fix(Dims d, const SubInfo* __restrict__ subs, int npz, double* __restrict__ utmp,
                               double* __restrict__ vtmp, double* __restrict__ ua, double* __restrict__ va) {
@@ -184,78 +145,19 @@ __global__ void __launch_bounds__(256) cs_cgrid(Dims d, const SubInfo* __restric
   AT(vt, 0, 0) = vtv;
 }
 
-// c_sw: upwind transport of delp/pt/w -> delpc/ptc/wc and the cell kinetic energy ke
-__global__ void __launch_bounds__(256) cs_transport_ke(
-    Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M, int npz, double dt2,
-    const double* __restrict__ delp, const double* __restrict__ pt, const double* __restrict__ w,
-    const double* __restrict__ u, const double* __restrict__ v, const double* __restrict__ uc,
-    const double* __restrict__ vc, const double* __restrict__ ua, const double* __restrict__ va,
-    const double* __restrict__ ut, const double* __restrict__ vt, double* __restrict__ delpc,
-    double* __restrict__ ptc, double* __restrict__ wc, double* __restrict__ ke) {
-  Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
-  KSETUP(npz)
-  const double* dp = delp + zo;
-  const double* pp = pt + zo;
-  const double* ww = w + zo;
-  // x fluxes at faces i and i+1 (x-corner-filled scalars), y fluxes at j and j+1 (y-filled)
-  double fx1[2], fx[2], fx2[2], fy1[2], fy[2], fy2[2];
-#pragma unroll
-  for (int f = 0; f < 2; ++f) {
-    const long oi = o + f;  // face (i+f, j)
-    double c = ut[zo + oi];
-    long src = c > 0.0 ? cc_off(d, sub, i + f - 1, j, 1) : cc_off(d, sub, i + f, j, 1);
-    fx1[f] = c * dp[src];
-    fx[f] = fx1[f] * pp[src];
-    fx2[f] = fx1[f] * ww[src];
-    const long oj = o + (long)f * d.pitch;
-    double cy = vt[zo + oj];
-    long sy = cy > 0.0 ? cc_off(d, sub, i, j + f - 1, 2) : cc_off(d, sub, i, j + f, 2);
-    fy1[f] = cy * dp[sy];
-    fy[f] = fy1[f] * pp[sy];
-    fy2[f] = fy1[f] * ww[sy];
-  }
-  const long oc = cc_off(d, sub, i, j, 2);
-  const double ra = MA(MT(M_RAREA), 0, 0);
-  const double dpc = dp[oc] + (fx1[0] - fx1[1] + fy1[0] - fy1[1]) * ra;
-  AT(delpc, 0, 0) = dpc;
-  AT(ptc, 0, 0) = (pp[oc] * dp[oc] + (fx[0] - fx[1] + fy[0] - fy[1]) * ra) / dpc;
-  AT(wc, 0, 0) = (ww[oc] * dp[oc] + (fx2[0] - fx2[1] + fy2[0] - fy2[1]) * ra) / dpc;
-  // kinetic energy
-  double kk, vv;
-  if (AT(ua, 0, 0) > 0.0) {
-    if (I == 0 || I == N) kk = AT(uc, 0, 0) * MA(MT(M_SIN1), 0, 0) + AT(v, 0, 0) * MA(MT(M_COS1), 0, 0);
-    else kk = AT(uc, 0, 0);
-  } else {
-    if (I == -1 || I == N - 1) kk = AT(uc, 1, 0) * MA(MT(M_SIN3), 0, 0) + AT(v, 1, 0) * MA(MT(M_COS3), 0, 0);
-    else kk = AT(uc, 1, 0);
-  }
-  if (AT(va, 0, 0) > 0.0) {
-    if (J == 0 || J == N) vv = AT(vc, 0, 0) * MA(MT(M_SIN2), 0, 0) + AT(u, 0, 0) * MA(MT(M_COS2), 0, 0);
-    else vv = AT(vc, 0, 0);
-  } else {
-    if (J == -1 || J == N - 1) vv = AT(vc, 0, 1) * MA(MT(M_SIN4), 0, 0) + AT(u, 0, 1) * MA(MT(M_COS4), 0, 0);
-    else vv = AT(vc, 0, 1);
-  }
-  const double dt4 = 0.5 * dt2;
-  AT(ke, 0, 0) = dt4 * (AT(ua, 0, 0) * kk + AT(va, 0, 0) * vv);
-}
+// ---- loads-first forms: every input a point needs is loaded before any arithmetic --
+// addresses of the points outside the kernel's ranges clamped to an interior point, tile-edge
+// inputs loaded only by the waves holding tile-edge lines, both upwind candidates of a
+// data-dependent pick loaded and selected afterwards -- so a wave keeps its loads in flight
+// together instead of waiting out a chain of dependent round trips through the branches
+// (the branch-ordered forms, bit-identical and deleted in round 4, had 11-15
+// vmcnt(0) waits per wave; rocprof SQ counters 63-65 % of wave cycles waiting).  The same form
+// of cs_cgrid and ds_courant measured slower (1.84 -> 1.87 and 1.33 -> 1.47 ms per step):
+// loading both upwind choices of their metric terms costs more than the round trips it saves.
 
-// ---- loads-first forms (GTFV3_LOADS_FIRST, default on): the same expressions in the same
-// order as the kernel each replaces (bit-identical), with every input a point needs loaded
-// before any arithmetic -- addresses of the points outside the kernel's ranges clamped to an
-// interior point, tile-edge inputs loaded only by the waves holding tile-edge lines -- so a
-// wave keeps its loads in flight together instead of waiting out a chain of dependent round
-// trips through the branches (11-15 vmcnt(0) waits per wave in the branch-ordered
-// forms, rocprof SQ counters 63-65 % of wave cycles waiting).  The same form of cs_cgrid and
-// ds_courant measured slower (1.84 -> 1.87 and 1.33 -> 1.47 ms per step): loading both
-// upwind choices of their metric terms costs more than the round trips it saves.
-bool loads_first_env() {
-  const char* e = std::getenv("GTFV3_LOADS_FIRST");
-  return !(e && e[0] == '0');
-}
-
-// cs_transport_ke (above), loads first: the Courant numbers, the cell's own values and the
-// kinetic-energy inputs in one group, then the four upwind sources the signs select
+// c_sw: upwind transport of delp/pt/w -> delpc/ptc/wc and the cell kinetic energy ke.  The
+// Courant numbers, the cell's own values and the kinetic-energy inputs in one group, then
+// the four upwind sources the signs select
 __global__ void __launch_bounds__(256) cs_transport_ke_ld(
     Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M, int npz, double dt2,
     const double* __restrict__ delp, const double* __restrict__ pt, const double* __restrict__ w,
@@ -319,9 +221,10 @@ __global__ void __launch_bounds__(256) cs_transport_ke_ld(
   AT(ke, 0, 0) = dt4 * (uav * kk + vav * vv);
 }
 
-// cs_tmp (above), loads first: the four u rows and four v columns of the 4th-order forms
-// (the outer two at offset 0 where the point takes no 4th-order value) and the two metric
-// terms in one group; the 4th-order / tile-edge / BIG choice made afterwards
+// d2a2c_vect part 1: utmp, vtmp (4th order interior / 2nd order near tile edges) and generic
+// ua, va.  The four u rows and four v columns of the 4th-order forms (the outer two at offset
+// 0 where the point takes no 4th-order value) and the two metric terms in one group; the
+// 4th-order / tile-edge / BIG choice made afterwards
 __global__ void __launch_bounds__(256) cs_tmp_ld(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
                                                  int npz, const double* __restrict__ u, const double* __restrict__ v,
                                                  double* __restrict__ utmp, double* __restrict__ vtmp,
@@ -385,30 +288,8 @@ __global__ void __launch_bounds__(256) cs_vort(Dims d, const SubInfo* __restrict
   AT(vort, 0, 0) = MA(MT(M_FC), 0, 0) + MA(MT(M_RAREA_C), 0, 0) * vt;
 }
 
-// c_sw: time-centred C-grid winds (vorticity flux + KE gradient)
-__global__ void __launch_bounds__(256) cs_update(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
-                                                 int npz, double dt2, const double* __restrict__ u,
-                                                 const double* __restrict__ v, const double* __restrict__ vort,
-                                                 const double* __restrict__ ke, double* __restrict__ uc,
-                                                 double* __restrict__ vc) {
-  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  KSETUP(npz)
-  if (j < d.ny) {
-    double fy1 = (I == 0 || I == N) ? dt2 * AT(v, 0, 0)
-                                    : dt2 * (AT(v, 0, 0) - AT(uc, 0, 0) * MA(MT(M_COSA_U), 0, 0)) / MA(MT(M_SINA_U), 0, 0);
-    double fy = fy1 > 0.0 ? AT(vort, 0, 0) : AT(vort, 0, 1);
-    AT(uc, 0, 0) = AT(uc, 0, 0) + fy1 * fy + MA(MT(M_RDXC), 0, 0) * (AT(ke, -1, 0) - AT(ke, 0, 0));
-  }
-  if (i < d.nx) {
-    double fx1 = (J == 0 || J == N) ? dt2 * AT(u, 0, 0)
-                                    : dt2 * (AT(u, 0, 0) - AT(vc, 0, 0) * MA(MT(M_COSA_V), 0, 0)) / MA(MT(M_SINA_V), 0, 0);
-    double fx = fx1 > 0.0 ? AT(vort, 0, 0) : AT(vort, 1, 0);
-    AT(vc, 0, 0) = AT(vc, 0, 0) - fx1 * fx + MA(MT(M_RDYC), 0, 0) * (AT(ke, 0, -1) - AT(ke, 0, 0));
-  }
-}
-
-// cs_update (above), loads first: both upwind vorticity values are loaded (the neighbour's
-// are the same cache lines) and selected afterwards
+// c_sw: time-centred C-grid winds (vorticity flux + KE gradient).  Both upwind vorticity
+// values are loaded (the neighbour's are the same cache lines) and selected afterwards
 __global__ void __launch_bounds__(256) cs_update_ld(Dims d, const SubInfo* __restrict__ subs,
                                                     const double* __restrict__ M, int npz, double dt2,
                                                     const double* __restrict__ u, const double* __restrict__ v,
@@ -596,7 +477,6 @@ __global__ void __launch_bounds__(256) ds_courant(Dims d, const SubInfo* __restr
 // the point are loaded once for its block of levels (which of them a point needs is fixed by
 // its position), then the same expressions per level as above.  (The same form of
 // ds_courant and ds_ke measured slower: 1.56 -> 1.68 and 2.65 -> 3.37 ms per step)
-template <bool LF>
 __global__ void __launch_bounds__(256) ds_utvt1_kl(Dims d, const SubInfo* __restrict__ subs,
                                                    const double* __restrict__ M, int npz, int nkb, int klb,
                                                    double dt, const double* __restrict__ uc,
@@ -624,42 +504,20 @@ __global__ void __launch_bounds__(256) ds_utvt1_kl(Dims d, const SubInfo* __rest
       my = 2; ay = met(M, d, M_COSA_V, s)[o]; by = met(M, d, M_RSIN_V, s)[o];
     }
   }
-  if (LF) {
-    // loads first (GTFV3_LOADS_FIRST): the point's uc / vc and the four neighbours of each
-    // generic form in one group per level (offset 0 where the form is not taken), then the
-    // same expressions as below
-    const long xw = mx == 2 ? -1 : 0, xn = mx == 2 ? pt : 0;
-    const long ys = my == 2 ? -pt : 0, ye = my == 2 ? 1 : 0;
-    for (int k = k0; k < k1; ++k) {
-      const long lk = ((long)s * npz + k) * P + o;
-      const double u0 = uc[lk], v0 = vc[lk];
-      const double vw = vc[lk + xw], vwn = vc[lk + xw + xn], vn = vc[lk + xn];
-      const double us = uc[lk + ys], use = uc[lk + ye + ys], ue = uc[lk + ye];
-      double a = 0.0, b = 0.0;
-      if (mx == 1) a = u0 * dt > 0.0 ? u0 / ax : u0 / bx;
-      else if (mx == 2) a = (u0 - 0.25 * ax * (vw + v0 + vwn + vn)) * bx;
-      if (my == 1) b = v0 * dt > 0.0 ? v0 / ay : v0 / by;
-      else if (my == 2) b = (v0 - 0.25 * ay * (us + use + u0 + ue)) * by;
-      ut[lk] = a;
-      vt[lk] = b;
-    }
-    return;
-  }
+  // loads first: the point's uc / vc and the four neighbours of each generic form in one
+  // group per level (offset 0 where the form is not taken)
+  const long xw = mx == 2 ? -1 : 0, xn = mx == 2 ? pt : 0;
+  const long ys = my == 2 ? -pt : 0, ye = my == 2 ? 1 : 0;
   for (int k = k0; k < k1; ++k) {
     const long lk = ((long)s * npz + k) * P + o;
+    const double u0 = uc[lk], v0 = vc[lk];
+    const double vw = vc[lk + xw], vwn = vc[lk + xw + xn], vn = vc[lk + xn];
+    const double us = uc[lk + ys], use = uc[lk + ye + ys], ue = uc[lk + ye];
     double a = 0.0, b = 0.0;
-    if (mx == 1) {
-      const double c = uc[lk];
-      a = c * dt > 0.0 ? c / ax : c / bx;
-    } else if (mx == 2) {
-      a = (uc[lk] - 0.25 * ax * (vc[lk - 1] + vc[lk] + vc[lk - 1 + pt] + vc[lk + pt])) * bx;
-    }
-    if (my == 1) {
-      const double c = vc[lk];
-      b = c * dt > 0.0 ? c / ay : c / by;
-    } else if (my == 2) {
-      b = (vc[lk] - 0.25 * ay * (uc[lk - pt] + uc[lk + 1 - pt] + uc[lk] + uc[lk + 1])) * by;
-    }
+    if (mx == 1) a = u0 * dt > 0.0 ? u0 / ax : u0 / bx;
+    else if (mx == 2) a = (u0 - 0.25 * ax * (vw + v0 + vwn + vn)) * bx;
+    if (my == 1) b = v0 * dt > 0.0 ? v0 / ay : v0 / by;
+    else if (my == 2) b = (v0 - 0.25 * ay * (us + use + u0 + ue)) * by;
     ut[lk] = a;
     vt[lk] = b;
   }
@@ -699,108 +557,9 @@ __global__ void __launch_bounds__(256) ds_thermo(Dims d, const SubInfo* __restri
   AT(w, 0, 0) = wn / dpn;
 }
 
-// kinetic energy at cell corners: B-grid contravariant winds, upwind PPM of v (ytp_v)
-// and u (xtp_u), cube-corner values, plus nord=0 divergence damping added to ke
-__global__ void __launch_bounds__(256) ds_ke(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
-                                             int npz, double dt, int hord_mt, double dddmp, double d2_bg,
-                                             double da_min_c, const double* __restrict__ u,
-                                             const double* __restrict__ v, const double* __restrict__ uc,
-                                             const double* __restrict__ vc, const double* __restrict__ ua,
-                                             const double* __restrict__ va, const double* __restrict__ ut,
-                                             const double* __restrict__ vt, double* __restrict__ ke, int nord,
-                                             double* __restrict__ vd) {
-  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  KSETUP(npz)
-  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
-  const double dt5 = 0.5 * dt, dt4 = 0.25 * dt;
-  const int Ilo = max(1, io), Ihi = min(N - 1, io + nx), Jlo = max(1, jo), Jhi = min(N - 1, jo + ny);
-  const bool inner = I >= Ilo && I <= Ihi && J >= Jlo && J <= Jhi;
-  const double cosa = MA(MT(M_COSA), 0, 0), rsina = MA(MT(M_RSINA), 0, 0);
-  double vb = 0.0, ub = 0.0;
-  if (inner) vb = dt5 * (AT(vc, -1, 0) + AT(vc, 0, 0) - (AT(uc, 0, -1) + AT(uc, 0, 0)) * cosa) * rsina;
-  if (I == 0 || I == N) vb = dt4 * (-AT(vt, -2, 0) + 3.0 * (AT(vt, -1, 0) + AT(vt, 0, 0)) - AT(vt, 1, 0));
-  else if ((J == 0 || J == N) && I >= Ilo && I <= Ihi) vb = dt5 * (AT(vt, -1, 0) + AT(vt, 0, 0));
-  if (inner) ub = dt5 * (AT(uc, 0, -1) + AT(uc, 0, 0) - (AT(vc, -1, 0) + AT(vc, 0, 0)) * cosa) * rsina;
-  if (J == 0 || J == N) ub = dt4 * (-AT(ut, 0, -2) + 3.0 * (AT(ut, 0, -1) + AT(ut, 0, 0)) - AT(ut, 0, 1));
-  else if ((I == 0 || I == N) && J >= Jlo && J <= Jhi) ub = dt5 * (AT(ut, 0, -1) + AT(ut, 0, 0));
-  // ytp_v: flux of v through corner (i,j) along j.  Away from the tile edges (interfaces
-  // g-1..g+1 off the edge forms) the interior PPM applies and the metric stencil is not
-  // read: the edge form (six metric loads, divided-difference al) runs only near edges.
-  double qv[6], sp[6];
-  const double* dy = MT(M_DY);
-  const double* dxm = MT(M_DX);
-  auto flux = [&](int g, double c) {
-    const bool edge = !(g - 1 >= 2 && g + 1 <= N - 2);
-    if (edge) return ppm_flux_ord(hord_mt, g, N, qv, sp, c);
-    return hord_mt == 5 ? ppm_flux<5, false>(g, N, qv, sp, c) : ppm_flux<6, false>(g, N, qv, sp, c);
-  };
-#pragma unroll
-  for (int m = 0; m < 6; ++m) {
-    qv[m] = AT(v, 0, m - 3);
-    sp[m] = (J - 1 >= 2 && J + 1 <= N - 2) ? 0.0 : MA(dy, 0, m - 3);
-  }
-  double cfl = vb > 0.0 ? vb * MA(MT(M_RDY), 0, -1) : vb * MA(MT(M_RDY), 0, 0);
-  double ubf = flux(J, cfl);
-  double kk = vb * ubf;
-#pragma unroll
-  for (int m = 0; m < 6; ++m) {
-    qv[m] = AT(u, m - 3, 0);
-    sp[m] = (I - 1 >= 2 && I + 1 <= N - 2) ? 0.0 : MA(dxm, m - 3, 0);
-  }
-  cfl = ub > 0.0 ? ub * MA(MT(M_RDX), -1, 0) : ub * MA(MT(M_RDX), 0, 0);
-  double vbf = flux(I, cfl);
-  kk = 0.5 * (kk + ub * vbf);
-  const double dt6 = dt / 6.0;
-  if (I == 0 && J == 0)
-    kk = dt6 * ((AT(ut, 0, 0) + AT(ut, 0, -1)) * AT(u, 0, 0) + (AT(vt, 0, 0) + AT(vt, -1, 0)) * AT(v, 0, 0) +
-                (AT(ut, 0, 0) + AT(vt, 0, 0)) * AT(u, -1, 0));
-  else if (I == N && J == 0)
-    kk = dt6 * ((AT(ut, 0, 0) + AT(ut, 0, -1)) * AT(u, -1, 0) + (AT(vt, 0, 0) + AT(vt, -1, 0)) * AT(v, 0, 0) +
-                (AT(ut, 0, 0) - AT(vt, -1, 0)) * AT(u, 0, 0));
-  else if (I == N && J == N)
-    kk = dt6 * ((AT(ut, 0, 0) + AT(ut, 0, -1)) * AT(u, -1, 0) + (AT(vt, 0, 0) + AT(vt, -1, 0)) * AT(v, 0, -1) +
-                (AT(ut, 0, -1) + AT(vt, -1, 0)) * AT(u, 0, 0));
-  else if (I == 0 && J == N)
-    kk = dt6 * ((AT(ut, 0, 0) + AT(ut, 0, -1)) * AT(u, 0, 0) + (AT(vt, 0, 0) + AT(vt, -1, 0)) * AT(v, 0, -1) +
-                (AT(ut, 0, -1) - AT(vt, 0, 0)) * AT(u, -1, 0));
-  if (nord > 0) {  // the higher-order damping term is added by divergence_damping (damp.hip)
-    AT(ke, 0, 0) = kk;
-    return;
-  }
-  // divergence damping (nord = 0): delpc at the corner from the edge divergence terms
-  auto ptc_at = [&](int di) {  // x-edge (i+di, j): u * dyc with the non-orthogonal correction
-    const int Jj = J;
-    const long oo = o + di;
-    const double dyc = MT(M_DYC)[oo];
-    const double uu = u[zo + oo];
-    if (Jj == 0 || Jj == N)
-      return vc[zo + oo] > 0.0 ? uu * dyc * MT(M_SIN4)[oo - d.pitch] : uu * dyc * MT(M_SIN2)[oo];
-    return (uu - 0.5 * (va[zo + oo - d.pitch] + va[zo + oo]) * MT(M_COSA_V)[oo]) * dyc * MT(M_SINA_V)[oo];
-  };
-  auto vrt_at = [&](int dj) {  // y-edge (i, j+dj)
-    const int Jj = J + dj;
-    (void)Jj;
-    const long oo = o + (long)dj * d.pitch;
-    const double dxc = MT(M_DXC)[oo];
-    const double vv = v[zo + oo];
-    if (I == 0 || I == N)
-      return uc[zo + oo] > 0.0 ? vv * dxc * MT(M_SIN3)[oo - 1] : vv * dxc * MT(M_SIN1)[oo];
-    if (I >= Ilo && I <= Ihi)
-      return (vv - 0.5 * (ua[zo + oo - 1] + ua[zo + oo]) * MT(M_COSA_U)[oo]) * dxc * MT(M_SINA_U)[oo];
-    return 0.0;
-  };
-  double vS = vrt_at(-1), v0 = vrt_at(0);
-  double dpc = vS - v0 + ptc_at(-1) - ptc_at(0);
-  if ((I == 0 && J == 0) || (I == N && J == 0)) dpc = dpc - vS;
-  if ((I == N && J == N) || (I == 0 && J == N)) dpc = dpc + v0;
-  dpc = MA(MT(M_RAREA_C), 0, 0) * dpc;
-  double damp = da_min_c * fmax(d2_bg, fmin(0.20, dddmp * fabs(dpc * dt)));
-  AT(ke, 0, 0) = kk + damp * dpc;
-  if (vd) AT(vd, 0, 0) = damp * dpc;  // the damping term on its own (d_con heat)
-}
-
-// ds_ke with its loads issued up front (ds_ke_ld): the same expressions in the same order
-// (bit-identical), but every value an interior corner needs -- the B-grid wind inputs, both
+// kinetic energy at cell corners: B-grid contravariant winds, upwind PPM of v (ytp_v) and u
+// (xtp_u), cube-corner values, plus nord = 0 divergence damping added to ke.  Every value an
+// interior corner needs -- the B-grid wind inputs, both
 // six-point PPM stencils, the Courant metric and the divergence-damping terms -- is loaded
 // unconditionally before any arithmetic, so a wave has ~45 loads in flight at once instead of
 // ~15 dependent round trips through branches (rocprof SQ counters: ds_ke waited 63 % of its
@@ -950,16 +709,6 @@ __global__ void __launch_bounds__(256) ds_vort(Dims d, const SubInfo* __restrict
   AT(vort, 0, 0) = wk + MA(MT(M_F0), 0, 0);
 }
 
-// final D-grid momentum (left multiplied by dx / dy; the pressure gradient divides)
-__global__ void __launch_bounds__(256) ds_uv(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
-                                             int npz, const double* __restrict__ ke, const double* __restrict__ fxv,
-                                             const double* __restrict__ fyv, double* __restrict__ u,
-                                             double* __restrict__ v) {
-  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  KSETUP(npz)
-  if (i < d.nx) AT(u, 0, 0) = AT(u, 0, 0) * MA(MT(M_DX), 0, 0) + AT(ke, 0, 0) - AT(ke, 1, 0) + AT(fyv, 0, 0);
-  if (j < d.ny) AT(v, 0, 0) = AT(v, 0, 0) * MA(MT(M_DY), 0, 0) + AT(ke, 0, 0) - AT(ke, 0, 1) - AT(fxv, 0, 0);
-}
 
 inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
   (void)d;
@@ -967,8 +716,6 @@ inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
 }
 
 }  // namespace
-
-bool loads_first() { return loads_first_env(); }
 
 void c_sw(const Ctx& c, const CswArgs& a) {
   c_sw_transport(c, a);
@@ -981,12 +728,8 @@ void c_sw_transport(const Ctx& c, const CswArgs& a) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  if (loads_first_env())
-    GT_LAUNCH_N("cs_tmp", cs_tmp_ld, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v,
-                a.utmp, a.vtmp, a.ua, a.va);
-  else
-    GT_LAUNCH(cs_tmp, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.utmp,
-                       a.vtmp, a.ua, a.va);
+  GT_LAUNCH_N("cs_tmp", cs_tmp_ld, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v,
+              a.utmp, a.vtmp, a.ua, a.va);
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   const double L = a.npz;
@@ -998,12 +741,8 @@ void c_sw_transport(const Ctx& c, const CswArgs& a) {
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (3 * e.X + 3 * e.Y + 4 * e.C) + 12 * e.C);
   Launch2D Lt{-1, -1, d.nx + 2, d.ny + 2};
-  if (loads_first_env())
-    GT_LAUNCH_N("cs_transport_ke", cs_transport_ke_ld, g2(d, Lt, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
-                a.npz, a.dt2, a.delp, a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke);
-  else
-    GT_LAUNCH(cs_transport_ke, g2(d, Lt, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.delp,
-                       a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke);
+  GT_LAUNCH_N("cs_transport_ke", cs_transport_ke_ld, g2(d, Lt, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
+              a.npz, a.dt2, a.delp, a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke);
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (9 * e.C + 3 * e.X + 3 * e.Y) + 9 * e.C);
 }
@@ -1019,12 +758,8 @@ void c_sw_winds(const Ctx& c, const CswArgs& a) {
   GT_LAUNCH(cs_vort, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.vort);
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (e.X + e.Y + e.K) + 4 * e.C);
-  if (loads_first_env())
-    GT_LAUNCH_N("cs_update", cs_update_ld, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2,
-                a.u, a.v, a.vort, a.ke, a.uc, a.vc);
-  else
-    GT_LAUNCH(cs_update, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
-                       a.vort, a.ke, a.uc, a.vc);
+  GT_LAUNCH_N("cs_update", cs_update_ld, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2,
+              a.u, a.v, a.vort, a.ke, a.uc, a.vc);
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (e.C + e.K + 3 * e.X + 3 * e.Y) + 6 * e.C);
 }
@@ -1050,12 +785,8 @@ void d_sw_courant(const Ctx& c, const DswArgs& a) {
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   const int klb = kloop_levels(), nkb = klb ? (a.npz + klb - 1) / klb : 0;
   if (klb) {
-    if (loads_first_env())
-      GT_LAUNCH_N("ds_utvt1_kl", ds_utvt1_kl<true>, kloop_grid(full, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs,
-                  c.met, a.npz, nkb, klb, a.dt, a.uc, a.vc, a.ut, a.vt);
-    else
-      GT_LAUNCH_N("ds_utvt1_kl", ds_utvt1_kl<false>, kloop_grid(full, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs,
-                  c.met, a.npz, nkb, klb, a.dt, a.uc, a.vc, a.ut, a.vt);
+    GT_LAUNCH_N("ds_utvt1_kl", ds_utvt1_kl, kloop_grid(full, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs,
+                c.met, a.npz, nkb, klb, a.dt, a.uc, a.vc, a.ut, a.vt);
   } else
     GT_LAUNCH(ds_utvt1, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.uc, a.vc,
                        a.ut, a.vt);
@@ -1132,12 +863,7 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
   // kinetic energy (+ divergence damping) at corners
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
   const bool dcon = a.d_con > 1e-5, vdamp = a.vtdm4 > 1e-5;
-  // GTFV3_LOADS_FIRST=0: the branch-ordered form (same results, bit for bit)
-  if (!loads_first_env()) {
-    GT_LAUNCH(ds_ke, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.hord_mt, a.dddmp,
-                       a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke, a.nord,
-                       dcon ? a.vd : nullptr);
-  } else {
+  {
     const bool damp = a.nord == 0;
     double* vdp = dcon ? a.vd : nullptr;
 #define KE_LD(O, D)                                                                                          \
@@ -1175,20 +901,11 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
   t.mfx = nullptr; t.mfy = nullptr;
   t.q = a.vort; t.fx = a.gvx; t.fy = a.gvy; t.ord = a.hord_vt;
   // u, v updated inside the vorticity march (tp.hip TM = 3: ds_uv's expressions on the
-  // fluxes in registers, no gvx / gvy planes); GTFV3_UV_FUSED=0: fluxes, then ds_uv
-  const char* ev = std::getenv("GTFV3_UV_FUSED");
-  if (!(ev && ev[0] == '0')) {
-    t.ke_uv = a.ke;
-    t.u_uv = a.u;
-    t.v_uv = a.v;
-    fv_tp_2d(c, t);
-    return;
-  }
+  // fluxes in registers, no flux planes)
+  t.ke_uv = a.ke;
+  t.u_uv = a.u;
+  t.v_uv = a.v;
   fv_tp_2d(c, t);
-  GT_LAUNCH(ds_uv, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.ke, a.gvx, a.gvy, a.u,
-                     a.v);
-  HIP_LAUNCH_CHECK();
-  gt_bytes(L * (e.K + 3 * e.X + 3 * e.Y) + 2 * e.C);
 }
 
 void d_sw_post(const Ctx& c, const DswArgs& a) {

@@ -234,33 +234,3 @@ def test_acoustic_graph_bitwise(pkg, require_gpu, monkeypatch, proxy):
         d.close()
     for k in out["0"]:
         assert np.array_equal(out["0"][k], out["1"][k], equal_nan=bool(proxy)), f"{k}: graph replay differs"
-
-
-@pytest.mark.parametrize("env", ["GTFV3_UV_FUSED", "GTFV3_LOADS_FIRST"])
-@pytest.mark.parametrize("npx,lay", [(25, 2), (49, 1)])
-def test_uv_fused_bitwise(pkg, require_gpu, monkeypatch, npx, lay, env):
-    """Two forms of d_sw's wind stage, bit for bit over two L20 steps on every state field,
-    at C24 with 2x2 sub-domains per tile (short strips, many tile-edge points) and at C48 with
-    whole tiles: GTFV3_UV_FUSED -- the final wind update (ds_uv) inside the vorticity march
-    (tp.hip TM = 3, u and v from the fluxes in registers) against the march writing flux
-    planes and ds_uv reading them; GTFV3_LOADS_FIRST -- c_sw's cs_tmp / cs_transport_ke / cs_update and
-    d_sw's ds_ke / ds_utvt1_kl and udzc_kl / pgradc_kl / nhpgrad_kl with every load issued before their arithmetic (the *_ld
-    kernels) against the branch-ordered kernels."""
-    state = importlib.import_module(pkg.__name__ + ".state")
-    npz = 20
-    ak, bk, ks = state.hybrid_levels(npz)
-    out = {}
-    for mode in ("0", "1"):
-        monkeypatch.setenv(env, mode)
-        d = pkg.Domain(npx=npx, npz=npz, nq=2, layout_x=lay, layout_y=lay)
-        st = state.jablonowski_williamson(d, ak, bk)
-        d.set_vertical(ak, bk, ks)
-        for k, v in st.items():
-            d.upload(k, v)
-        for _ in range(2):
-            d.step(1)
-        out[mode] = {k: d.download(k) for k in ("u", "v", "w", "pt", "delp", "delz", "q", "ps", "pe")}
-        d.close()
-    for k in out["0"]:
-        assert np.isfinite(out["1"][k]).all(), f"{k}: non-finite"
-        assert np.array_equal(out["0"][k], out["1"][k]), f"{k}: {env}=1 differs from {env}=0"
