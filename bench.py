@@ -163,7 +163,7 @@ def parse():
     p.add_argument("--cpu-npx", type=int, default=0,
                    help="cpu_baseline sample grid npx (default 49: C48 L72, 6 tiles, ~20 s of one host core; "
                         "13 with --moist, ~40 s)")
-    p.add_argument("--cpu-procs", type=int, default=8,
+    p.add_argument("--cpu-procs", type=int, default=16,
                    help="cpu_baseline: concurrent single-threaded oracle replicas (= host cores used)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-kernel-timing", action="store_true")
