@@ -270,8 +270,20 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
   double* const sdw = sdx + (DXL ? (threadIdx.x / MW) * DXL_ROWS * 8 + dslot : 0);
   if constexpr (DXL) {
     const int rt = r_hi + 1 < ny + NG ? r_hi + 1 : ny + NG;
+    // sixteen rows' loads in flight at once, then their LDS writes (one row per round trip
+    // was ~50 dependent L2 / HBM latencies at the start of every tile-edge wave)
     if (dx_lane)
-      for (int rr = rb; rr <= rt; ++rr) sdw[(rr - rb) * 8] = dxa[(long)(rr + NG) * pitch + xo];
+      for (int r0 = rb; r0 <= rt; r0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) {
+          const int rr = r0 + u <= rt ? r0 + u : rt;
+          v[u] = dxa[(long)(rr + NG) * pitch + xo];
+        }
+#pragma unroll
+        for (int u = 0; u < 16; ++u)
+          if (r0 + u <= rt) sdw[(r0 + u - rb) * 8] = v[u];
+      }
     __builtin_amdgcn_wave_barrier();
   }
   // dxa of row r (clamped as the loads clamp) for the tile-edge PPM forms
@@ -686,10 +698,28 @@ __device__ void tracer_carry(const TpM& a, int z, int strip, int j0, int j1) {
   if (!(lane >= NG && lane < NG + MOUT && x < d.nx)) return;
   const long zo = ((long)(s * a.nt + tg * NF) * a.nk + k) * d.plane, fo = ((long)s * a.nk + k) * d.plane;
   const long tstride = (long)a.nk * d.plane;
-  for (int j = j0; j < j1; ++j) {
-    const long o = (long)(j + NG) * d.pitch + x + NG;
-    for (int f = 0; f < NF; ++f) a.qo[0][zo + f * tstride + o] = a.qf[0][zo + f * tstride + o];
-    if (tg == 0) a.dp2o[fo + o] = a.dp1[fo + o];
+  const double* __restrict__ qi = a.qf[0] + zo;
+  double* __restrict__ qo = a.qo[0] + zo;
+  const double* __restrict__ di = a.dp1 + fo;
+  double* __restrict__ dout = a.dp2o + fo;
+  // four rows' loads in flight before their stores (the planes do not overlap)
+  for (int j = j0; j < j1; j += 4) {
+    double v[4][NF], w[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const long o = (long)((j + u < j1 ? j + u : j1 - 1) + NG) * d.pitch + x + NG;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) v[u][f] = qi[f * tstride + o];
+      w[u] = tg == 0 ? di[o] : 0.0;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      if (j + u >= j1) break;
+      const long o = (long)(j + u + NG) * d.pitch + x + NG;
+#pragma unroll
+      for (int f = 0; f < NF; ++f) qo[f * tstride + o] = v[u][f];
+      if (tg == 0) dout[o] = w[u];
+    }
   }
 }
 
