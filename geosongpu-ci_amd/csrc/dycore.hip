@@ -552,9 +552,10 @@ void Dycore::step() {
   za.dp0 = dp_ref;
   za.crx = da.crx; za.cry = da.cry; za.xfx = da.xfx; za.yfx = da.yfx;
   za.crx_e = S("_ud_crx", k1); za.cry_e = S("_ud_cry", k1); za.xfx_e = S("_ud_xfx", k1); za.yfx_e = S("_ud_yfx", k1);
-  za.fx = S("_ud_fx", k1); za.fy = S("_ud_fy", k1);
-  za.gam = S("_ud_gam", k1);
   za.zh = zh;
+  // update_dz_d writes the new heights into a second set of planes (the march reads the
+  // old heights' neighbours), which then become "zh" (pointer swap, as the thermo fields)
+  za.zh_out = S("_zh_alt", k1);
 
   Riem3Args ra{};
   ra.npz = npz;
@@ -591,6 +592,16 @@ void Dycore::step() {
       copy_levels(c, field_elems(npz), cur3[f]->p, alt[f]->p);
     }
   }
+  auto zh_swap = [&]() {
+    Field& fz = field("zh", k1);
+    Field& fa = field("_zh_alt", k1);
+    std::swap(fz.p, fa.p);
+    zh = fz.p;
+    za.zh = zh;
+    za.zh_out = fa.p;
+    ra.zh = zh;
+    pa.gz = zh;
+  };
   auto thermo_swap = [&]() {
     for (int f = 0; f < 3; ++f) std::swap(cur3[f]->p, alt[f]->p);
     ca.delp = da.delp = delp.p;
@@ -646,6 +657,7 @@ void Dycore::step() {
       if (tfused) thermo_swap();
       d_sw_winds(c, da);
       update_dz_d(c, za);
+      zh_swap();
     } else {
     HIP_CHECK(hipEventRecord(ev_fork, st));
     HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
@@ -656,6 +668,7 @@ void Dycore::step() {
       cc.st = st_c;
       d_sw_winds(cb, da);
       update_dz_d(cc, za);
+      zh_swap();
     }
     d_sw_thermo(c, da);
     if (tfused) thermo_swap();

@@ -58,6 +58,10 @@ struct TpArgs {
   // v += ... - fx with the corner kinetic energy ke (ds_uv's expressions); no flux plane
   const double* ke_uv = nullptr;
   double *u_uv = nullptr, *v_uv = nullptr;
+  // update_dz_d's height update fused into the march (nt = 1, no mass fluxes): zh_out =
+  // (zh area + flux divergence) / (area + area-flux divergence), zh_update's expressions; no
+  // flux plane
+  double* zh_out = nullptr;
 };
 void fv_tp_2d(const Ctx& c, const TpArgs& a);
 

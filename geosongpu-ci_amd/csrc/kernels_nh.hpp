@@ -22,8 +22,9 @@ struct UdzdArgs {
   int npz, hord;
   const double* dp0;
   const double *crx, *cry, *xfx, *yfx;
-  double *crx_e, *cry_e, *xfx_e, *yfx_e, *fx, *fy, *gam;
-  double* zh;
+  double *crx_e, *cry_e, *xfx_e, *yfx_e;
+  const double* zh;
+  double* zh_out;  // the updated heights (out of place: the march reads zh's neighbours)
 };
 void update_dz_d(const Ctx& c, const UdzdArgs& a);
 // update_dz_d's edge_profile of (crx, xfx) on x-face and (cry, yfx) on y-face columns.

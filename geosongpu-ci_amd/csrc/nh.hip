@@ -290,23 +290,6 @@ __global__ void __launch_bounds__(256) edge_prof_reg_k(Dims d, int npz, const do
   }
 }
 
-// ra_x, ra_y for the interface-level transport of zh
-// zh update from the transported fluxes (compute cells, all interfaces)
-// (ra_x = area + xfx|i - xfx|i+1 and ra_y = area + yfx|j - yfx|j+1 formed here, as in
-// fv_tp_2d, instead of being stored as planes)
-__global__ void __launch_bounds__(256) zh_update_k(Dims d, const SubInfo* __restrict__ subs,
-                                                   const double* __restrict__ M, int nk, const double* __restrict__ fx,
-                                                   const double* __restrict__ fy, const double* __restrict__ xfx,
-                                                   const double* __restrict__ yfx, double* __restrict__ zh) {
-  Launch2D L{0, 0, d.nx, d.ny};
-  KSETUP2(nk)
-  const double area = MA(MT(M_AREA), 0, 0);
-  const double ra_x = area + AT(xfx, 0, 0) - AT(xfx, 1, 0);
-  const double ra_y = area + AT(yfx, 0, 0) - AT(yfx, 0, 1);
-  AT(zh, 0, 0) = (AT(zh, 0, 0) * area + AT(fx, 0, 0) - AT(fx, 1, 0) + AT(fy, 0, 0) - AT(fy, 0, 1)) /
-                 (ra_x + ra_y - area);
-}
-
 // pk3 on the 2-wide halo ring and pe on the 1-wide ring (from the halo-updated delp):
 // one lane per (ring column, level); each lane sums delp from the top in the same order
 // as the sequential column loop, so the values are identical
@@ -1070,14 +1053,12 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
   TpArgs t{};
   t.q = a.zh; t.nt = 1; t.nk = k1;
   t.crx = a.crx_e; t.cry = a.cry_e; t.xfx = a.xfx_e; t.yfx = a.yfx_e;
-  t.mfx = nullptr; t.mfy = nullptr; t.fx = a.fx; t.fy = a.fy; t.ord = a.hord;
+  t.mfx = nullptr; t.mfy = nullptr; t.ord = a.hord;
+  // the flux-form height update inside the march (tp.hip TM = 4, zh_update's expressions and
+  // order): no flux planes; the new heights go to zh_out
+  t.zh_out = a.zh_out;
   fv_tp_2d(c, t);
-  Launch2D Li{0, 0, d.nx, d.ny};
-  GT_LAUNCH(zh_update_k, g2lv(Li, d.nsub * k1), dim3(BX, BY), 0, c.st, d, c.subs, c.met, k1, a.fx, a.fy,
-                     a.xfx_e, a.yfx_e, a.zh);
-  HIP_LAUNCH_CHECK();
-  const Ext e = ext(d);
-  gt_bytes(k1 * (2 * e.X + 2 * e.Y + 2 * e.C) + e.C);
+  (void)d;
 }
 
 void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* delp, double* pk3, double* pe) {

@@ -293,9 +293,14 @@ std::map<std::string, Fn>& reg() {
          za.crx = F(dy, f[1]).p; za.cry = F(dy, f[2]).p; za.xfx = F(dy, f[3]).p; za.yfx = F(dy, f[4]).p;
          za.crx_e = dy.field("_ud_crx", k1).p; za.cry_e = dy.field("_ud_cry", k1).p;
          za.xfx_e = dy.field("_ud_xfx", k1).p; za.yfx_e = dy.field("_ud_yfx", k1).p;
-         za.fx = dy.field("_ud_fx", k1).p; za.fy = dy.field("_ud_fy", k1).p; za.gam = dy.field("_ud_gam", k1).p;
          za.zh = zh.p;
+         Field& zo = dy.field("_ud_zh", k1);
+         za.zh_out = zo.p;
          update_dz_d(dy.ctx(), za);
+         // in place for the caller: the march writes the compute cells only, so the field's halo
+         // ring goes onto the new planes first, then the planes back into the field
+         copy_halo_ring(dy.ctx(), dy.d.nsub * k1, zh.p, zo.p);
+         copy_levels(dy.ctx(), dy.field_elems(k1), zo.p, zh.p);
        }},
       // a2b_ord4(q | qout): cell means -> cell corners (4th order, cubed-sphere edge forms)
       {"a2b_ord4",

@@ -204,9 +204,9 @@ struct YRoll {
 // a level k+1 (odd level count: the upper half repeats level k and stores nothing)
 template <int ORD, bool EX, bool AHEAD2, bool MF, int NF, int TM>
 __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, int pair) {
-  static_assert(TM == 0 || (TM == 1 && NF == 3 && MF) || (TM == 2 && MF) || (TM == 3 && NF == 1 && !MF),
+  static_assert(TM == 0 || (TM == 1 && NF == 3 && MF) || (TM == 2 && MF) || ((TM == 3 || TM == 4) && NF == 1 && !MF),
                 "thermo march: delp, w, pt with the accumulators as MX / MY; tracer march: mass fluxes; "
-                "ds_uv march: one field, no mass fluxes");
+                "ds_uv and height marches: one field, no mass fluxes");
   const Dims& d = a.d;
   const int lane = threadIdx.x & (MW - 1);
   const int hl = pair ? (lane & 31) : lane;  // lane within the strip
@@ -633,6 +633,23 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
         for (int f = 0; f < NF; ++f) fyo_prev[f] = fyo[f];
         my_prev = cur.my;
       }
+      if constexpr (TM == 4) {
+        if (rowm) {
+          // zh_update on row m (same expressions and order): the x fluxes of the cell's two
+          // edges (x neighbour by DPP), the y fluxes of edges m (previous step) and m + 1, the
+          // area fluxes xfx of row m and yfx of edges m, m + 1
+          const double area = arw[0];
+          const double rxm = area + hxf[0] - dpp_next(hxf[0]);
+          const double fxe = dpp_next(fxo[0]);
+          const double zn = (qyw[0][0] * area + fxo[0] - fxe + fyo_prev[0] - fyo[0]) / (rxm + ray - area);
+          if (GEN) {
+            if (s_fy && mrow < j1) bst(rFX[0], se - rowb, zn);
+          } else {
+            bstv(rFX[0], vfy, se - rowb, zn);
+          }
+        }
+        fyo_prev[0] = fyo[0];
+      }
     }
     yfx_prev = cur.yfx;
     if constexpr (TM == 3) ke_m = t_ke;
@@ -1046,6 +1063,12 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
       m.nsplt = a.nsplt;
       m.it = a.it;
     }
+    const bool zup = a.zh_out != nullptr;
+    if (zup) {
+      if (pair2 || tupd || a.nt != 1 || a.mfx || a.u_uv)
+        throw std::runtime_error("fv_tp_2d with the height update: one field, no mass fluxes");
+      m.qo[0] = a.zh_out;
+    }
     const bool uv = a.u_uv != nullptr;
     if (uv) {
       if (pair2 || tupd || a.nt != 1 || a.mfx || !a.ke_uv || !a.v_uv)
@@ -1055,7 +1078,7 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
       m.vv = a.v_uv;
     }
     for (int f = 0; f < NFw; ++f)
-      if (!m.qf[f] || (tupd ? !m.qo[f] : (!uv && (!m.fxf[f] || !m.fyf[f]))))
+      if (!m.qf[f] || (tupd || zup ? !m.qo[f] : (!uv && (!m.fxf[f] || !m.fyf[f]))))
         throw std::runtime_error("fv_tp_2d: field slot " + std::to_string(f) + " of a " + std::to_string(NFw) +
                                  "-field group is not set");
     m.nt = a.nt;
@@ -1111,6 +1134,15 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
       else GT_LAUNCH_N("tp_march_uv<6>", (tp_march<6, true, false, 1, 3>), g, b, 0, c.st, m);
       HIP_LAUNCH_CHECK();
       gt_bytes(ub / 8.0);
+      return;
+    }
+    if (zup) {
+      // zh read and written; crx cry xfx yfx read (the 2-D area plane not counted)
+      const double zb = 8.0 * a.nk * (2 * e.C + 2 * (e.X + e.Y));
+      if (a.ord == 5) GT_LAUNCH_N("tp_march_zh<5>", (tp_march<5, true, false, 1, 4>), g, b, 0, c.st, m);
+      else GT_LAUNCH_N("tp_march_zh<6>", (tp_march<6, true, false, 1, 4>), g, b, 0, c.st, m);
+      HIP_LAUNCH_CHECK();
+      gt_bytes(zb / 8.0);
       return;
     }
     if (tupd) {
