@@ -96,6 +96,22 @@ def manifest_family(fam):
     return spec["same_as"] if isinstance(spec, dict) and "same_as" in spec else fam
 
 
+# launch names (GT_LAUNCH_N) whose kernel symbol, as rocprof records it, differs
+LAUNCH_SYMBOL = {
+    "tp_march_thermo<6, ex>": "tp_march<6, false, true, 3, 1, 2, 1>",
+    "tp_march_thermo<6, in>": "tp_march<6, false, true, 3, 1, 2, 2>",
+    "tp_march_thermo<5, ex>": "tp_march<5, false, true, 3, 1, 2, 1>",
+    "tp_march_thermo<5, in>": "tp_march<5, false, true, 3, 1, 2, 2>",
+    "tp_march_uv<6>": "tp_march<6, true, false, 1, 3, 0, 0>",
+    "tp_march_zh<6>": "tp_march<6, true, false, 1, 4, 0, 0>",
+    "tp_march_tracer<6, 2>": "tp_march<6, true, true, 2, 2, 0, 0>",
+    "ds_ke": "ds_ke_ld<6, true>",
+    "cs_transport_ke": "cs_transport_ke_ld",
+    "cs_update": "cs_update_ld",
+    "cs_tmp": "cs_tmp_ld",
+}
+
+
 def pmc_traffic(fam, launches):
     """HBM bytes per launch of kernel family `fam` (launch-weighted over the instantiations
     timed, `launches` = {launch name: count}) from the newest committed PMC summary
@@ -106,7 +122,7 @@ def pmc_traffic(fam, launches):
     for f in reversed(files):
         with open(f) as fh:
             t = json.load(fh)
-        keys = {k: k.strip("()").replace(" ", "") for k in launches}
+        keys = {k: LAUNCH_SYMBOL.get(k.strip("()"), k.strip("()")).replace(" ", "") for k in launches}
         tk = {k.replace(" ", ""): v for k, v in t.items()}
         for k, v in keys.items():  # rocprof spells out defaulted template arguments
             if v not in tk and v.endswith(">"):
