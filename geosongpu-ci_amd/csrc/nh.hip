@@ -752,7 +752,9 @@ __global__ void __launch_bounds__(AM_W * AM_WAVES) a2b_march_k(A2bM a) {
   // wave index through readfirstlane: the plane, strip, segment and the pointers derived
   // from them stay in SGPRs (114 -> 78 VGPRs, 4 -> 6 waves per SIMD: C180 2.57 -> 1.96 ms
   // per step; prefetch blocks of 4 rows instead of 2 measured 2.22 ms)
-  const long w = (long)blockIdx.x * AM_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x / AM_W);
+  // XCD-aware order (xcd_block): neighbouring segments, which re-read each other's halo rows,
+  // behind one L2
+  const long w = (long)xcd_block() * AM_WAVES + __builtin_amdgcn_readfirstlane(threadIdx.x / AM_W);
   const int strip = (int)(w % a.nstrip);
   const long t = w / a.nstrip;
   const int seg = (int)(t % a.nseg);
@@ -1111,7 +1113,7 @@ void a2b_ord4_multi(const Ctx& c, int nf, const int* nk, const double* const* q,
   }
   m.seg = (int)cdiv(d.ny + 1, m.nseg);
   const long waves = (long)m.nz * m.nstrip * m.nseg;
-  GT_LAUNCH(a2b_march_k, dim3(cdiv(waves, AM_WAVES)), dim3(AM_W * AM_WAVES), 0, c.st, m);
+  GT_LAUNCH(a2b_march_k, dim3(xcd_pad(cdiv(waves, AM_WAVES))), dim3(AM_W * AM_WAVES), 0, c.st, m);
   HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   gt_bytes(lev * (e.C + e.K));  // q (cells) read, qout (corners) written

@@ -341,7 +341,10 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
   const int ni = d.nx + 2 * a.ring, nj = d.ny + 2 * a.ring;
   const int ncol = ni * nj;
   const int s = blockIdx.y;
-  const int c0 = (blockIdx.x * RS_WAVES + wv) * NC;
+  // XCD-aware order (xcd_block): a wave's 8 columns are 64 B of each level's 128-B lines, the
+  // other half read by the neighbouring wave; with each XCD on a contiguous run of workgroups
+  // the neighbours that share lines sit behind one L2
+  const int c0 = ((int)xcd_block() * RS_WAVES + wv) * NC;
   if (c0 >= ncol) return;  // whole wavefront; no workgroup barrier in this kernel
   int c = c0 + lane / NB;
   const bool valid = c < ncol;  // writes
@@ -680,7 +683,9 @@ void launch_riem(const Ctx& c, const RiemArgs& a) {
   // scan form when the column splits into NB blocks of an instantiated M (all but the last
   // block full): (NB - 1) M < km <= NB M
   auto fits = [&](int m, int nb) { return (nb - 1) * m < km && km <= nb * m; };
-  auto grid = [&](int nb) { return dim3(cdiv(cdiv(ncol, 64 / nb), RS_WAVES), c.d.nsub); };
+  auto grid = [&](int nb) {
+    return dim3(xcd_pad(cdiv(cdiv(ncol, 64 / nb), RS_WAVES)), c.d.nsub);
+  };
   const bool scan = riem_variant() != 1;
   RiemArgs& am = const_cast<RiemArgs&>(a);
   am.dbg = g_riem_dbg;

@@ -54,6 +54,8 @@ __device__ __forceinline__ bool thread_point(const Launch2D& L, int& i, int& j) 
 // grid for thread_point over region L and nz planes (blockIdx.z), padded to a multiple of 8
 // blocks per plane (xcd_block; GTFV3_XCD=0: one block more, which keeps the identity order)
 bool xcd_order_enabled();
+// a 1-D workgroup count padded for xcd_block (its extra workgroups must find no work)
+inline unsigned xcd_pad(long g) { return (unsigned)(xcd_order_enabled() ? (g + 7) / 8 * 8 : (g + 7) / 8 * 8 + 1); }
 inline dim3 plane_grid(const Launch2D& L, long nz) {
   long gx = ((long)L.ni * L.nj + BX * BY - 1) / (BX * BY);
   gx = xcd_order_enabled() ? (gx + 7) / 8 * 8 : (gx + 7) / 8 * 8 + 1;
