@@ -1002,7 +1002,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES) remap_blk_k(RemapArgs a) {
   // the job's columns: cells nx x ny, u edges nx x (ny + 1), v edges (nx + 1) x ny
   const int ni = job == J_V ? d.nx + 1 : d.nx, nj = job == J_U ? d.ny + 1 : d.ny;
   const int ncol = ni * nj;
-  const int c0 = (blockIdx.x * RB_WAVES + wv) * NC;
+  const int c0 = ((int)xcd_block() * RB_WAVES + wv) * NC;  // XCD-aware order, as riem_scan_k
   if (c0 >= ncol) return;  // whole wavefront (no barrier follows)
   int c = c0 + cl;
   const bool valid = c < ncol;
@@ -1333,7 +1333,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) remap_blkq_k(RemapArgs a) {
   auto real = [&](int m) { return !PART || m < nv; };
   const int s = blockIdx.z;
   const int ncol = d.nx * d.ny;
-  const int c0 = (blockIdx.x * RB_WAVES + wv) * NC;
+  const int c0 = ((int)xcd_block() * RB_WAVES + wv) * NC;  // XCD-aware order, as riem_scan_k
   if (c0 >= ncol) return;  // whole wavefront (no barrier follows)
   int c = c0 + cl;
   const bool valid = c < ncol;
@@ -1686,7 +1686,7 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
   auto blk = [&](auto Mc, auto NBc, auto PARTc) {
     constexpr int M = decltype(Mc)::value, NB = decltype(NBc)::value;
     constexpr bool PART = decltype(PARTc)::value;
-    const unsigned gx = cdiv(cdiv(nce, 64 / NB), RB_WAVES);
+    const unsigned gx = xcd_pad(cdiv(cdiv(nce, 64 / NB), RB_WAVES));
     const dim3 tb(64 * RB_WAVES);
     if (p1) {
       GT_LAUNCH((remap_blk_k<M, NB, PART, JK_PT>), dim3(gx, 1, d.nsub), tb, 0, c.st, a);
