@@ -38,6 +38,7 @@ DEVICE_SYMBOLS = [
     "gtfv3_get_metric",
     "gtfv3_get_xyz",
     "gtfv3_get_scalars",
+    "gtfv3_level_damping",
     "gtfv3_halo_table",
     "gtfv3_halo_update",
     "gtfv3_stencil",
@@ -95,6 +96,7 @@ def lib():
         "gtfv3_get_metric": (I, [P, S, DP]),
         "gtfv3_get_xyz": (I, [P, DP]),
         "gtfv3_get_scalars": (I, [P, DP]),
+        "gtfv3_level_damping": (I, [P, DP, I]),
         "gtfv3_halo_table": (I, [P, I, IP, I]),
         "gtfv3_halo_update": (I, [P, S]),
         "gtfv3_stencil": (I, [P, S, S, DP, I]),

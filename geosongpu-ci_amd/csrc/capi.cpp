@@ -66,7 +66,7 @@ Namelist parse_config(const char* cfg, const Namelist& base) {
     if (v.empty() || used != v.size()) throw std::runtime_error("config value of " + k + " is not a number: '" + v + "'");
     int ix = (int)x;
     static const char* real_keys[] = {"dt", "dddmp", "d2_bg", "d4_bg", "vtdm4", "d_con", "delt_max", "p_fac",
-                                      "dz_min", "ptop"};
+                                      "dz_min", "ptop", "d2_bg_k1", "d2_bg_k2", "ke_bg"};
     bool is_real = false;
     for (const char* rk : real_keys) is_real = is_real || k == rk;
     if (!is_real && (double)ix != x) throw std::runtime_error("config value of " + k + " must be an integer: '" + v + "'");
@@ -104,14 +104,31 @@ Namelist parse_config(const char* cfg, const Namelist& base) {
     else if (k == "host_only") nl.host_only = ix != 0;
     else if (k == "loopback") nl.loopback = ix;
     else if (k == "do_vort_damp") nl.do_vort_damp = ix != 0;
+    else if (k == "n_sponge") nl.n_sponge = ix;
+    else if (k == "d2_bg_k1") nl.d2_bg_k1 = x;
+    else if (k == "d2_bg_k2") nl.d2_bg_k2 = x;
+    else if (k == "ke_bg") nl.ke_bg = x;
+    else if (k == "convert_ke") nl.convert_ke = ix != 0;
     else throw std::runtime_error("unknown config key: " + k);
   }
   // fv_core_nml semantics: the vorticity damping order follows nord (FV3 dyn_core:
-  // nord_v = min(2, nord)) unless given, and vtdm4 acts only with do_vort_damp
+  // nord_v = min(2, nord)) unless given; vtdm4 damps vorticity, delp, w and pt only with
+  // do_vort_damp (damp.hip column_damping), while vtdm4 > 1e-4 alone still puts the d_con heat
+  // on every level (heat_levels) -- said once on stderr, since that combination is easy to
+  // write by accident
   if (!nord_v_given) nl.nord_v = nl.nord < 2 ? nl.nord : 2;
-  if (!nl.do_vort_damp) nl.vtdm4 = 0.0;
+  if (nl.vtdm4 > 0.0 && !nl.do_vort_damp)
+    std::fprintf(stderr,
+                 "gtfv3: vtdm4 = %g without do_vort_damp = 1: no vorticity / delp / w / pt del-n damping "
+                 "(FV3 fv_core_nml semantics); d_con heat on every level\n",
+                 nl.vtdm4);
   for (int h : {nl.hord_mt, nl.hord_vt, nl.hord_tm, nl.hord_dp, nl.hord_tr})
     if (h != 5 && h != 6) throw std::runtime_error("hord must be 5 or 6");
+  // the remap implements FV3's kord = 9 profile only (remap.hip): any other order is refused
+  // rather than run as kord 9 (kord_tm = -9: the same profile for T in log p)
+  for (int kd : {nl.kord_mt, nl.kord_wz, nl.kord_tr})
+    if (kd != 9) throw std::runtime_error("kord_mt / kord_wz / kord_tr must be 9 (the implemented PPM remap)");
+  if (nl.kord_tm != -9) throw std::runtime_error("kord_tm must be -9 (the implemented PPM remap of T in log p)");
   if (nl.nord < 0 || nl.nord > 3) throw std::runtime_error("nord must be 0 .. 3");
   if (nl.nord_v < 0 || nl.nord_v > 2) throw std::runtime_error("nord_v must be 0 .. 2");
   return nl;
@@ -278,6 +295,24 @@ int gtfv3_get_scalars(void* h, double* out) {
   out[1] = d->hm.da_min_c;
   for (size_t i = 0; i < d->hm.corner_w.size(); ++i) out[2 + i] = d->hm.corner_w[i];
   API_CATCH
+}
+
+int gtfv3_level_damping(void* h, double* out, int cap) {
+  try {
+    Dycore* d = D(h);
+    const std::vector<LevelDamp> col = column_damping(d->nl, d->hm.da_min, d->hm.da_min_c);
+    if (out && cap >= (int)col.size())
+      for (size_t k = 0; k < col.size(); ++k) {
+        const LevelDamp& l = col[k];
+        const double row[10] = {l.d2_divg, l.vt4, l.dp4, l.w4, l.pt4, l.d_con,
+                                (double)l.nord, (double)l.nord_v, (double)l.nord_w, (double)l.nord_t};
+        std::memcpy(out + 10 * k, row, sizeof(row));
+      }
+    return heat_levels(d->nl);
+  } catch (const std::exception& e) {
+    set_error(e.what());
+    return -1;
+  }
 }
 
 int gtfv3_halo_table(void* h, int kind, int* out, int cap) {

@@ -1,17 +1,28 @@
-// damp.hip — d_sw's damping options beyond nord = 0 on gfx950 (FV3 sw_core d_sw / c_sw
-// divergence_corner / del6_vt_flux, fv_grid_utils fill_corners; restated in
-// oracle/sw_core.py with the same expressions and order):
+// damp.hip — d_sw's damping on gfx950 (FV3 dyn_core's per-level parameters, sw_core d_sw /
+// c_sw divergence_corner / del6_vt_flux, tp_core deln_flux, del2_cubed, fv_grid_utils
+// fill_corners; restated in oracle/sw_core.py with the same expressions and order):
+//   * the column of d_sw parameters (column_damping): every level nord, min(0.2, d2_bg),
+//     nord_v = min(2, nord), damp_vt = vtdm4 with do_vort_damp, w and pt following nord_v /
+//     damp_vt; the sponge layers (n_sponge >= 0) in the top three levels: del-2 divergence
+//     damping from d2_bg_k1 / d2_bg_k2, del-2 w damping, vorticity / delp del-2 damping with
+//     do_vort_damp, d_con 0;
 //   * nord = 1..3: del-(2 nord + 2) damping of the corner divergence (c_sw's divg_d, halo
 //     exchanged as a corner field) with d4_bg, plus the del-2 Smagorinsky-type term whose
 //     coefficient uses the corner vorticity (a2b_ord4 of the cell vorticity wk) when dddmp > 0;
-//   * vtdm4 > 0: del-(2 nord_v + 2) diffusive fluxes of wk added to u, v;
-//   * d_con > 0: the kinetic energy both remove as a heat source (summed over the acoustic
-//     sub-steps, added to pt after them with the delt_max limiter) and the dissipation
-//     estimate diss_est.
-// None of this runs in the Held-Suarez benchmark namelist (nord = 0, vtdm4 = 0, d_con = 0).
+//   * damp_vt: del-(2 nord_v + 2) diffusive fluxes of wk added to u, v, and of delp added to
+//     the mass fluxes inside fv_tp_2d; damp_t: mass-weighted del-(2 nord_t + 2) fluxes of pt;
+//     damp_w: w's del-(2 nord_w + 2) increment and its heat;
+//   * d_con > 0: the kinetic energy the damping removes as a heat source (summed over the
+//     acoustic sub-steps, smoothed by del2_cubed on the top n_con levels, added to pt there
+//     with the delt_max limiter) and the dissipation estimate diss_est.
+// In the Held-Suarez benchmark namelist (nord = 0, vtdm4 = 0, d_con = 0) only the sponge's
+// per-level divergence damping and the top levels' w damping run.
 // The cube-corner fills (B-grid XDir / YDir, the D-grid vector pair, copy_corners of the
 // cell field) are not separate passes: each kernel reads a cube-corner halo point through
 // the fill's source map, which leaves every other value as it was.
+// Kernels on a level window [k0, k0 + nkw) of an npz-level field take (npz, k0, nkw) and a
+// grid of nsub * nkw planes (WSETUP).
+#include <algorithm>
 #include <cmath>
 #include <stdexcept>
 
@@ -32,6 +43,16 @@ namespace {
   const long zo = (long)z * d.plane;                                 \
   const long o = pidx(d, i, j);                                      \
   (void)I; (void)J; (void)N; (void)zo;
+#define WSETUP()                                                          \
+  int i, j;                                                               \
+  if (!thread_point(L, i, j)) return;                                     \
+  const int s = (int)blockIdx.z / nkw, k = k0 + (int)blockIdx.z % nkw;    \
+  const SubInfo sub = subs[s];                                            \
+  const int N = sub.N;                                                    \
+  const int I = i + sub.ioff, J = j + sub.joff;                           \
+  const long zo = ((long)s * npz + k) * d.plane;                          \
+  const long o = pidx(d, i, j);                                           \
+  (void)I; (void)J; (void)N; (void)zo; (void)k;
 #define MT(name) met(M, d, name, s)
 #define MA(arr, di, dj) arr[o + (long)(dj) * d.pitch + (di)]
 #define AT(arr, di, dj) arr[zo + o + (long)(dj) * d.pitch + (di)]
@@ -174,21 +195,25 @@ __global__ void __launch_bounds__(256) dd_div_k(Dims d, const SubInfo* __restric
 }
 
 // the corner damping term vd = damp2 * delpc + dd8 * dd (delpc: c_sw's divergence), added
-// to ke; vort: the corner vorticity (a2b_ord4 of wk) or null (dddmp = 0)
-__global__ void __launch_bounds__(256) dd_term_k(Dims d, const SubInfo* __restrict__ subs, int npz, double dt,
-                                                 double dddmp, double d2_bg, double da_min_c, double dd8,
+// to ke; vort: the corner vorticity (a2b_ord4 of wk) or null (dddmp = 0).  Levels whose
+// column parameters say nord = 0 (the sponge layers) took ds_ke's del-2 term instead.
+__global__ void __launch_bounds__(256) dd_term_k(Dims d, const SubInfo* __restrict__ subs, int npz,
+                                                 const LevelDamp* __restrict__ lv, double dt, double dddmp,
+                                                 double da_min_c, double dd8,
                                                  const double* __restrict__ delpc, const double* __restrict__ dd,
                                                  const double* __restrict__ vort, double* __restrict__ ke,
                                                  double* __restrict__ vd) {
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
   DSETUP(npz)
+  const LevelDamp& lk = lv[z % npz];
+  if (lk.nord == 0) return;
   const double dp = AT(delpc, 0, 0);
   double vc = 0.0;
   if (vort) {
     const double w = AT(vort, 0, 0);
     vc = fabs(dt) * sqrt(dp * dp + w * w);
   }
-  const double damp2 = da_min_c * fmax(d2_bg, fmin(0.20, dddmp * vc));
+  const double damp2 = da_min_c * fmax(lk.d2_divg, fmin(0.20, dddmp * vc));
   const double t = damp2 * dp + dd8 * AT(dd, 0, 0);
   AT(ke, 0, 0) = AT(ke, 0, 0) + t;
   AT(vd, 0, 0) = t;
@@ -207,24 +232,33 @@ __global__ void __launch_bounds__(256) dd_wk_k(Dims d, const SubInfo* __restrict
   AT(wk, 0, 0) = MA(MT(M_RAREA), 0, 0) * (udx0 - udx1 + vdy1 - vdy0);
 }
 
-// ---- del6_vt_flux ----
-// d2 = damp * wk over [-nord, n-1+nord], zero elsewhere on the plane
-__global__ void __launch_bounds__(256) d6_init_k(Dims d, const SubInfo* __restrict__ subs, int npz, int nord,
-                                                 double damp, const double* __restrict__ wk, double* __restrict__ d2) {
+// ---- tp_core deln_flux / del6_vt_flux on a level window ----
+// d2 = coef * q over [-1-nord, n+nord] (coef from the level's LevelDamp, DL_ONE: 1), zero
+// elsewhere on the plane
+__device__ __forceinline__ double deln_coef(const LevelDamp& l, int coef) {
+  return coef == DL_VT4 ? l.vt4 : (coef == DL_DP4 ? l.dp4 : (coef == DL_W4 ? l.w4 : 1.0));
+}
+__global__ void __launch_bounds__(256) dl_init_k(Dims d, const SubInfo* __restrict__ subs, int npz, int k0, int nkw,
+                                                 int nord, const LevelDamp* __restrict__ lv, int coef,
+                                                 const double* __restrict__ q, double* __restrict__ d2) {
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  DSETUP(npz)
-  AT(d2, 0, 0) = in_reg(i, j, -nord, d.nx - 1 + nord, -nord, d.ny - 1 + nord) ? damp * AT(wk, 0, 0) : 0.0;
+  WSETUP()
+  if (!in_reg(i, j, -1 - nord, d.nx + nord, -1 - nord, d.ny + nord)) {
+    AT(d2, 0, 0) = 0.0;
+    return;
+  }
+  AT(d2, 0, 0) = coef == DL_ONE ? AT(q, 0, 0) : deln_coef(lv[k], coef) * AT(q, 0, 0);
 }
 
 // fx2 on y-edges over [-r, nx+r] x [-r, ny-1+r], fy2 on x-edges over [-r, nx-1+r] x [-r, ny+r]
 // (zero elsewhere) from d2 read through copy_corners (cc: XDir for fx2, YDir for fy2);
-// first: (d2(i-1) - d2(i)) as del6_vt_flux's first pass, else (d2(i) - d2(i-1))
-__global__ void __launch_bounds__(256) d6_flux_k(Dims d, const SubInfo* __restrict__ subs,
-                                                 const double* __restrict__ M, int npz, int r, int cc, int first,
-                                                 const double* __restrict__ d2, double* __restrict__ fx2,
+// first: (d2(i-1) - d2(i)) as deln_flux's first pass and del2_cubed, else (d2(i) - d2(i-1))
+__global__ void __launch_bounds__(256) dl_flux_k(Dims d, const SubInfo* __restrict__ subs,
+                                                 const double* __restrict__ M, int npz, int k0, int nkw, int r, int cc,
+                                                 int first, const double* __restrict__ d2, double* __restrict__ fx2,
                                                  double* __restrict__ fy2) {
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  DSETUP(npz)
+  WSETUP()
   auto at = [&](int ii, int jj, int dir) { return d2[zo + (cc ? cc_off(d, sub, ii, jj, dir) : pidx(d, ii, jj))]; };
   double fx = 0.0, fy = 0.0;
   if (in_reg(i, j, -r, d.nx + r, -r, d.ny - 1 + r)) {
@@ -240,33 +274,107 @@ __global__ void __launch_bounds__(256) d6_flux_k(Dims d, const SubInfo* __restri
 }
 
 // d2 = (fx2 - fx2(i+1) + fy2 - fy2(j+1)) * rarea over [-nt-1, n+nt], zero elsewhere
-__global__ void __launch_bounds__(256) d6_div_k(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
-                                                int npz, int nt, const double* __restrict__ fx2,
+__global__ void __launch_bounds__(256) dl_div_k(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
+                                                int npz, int k0, int nkw, int nt, const double* __restrict__ fx2,
                                                 const double* __restrict__ fy2, double* __restrict__ d2) {
   Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  DSETUP(npz)
+  WSETUP()
   AT(d2, 0, 0) = in_reg(i, j, -nt - 1, d.nx + nt, -nt - 1, d.ny + nt)
                      ? (AT(fx2, 0, 0) - AT(fx2, 1, 0) + AT(fy2, 0, 0) - AT(fy2, 0, 1)) * MA(MT(M_RAREA), 0, 0)
                      : 0.0;
 }
 
+// deln_flux's last step: the diffusive fluxes into the transport fluxes on [0, nx] x [0, ny-1]
+// (fx) and [0, nx-1] x [0, ny] (fy); with mass, weighted by 0.5 pt4 (mass(i-1) + mass(i))
+__global__ void __launch_bounds__(256) dl_add_k(Dims d, const SubInfo* __restrict__ subs, int npz, int k0, int nkw,
+                                                const LevelDamp* __restrict__ lv, const double* __restrict__ fx2,
+                                                const double* __restrict__ fy2, const double* __restrict__ mass,
+                                                double* __restrict__ fx, double* __restrict__ fy) {
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  WSETUP()
+  if (mass) {
+    const double damp2 = 0.5 * lv[k].pt4;
+    if (j < d.ny) AT(fx, 0, 0) = AT(fx, 0, 0) + damp2 * (AT(mass, -1, 0) + AT(mass, 0, 0)) * AT(fx2, 0, 0);
+    if (i < d.nx) AT(fy, 0, 0) = AT(fy, 0, 0) + damp2 * (AT(mass, 0, -1) + AT(mass, 0, 0)) * AT(fy2, 0, 0);
+  } else {
+    if (j < d.ny) AT(fx, 0, 0) = AT(fx, 0, 0) + AT(fx2, 0, 0);
+    if (i < d.nx) AT(fy, 0, 0) = AT(fy, 0, 0) + AT(fy2, 0, 0);
+  }
+}
+
+// d_sw's w damping on compute cells: dw = div(fx2, fy2) rarea, hw = ke_bg |dt| - dw (w + dw / 2)
+__global__ void __launch_bounds__(256) dl_wdamp_k(Dims d, const SubInfo* __restrict__ subs,
+                                                  const double* __restrict__ M, int npz, int k0, int nkw,
+                                                  double ke_dt, const double* __restrict__ fx2,
+                                                  const double* __restrict__ fy2, const double* __restrict__ w,
+                                                  double* __restrict__ dw, double* __restrict__ hw) {
+  Launch2D L{0, 0, d.nx, d.ny};
+  WSETUP()
+  const double x = (AT(fx2, 0, 0) - AT(fx2, 1, 0) + AT(fy2, 0, 0) - AT(fy2, 0, 1)) * MA(MT(M_RAREA), 0, 0);
+  AT(dw, 0, 0) = x;
+  AT(hw, 0, 0) = ke_dt - x * (AT(w, 0, 0) + 0.5 * x);
+}
+
+__global__ void __launch_bounds__(256) dl_wadd_k(Dims d, const SubInfo* __restrict__ subs, int npz, int k0, int nkw,
+                                                 const double* __restrict__ dw, double* __restrict__ w) {
+  Launch2D L{0, 0, d.nx, d.ny};
+  WSETUP()
+  AT(w, 0, 0) = AT(w, 0, 0) + AT(dw, 0, 0);
+}
+
+// the nord_w = 0 w damping in one pass after the fused thermo march: the del-2 fluxes of
+// d2 = w4 w from the OLD w (the march wrote the new values to w_new and left w as it was), dw
+// and its heat, w_new += dw -- the expressions and order of dl_init_k / dl_flux_k /
+// dl_wdamp_k / dl_wadd_k, without their planes
+__global__ void __launch_bounds__(256) dl_wdamp0_k(Dims d, const SubInfo* __restrict__ subs,
+                                                   const double* __restrict__ M, int npz, int k0, int nkw,
+                                                   const LevelDamp* __restrict__ lv, double ke_dt,
+                                                   const double* __restrict__ w, double* __restrict__ w_new,
+                                                   double* __restrict__ hw) {
+  Launch2D L{0, 0, d.nx, d.ny};
+  WSETUP()
+  const double damp = lv[k].w4;
+  const double *sau = MT(M_SINA_U), *dy = MT(M_DY), *dxc = MT(M_DXC);
+  const double *sav = MT(M_SINA_V), *dx = MT(M_DX), *dyc = MT(M_DYC);
+  const double d2c = damp * AT(w, 0, 0), d2w = damp * AT(w, -1, 0), d2e = damp * AT(w, 1, 0);
+  const double d2s = damp * AT(w, 0, -1), d2n = damp * AT(w, 0, 1);
+  const double fx0 = MA(sau, 0, 0) * MA(dy, 0, 0) / MA(dxc, 0, 0) * (d2w - d2c);
+  const double fx1 = MA(sau, 1, 0) * MA(dy, 1, 0) / MA(dxc, 1, 0) * (d2c - d2e);
+  const double fy0 = MA(sav, 0, 0) * MA(dx, 0, 0) / MA(dyc, 0, 0) * (d2s - d2c);
+  const double fy1 = MA(sav, 0, 1) * MA(dx, 0, 1) / MA(dyc, 0, 1) * (d2c - d2n);
+  const double x = (fx0 - fx1 + fy0 - fy1) * MA(MT(M_RAREA), 0, 0);
+  if (hw) AT(hw, 0, 0) = ke_dt - x * (AT(w, 0, 0) + 0.5 * x);
+  AT(w_new, 0, 0) = AT(w_new, 0, 0) + x;
+}
+
 // d_con: the damped kinetic energy on compute cells into heat (+=) and diss (+=); u, v: the
-// updated winds times dx / dy before the vorticity-damping fluxes; fx2 / fy2 may be null
+// updated winds times dx / dy before the vorticity-damping fluxes.  Per level: the
+// vorticity-damping fluxes where lv.vt4 > 0, the w damping's heat hw where lv.w4 > 0; levels
+// with d_con_k <= 1e-5 (the sponge) add hw alone.
 __global__ void __launch_bounds__(256) dd_heat_k(Dims d, const SubInfo* __restrict__ subs,
-                                                 const double* __restrict__ M, int npz, double d_con,
+                                                 const double* __restrict__ M, int npz, const LevelDamp* __restrict__ lv,
                                                  const double* __restrict__ u, const double* __restrict__ v,
                                                  const double* __restrict__ vd, const double* __restrict__ fx2,
-                                                 const double* __restrict__ fy2, const double* __restrict__ delp,
-                                                 double* __restrict__ heat, double* __restrict__ diss) {
+                                                 const double* __restrict__ fy2, const double* __restrict__ hw,
+                                                 const double* __restrict__ delp, double* __restrict__ heat,
+                                                 double* __restrict__ diss) {
   Launch2D L{0, 0, d.nx, d.ny};
   DSETUP(npz)
+  const LevelDamp lk = lv[z % npz];
+  const double hwv = hw && lk.w4 > 0.0 ? AT(hw, 0, 0) : 0.0;
+  if (!(lk.d_con > 1e-5)) {
+    AT(heat, 0, 0) = AT(heat, 0, 0) + hwv;
+    AT(diss, 0, 0) = AT(diss, 0, 0) + hwv;
+    return;
+  }
+  const bool vt = lk.vt4 > 0.0;
   const double *rdx = MT(M_RDX), *rdy = MT(M_RDY);
   auto ub = [&](int dj) {
-    const double f2 = fy2 ? AT(fy2, 0, dj) : 0.0;
+    const double f2 = vt ? AT(fy2, 0, dj) : 0.0;
     return (AT(vd, 0, dj) - AT(vd, 1, dj) + f2) * MA(rdx, 0, dj);
   };
   auto vb = [&](int di) {
-    const double f2 = fx2 ? AT(fx2, di, 0) : 0.0;
+    const double f2 = vt ? AT(fx2, di, 0) : 0.0;
     return (AT(vd, di, 0) - AT(vd, di, 1) - f2) * MA(rdy, di, 0);
   };
   const double ub0 = ub(0), ub1 = ub(1), vb0 = vb(0), vb1 = vb(1);
@@ -277,36 +385,74 @@ __global__ void __launch_bounds__(256) dd_heat_k(Dims d, const SubInfo* __restri
   const double t = (ub0 * ub0 + ub1 * ub1 + vb0 * vb0 + vb1 * vb1) + 2.0 * (gy0 + gy1 + gx0 + gx1) -
                    MA(MT(M_COSA_S), 0, 0) * (u2 * dv2 + v2 * du2 + du2 * dv2);
   const double rs2 = MA(MT(M_RSIN2), 0, 0);
-  AT(heat, 0, 0) = AT(heat, 0, 0) + AT(delp, 0, 0) * (0.0 - 0.25 * d_con * rs2 * t);
-  AT(diss, 0, 0) = AT(diss, 0, 0) + -rs2 * t;
+  AT(heat, 0, 0) = AT(heat, 0, 0) + AT(delp, 0, 0) * (hwv - 0.25 * lk.d_con * rs2 * t);
+  AT(diss, 0, 0) = AT(diss, 0, 0) + (hwv - rs2 * t);
 }
 
-// vorticity damping: u += fy2 on x-edges, v -= fx2 on y-edges
+// vorticity damping: u += fy2 on x-edges, v -= fx2 on y-edges, on the levels that have it
 __global__ void __launch_bounds__(256) dd_vflux_k(Dims d, const SubInfo* __restrict__ subs, int npz,
-                                                  const double* __restrict__ fx2, const double* __restrict__ fy2,
-                                                  double* __restrict__ u, double* __restrict__ v) {
+                                                  const LevelDamp* __restrict__ lv, const double* __restrict__ fx2,
+                                                  const double* __restrict__ fy2, double* __restrict__ u,
+                                                  double* __restrict__ v) {
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
   DSETUP(npz)
+  if (!(lv[z % npz].vt4 > 0.0)) return;
   if (i < d.nx) AT(u, 0, 0) = AT(u, 0, 0) + AT(fy2, 0, 0);
   if (j < d.ny) AT(v, 0, 0) = AT(v, 0, 0) - AT(fx2, 0, 0);
 }
 
-// after the acoustic sub-steps: dT = heat / (cp delp), limited to delt (0.1x / 0.5x in the top
-// two layers), added to the potential temperature through pkz of the current state
-__global__ void __launch_bounds__(256) dd_heat_apply_k(Dims d, const SubInfo* __restrict__ subs, int npz,
-                                                       double delt, const double* __restrict__ heat,
+// ---- del2_cubed ----
+// the cube-corner cells this sub-domain owns and their west / east and south / north halo
+// neighbours set to the three's mean (one lane per plane and corner)
+__global__ void __launch_bounds__(64) h2_corner_k(Dims d, const SubInfo* __restrict__ subs, int npz, int k0, int nkw,
+                                                  double* __restrict__ q) {
+  const int t = (int)(blockIdx.x * blockDim.x + threadIdx.x);
+  if (t >= d.nsub * nkw * 4) return;
+  const int c = t & 3, z = t >> 2, s = z / nkw, k = k0 + z % nkw;
+  const SubInfo sub = subs[s];
+  const int N = sub.N;
+  const bool west = sub.ioff == 0, east = sub.ioff + d.nx == N, south = sub.joff == 0, north = sub.joff + d.ny == N;
+  int ci, cj, di, dj;  // corner cell (global) and the side of its halo neighbours
+  if (c == 0) { if (!(west && south)) return; ci = 0; cj = 0; di = -1; dj = -1; }
+  else if (c == 1) { if (!(east && south)) return; ci = N - 1; cj = 0; di = 1; dj = -1; }
+  else if (c == 2) { if (!(east && north)) return; ci = N - 1; cj = N - 1; di = 1; dj = 1; }
+  else { if (!(west && north)) return; ci = 0; cj = N - 1; di = -1; dj = 1; }
+  double* p = q + ((long)s * npz + k) * d.plane;
+  const int i = ci - sub.ioff, j = cj - sub.joff;
+  const long a = pidx(d, i, j), b = pidx(d, i + di, j), e = pidx(d, i, j + dj);
+  const double avg = (p[a] + p[b] + p[e]) * (1.0 / 3.0);
+  p[a] = avg;
+  p[b] = avg;
+  p[e] = avg;
+}
+
+// q += cd rarea (fx - fx(i+1) + fy - fy(j+1)) over [-nt, n-1+nt]
+__global__ void __launch_bounds__(256) h2_update_k(Dims d, const SubInfo* __restrict__ subs,
+                                                   const double* __restrict__ M, int npz, int k0, int nkw, int nt,
+                                                   double cd, const double* __restrict__ fx,
+                                                   const double* __restrict__ fy, double* __restrict__ q) {
+  Launch2D L{-nt, -nt, d.nx + 2 * nt, d.ny + 2 * nt};
+  WSETUP()
+  AT(q, 0, 0) = AT(q, 0, 0) + cd * MA(MT(M_RAREA), 0, 0) *
+                                  (AT(fx, 0, 0) - AT(fx, 1, 0) + AT(fy, 0, 0) - AT(fy, 0, 1));
+}
+
+// after the acoustic sub-steps, levels [0, n_con): dT = heat / (cv_air delp), limited to delt
+// (0.1x / 0.5x in the top two layers), added to the potential temperature through pkz of the
+// current state
+__global__ void __launch_bounds__(256) dd_heat_apply_k(Dims d, const SubInfo* __restrict__ subs, int npz, int k0,
+                                                       int nkw, double delt, const double* __restrict__ heat,
                                                        const double* __restrict__ delp,
                                                        const double* __restrict__ delz, double* __restrict__ pt) {
   Launch2D L{0, 0, d.nx, d.ny};
-  DSETUP(npz)
-  const int k = z % npz;
+  WSETUP()
   constexpr double RDG = -Constants::rdgas * (1.0 / Constants::grav);
   constexpr double K1K = Constants::kappa / (1.0 - Constants::kappa);
-  constexpr double CP = Constants::rdgas / Constants::kappa;
+  constexpr double CV = Constants::rdgas / Constants::kappa - Constants::rdgas;
   const double lim = k == 0 ? 0.1 * delt : (k == 1 ? 0.5 * delt : delt);
   const double dp = AT(delp, 0, 0);
   const double pkz = exp(K1K * log(RDG * dp / AT(delz, 0, 0) * AT(pt, 0, 0)));
-  const double dtmp = AT(heat, 0, 0) / (CP * dp);
+  const double dtmp = AT(heat, 0, 0) / (CV * dp);
   const double sg = dtmp > 0.0 ? 1.0 : (dtmp < 0.0 ? -1.0 : 0.0);
   AT(pt, 0, 0) = AT(pt, 0, 0) + sg * fmin(lim, fabs(dtmp)) / pkz;
 }
@@ -355,7 +501,7 @@ void divergence_damping(const Ctx& c, const DampArgs& a) {
   }
   const double dd8 = std::pow(c.da_min_c * a.d4_bg, (double)(a.nord + 1));
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
-  GT_LAUNCH(dd_term_k, g2(Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, a.npz, a.dt, a.dddmp, a.d2_bg, c.da_min_c, dd8,
+  GT_LAUNCH(dd_term_k, g2(Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, a.npz, a.lv, a.dt, a.dddmp, c.da_min_c, dd8,
             a.divg, a.dd, vort, a.ke, a.vd);
   HIP_LAUNCH_CHECK();
 }
@@ -367,47 +513,164 @@ void vorticity_wk(const Ctx& c, int npz, const double* u, const double* v, doubl
   HIP_LAUNCH_CHECK();
 }
 
-void del6_vt_flux(const Ctx& c, int npz, int nord, double damp, const double* wk, double* d2, double* fx2,
-                  double* fy2) {
+std::vector<LevelDamp> column_damping(const Namelist& nl, double da_min, double da_min_c) {
+  const int npz = nl.npz;
+  struct P {
+    int nord, nord_v, nord_w, nord_t;
+    double d2, dvt, dw, dt, dcon;
+  };
+  const double dvt = nl.do_vort_damp ? nl.vtdm4 : 0.0;
+  std::vector<P> p(npz, P{nl.nord, nl.nord_v, nl.nord_v, nl.nord_v, std::min(0.20, nl.d2_bg), dvt, dvt, dvt, nl.d_con});
+  if (npz == 1 || nl.n_sponge < 0) {
+    for (P& x : p) x.d2 = nl.d2_bg;
+  } else {
+    // sponge layers: del-2 damping of divergence, w and (with do_vort_damp) vorticity and delp;
+    // no special damping of pt
+    auto sponge = [&](P& x, double d2, bool vort) {
+      x.nord = 0;
+      x.d2 = d2;
+      x.nord_w = 0;
+      x.dw = d2;
+      x.dcon = 0.0;
+      if (vort && nl.do_vort_damp) {
+        x.nord_v = 0;
+        x.dvt = 0.5 * d2;
+      }
+    };
+    sponge(p[0], std::max(std::max(0.01, nl.d2_bg), nl.d2_bg_k1), true);
+    if (npz > 1 && nl.d2_bg_k2 > 0.01) sponge(p[1], std::max(nl.d2_bg, nl.d2_bg_k2), true);
+    if (npz > 2 && nl.d2_bg_k2 > 0.05) sponge(p[2], std::max(nl.d2_bg, 0.2 * nl.d2_bg_k2), false);
+  }
+  std::vector<LevelDamp> out(npz);
+  for (int k = 0; k < npz; ++k) {
+    const P& x = p[k];
+    LevelDamp& l = out[k];
+    l.d2_divg = x.d2;
+    l.vt4 = x.dvt > 1e-5 ? std::pow(x.dvt * da_min_c, (double)(x.nord_v + 1)) : 0.0;
+    l.dp4 = x.dvt > 1e-4 ? std::pow(x.dvt * da_min, (double)(x.nord_v + 1)) : 0.0;
+    l.w4 = x.dw > 1e-5 ? std::pow(x.dw * da_min_c, (double)(x.nord_w + 1)) : 0.0;
+    l.pt4 = x.dt > 1e-4 ? std::pow(x.dt * da_min, (double)(x.nord_t + 1)) : 0.0;
+    l.d_con = x.dcon;
+    l.nord = x.nord;
+    l.nord_v = x.nord_v;
+    l.nord_w = x.nord_w;
+    l.nord_t = x.nord_t;
+  }
+  return out;
+}
+
+int heat_levels(const Namelist& nl) {
+  int n = 2;
+  if (nl.convert_ke || nl.vtdm4 > 1e-4) n = nl.npz;
+  else if (nl.d2_bg_k1 < 1e-3) n = 0;
+  else if (nl.d2_bg_k2 < 1e-3) n = 1;
+  return std::min(n, nl.npz);
+}
+
+bool any_level(const LevelDamp* lv, int n, double LevelDamp::*coef) {
+  for (int k = 0; k < n; ++k)
+    if (lv[k].*coef > 0.0) return true;
+  return false;
+}
+
+void deln_fluxes(const Ctx& c, int npz, int k0, int nk, int nord, const LevelDamp* lv, int coef, const double* q,
+                 double* d2, double* fx2, double* fy2) {
   const Dims& d = c.d;
-  if (nord < 0 || nord > 2) throw std::runtime_error("del6_vt_flux: nord_v must be 0, 1 or 2");
-  const int nz = d.nsub * npz;
+  if (nord < 0 || nord > 2) throw std::runtime_error("deln_flux: nord must be 0, 1 or 2");
+  if (k0 < 0 || nk < 1 || k0 + nk > npz) throw std::runtime_error("deln_flux: level window outside the field");
+  const int nz = d.nsub * nk;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  GT_LAUNCH(d6_init_k, g2(full, nz), dim3(BX, BY), 0, c.st, d, c.subs, npz, nord, damp, wk, d2);
+  GT_LAUNCH(dl_init_k, g2(full, nz), dim3(BX, BY), 0, c.st, d, c.subs, npz, k0, nk, nord, lv, coef, q, d2);
   HIP_LAUNCH_CHECK();
-  GT_LAUNCH(d6_flux_k, g2(full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, nord, nord > 0 ? 1 : 0, 1, d2, fx2,
-            fy2);
+  GT_LAUNCH(dl_flux_k, g2(full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, k0, nk, nord, nord > 0 ? 1 : 0, 1,
+            d2, fx2, fy2);
   HIP_LAUNCH_CHECK();
   for (int n = 1; n <= nord; ++n) {
     const int nt = nord - n;
-    GT_LAUNCH(d6_div_k, g2(full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, nt, fx2, fy2, d2);
+    GT_LAUNCH(dl_div_k, g2(full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, k0, nk, nt, fx2, fy2, d2);
     HIP_LAUNCH_CHECK();
-    GT_LAUNCH(d6_flux_k, g2(full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, nt, 1, 0, d2, fx2, fy2);
+    GT_LAUNCH(dl_flux_k, g2(full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, k0, nk, nt, 1, 0, d2, fx2, fy2);
     HIP_LAUNCH_CHECK();
   }
 }
 
-void damping_heat(const Ctx& c, int npz, double d_con, const double* u, const double* v, const double* vd,
-                  const double* fx2, const double* fy2, const double* delp, double* heat, double* diss) {
+void deln_add(const Ctx& c, int npz, int k0, int nk, const LevelDamp* lv, const double* fx2, const double* fy2,
+              const double* mass, double* fx, double* fy) {
+  const Dims& d = c.d;
+  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
+  GT_LAUNCH(dl_add_k, g2(L, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, npz, k0, nk, lv, fx2, fy2, mass, fx, fy);
+  HIP_LAUNCH_CHECK();
+}
+
+void w_damping(const Ctx& c, int npz, int k0, int nk, double ke_dt, const double* fx2, const double* fy2,
+               const double* w, double* dw, double* hw) {
   const Dims& d = c.d;
   Launch2D L{0, 0, d.nx, d.ny};
-  GT_LAUNCH(dd_heat_k, g2(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, d_con, u, v, vd, fx2, fy2,
+  GT_LAUNCH(dl_wdamp_k, g2(L, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, k0, nk, ke_dt, fx2, fy2, w,
+            dw, hw);
+  HIP_LAUNCH_CHECK();
+}
+
+void w_damping0_fused(const Ctx& c, int npz, int k0, int nk, const LevelDamp* lv, double ke_dt, const double* w,
+                      double* w_new, double* hw) {
+  const Dims& d = c.d;
+  Launch2D L{0, 0, d.nx, d.ny};
+  GT_LAUNCH(dl_wdamp0_k, g2(L, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, k0, nk, lv, ke_dt, w, w_new,
+            hw);
+  HIP_LAUNCH_CHECK();
+}
+
+void w_damping_add(const Ctx& c, int npz, int k0, int nk, const double* dw, double* w) {
+  const Dims& d = c.d;
+  Launch2D L{0, 0, d.nx, d.ny};
+  GT_LAUNCH(dl_wadd_k, g2(L, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, npz, k0, nk, dw, w);
+  HIP_LAUNCH_CHECK();
+}
+
+void damping_heat(const Ctx& c, int npz, const LevelDamp* lv, const double* u, const double* v, const double* vd,
+                  const double* fx2, const double* fy2, const double* hw, const double* delp, double* heat,
+                  double* diss) {
+  const Dims& d = c.d;
+  Launch2D L{0, 0, d.nx, d.ny};
+  GT_LAUNCH(dd_heat_k, g2(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, lv, u, v, vd, fx2, fy2, hw,
             delp, heat, diss);
   HIP_LAUNCH_CHECK();
 }
 
-void vorticity_damping_apply(const Ctx& c, int npz, const double* fx2, const double* fy2, double* u, double* v) {
+void vorticity_damping_apply(const Ctx& c, int npz, const LevelDamp* lv, const double* fx2, const double* fy2,
+                             double* u, double* v) {
   const Dims& d = c.d;
   Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  GT_LAUNCH(dd_vflux_k, g2(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, fx2, fy2, u, v);
+  GT_LAUNCH(dd_vflux_k, g2(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, lv, fx2, fy2, u, v);
   HIP_LAUNCH_CHECK();
 }
 
-void damping_heat_apply(const Ctx& c, int npz, double delt, const double* heat, const double* delp, const double* delz,
-                        double* pt) {
+void del2_cubed(const Ctx& c, int npz, int k0, int nk, int nmax, double cd, double* q, double* fx, double* fy) {
   const Dims& d = c.d;
+  if (k0 < 0 || nk < 1 || k0 + nk > npz) throw std::runtime_error("del2_cubed: level window outside the field");
+  const int nz = d.nsub * nk;
+  const int ntimes = std::min(3, nmax);
+  Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  for (int n = 1; n <= ntimes; ++n) {
+    const int nt = ntimes - n;
+    GT_LAUNCH(h2_corner_k, dim3((unsigned)((nz * 4 + 63) / 64)), dim3(64), 0, c.st, d, c.subs, npz, k0, nk, q);
+    HIP_LAUNCH_CHECK();
+    GT_LAUNCH(dl_flux_k, g2(full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, k0, nk, nt, nt > 0 ? 1 : 0, 1, q,
+              fx, fy);
+    HIP_LAUNCH_CHECK();
+    Launch2D Lu{-nt, -nt, d.nx + 2 * nt, d.ny + 2 * nt};
+    GT_LAUNCH(h2_update_k, g2(Lu, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, k0, nk, nt, cd, fx, fy, q);
+    HIP_LAUNCH_CHECK();
+  }
+}
+
+void damping_heat_apply(const Ctx& c, int npz, int n_con, double delt, const double* heat, const double* delp,
+                        const double* delz, double* pt) {
+  const Dims& d = c.d;
+  if (n_con < 1) return;
   Launch2D L{0, 0, d.nx, d.ny};
-  GT_LAUNCH(dd_heat_apply_k, g2(L, d.nsub * npz), dim3(BX, BY), 0, c.st, d, c.subs, npz, delt, heat, delp, delz, pt);
+  GT_LAUNCH(dd_heat_apply_k, g2(L, d.nsub * n_con), dim3(BX, BY), 0, c.st, d, c.subs, npz, 0, n_con, delt, heat, delp,
+            delz, pt);
   HIP_LAUNCH_CHECK();
 }
 

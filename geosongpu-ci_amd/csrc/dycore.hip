@@ -104,6 +104,7 @@ Dycore::~Dycore() {
   if (h_cmax) (void)hipHostFree(h_cmax);
   if (ev_cmax) (void)hipEventDestroy(ev_cmax);
   if (dsubs) (void)hipFree(dsubs);
+  if (dlevel) (void)hipFree(dlevel);
   if (dmet) (void)hipFree(dmet);
   if (dcornerw) (void)hipFree(dcornerw);
   if (darea2) (void)hipFree(darea2);
@@ -358,6 +359,24 @@ const double* Dycore::vertical_dev() {
   return v.p;
 }
 
+const LevelDamp* Dycore::level_table(const std::vector<LevelDamp>& t) {
+  const size_t bytes = sizeof(LevelDamp) * t.size();
+  if (dlevel && t.size() == hlevel.size() && std::memcmp(t.data(), hlevel.data(), bytes) == 0) return dlevel;
+  if (t.size() > dlevel_cap) {
+    // nothing queued may still read the old table
+    if (dlevel) {
+      HIP_CHECK(hipDeviceSynchronize());
+      HIP_CHECK(hipFree(dlevel));
+    }
+    HIP_CHECK(hipMalloc(&dlevel, bytes));
+    dlevel_cap = t.size();
+  }
+  hlevel = t;
+  HIP_CHECK(hipMemcpyAsync(dlevel, hlevel.data(), bytes, hipMemcpyHostToDevice, st));
+  HIP_CHECK(hipStreamSynchronize(st));
+  return dlevel;
+}
+
 // One fv_dynamics call (FV3 fv_dynamics.F90 / dyn_core.F90 sequence, non-hydrostatic,
 // k_split remap cycles of n_split acoustic sub-steps, tracer_2d_1l, Lagrangian-to-
 // Eulerian remap, then T/omega/A-grid winds for the caller).
@@ -518,7 +537,7 @@ void Dycore::step() {
 
   DswArgs da{};
   da.npz = npz;
-  da.dt = dt; da.dddmp = nl.dddmp; da.d2_bg = nl.d2_bg;
+  da.dt = dt; da.dddmp = nl.dddmp;
   da.hord_mt = nl.hord_mt; da.hord_vt = nl.hord_vt; da.hord_tm = nl.hord_tm; da.hord_dp = nl.hord_dp;
   da.delp = delp.p; da.pt = pt.p; da.w = w.p; da.u = u.p; da.v = v.p;
   da.uc = uc; da.vc = vc; da.ua = ua; da.va = va;
@@ -527,9 +546,17 @@ void Dycore::step() {
   da.ut = S("_ds_ut", npz); da.vt = S("_ds_vt", npz);
   da.fx = S("_ds_fx", npz); da.fy = S("_ds_fy", npz); da.gwx = S("_ds_gwx", npz); da.gwy = S("_ds_gwy", npz);
   da.gtx = S("_ds_gtx", npz); da.gty = S("_ds_gty", npz); da.ke = S("_ds_ke", npz); da.vort = S("_ds_vort", npz);
-  // damping beyond nord = 0 (damp.hip): off in the Held-Suarez namelist
-  da.nord = nl.nord; da.nord_v = nl.nord_v; da.d4_bg = nl.d4_bg; da.vtdm4 = nl.vtdm4; da.d_con = nl.d_con;
-  const bool dcon = nl.d_con > 1e-5, vdamp = nl.vtdm4 > 1e-5;
+  // d_sw's damping (damp.hip): the column of per-level parameters of FV3 dyn_core (the sponge
+  // layers' divergence and w damping at the top in the Held-Suarez namelist)
+  const std::vector<LevelDamp> col = column_damping(nl, c.da_min, c.da_min_c);
+  da.lv = level_table(col);
+  da.hlv = hlevel.data();
+  da.nord = nl.nord; da.d4_bg = nl.d4_bg; da.d_con = nl.d_con;
+  da.ke_dt = nl.ke_bg * std::fabs(dt);
+  const bool dcon = nl.d_con > 1e-5;
+  const bool vdamp = any_level(col.data(), npz, &LevelDamp::vt4);
+  const bool tdamp = vdamp || any_level(col.data(), npz, &LevelDamp::w4) ||
+                     any_level(col.data(), npz, &LevelDamp::dp4) || any_level(col.data(), npz, &LevelDamp::pt4);
   if (nl.nord > 0) {
     da.divg = S("divgd", npz);
     da.dd = S("_dd_dd", npz); da.dvcx = S("_dd_vcx", npz); da.ducy = S("_dd_ucy", npz);
@@ -538,6 +565,10 @@ void Dycore::step() {
   if (nl.nord > 0 || vdamp) da.wk = S("_dd_wk", npz);
   if (vdamp) {
     da.d2 = S("_dd_d2", npz); da.fx2 = S("_dd_fx2", npz); da.fy2 = S("_dd_fy2", npz);
+  }
+  if (tdamp) {
+    da.td2 = S("_dl_d2", npz); da.tfx2 = S("_dl_fx2", npz); da.tfy2 = S("_dl_fy2", npz);
+    da.dw = S("_dl_dw", npz); da.hw = S("_dl_hw", npz);
   }
   if (dcon) {
     // heat source and the dissipation estimate summed over this call's acoustic sub-steps
@@ -581,6 +612,8 @@ void Dycore::step() {
   DswArgs probe{};
   probe.hord_vt = nl.hord_vt; probe.hord_tm = nl.hord_tm; probe.hord_dp = nl.hord_dp;
   probe.delp_o = probe.w_o = probe.pt_o = delp.p;  // (only their presence is tested)
+  probe.npz = npz;
+  probe.hlv = da.hlv;
   const bool tfused = d_sw_thermo_fused(probe);
   Field* alt[3] = {nullptr, nullptr, nullptr};
   Field* cur3[3] = {&delp, &w, &pt};
@@ -617,6 +650,10 @@ void Dycore::step() {
 
   zh_init(c, npz, phis.p, delz.p, zh);  // compute domain: reads no halo
   halo_update({{"u", 'd'}, {"v", 'd'}, {"delp", 'c'}, {"pt", 'c'}, {"w", 'c'}, {"phis", 'c'}, {"zh", 'c'}});
+  // the height planes alternate with _zh_alt (the march writes compute points only): give the
+  // second set the halo ring of the first, so a halo point no exchange fills (the cube-corner
+  // regions) holds the same value whichever set is current -- the in-place update's semantics
+  copy_halo_ring(c, d.nsub * k1, zh, za.zh_out);
   auto acoustic = [&]() {
   for (int it = 0; it < nl.n_split; ++it) {
     const bool last = it == nl.n_split - 1;
@@ -687,7 +724,7 @@ void Dycore::step() {
     halo_update({{"delp", 'c'}, {"pt", 'c'}, {"zh", 'c'}, {"ppe", 'c'}, {"w", 'c'}});
     pk3_pe_halo(c, npz, ptop, last, delp.p, pk3, pe);
     if (fork_substep) HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
-    if (dcon || vdamp) d_sw_post(c, da);  // the new delp and u, v: after both d_sw stages
+    if (d_sw_post_needed(da)) d_sw_post(c, da);  // the new delp and u, v: after both d_sw stages
     nh_p_grad(c, pa);
     if (!last) halo_update({{"u", 'd'}, {"v", 'd'}});
   }
@@ -705,6 +742,7 @@ void Dycore::step() {
     std::vector<double> key = {(double)field_gen, dt, dt2, ptop, (double)fork_substep, (double)tfused,
                                (double)nl.n_split, nl.dddmp, nl.d2_bg, nl.p_fac, nl.dz_min, nl.d4_bg, nl.vtdm4,
                                nl.d_con, (double)nl.nord, (double)nl.nord_v, (double)nl.hord_mt, (double)nl.hord_vt,
+                               (double)nl.n_sponge, nl.d2_bg_k1, nl.d2_bg_k2, nl.ke_bg, (double)nl.do_vort_damp,
                                (double)nl.hord_tm, (double)nl.hord_dp,
                                // launch-shape switches read at every launch (tests flip them in-process)
                                (double)kloop_levels(),
@@ -734,7 +772,14 @@ void Dycore::step() {
     thermo_swap();
   }
   // d_con: the damped kinetic energy, summed over the sub-steps, into the potential temperature
-  if (dcon) damping_heat_apply(c, npz, std::fabs(bdt * nl.delt_max), da.heat, delp.p, delz.p, pt.p);
+  // of the top n_con levels, smoothed first by del2_cubed (FV3 dyn_core "Add dissipative heating")
+  const int n_con = heat_levels(nl);
+  if (dcon && n_con > 0) {
+    halo_update({{"_dd_heat", 'c'}});
+    del2_cubed(c, npz, 0, n_con, std::min(3, nl.nord + 1), 0.2 * c.da_min, da.heat, S("_dd_h2x", npz),
+               S("_dd_h2y", npz));
+    damping_heat_apply(c, npz, n_con, std::fabs(bdt * nl.delt_max), da.heat, delp.p, delz.p, pt.p);
+  }
   HIP_CHECK(hipEventRecord(ev[1], st));
 
   // ---- tracer transport with the accumulated mass fluxes, beside the remap of T_v, delz,

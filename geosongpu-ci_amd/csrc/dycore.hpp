@@ -14,6 +14,7 @@
 #include "grid.hpp"
 #include "halo.hpp"
 #include "kernels.hpp"
+#include "kernels_damp.hpp"
 
 namespace gtfv3 {
 
@@ -82,6 +83,12 @@ class Dycore {
   Field* find(const std::string& name);
   Field& need(const std::string& name, int nk);  // existing field, level count checked
   const double* vertical_dev();                  // ak | bk | dp_ref on device
+  // a column of d_sw parameters on the device (uploaded when it differs from the last one;
+  // the pointer stays valid until the next upload of a longer column)
+  const LevelDamp* level_table(const std::vector<LevelDamp>& t);
+  std::vector<LevelDamp> hlevel;
+  LevelDamp* dlevel = nullptr;
+  size_t dlevel_cap = 0;
   Ctx ctx() const;
   long field_elems(int nk) const { return (long)d.nsub * nk * d.plane; }
 

@@ -52,6 +52,14 @@ struct Namelist {
   int nord = 0, nord_v = 0;
   double d4_bg = 0.0, vtdm4 = 0.0, d_con = 0.0, delt_max = 1.0;
   bool do_vort_damp = false;
+  // sponge layers (FV3 dyn_core's k loop, damp.hip column_damping): with n_sponge >= 0 the top
+  // level takes del-2 divergence damping d2_bg_k1 (and del-2 w damping, d_con 0), the next
+  // two d2_bg_k2 / 0.2 d2_bg_k2 when d2_bg_k2 > 0.01 / 0.05.  FV3's own defaults (4, 2) are
+  // placeholders its documentation says to set; these are the values of the GEOS / pyFV3
+  // test namelists.  ke_bg: background heating of the w damping; convert_ke: heat on every level.
+  int n_sponge = 1;
+  double d2_bg_k1 = 0.20, d2_bg_k2 = 0.10, ke_bg = 0.0;
+  bool convert_ke = false;
   double p_fac = 0.05;               // SIM1 solver pressure floor factor
   double dz_min = 2.0;
   bool fill = true;                  // fillz negative tracers after remap

@@ -2,6 +2,7 @@
 // non-hydrostatic / vertical pieces (nh.hip, remap.hip).
 #pragma once
 #include "kernels.hpp"
+#include "kernels_damp.hpp"
 
 namespace gtfv3 {
 
@@ -20,7 +21,7 @@ int kloop_levels();                                          // GTFV3_KLOOP (ste
 
 struct DswArgs {
   int npz;
-  double dt, dddmp, d2_bg;
+  double dt, dddmp;  // (d2_bg per level: lv[k].d2_divg)
   int hord_mt, hord_vt, hord_tm, hord_dp;
   double *delp, *pt, *w, *u, *v;      // updated in place (u, v left multiplied by dx, dy)
   // optional: delp, pt, w updated into these (fused thermo march, d_sw_thermo_fused) --
@@ -31,13 +32,20 @@ struct DswArgs {
   double *cx, *cy, *mfx, *mfy;        // accumulated
   double *ut, *vt, *fx, *fy, *gwx, *gwy, *gtx, *gty, *ke, *vort;  // scratch
   double *gvx, *gvy;  // vorticity fluxes (own planes: the wind stage may run beside the thermo stage)
-  // damping beyond nord = 0 (damp.hip; all off in the Held-Suarez namelist)
-  int nord = 0, nord_v = 0;
-  double d4_bg = 0.0, vtdm4 = 0.0, d_con = 0.0;
+  // damping (damp.hip): the column of per-level parameters (column_damping; device table lv,
+  // its host copy hlv, npz entries each) -- required -- and the namelist-wide switches
+  const LevelDamp* lv = nullptr;
+  const LevelDamp* hlv = nullptr;
+  int nord = 0;         // the namelist nord (c_sw's divg exists when > 0)
+  double d4_bg = 0.0;
+  double d_con = 0.0;   // the namelist d_con: > 1e-5 sums the heat / diss_est of every level
+  double ke_dt = 0.0;   // ke_bg |dt| (the w damping's background heat)
   const double* divg = nullptr;  // nord > 0: c_sw's corner divergence, halo exchanged
   double *wk = nullptr, *vd = nullptr;  // cell vorticity; the corner damping term (d_con)
   double *dd = nullptr, *dvcx = nullptr, *ducy = nullptr, *dvort = nullptr, *dqx = nullptr, *dqy = nullptr;
-  double *d2 = nullptr, *fx2 = nullptr, *fy2 = nullptr;  // vorticity damping
+  double *d2 = nullptr, *fx2 = nullptr, *fy2 = nullptr;  // vorticity damping (winds stage)
+  // del-n of delp / pt / w (thermo stage): scratch, the w increment and its heat
+  double *td2 = nullptr, *tfx2 = nullptr, *tfy2 = nullptr, *dw = nullptr, *hw = nullptr;
   double *heat = nullptr, *diss = nullptr;               // d_con: summed over the sub-steps
 };
 void d_sw(const Ctx& c, const DswArgs& a);  // the three stages in order
@@ -46,6 +54,7 @@ void d_sw_thermo(const Ctx& c, const DswArgs& a);   // delp / w / pt transport, 
 void d_sw_winds(const Ctx& c, const DswArgs& a);    // kinetic energy, vorticity transport, u, v
 // after both stages (needs the updated delp): d_con heat / diss_est, vorticity-damping fluxes
 void d_sw_post(const Ctx& c, const DswArgs& a);
+bool d_sw_post_needed(const DswArgs& a);
 bool d_sw_thermo_fused(const DswArgs& a);           // delp/w/pt go to *_o (one march)
 
 }  // namespace gtfv3

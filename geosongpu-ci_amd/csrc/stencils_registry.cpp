@@ -90,6 +90,7 @@ std::map<std::string, Fn>& reg() {
        }},
       // d_sw(delp, pt, w, u, v, uc, vc, ua, va | crx, cry, xfx, yfx, cx, cy, mfx, mfy, ke)
       // params: dt, dddmp, d2_bg, hord_mt, hord_vt, hord_tm, hord_dp[, fused thermo march]
+      // (no sponge layers: d2_bg on every level, nord = 0, no other damping)
       {"d_sw",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
          need(f, 18, "d_sw");
@@ -98,7 +99,14 @@ std::map<std::string, Fn>& reg() {
          auto scr = [&](const char* n) { return dy.field(n, npz).p; };
          DswArgs a{};
          a.npz = npz;
-         a.dt = p.at(0); a.dddmp = p.at(1); a.d2_bg = p.at(2);
+         a.dt = p.at(0); a.dddmp = p.at(1);
+         {
+           Namelist nl{};
+           nl.npz = npz; nl.d2_bg = p.at(2); nl.n_sponge = -1;
+           const std::vector<LevelDamp> col = column_damping(nl, dy.ctx().da_min, dy.ctx().da_min_c);
+           a.lv = dy.level_table(col);
+           a.hlv = dy.hlevel.data();
+         }
          a.hord_mt = (int)p.at(3); a.hord_vt = (int)p.at(4); a.hord_tm = (int)p.at(5); a.hord_dp = (int)p.at(6);
          a.delp = F(dy, f[0]).p; a.pt = F(dy, f[1]).p; a.w = F(dy, f[2]).p; a.u = F(dy, f[3]).p; a.v = F(dy, f[4]).p;
          a.uc = F(dy, f[5]).p; a.vc = F(dy, f[6]).p; a.ua = F(dy, f[7]).p; a.va = F(dy, f[8]).p;
@@ -134,10 +142,12 @@ std::map<std::string, Fn>& reg() {
          divergence_corner(dy.ctx(), npz, F(dy, f[0]).p, F(dy, f[1]).p, F(dy, f[2]).p, F(dy, f[3]).p,
                            dy.field(f[4], npz).p);
        }},
-      // d_sw_damped(the 18 d_sw fields, divg, heat, diss): d_sw (fused thermo march) with the
-      // damping options, then d_sw_post (d_con heat / diss += and the vorticity-damping
-      // fluxes).  params: dt, dddmp, d2_bg, hord_mt, hord_vt, hord_tm, hord_dp, nord, d4_bg,
-      // vtdm4, nord_v, d_con
+      // d_sw_damped(the 18 d_sw fields, divg, heat, diss): d_sw (fused thermo march unless
+      // delp / pt take del-n damping) with the column of damping parameters of the namelist
+      // below (damp.hip column_damping), then d_sw_post (d_con heat / diss += and the
+      // vorticity-damping fluxes).  params: dt, dddmp, d2_bg, hord_mt, hord_vt, hord_tm, hord_dp,
+      // nord, d4_bg, vtdm4, nord_v, d_con[, do_vort_damp (1), n_sponge (-1: none), d2_bg_k1,
+      // d2_bg_k2, ke_bg]
       {"d_sw_damped",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
          need(f, 21, "d_sw_damped");
@@ -147,10 +157,23 @@ std::map<std::string, Fn>& reg() {
          auto scr = [&](const char* n) { return dy.field(n, npz).p; };
          DswArgs a{};
          a.npz = npz;
-         a.dt = p[0]; a.dddmp = p[1]; a.d2_bg = p[2];
+         a.dt = p[0]; a.dddmp = p[1];
          a.hord_mt = (int)p[3]; a.hord_vt = (int)p[4]; a.hord_tm = (int)p[5]; a.hord_dp = (int)p[6];
-         a.nord = (int)p[7]; a.d4_bg = p[8]; a.vtdm4 = p[9]; a.nord_v = (int)p[10]; a.d_con = p[11];
-         if (a.nord < 0 || a.nord > 3 || a.nord_v < 0 || a.nord_v > 2) throw std::runtime_error("d_sw_damped: nord");
+         Namelist nl{};
+         nl.npz = npz;
+         nl.d2_bg = p[2]; nl.nord = (int)p[7]; nl.d4_bg = p[8]; nl.vtdm4 = p[9]; nl.nord_v = (int)p[10];
+         nl.d_con = p[11];
+         nl.do_vort_damp = p.size() > 12 ? p[12] != 0.0 : true;
+         nl.n_sponge = p.size() > 13 ? (int)p[13] : -1;
+         nl.d2_bg_k1 = p.size() > 14 ? p[14] : 0.0;
+         nl.d2_bg_k2 = p.size() > 15 ? p[15] : 0.0;
+         nl.ke_bg = p.size() > 16 ? p[16] : 0.0;
+         if (nl.nord < 0 || nl.nord > 3 || nl.nord_v < 0 || nl.nord_v > 2) throw std::runtime_error("d_sw_damped: nord");
+         const std::vector<LevelDamp> col = column_damping(nl, dy.ctx().da_min, dy.ctx().da_min_c);
+         a.lv = dy.level_table(col);
+         a.hlv = dy.hlevel.data();
+         a.nord = nl.nord; a.d4_bg = nl.d4_bg; a.d_con = nl.d_con;
+         a.ke_dt = nl.ke_bg * std::fabs(a.dt);
          a.delp = F(dy, f[0]).p; a.pt = F(dy, f[1]).p; a.w = F(dy, f[2]).p; a.u = F(dy, f[3]).p; a.v = F(dy, f[4]).p;
          a.uc = F(dy, f[5]).p; a.vc = F(dy, f[6]).p; a.ua = F(dy, f[7]).p; a.va = F(dy, f[8]).p;
          a.crx = out(9); a.cry = out(10); a.xfx = out(11); a.yfx = out(12);
@@ -165,6 +188,8 @@ std::map<std::string, Fn>& reg() {
          a.dd = scr("_dd_dd"); a.dvcx = scr("_dd_vcx"); a.ducy = scr("_dd_ucy"); a.dvort = scr("_dd_vort");
          a.dqx = scr("_dd_qx"); a.dqy = scr("_dd_qy");
          a.d2 = scr("_dd_d2"); a.fx2 = scr("_dd_fx2"); a.fy2 = scr("_dd_fy2");
+         a.td2 = scr("_dl_d2"); a.tfx2 = scr("_dl_fx2"); a.tfy2 = scr("_dl_fy2"); a.dw = scr("_dl_dw");
+         a.hw = scr("_dl_hw");
          a.delp_o = scr("_ds_delp_o"); a.w_o = scr("_ds_w_o"); a.pt_o = scr("_ds_pt_o");
          const long n = dy.field_elems(npz);
          copy_levels(dy.ctx(), n, a.delp, a.delp_o);

@@ -564,12 +564,14 @@ __global__ void __launch_bounds__(256) ds_thermo(Dims d, const SubInfo* __restri
 // unconditionally before any arithmetic, so a wave has ~45 loads in flight at once instead of
 // ~15 dependent round trips through branches (rocprof SQ counters: ds_ke waited 63 % of its
 // wave cycles).  Tile-edge inputs (vt / ut stencils, dx / dy for the edge PPM forms, sin1-4)
-// are loaded only by the waves holding such points.  hord_mt and nord = 0 are template
-// constants.
+// are loaded only by the waves holding such points.  hord_mt and "some level has nord = 0"
+// are template constants; the level's own parameters (nord, d2_divg: the sponge layers') come
+// from the column table lv, one value per wave.
 template <int ORD, bool DAMP>
 __global__ void __launch_bounds__(256) ds_ke_ld(Dims d, const SubInfo* __restrict__ subs,
                                                 const double* __restrict__ M, int npz, double dt, double dddmp,
-                                                double d2_bg, double da_min_c, const double* __restrict__ u,
+                                                const LevelDamp* __restrict__ lv, double da_min_c,
+                                                const double* __restrict__ u,
                                                 const double* __restrict__ v, const double* __restrict__ uc,
                                                 const double* __restrict__ vc, const double* __restrict__ ua,
                                                 const double* __restrict__ va, const double* __restrict__ ut,
@@ -580,6 +582,8 @@ __global__ void __launch_bounds__(256) ds_ke_ld(Dims d, const SubInfo* __restric
   const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
   const long p = d.pitch;
   const double dt5 = 0.5 * dt, dt4 = 0.25 * dt;
+  const int kl = z - s * npz;
+  const bool dmp = DAMP && lv[kl].nord == 0;  // nord = 0 divergence damping at this level
   const int Ilo = max(1, io), Ihi = min(N - 1, io + nx), Jlo = max(1, jo), Jhi = min(N - 1, jo + ny);
   const bool inner = I >= Ilo && I <= Ihi && J >= Jlo && J <= Jhi;
   const bool xe = !(I - 1 >= 2 && I + 1 <= N - 2), ye = !(J - 1 >= 2 && J + 1 <= N - 2);
@@ -599,7 +603,7 @@ __global__ void __launch_bounds__(256) ds_ke_ld(Dims d, const SubInfo* __restric
   const double rdym = rdy[-p], rdy0 = rdy[0], rdxm = rdx[-1], rdx0 = rdx[0];
   double dycm = 0, dyc0 = 0, vamm = 0, vam0 = 0, va0m = 0, va00 = 0, cvm = 0, cv0 = 0, svm = 0, sv0 = 0;
   double dxcm = 0, dxc0 = 0, uamm = 0, ua0m = 0, uam0 = 0, ua00 = 0, cum = 0, cu0 = 0, sum_ = 0, su0 = 0, rac = 0;
-  if (DAMP) {
+  if (dmp) {
     const double* dyc = MT(M_DYC) + o;
     const double* dxc = MT(M_DXC) + o;
     const double* cav = MT(M_COSA_V) + o;
@@ -632,7 +636,7 @@ __global__ void __launch_bounds__(256) ds_ke_ld(Dims d, const SubInfo* __restric
       spy[m] = ye ? dy[(long)(m - 3) * p] : 0.0;
       spx[m] = xe ? dxm[m - 3] : 0.0;
     }
-    if (DAMP) {
+    if (dmp) {
       const double* s4 = MT(M_SIN4) + o;
       const double* s2 = MT(M_SIN2) + o;
       const double* s3 = MT(M_SIN3) + o;
@@ -665,7 +669,7 @@ __global__ void __launch_bounds__(256) ds_ke_ld(Dims d, const SubInfo* __restric
     kk = dt6 * ((uts[2] + uts[1]) * qu[2] + (vts[2] + vts[1]) * qv[2] + (uts[1] + vts[1]) * qu[3]);
   else if (I == 0 && J == N)
     kk = dt6 * ((uts[2] + uts[1]) * qu[3] + (vts[2] + vts[1]) * qv[2] + (uts[1] - vts[2]) * qu[2]);
-  if (!DAMP) {
+  if (!dmp) {
     AT(ke, 0, 0) = kk;
     return;
   }
@@ -690,7 +694,7 @@ __global__ void __launch_bounds__(256) ds_ke_ld(Dims d, const SubInfo* __restric
   if ((I == 0 && J == 0) || (I == N && J == 0)) dpc = dpc - vS;
   if ((I == N && J == N) || (I == 0 && J == N)) dpc = dpc + v0;
   dpc = rac * dpc;
-  double damp = da_min_c * fmax(d2_bg, fmin(0.20, dddmp * fabs(dpc * dt)));
+  double damp = da_min_c * fmax(lv[kl].d2_divg, fmin(0.20, dddmp * fabs(dpc * dt)));
   AT(ke, 0, 0) = kk + damp * dpc;
   if (vd) AT(vd, 0, 0) = damp * dpc;
 }
@@ -776,7 +780,9 @@ bool d_sw_thermo_fused(const DswArgs& a) {
     const char* e = getenv("GTFV3_THERMO_FUSED");
     return !(e && e[0] == '0');
   }();
-  return on && a.delp_o && a.w_o && a.pt_o && a.hord_dp == a.hord_vt && a.hord_vt == a.hord_tm;
+  // the march carries no del-n flux damping of delp / pt: levels with it take the separate launches
+  const bool deln = a.hlv && (any_level(a.hlv, a.npz, &LevelDamp::dp4) || any_level(a.hlv, a.npz, &LevelDamp::pt4));
+  return on && !deln && a.delp_o && a.w_o && a.pt_o && a.hord_dp == a.hord_vt && a.hord_vt == a.hord_tm;
 }
 
 void d_sw_courant(const Ctx& c, const DswArgs& a) {
@@ -812,9 +818,35 @@ static TpArgs d_sw_tp(const DswArgs& a) {
   return t;
 }
 
+// d_sw's w damping (non-hydrostatic, before w's transport) on the levels that have it: the
+// increment dw of w's del-(2 nord_w + 2) fluxes and its heat hw.  fused0: the nord_w = 0 runs
+// are left to d_sw_w_damping_add (one pass after the fused march, from the old w it leaves)
+static void d_sw_w_damping(const Ctx& c, const DswArgs& a, bool fused0) {
+  level_runs(a.hlv, a.npz, [](const LevelDamp& l) { return l.w4 > 0.0 ? l.nord_w : -1; },
+             [&](int k0, int nk, int nord) {
+               if (fused0 && nord == 0) return;
+               deln_fluxes(c, a.npz, k0, nk, nord, a.lv, DL_W4, a.w, a.td2, a.tfx2, a.tfy2);
+               w_damping(c, a.npz, k0, nk, a.ke_dt, a.tfx2, a.tfy2, a.w, a.dw, a.hw);
+             });
+}
+
+// w = w / delp + dw (after the transport's update, into w_new)
+static void d_sw_w_damping_add(const Ctx& c, const DswArgs& a, double* w_new, bool fused0) {
+  level_runs(a.hlv, a.npz, [](const LevelDamp& l) { return l.w4 > 0.0 ? l.nord_w : -1; },
+             [&](int k0, int nk, int nord) {
+               if (fused0 && nord == 0)
+                 w_damping0_fused(c, a.npz, k0, nk, a.lv, a.ke_dt, a.w, w_new, a.d_con > 1e-5 ? a.hw : nullptr);
+               else
+                 w_damping_add(c, a.npz, k0, nk, a.dw, w_new);
+             });
+}
+
 void d_sw_thermo(const Ctx& c, const DswArgs& a) {
   const Dims& d = c.d;
-  if (d_sw_thermo_fused(a)) {
+  if (!a.lv || !a.hlv) throw std::runtime_error("d_sw: the column damping table is required");
+  const bool fused = d_sw_thermo_fused(a);
+  d_sw_w_damping(c, a, fused);
+  if (fused) {
     ThermoArgs t{};
     t.npz = a.npz;
     t.ord = a.hord_dp;
@@ -823,14 +855,21 @@ void d_sw_thermo(const Ctx& c, const DswArgs& a) {
     t.crx = a.crx; t.cry = a.cry; t.xfx = a.xfx; t.yfx = a.yfx;
     t.mfx = a.mfx; t.mfy = a.mfy;
     d_sw_thermo_march(c, t);
+    d_sw_w_damping_add(c, a, a.w_o, true);
     return;
   }
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   TpArgs t = d_sw_tp(a);
-  // mass fluxes
+  // mass fluxes, with delp's del-(2 nord_v + 2) diffusive fluxes where damp_vt > 1e-4
+  // (fv_tp_2d(delp, ..., nord = nord_v, damp_c = damp_vt))
   t.q = a.delp; t.mfx = nullptr; t.mfy = nullptr; t.fx = a.fx; t.fy = a.fy; t.ord = a.hord_dp;
   fv_tp_2d(c, t);
+  level_runs(a.hlv, a.npz, [](const LevelDamp& l) { return l.dp4 > 0.0 ? l.nord_v : -1; },
+             [&](int k0, int nk, int nord) {
+               deln_fluxes(c, a.npz, k0, nk, nord, a.lv, DL_DP4, a.delp, a.td2, a.tfx2, a.tfy2);
+               deln_add(c, a.npz, k0, nk, a.lv, a.tfx2, a.tfy2, nullptr, a.fx, a.fy);
+             });
   GT_LAUNCH(ds_accum, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, a.npz, a.crx, a.cry, a.fx, a.fy,
                      a.cx, a.cy, a.mfx, a.mfy);
   HIP_LAUNCH_CHECK();
@@ -850,29 +889,39 @@ void d_sw_thermo(const Ctx& c, const DswArgs& a) {
     t.q = a.pt; t.fx = a.gtx; t.fy = a.gty; t.ord = a.hord_tm;
     fv_tp_2d(c, t);
   }
+  // pt's mass-weighted del-(2 nord_t + 2) fluxes where damp_t > 1e-4 (fv_tp_2d(pt, ..., mass =
+  // delp, nord = nord_t, damp_c = damp_t))
+  level_runs(a.hlv, a.npz, [](const LevelDamp& l) { return l.pt4 > 0.0 ? l.nord_t : -1; },
+             [&](int k0, int nk, int nord) {
+               deln_fluxes(c, a.npz, k0, nk, nord, a.lv, DL_ONE, a.pt, a.td2, a.tfx2, a.tfy2);
+               deln_add(c, a.npz, k0, nk, a.lv, a.tfx2, a.tfy2, a.delp, a.gtx, a.gty);
+             });
   Launch2D Li{0, 0, d.nx, d.ny};
   GT_LAUNCH(ds_thermo, g2(d, Li, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.fx, a.fy, a.gwx,
                      a.gwy, a.gtx, a.gty, a.delp, a.pt, a.w);
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (6 * e.C + 3 * e.X + 3 * e.Y) + e.C);
+  d_sw_w_damping_add(c, a, a.w, false);
 }
 
 void d_sw_winds(const Ctx& c, const DswArgs& a) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
+  if (!a.lv || !a.hlv) throw std::runtime_error("d_sw: the column damping table is required");
   // kinetic energy (+ divergence damping) at corners
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
-  const bool dcon = a.d_con > 1e-5, vdamp = a.vtdm4 > 1e-5;
+  const bool dcon = a.d_con > 1e-5, vdamp = any_level(a.hlv, a.npz, &LevelDamp::vt4);
+  bool nord0 = false, nordn = false;  // some level with nord = 0 / nord > 0
+  for (int k = 0; k < a.npz; ++k) (a.hlv[k].nord == 0 ? nord0 : nordn) = true;
   {
-    const bool damp = a.nord == 0;
     double* vdp = dcon ? a.vd : nullptr;
 #define KE_LD(O, D)                                                                                          \
   GT_LAUNCH_N("ds_ke", (ds_ke_ld<O, D>), g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, \
-              a.dddmp, a.d2_bg, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke, vdp)
+              a.dddmp, a.lv, c.da_min_c, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.ke, vdp)
     if (a.hord_mt == 5) {
-      if (damp) KE_LD(5, true); else KE_LD(5, false);
+      if (nord0) KE_LD(5, true); else KE_LD(5, false);
     } else {
-      if (damp) KE_LD(6, true); else KE_LD(6, false);
+      if (nord0) KE_LD(6, true); else KE_LD(6, false);
     }
 #undef KE_LD
   }
@@ -881,17 +930,19 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
   const double L = a.npz;
   gt_bytes(L * (2 * e.C + 3 * e.X + 3 * e.Y + e.K) + 17 * e.C);
   // damping beyond nord = 0 (damp.hip), from the old winds' cell vorticity
-  if (a.nord > 0 || vdamp) vorticity_wk(c, a.npz, a.u, a.v, a.wk);
-  if (a.nord > 0) {
+  if (nordn && !a.divg) throw std::runtime_error("d_sw: nord > 0 needs c_sw's corner divergence");
+  if (nordn || vdamp) vorticity_wk(c, a.npz, a.u, a.v, a.wk);
+  if (nordn) {
     DampArgs da{};
     da.npz = a.npz; da.nord = a.nord;
-    da.dt = a.dt; da.dddmp = a.dddmp; da.d2_bg = a.d2_bg; da.d4_bg = a.d4_bg;
+    da.dt = a.dt; da.dddmp = a.dddmp; da.d4_bg = a.d4_bg; da.lv = a.lv;
     da.divg = a.divg; da.wk = a.wk; da.ke = a.ke; da.vd = a.vd;
     da.dd = a.dd; da.vcx = a.dvcx; da.ucy = a.ducy; da.vort = a.dvort; da.qx = a.dqx; da.qy = a.dqy;
     divergence_damping(c, da);
   }
-  if (vdamp) del6_vt_flux(c, a.npz, a.nord_v, std::pow(a.vtdm4 * c.da_min_c, (double)(a.nord_v + 1)), a.wk, a.d2,
-                          a.fx2, a.fy2);
+  // vorticity damping fluxes (del6_vt_flux) on the levels that have it
+  level_runs(a.hlv, a.npz, [](const LevelDamp& l) { return l.vt4 > 0.0 ? l.nord_v : -1; },
+             [&](int k0, int nk, int nord) { deln_fluxes(c, a.npz, k0, nk, nord, a.lv, DL_VT4, a.wk, a.d2, a.fx2, a.fy2); });
   // vorticity transport
   Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
   GT_LAUNCH(ds_vort, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.vort);
@@ -908,12 +959,16 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
   fv_tp_2d(c, t);
 }
 
+bool d_sw_post_needed(const DswArgs& a) {
+  return a.d_con > 1e-5 || (a.hlv && any_level(a.hlv, a.npz, &LevelDamp::vt4));
+}
+
 void d_sw_post(const Ctx& c, const DswArgs& a) {
-  const bool vdamp = a.vtdm4 > 1e-5;
+  const bool vdamp = any_level(a.hlv, a.npz, &LevelDamp::vt4);
   if (a.d_con > 1e-5)
-    damping_heat(c, a.npz, a.d_con, a.u, a.v, a.vd, vdamp ? a.fx2 : nullptr, vdamp ? a.fy2 : nullptr, a.delp,
-                 a.heat, a.diss);
-  if (vdamp) vorticity_damping_apply(c, a.npz, a.fx2, a.fy2, a.u, a.v);
+    damping_heat(c, a.npz, a.lv, a.u, a.v, a.vd, a.fx2, a.fy2,
+                 any_level(a.hlv, a.npz, &LevelDamp::w4) ? a.hw : nullptr, a.delp, a.heat, a.diss);
+  if (vdamp) vorticity_damping_apply(c, a.npz, a.lv, a.fx2, a.fy2, a.u, a.v);
 }
 
 void d_sw(const Ctx& c, const DswArgs& a) {

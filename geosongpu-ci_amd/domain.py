@@ -85,6 +85,16 @@ class Domain:
         check(lib().gtfv3_get_scalars(self.h, dptr(out)))
         return dict(da_min=out[0], da_min_c=out[1], corner_w=out[2:].reshape(self.nsub, 4, 3))
 
+    def level_damping(self):
+        """the namelist's column of d_sw damping parameters (damp.hip column_damping): a list of
+        per-level dicts and n_con, the number of top levels the d_con heat reaches"""
+        out = np.zeros((self.npz, 10))
+        n_con = lib().gtfv3_level_damping(self.h, dptr(out), self.npz)
+        if n_con < 0:
+            check(n_con)
+        keys = ("d2_divg", "vt4", "dp4", "w4", "pt4", "d_con", "nord", "nord_v", "nord_w", "nord_t")
+        return [dict(zip(keys, row)) for row in out], n_con
+
     # ---- fields ----
     def create(self, name, nk):
         check(lib().gtfv3_field_create(self.h, name.encode(), nk))

@@ -55,6 +55,11 @@ int gtfv3_get_metric(void* h, const char* name, double* out);
 /* corner points xyz [nsub][ny+2*NG+3][nx+2*NG+3][3] and scalars da_min, da_min_c */
 int gtfv3_get_xyz(void* h, double* out);
 int gtfv3_get_scalars(void* h, double* out);
+/* the column of d_sw damping parameters of the namelist (FV3 dyn_core's k loop, sponge layers
+ * included): 10 doubles per level {d2_divg, vt4, dp4, w4, pt4, d_con, nord, nord_v, nord_w,
+ * nord_t} (the coefficients as (damp * da_min[_c])^(n+1), 0 where the branch is off; written
+ * when cap >= npz); returns n_con, the number of top levels the d_con heat reaches. */
+int gtfv3_level_damping(void* h, double* out, int cap);
 
 /* host copy of the same-rank halo table of a kind (0 cell, 1 corner, 2 D-grid, 3 C-grid,
  * 4 A-grid, 5 C-grid tile-edge sync, 6 = 5 then 3 as one exchange): 6 ints per entry

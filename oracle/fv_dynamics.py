@@ -19,6 +19,7 @@ import numpy as np
 
 from . import NG
 from . import fv_mapz, nh_core, sw_core, tp_core
+from . import grid as og
 from .halo import Layout, fill_scalar, fill_vector, sync_edges
 from .util import Plane, sh
 
@@ -33,18 +34,60 @@ ZVIR = (8314.47 / 18.015) / (8314.47 / 28.965) - 1.0
 class Grid:
     """Everything the oracle needs about the decomposition and metrics."""
 
-    def __init__(self, N, lx, ly, ms, corner_w, da_min_c, nj, pitch):
+    def __init__(self, N, lx, ly, ms, corner_w, da_min_c, nj, pitch, da_min=None):
         self.layout = Layout(N, lx, ly)
         self.subs = self.layout.subs()
         self.nx, self.ny = self.layout.nx, self.layout.ny
         self.ms = ms
         self.corner_w = corner_w
         self.da_min_c = da_min_c
+        # the smallest cell area (fv_tp_2d's del-n damping, del2_cubed): the oracle grid's own
+        self.da_min = og.min_areas(N)[0] if da_min is None else da_min
         self.P = [Plane(s, self.nx, self.ny, nj, pitch) for s in self.subs]
 
     @property
     def nsub(self):
         return len(self.subs)
+
+
+SPONGE_DEFAULTS = dict(n_sponge=1, d2_bg_k1=0.20, d2_bg_k2=0.10)
+
+
+def sponge_defaults(nl):
+    """the sponge keys of nl with the product's Namelist defaults (gtfv3.hpp)"""
+    return {k: type(v)(nl.get(k, v)) for k, v in SPONGE_DEFAULTS.items()}
+
+
+def level_groups(cols):
+    """contiguous runs of levels with equal d_sw parameters: [(k0, k1, params)]"""
+    out = []
+    for k, c in enumerate(cols):
+        if out and out[-1][2] == c:
+            out[-1] = (out[-1][0], k + 1, c)
+        else:
+            out.append((k, k + 1, c))
+    return out
+
+
+def d_sw_levels(st, s, sub, m, nx, ny, dt, ords, dddmp, groups, da_min_c, da_min, d4_bg=0.0, ke_bg=0.0, divg_d=None,
+                corner_w=None):
+    """sw_core.d_sw over the whole column of sub-domain s of the state dict st, one call per run
+    of levels with equal parameters (groups from level_groups), outputs joined along the level
+    axis; heat / diss are zero on the levels that make none"""
+    parts = []
+    for k0, k1, c in groups:
+        ks = slice(k0, k1)
+        parts.append(sw_core.d_sw(
+            st["delp"][s, ks], st["pt"][s, ks], st["u"][s, ks], st["v"][s, ks], st["w"][s, ks], st["uc"][s, ks],
+            st["vc"][s, ks], st["ua"][s, ks], st["va"][s, ks], sub, m, nx, ny, dt, ords, dddmp, c["d2_divg"], da_min_c,
+            nord=c["nord"], d4_bg=d4_bg, divg_d=divg_d[ks] if c["nord"] > 0 else None, vtdm4=c["damp_vt"],
+            nord_v=c["nord_v"], d_con=c["d_con"], corner_w=corner_w, damp_w=c["damp_w"], nord_w=c["nord_w"],
+            damp_t=c["damp_t"], nord_t=c["nord_t"], ke_bg=ke_bg, da_min=da_min))
+    r = {name: np.concatenate([p[name] for p in parts])
+         for name in ("delp", "pt", "w", "u", "v", "crx", "cry", "xfx", "yfx", "fx", "fy", "ke")}
+    for name in ("heat", "diss"):
+        r[name] = np.concatenate([p[name] if name in p else np.zeros_like(p["delp"]) for p in parts])
+    return r
 
 
 def _halo(g, st, items):
@@ -138,10 +181,15 @@ def fv_dynamics(st, ak, bk, g, nl):
     _halo(g, st, [("zh", "c")])
     ords = (nl["hord_mt"], nl["hord_vt"], nl["hord_tm"], nl["hord_dp"])
     nord, d_con = int(nl.get("nord", 0)), float(nl.get("d_con", 0.0))
-    # fv_core_nml: nord_v = min(2, nord) unless given; vtdm4 only with do_vort_damp
-    vtdm4 = float(nl.get("vtdm4", 0.0)) if nl.get("do_vort_damp", 0) else 0.0
-    damp_kw = dict(nord=nord, d4_bg=float(nl.get("d4_bg", 0.0)), vtdm4=vtdm4,
-                   nord_v=int(nl.get("nord_v", min(2, nord))), d_con=d_con)
+    # FV3 dyn_core's per-level d_sw parameters (sw_core.column_namelist): nord_v = min(2, nord)
+    # unless given, vtdm4 acts only with do_vort_damp, the sponge-layer overrides in the top
+    # levels (the product's Namelist defaults: n_sponge 1, d2_bg_k1 0.2, d2_bg_k2 0.1)
+    sp = sponge_defaults(nl)
+    cols = sw_core.column_namelist(npz, nord=nord, d2_bg=nl["d2_bg"], vtdm4=float(nl.get("vtdm4", 0.0)),
+                                   do_vort_damp=bool(nl.get("do_vort_damp", 0)), nord_v=nl.get("nord_v"),
+                                   d_con=d_con, **sp)
+    groups = level_groups(cols)
+    d4_bg, ke_bg = float(nl.get("d4_bg", 0.0)), float(nl.get("ke_bg", 0.0))
     if nord > 0:
         st["divgd"] = np.zeros(shp)
     if d_con > 1e-5:
@@ -174,10 +222,8 @@ def fv_dynamics(st, ak, bk, g, nl):
         ds = []
         for s in range(nsub):
             m, sub, P = g.ms[s], g.subs[s], g.P[s]
-            r = sw_core.d_sw(st["delp"][s], st["pt"][s], st["u"][s], st["v"][s], st["w"][s], st["uc"][s],
-                             st["vc"][s], st["ua"][s], st["va"][s], sub, m, nx, ny, dt, ords, nl["dddmp"],
-                             nl["d2_bg"], g.da_min_c, divg_d=st["divgd"][s] if nord > 0 else None,
-                             corner_w=g.corner_w[s], **damp_kw)
+            r = d_sw_levels(st, s, sub, m, nx, ny, dt, ords, nl["dddmp"], groups, g.da_min_c, g.da_min, d4_bg, ke_bg,
+                            st["divgd"][s] if nord > 0 else None, g.corner_w[s])
             for name in ("delp", "pt", "w", "u", "v"):
                 st[name][s] = r[name]
             if d_con > 1e-5:
@@ -220,22 +266,31 @@ def fv_dynamics(st, ak, bk, g, nl):
             _halo(g, st, [("u", "d"), ("v", "d")])
 
     # ---- d_con: the kinetic energy the damping removed, as heat (dyn_core after the acoustic
-    # loop): dT = heat / (cp delp), limited to delt_max * bdt per call (0.1x / 0.5x in the top
+    # loop, "Add dissipative heating"), on the top n_con levels (sw_core.heat_levels): the heat
+    # source's halo filled, smoothed by del2_cubed (min(3, nord + 1) passes, 0.2 da_min), then
+    # dT = heat / (cv_air delp), limited to delt_max * bdt per call (0.1x / 0.5x in the top
     # two layers), added to the potential temperature through pkz ----
-    if d_con > 1e-5:
-        cp = RDGAS / KAPPA
+    n_con = sw_core.heat_levels(npz, float(nl.get("vtdm4", 0.0)), sp["d2_bg_k1"], sp["d2_bg_k2"],
+                                bool(nl.get("convert_ke", 0)))
+    if d_con > 1e-5 and n_con > 0:
+        fill_scalar(heat, g.layout, "cell")
+        for s in range(nsub):
+            heat[s, :n_con] = sw_core.del2_cubed(heat[s, :n_con], 0.2 * g.da_min, g.subs[s], g.ms[s], nx, ny,
+                                                 min(3, nord + 1))
+        cv = RDGAS / KAPPA - RDGAS
         k1k = KAPPA / (1.0 - KAPPA)
         delt = abs(bdt * float(nl.get("delt_max", 1.0)))
-        lim = np.full(npz, delt)
+        lim = np.full(n_con, delt)
         lim[0] = 0.1 * delt
-        if npz > 1:
+        if n_con > 1:
             lim[1] = 0.5 * delt
         lim = lim[:, None, None]
+        kc = slice(0, n_con)
         for s in range(nsub):
-            pkz = np.exp(k1k * np.log(rdg * st["delp"][s] / st["delz"][s] * st["pt"][s]))
-            dtmp = heat[s] / (cp * st["delp"][s])
-            st["pt"][s] = np.where(comp[s], st["pt"][s] + np.sign(dtmp) * np.minimum(lim, np.abs(dtmp)) / pkz,
-                                   st["pt"][s])
+            dp, pt = st["delp"][s, kc], st["pt"][s, kc]
+            pkz = np.exp(k1k * np.log(rdg * dp / st["delz"][s, kc] * pt))
+            dtmp = heat[s, kc] / (cv * dp)
+            st["pt"][s, kc] = np.where(comp[s], pt + np.sign(dtmp) * np.minimum(lim, np.abs(dtmp)) / pkz, pt)
 
     # ---- tracer transport ----
     st["q"], nsplt = tp_core.tracer_2d_1l(st["q"], st["dp1"], st["mfx"], st["mfy"], st["cx"], st["cy"], g.subs,

@@ -1,8 +1,11 @@
 """Oracle: FV3 sw_core — c_sw (with d2a2c_vect and, for nord > 0, divergence_corner) and
 d_sw (divergence damping nord = 0 .. 3 with the del-2 Smagorinsky-type coefficient, del-2n
-vorticity damping vtdm4 / nord_v, the d_con conversion of the damped kinetic energy into heat
-and the dissipation estimate diss_est; no w damping, no sponge-level overrides) in fp64 numpy.
-TEST INFRASTRUCTURE ONLY.
+vorticity damping damp_vt / nord_v, the del-n mass-flux damping of delp (damp_vt / nord_v) and
+the mass-weighted del-n damping of pt (damp_t / nord_t) inside fv_tp_2d (tp_core deln_flux),
+the w damping (damp_w / nord_w) with its heat, the d_con conversion of the damped kinetic
+energy into heat and the dissipation estimate diss_est) in fp64 numpy, with the per-level
+parameters of FV3 dyn_core's k loop -- the sponge-layer overrides in the top three levels
+included (column_namelist).  TEST INFRASTRUCTURE ONLY.
 
 Restated from the FV3 C-D grid shallow-water solver (Lin & Rood 1997; Harris &
 Lin 2013; FV3 sw_core.F90 structure).  Fortran 1-based indices f are written
@@ -313,19 +316,77 @@ def d_sw_ut_vt(uc, vc, P, m, dt):
     return ut, vt
 
 
+def column_namelist(npz, nord=0, d2_bg=0.0, vtdm4=0.0, do_vort_damp=False, nord_v=None, d_con=0.0, n_sponge=-1,
+                    d2_bg_k1=0.0, d2_bg_k2=0.0):
+    """The per-level d_sw parameters of FV3 dyn_core's k loop (dyn_core.F90 before the d_sw
+    call; the same rule as pyFV3 dyn_core get_column_namelist), one dict per level (0 = top):
+    nord, d2_divg, nord_v, damp_vt, nord_w, damp_w, nord_t, damp_t, d_con.
+
+    Every level: nord_v = min(2, nord) (nord_v given: the GTFV3_CONFIG extension),
+    d2_divg = min(0.2, d2_bg), damp_vt = vtdm4 with do_vort_damp (else 0), w and pt take
+    nord_v / damp_vt.  Sponge layers (npz > 1, n_sponge >= 0), no special damping of pt:
+      level 0:  nord 0, d2_divg = max(0.01, d2_bg, d2_bg_k1), w del-2 with damp_w = d2_divg,
+                with do_vort_damp vorticity / delp del-2 with damp_vt = d2_divg / 2, d_con 0;
+      level 1 (d2_bg_k2 > 0.01): the same with d2_divg = max(d2_bg, d2_bg_k2);
+      level 2 (d2_bg_k2 > 0.05): nord 0, d2_divg = max(d2_bg, 0.2 d2_bg_k2), w del-2, d_con 0.
+    npz = 1 or n_sponge < 0: d2_divg = d2_bg on every level."""
+    nv = min(2, nord) if nord_v is None else int(nord_v)
+    dvt = float(vtdm4) if do_vort_damp else 0.0
+    base = dict(nord=int(nord), d2_divg=min(0.20, d2_bg), nord_v=nv, damp_vt=dvt, nord_w=nv, damp_w=dvt, nord_t=nv,
+                damp_t=dvt, d_con=float(d_con))
+    cols = [dict(base) for _ in range(npz)]
+    if npz == 1 or n_sponge < 0:
+        for c in cols:
+            c["d2_divg"] = d2_bg
+        return cols
+
+    def sponge(c, d2, vort):
+        c.update(nord=0, d2_divg=d2, nord_w=0, damp_w=d2, d_con=0.0)
+        if vort and do_vort_damp:
+            c.update(nord_v=0, damp_vt=0.5 * d2)
+    sponge(cols[0], max(0.01, d2_bg, d2_bg_k1), True)
+    if npz > 1 and d2_bg_k2 > 0.01:
+        sponge(cols[1], max(d2_bg, d2_bg_k2), True)
+    if npz > 2 and d2_bg_k2 > 0.05:
+        sponge(cols[2], max(d2_bg, 0.2 * d2_bg_k2), False)
+    return cols
+
+
+def heat_levels(npz, vtdm4=0.0, d2_bg_k1=0.0, d2_bg_k2=0.0, convert_ke=False):
+    """FV3 dyn_core n_con: the levels (from the top) whose dissipated kinetic energy heats the
+    air -- all with convert_ke or vtdm4 > 1e-4 (the namelist vtdm4, do_vort_damp or not), else
+    the sponge levels d2_bg_k1 / d2_bg_k2 switch on (0, 1 or 2)"""
+    if convert_ke or vtdm4 > 1e-4:
+        return npz
+    if d2_bg_k1 < 1e-3:
+        return 0
+    if d2_bg_k2 < 1e-3:
+        return 1
+    return 2
+
+
 def d_sw(delp, pt, u, v, w, uc, vc, ua, va, sub, m, nx, ny, dt, ords, dddmp, d2_bg, da_min_c, nord=0,
-         d4_bg=0.0, divg_d=None, vtdm4=0.0, nord_v=0, d_con=0.0, corner_w=None):
-    """FV3 d_sw for all levels at once.  ords = (hord_mt, hord_vt, hord_tm, hord_dp).
+         d4_bg=0.0, divg_d=None, vtdm4=0.0, nord_v=0, d_con=0.0, corner_w=None, damp_w=0.0, nord_w=0,
+         damp_t=0.0, nord_t=0, ke_bg=0.0, da_min=None):
+    """FV3 d_sw for the given levels at once (one parameter set: the caller splits the column by
+    column_namelist).  ords = (hord_mt, hord_vt, hord_tm, hord_dp).
     Returns dict: delp, pt, w (updated), u, v (times dx / dy: finished by the pressure
-    gradient), crx, cry, xfx, yfx (advective), fx, fy (mass fluxes), and with d_con > 0 the
-    heat source and the dissipation-estimate increment of this call (heat, diss).
-    Damping: nord = 0 del-2 divergence damping (dddmp, d2_bg); nord = 1..3 the del-(2 nord + 2)
-    damping of the corner divergence divg_d (c_sw's, halo filled) with d4_bg plus the del-2
-    Smagorinsky-type term; vtdm4 > 0 del-(2 nord_v + 2) vorticity damping fluxes added to u, v;
-    d_con > 0 the damped kinetic energy returned as heat."""
+    gradient), crx, cry, xfx, yfx (advective), fx, fy (mass fluxes, delp's diffusive fluxes
+    included), and with d_con > 0 or damp_w > 0 the heat source and the dissipation-estimate
+    increment of this call (heat, diss).
+    Damping: nord = 0 del-2 divergence damping (dddmp, d2_bg = d2_divg); nord = 1..3 the
+    del-(2 nord + 2) damping of the corner divergence divg_d (c_sw's, halo filled) with d4_bg
+    plus the del-2 Smagorinsky-type term; vtdm4 (= damp_vt) > 1e-5 del-(2 nord_v + 2) vorticity
+    damping fluxes added to u, v and, > 1e-4, del-(2 nord_v + 2) diffusive fluxes of delp added
+    to the mass fluxes (coefficient from da_min); damp_t > 1e-4 the mass-weighted
+    del-(2 nord_t + 2) fluxes of pt added to pt's fluxes; damp_w > 1e-5 w's del-(2 nord_w + 2)
+    increment dw (w = w / delp + dw) and its heat ke_bg |dt| - dw (w + dw / 2); d_con > 0 the
+    damped kinetic energy returned as heat."""
     hord_mt, hord_vt, hord_tm, hord_dp = ords
     P = Plane(sub, nx, ny, u.shape[-2], u.shape[-1])
     N, I, J, io, jo = P.N, P.I, P.J, P.io, P.jo
+    if (vtdm4 > 1e-4 or damp_t > 1e-4) and da_min is None:
+        raise ValueError("d_sw: the delp / pt del-n damping needs da_min")
     ut, vt = d_sw_ut_vt(uc, vc, P, m, dt)
     s1, s2, s3, s4 = m["sin_sg1"], m["sin_sg2"], m["sin_sg3"], m["sin_sg4"]
     dx, dy, rdxa, rdya, area, rarea = m["dx"], m["dy"], m["rdxa"], m["rdya"], m["area"], m["rarea"]
@@ -341,19 +402,39 @@ def d_sw(delp, pt, u, v, w, uc, vc, ua, va, sub, m, nx, ny, dt, ords, dddmp, d2_
     yfx = np.where(reg, np.where(yf > 0.0, dx * yf * sh(s4, 0, -1), dx * yf * s2), z)
     ra_y = np.where(P.reg(-NG, nx + NG - 1, 0, ny - 1), area + yfx - sh(yfx, 0, 1), z)
     ra_x = np.where(P.reg(0, nx - 1, -NG, ny + NG - 1), area + xfx - sh(xfx, 1, 0), z)
-    # mass fluxes
+    # mass fluxes (fv_tp_2d(delp, ..., nord = nord_v, damp_c = damp_vt): the diffusive fluxes
+    # of delp added inside fv_tp_2d, so the flux capacitor and w / pt see them)
     fx, fy = fv_tp_2d(delp, crx, cry, xfx, yfx, ra_x, ra_y, sub, m, nx, ny, hord_dp)
+    xreg, yreg = P.reg(0, nx, 0, ny - 1), P.reg(0, nx - 1, 0, ny)
+    if vtdm4 > 1e-4:
+        fx2, fy2 = deln_flux(nord_v, (vtdm4 * da_min) ** (nord_v + 1), delp, sub, m, nx, ny)
+        fx = np.where(xreg, fx + fx2, fx)
+        fy = np.where(yreg, fy + fy2, fy)
     comp = P.reg(0, nx - 1, 0, ny - 1)
+    # w damping (non-hydrostatic d_sw, before w's transport): dw and its heat
+    heat_w = dw = None
+    if damp_w > 1e-5:
+        dd8 = ke_bg * abs(dt)
+        fx2, fy2 = deln_flux(nord_w, (damp_w * da_min_c) ** (nord_w + 1), w, sub, m, nx, ny)
+        dw = np.where(comp, (fx2 - sh(fx2, 1, 0) + fy2 - sh(fy2, 0, 1)) * rarea, 0.0)
+        heat_w = np.where(comp, dd8 - dw * (w + 0.5 * dw), 0.0)
     # w
     gx, gy = fv_tp_2d(w, crx, cry, xfx, yfx, ra_x, ra_y, sub, m, nx, ny, hord_vt, fx, fy)
     w_new = np.where(comp, delp * w + (gx - sh(gx, 1, 0) + gy - sh(gy, 0, 1)) * rarea, w)
-    # pt, delp
+    # pt (fv_tp_2d(pt, ..., mass = delp, nord = nord_t, damp_c = damp_t)), delp
     gx, gy = fv_tp_2d(pt, crx, cry, xfx, yfx, ra_x, ra_y, sub, m, nx, ny, hord_tm, fx, fy)
+    if damp_t > 1e-4:
+        damp2 = 0.5 * (damp_t * da_min) ** (nord_t + 1)
+        fx2, fy2 = deln_flux(nord_t, None, pt, sub, m, nx, ny)
+        gx = np.where(xreg, gx + damp2 * (sh(delp, -1, 0) + delp) * fx2, gx)
+        gy = np.where(yreg, gy + damp2 * (sh(delp, 0, -1) + delp) * fy2, gy)
     pt_new = pt * delp + (gx - sh(gx, 1, 0) + gy - sh(gy, 0, 1)) * rarea
     dp_new = delp + (fx - sh(fx, 1, 0) + fy - sh(fy, 0, 1)) * rarea
     pt_new = np.where(comp, pt_new / dp_new, pt)
     dp_new = np.where(comp, dp_new, delp)
     w_new = np.where(comp, w_new / dp_new, w_new)
+    if dw is not None:
+        w_new = np.where(comp, w_new + dw, w_new)
 
     # kinetic energy at corners (B-grid contravariant winds, upwind PPM of u and v)
     dt5, dt4 = 0.5 * dt, 0.25 * dt
@@ -418,7 +499,7 @@ def d_sw(delp, pt, u, v, w, uc, vc, ua, va, sub, m, nx, ny, dt, ords, dddmp, d2_
         ke = np.where(allx, ke + vd, ke)
         return _d_sw_finish(dict(delp=dp_new, pt=pt_new, w=w_new, crx=crx, cry=cry, xfx=xfx, yfx=yfx, fx=fx, fy=fy,
                                  ut=ut, vt=vt), ke, vd, wk, u, v, udx, vdy, dp_new, sub, m, nx, ny, crx, cry, xfx, yfx,
-                            ra_x, ra_y, hord_vt, da_min_c, vtdm4, nord_v, d_con, P)
+                            ra_x, ra_y, hord_vt, da_min_c, vtdm4, nord_v, d_con, P, heat_w)
     # divergence damping (nord = 0)
     ptc = z.copy()
     regp = P.reg(-1, nx, 0, ny)
@@ -442,13 +523,13 @@ def d_sw(delp, pt, u, v, w, uc, vc, ua, va, sub, m, nx, ny, dt, ords, dddmp, d2_
     ke = np.where(allx, ke + damp * delpc, ke)
     return _d_sw_finish(dict(delp=dp_new, pt=pt_new, w=w_new, crx=crx, cry=cry, xfx=xfx, yfx=yfx, fx=fx, fy=fy,
                              ut=ut, vt=vt), ke, vd, wk, u, v, udx, vdy, dp_new, sub, m, nx, ny, crx, cry, xfx, yfx,
-                        ra_x, ra_y, hord_vt, da_min_c, vtdm4, nord_v, d_con, P)
+                        ra_x, ra_y, hord_vt, da_min_c, vtdm4, nord_v, d_con, P, heat_w)
 
 
 def _d_sw_finish(out, ke, vd, wk, u, v, udx, vdy, dp_new, sub, m, nx, ny, crx, cry, xfx, yfx, ra_x, ra_y, hord_vt,
-                 da_min_c, vtdm4, nord_v, d_con, P):
+                 da_min_c, vtdm4, nord_v, d_con, P, heat_w=None):
     """vorticity transport and the momentum update, then the vorticity damping fluxes and the
-    d_con heat (FV3 d_sw's last part)"""
+    d_con heat (FV3 d_sw's last part); heat_w: the w damping's heat (None: no w damping)"""
     z = np.zeros_like(u)
     vort = np.where(P.reg(-NG, nx + NG - 1, -NG, ny + NG - 1), wk + m["f0"], z)
     fxv, fyv = fv_tp_2d(vort, crx, cry, xfx, yfx, ra_x, ra_y, sub, m, nx, ny, hord_vt)
@@ -459,7 +540,9 @@ def _d_sw_finish(out, ke, vd, wk, u, v, udx, vdy, dp_new, sub, m, nx, ny, crx, c
         damp4 = (vtdm4 * da_min_c) ** (nord_v + 1)
         fx2, fy2 = del6_vt_flux(nord_v, damp4, wk, sub, m, nx, ny)
     if d_con > 1e-5:
-        out["heat"], out["diss"] = damping_heat(u_new, v_new, vd, fx2, fy2, dp_new, m, P, d_con)
+        out["heat"], out["diss"] = damping_heat(u_new, v_new, vd, fx2, fy2, dp_new, m, P, d_con, heat_w)
+    elif heat_w is not None:  # the sponge levels (d_con_k = 0): the w damping's heat alone
+        out["heat"], out["diss"] = heat_w, heat_w.copy()
     if vtdm4 > 1e-5:
         u_new = np.where(P.reg(0, nx - 1, 0, ny), u_new + fy2, u_new)
         v_new = np.where(P.reg(0, nx, 0, ny - 1), v_new - fx2, v_new)
@@ -622,10 +705,20 @@ def divergence_damping_nord(divg_d, wk, sub, m, nx, ny, dt, nord, dddmp, d2_bg, 
 
 def del6_vt_flux(nord, damp, q, sub, m, nx, ny):
     """FV3 del6_vt_flux: del-(2 nord + 2) diffusive fluxes (fx2 on y-edges, fy2 on x-edges) of
-    the cell field q (the relative vorticity) with coefficient damp"""
+    the cell field q (the relative vorticity) with coefficient damp (the loops of deln_flux)"""
+    return deln_flux(nord, damp, q, sub, m, nx, ny)
+
+
+def deln_flux(nord, damp, q, sub, m, nx, ny):
+    """FV3 tp_core deln_flux's diffusive fluxes: fx2 on y-edges over [-nord, nx+nord] x
+    [-nord, ny-1+nord], fy2 on x-edges (zero elsewhere), from d2 = damp q on
+    [-1-nord, n+nord] (damp None: d2 = q, the mass-weighted form whose caller adds
+    0.5 damp (mass(i-1) + mass(i)) fx2), the cube-corner halo of d2 read through copy_corners
+    for nord > 0, then nord passes d2 = div(fluxes) rarea / fluxes of d2 with the opposite
+    sign, each one ring narrower"""
     P = Plane(sub, nx, ny, q.shape[-2], q.shape[-1])
     d6u, d6v, rarea = _del6_u(m), _del6_v(m), m["rarea"]
-    d2 = np.where(P.reg(-nord, nx - 1 + nord, -nord, ny - 1 + nord), damp * q, 0.0)
+    d2 = np.where(P.reg(-1 - nord, nx + nord, -1 - nord, ny + nord), q if damp is None else damp * q, 0.0)
     dx_ = copy_corners(d2, sub, 1) if nord > 0 else d2
     fx2 = np.where(P.reg(-nord, nx + nord, -nord, ny - 1 + nord), d6v * (sh(dx_, -1, 0) - dx_), 0.0)
     dy_ = copy_corners(d2, sub, 2) if nord > 0 else d2
@@ -641,11 +734,13 @@ def del6_vt_flux(nord, damp, q, sub, m, nx, ny):
     return fx2, fy2
 
 
-def damping_heat(u, v, vd, fx2, fy2, delp, m, P, d_con):
+def damping_heat(u, v, vd, fx2, fy2, delp, m, P, d_con, heat_w=None):
     """d_sw's d_con branch: the kinetic energy the divergence damping (corner term vd) and the
-    vorticity damping (fluxes fx2, fy2) remove, as a heat source delp * (-0.25 d_con ...) and
-    the dissipation estimate increment (-rsin2 ...), on compute cells.  u, v: the updated
-    D-grid winds times dx, dy before the vorticity-damping fluxes are added."""
+    vorticity damping (fluxes fx2, fy2) remove, as a heat source delp * (heat_w - 0.25 d_con ...)
+    and the dissipation estimate increment (heat_w - rsin2 ...), on compute cells; heat_w: the w
+    damping's heat (None: 0).  u, v: the updated D-grid winds times dx, dy before the
+    vorticity-damping fluxes are added."""
+    hw = 0.0 if heat_w is None else heat_w
     nx, ny = P.nx, P.ny
     ub = (vd - sh(vd, 1, 0) + fy2) * m["rdx"]
     fy = u * m["rdx"]
@@ -660,6 +755,46 @@ def damping_heat(u, v, vd, fx2, fy2, delp, m, P, d_con):
     t = (ub ** 2 + sh(ub, 0, 1) ** 2 + vb ** 2 + sh(vb, 1, 0) ** 2) + 2.0 * (gy + sh(gy, 0, 1) + gx + sh(gx, 1, 0)) \
         - m["cosa_s"] * (u2 * dv2 + v2 * du2 + du2 * dv2)
     comp = P.reg(0, nx - 1, 0, ny - 1)
-    heat = np.where(comp, delp * (0.0 - 0.25 * d_con * m["rsin2"] * t), 0.0)
-    diss = np.where(comp, -m["rsin2"] * t, 0.0)
+    heat = np.where(comp, delp * (hw - 0.25 * d_con * m["rsin2"] * t), 0.0)
+    diss = np.where(comp, hw - m["rsin2"] * t, 0.0)
     return heat, diss
+
+
+def del2_cubed(q, cd, sub, m, nx, ny, nmax):
+    """FV3 del2_cubed (dyn_core's smoothing of the heat source; pyFV3 HyperdiffusionDamping):
+    min(3, nmax) del-2 passes on a cell field whose halo was filled once, pass n over the
+    region [-nt, n-1+nt] (nt = ntimes - n): at the cube corners this sub-domain owns the corner
+    cell and its two halo neighbours are first set to their mean; fx on y-edges
+    del6_v (q(i-1) - q(i)) and fy on x-edges del6_u (q(j-1) - q(j)) (copy_corners for nt > 0);
+    q += cd rarea (fx - fx(i+1) + fy - fy(j+1)).  Returns the smoothed copy."""
+    P = Plane(sub, nx, ny, q.shape[-2], q.shape[-1])
+    N = P.N
+    q = q.copy()
+    d6u, d6v, rarea = _del6_u(m), _del6_v(m), m["rarea"]
+    r3 = 1.0 / 3.0
+    # (corner cell, its west / east halo neighbour, its south / north halo neighbour)
+    corners = []
+    if P.owns(0, 0):
+        corners.append(((0, 0), (-1, 0), (0, -1)))
+    if P.owns(N, 0):
+        corners.append(((N - 1, 0), (N, 0), (N - 1, -1)))
+    if P.owns(N, N):
+        corners.append(((N - 1, N - 1), (N, N - 1), (N - 1, N)))
+    if P.owns(0, N):
+        corners.append(((0, N - 1), (-1, N - 1), (0, N)))
+    ntimes = min(3, nmax)
+    for n in range(1, ntimes + 1):
+        nt = ntimes - n
+        for c0, c1, c2 in corners:
+            a, b, c = P.slot(*c0), P.slot(*c1), P.slot(*c2)
+            avg = (q[:, a[0], a[1]] + q[:, b[0], b[1]] + q[:, c[0], c[1]]) * r3
+            q[:, a[0], a[1]] = avg
+            q[:, b[0], b[1]] = avg
+            q[:, c[0], c[1]] = avg
+        qx = copy_corners(q, sub, 1) if nt > 0 else q
+        fx = np.where(P.reg(-nt, nx + nt, -nt, ny - 1 + nt), d6v * (sh(qx, -1, 0) - qx), 0.0)
+        qy = copy_corners(q, sub, 2) if nt > 0 else q
+        fy = np.where(P.reg(-nt, nx - 1 + nt, -nt, ny + nt), d6u * (sh(qy, 0, -1) - qy), 0.0)
+        q = np.where(P.reg(-nt, nx - 1 + nt, -nt, ny - 1 + nt),
+                     q + cd * rarea * (fx - sh(fx, 1, 0) + fy - sh(fy, 0, 1)), q)
+    return q

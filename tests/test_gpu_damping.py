@@ -72,6 +72,8 @@ def test_divergence_corner(pkg, require_gpu, npx):
 
 
 CASES = {
+    # one branch per case, the column uniform (no sponge); vtdm4 with do_vort_damp (the
+    # default here) damps vorticity, delp, w and pt (nord_v / damp_vt, FV3 dyn_core)
     "nord1": dict(nord=1, d4_bg=0.15),
     "nord2": dict(nord=2, d4_bg=0.15),
     "nord3_no_smag": dict(nord=3, d4_bg=0.12, dddmp=0.0),
@@ -79,15 +81,27 @@ CASES = {
     "vort_del6": dict(vtdm4=0.05, nord_v=2),
     "d_con": dict(nord=2, d4_bg=0.15, vtdm4=0.05, nord_v=1, d_con=1.0),
     "d_con_nord0": dict(d_con=0.8),
+    "vtdm4_without_switch": dict(nord=2, d4_bg=0.15, vtdm4=0.05, do_vort_damp=0, d_con=1.0),
+    # the sponge layers on the top three of four levels (FV3 dyn_core's overrides)
+    "sponge_held_suarez": dict(n_sponge=1, d2_bg_k1=0.2, d2_bg_k2=0.1),
+    "sponge_vort_d_con": dict(nord=2, d4_bg=0.15, vtdm4=0.05, d_con=1.0, n_sponge=1, d2_bg_k1=0.2, d2_bg_k2=0.1,
+                              ke_bg=2.0),
+    "sponge_nord1_k2_small": dict(nord=1, d4_bg=0.12, d_con=0.8, n_sponge=1, d2_bg_k1=0.15, d2_bg_k2=0.04),
 }
 
 
 @pytest.mark.parametrize("case", list(CASES))
 def test_d_sw_damping_c180(pkg, require_gpu, case):
-    """d_sw with one damping branch at C180 on two levels against the oracle"""
-    opt = dict(nord=0, d4_bg=0.0, vtdm4=0.0, nord_v=0, d_con=0.0, dddmp=0.2)
+    """d_sw with one damping namelist at C180 against the oracle (the per-level parameters of
+    sw_core.column_namelist; four levels, so a sponge case has three sponge levels and one
+    ordinary one)"""
+    from oracle import fv_dynamics as fvd
+    opt = dict(nord=0, d4_bg=0.0, vtdm4=0.0, nord_v=None, d_con=0.0, dddmp=0.2, do_vort_damp=1, n_sponge=-1,
+               d2_bg_k1=0.0, d2_bg_k2=0.0, ke_bg=0.0)
     opt.update(CASES[case])
-    npz = 2
+    if opt["nord_v"] is None:
+        opt["nord_v"] = min(2, opt["nord"])
+    npz = 4 if opt["n_sponge"] >= 0 else 2
     d = pkg.Domain(npx=181, npz=npz, nq=1)
     try:
         r = rng(91)
@@ -104,24 +118,46 @@ def test_d_sw_damping_c180(pkg, require_gpu, case):
         dt, d2_bg = 600.0, 0.0075
         d.stencil("d_sw_damped", ["d_" + n for n in D_NAMES] + ["d_divg", "d_heat", "d_diss"],
                   [dt, opt["dddmp"], d2_bg, 6, 6, 6, 6, opt["nord"], opt["d4_bg"], opt["vtdm4"], opt["nord_v"],
-                   opt["d_con"]])
-        got = {n: d.download("d_" + n) for n in ("delp", "pt", "w", "u", "v", "ke", "heat", "diss")}
+                   opt["d_con"], opt["do_vort_damp"], opt["n_sponge"], opt["d2_bg_k1"], opt["d2_bg_k2"], opt["ke_bg"]])
+        got = {n: d.download("d_" + n) for n in ("delp", "pt", "w", "u", "v", "ke", "heat", "diss", "mfx", "mfy")}
+        cols = sw_core.column_namelist(npz, nord=opt["nord"], d2_bg=d2_bg, vtdm4=opt["vtdm4"],
+                                       do_vort_damp=bool(opt["do_vort_damp"]), nord_v=opt["nord_v"], d_con=opt["d_con"],
+                                       n_sponge=opt["n_sponge"], d2_bg_k1=opt["d2_bg_k1"], d2_bg_k2=opt["d2_bg_k2"])
+        groups = fvd.level_groups(cols)
         nx, ny = d.nx, d.ny
         for s in (0, 3, 5):
             m, sc = checked_metrics(d, s)
-            ref = sw_core.d_sw(inp["delp"][s], inp["pt"][s], inp["u"][s], inp["v"][s], inp["w"][s], inp["uc"][s],
-                               inp["vc"][s], inp["ua"][s], inp["va"][s], d.subs[s], m, nx, ny, dt, (6, 6, 6, 6),
-                               opt["dddmp"], d2_bg, sc["da_min_c"], nord=opt["nord"], d4_bg=opt["d4_bg"],
-                               divg_d=divg[s], vtdm4=opt["vtdm4"], nord_v=opt["nord_v"], d_con=opt["d_con"],
-                               corner_w=sc["corner_w"])
+            ref = fvd.d_sw_levels(inp, s, d.subs[s], m, nx, ny, dt, (6, 6, 6, 6), opt["dddmp"], groups,
+                                  sc["da_min_c"], sc["da_min"], opt["d4_bg"], opt["ke_bg"], divg[s], sc["corner_w"])
             regions = dict(delp=(0, nx - 1, 0, ny - 1), pt=(0, nx - 1, 0, ny - 1), w=(0, nx - 1, 0, ny - 1),
                            u=(0, nx - 1, 0, ny), v=(0, nx, 0, ny - 1), ke=(0, nx, 0, ny))
             if opt["d_con"] > 0:
                 regions.update(heat=(0, nx - 1, 0, ny - 1), diss=(0, nx - 1, 0, ny - 1))
             for o, rg in regions.items():
-                close(reg(got[o][s], *rg), reg(ref[o], *rg), f"{case} sub{s} {o}", 1e-12)
+                for k in range(npz):  # level by level: a sponge level is its own scale
+                    close(reg(got[o][s][k], *rg), reg(ref[o][k], *rg), f"{case} sub{s} {o} level {k}", 1e-12)
+            # the flux capacitor holds delp's fluxes with their diffusive part
+            close(reg(got["mfx"][s], 0, nx, 0, ny - 1), reg(0.5 + ref["fx"], 0, nx, 0, ny - 1), f"{case} mfx", 1e-12)
+            close(reg(got["mfy"][s], 0, nx - 1, 0, ny), reg(0.5 + ref["fy"], 0, nx - 1, 0, ny), f"{case} mfy", 1e-12)
             if opt["d_con"] > 0:
                 assert np.abs(reg(ref["diss"], 0, nx - 1, 0, ny - 1)).max() > 0.0
+        if opt["n_sponge"] >= 0:
+            # every sponge override changed something: against the column without the sponge
+            nos = sw_core.column_namelist(npz, nord=opt["nord"], d2_bg=d2_bg, vtdm4=opt["vtdm4"],
+                                          do_vort_damp=bool(opt["do_vort_damp"]), nord_v=opt["nord_v"],
+                                          d_con=opt["d_con"], n_sponge=-1)
+            m, sc = checked_metrics(d, 0)
+            plain = fvd.d_sw_levels(inp, 0, d.subs[0], m, nx, ny, dt, (6, 6, 6, 6), opt["dddmp"],
+                                    fvd.level_groups(nos), sc["da_min_c"], sc["da_min"], opt["d4_bg"], opt["ke_bg"],
+                                    divg[0], sc["corner_w"])
+            ks = [k for k in range(3) if cols[k] != nos[k]]
+            assert ks, "no sponge level"
+            ref0 = fvd.d_sw_levels(inp, 0, d.subs[0], m, nx, ny, dt, (6, 6, 6, 6), opt["dddmp"], groups,
+                                   sc["da_min_c"], sc["da_min"], opt["d4_bg"], opt["ke_bg"], divg[0], sc["corner_w"])
+            for k in ks:  # the override's effect is far above the parity bar the GPU met
+                for o in ("u", "w"):
+                    a_, b_ = reg(ref0[o][k], 0, nx - 1, 0, ny - 1), reg(plain[o][k], 0, nx - 1, 0, ny - 1)
+                    assert np.abs(a_ - b_).max() > 1e-6 * np.abs(b_).mean(), f"{o} level {k}: sponge without effect"
     finally:
         d.close()
 
