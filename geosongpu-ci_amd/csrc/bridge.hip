@@ -394,9 +394,11 @@ void bridge_init(void* comm, int npx, int npy, int npz, int ntiles, int is, int 
     throw std::runtime_error("geos_gtfv3_init: one sub-domain per rank expected (6*layout ranks)");
   }
   // GTFV3_BRIDGE_PROXY=1 (measurement and test aid, never a numerical path): this rank alone
-  // on the null transport -- cross-rank halo messages are dropped -- so the one-sub-domain-
-  // per-rank array layout runs on a single GPU (tests/test_gpu_bridge.py compares the region
-  // the missing messages cannot reach with the six-tile run)
+  // on the null transport -- each cross-rank receive is answered with a copy of this rank's
+  // own send to that peer (comm.cpp), so the pack / copy / unpack work of a real exchange runs
+  // but the remote halo points hold the wrong rows -- so the one-sub-domain-per-rank array
+  // layout runs on a single GPU (tests/test_gpu_bridge.py compares the region the reflected
+  // messages cannot reach with the six-tile run)
   const char* const px[] = {"GTFV3_BRIDGE_PROXY", nullptr};
   const bool proxy = nranks > 1 && env_int(px, 0) == 1;
   if (proxy) nl.loopback = -1;

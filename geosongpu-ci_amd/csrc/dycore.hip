@@ -21,6 +21,11 @@ long Field::elems() const { return 0; }
 
 namespace {
 constexpr size_t kGuardElems = 2048;  // 16 KiB guard zones in GTFV3_SYNC_LAUNCH=1 mode
+// every field allocation ends in this many spare planes: the level-block kernels' loads of a
+// partial last block (remap_blkq_k: the level in the scalar offset, which the buffer range
+// check does not cover) may read up to a block (<= 16 levels) past the last sub-domain's
+// bottom level; those values are discarded, and the pad keeps them inside the allocation
+constexpr int kFieldTailPlanes = 16;
 }  // namespace
 
 Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) : nl(nl_) {
@@ -142,8 +147,9 @@ Field& Dycore::field(const std::string& name, int nk) {
     debug_canary(("guard-hi " + name).c_str(), f.p + field_elems(nk), pat.data(), gb);
     return fields[name] = f;
   }
-  HIP_CHECK(hipMalloc(&f.p, bytes));
-  HIP_CHECK(hipMemsetAsync(f.p, 0, bytes, st));
+  const size_t pad = sizeof(double) * (size_t)kFieldTailPlanes * d.plane;
+  HIP_CHECK(hipMalloc(&f.p, bytes + pad));
+  HIP_CHECK(hipMemsetAsync(f.p, 0, bytes + pad, st));
   return fields[name] = f;
 }
 

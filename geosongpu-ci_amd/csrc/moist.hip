@@ -788,7 +788,8 @@ __global__ void __launch_bounds__(64 * MB_WAVES) mpdrv_blk_k(MpArgs a) {
   const MpConst& kc = a.k;
   const unsigned long long cmask = NB == 64 ? ~0ull : ((1ull << NB) - 1) << (cl * NB);
   // buffer resources per field (the sub-domain's nk planes), one VGPR offset per lane (the
-  // lane's column at its block's first level), the level in the scalar offset
+  // lane's column at its block's first level) plus the level (inside the range-checked vector
+  // offset: a partial block's levels past the bottom read 0 and drop their stores)
   const uint32_t PB = (uint32_t)P * 8u;
   const uint32_t vb = (uint32_t)(o + (long)g0 * P) * 8u;
   auto rsrc = [&](const double* base) {
@@ -799,10 +800,10 @@ __global__ void __launch_bounds__(64 * MB_WAVES) mpdrv_blk_k(MpArgs a) {
   const auto rI = rsrc(a.qi + qo), rS = rsrc(a.qs + qo), rG = rsrc(a.qg + qo);
   const auto rP = rsrc(a.dp + (long)s * n * P), rZ = rsrc(a.dz + (long)s * n * P);
   auto ld = [&](__amdgpu_buffer_rsrc_t r, int m) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vb, (uint32_t)m * PB, 0));
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, vb + (uint32_t)m * PB, 0, 0));
   };
   auto st = [&](__amdgpu_buffer_rsrc_t r, int m, double v) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(MbU2, v), r, vb, (uint32_t)m * PB, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(MbU2, v), r, vb + (uint32_t)m * PB, 0, 0);
   };
   double t[M], qv[M], ql[M], qr[M], qi[M], qs[M], qg[M], dp[M], dz[M], den[M];
 #pragma unroll

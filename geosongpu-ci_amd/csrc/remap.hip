@@ -634,14 +634,14 @@ __global__ void __launch_bounds__(64) remap_reg_k(RemapArgs a) {
   }
   const long P = d.plane, o = pidx(d, i, j);
   // Memory through buffer descriptors (wave-uniform base of the sub-domain's field) with the
-  // lane's column as the 32-bit vector offset and the level as the scalar offset, so the
-  // 73 level addresses cost no VGPRs (64-bit per-level addresses ran the kernel out of them)
+  // lane's column plus the level as the 32-bit vector offset (the range check covers it; the
+  // scalar offset would not be checked), so the 73 level addresses cost no 64-bit VGPR pairs
   const uint32_t PB = (uint32_t)P * 8u, vo = (uint32_t)o * 8u;
   auto rsrc = [&](const double* base, int nk) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(nk * PB), 0x00020000);
   };
   auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t v, int lev) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, v, (uint32_t)lev * PB, 0));
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, v + (uint32_t)lev * PB, 0, 0));
   };
   const double* pe_s = a.S.pe + (long)s * (KM + 1) * P;
   const auto rPE = rsrc(pe_s, KM + 1);
@@ -694,7 +694,7 @@ __global__ void __launch_bounds__(64) remap_reg_k(RemapArgs a) {
     return lab[k] + 0.5 * lab[KM + 1 + k] * pb;
   };
   auto put = [&](int k, double v) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RmU2, v), rOUT, vo, (uint32_t)k * PB, 0);
+    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RmU2, v), rOUT, vo + (uint32_t)k * PB, 0, 0);
   };
   auto G = [&](int e) -> double& { return lg[e * 64 + lane]; };
 
@@ -1015,7 +1015,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES) remap_blk_k(RemapArgs a) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(nk * PB), 0x00020000);
   };
   auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t v, int lev) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, v, (uint32_t)lev * PB, 0));
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, v + (uint32_t)lev * PB, 0, 0));
   };
   const double* pe_s = a.S.pe + (long)s * (km + 1) * P;
   const auto rPE = rsrc(pe_s, km + 1);
@@ -1060,8 +1060,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES) remap_blk_k(RemapArgs a) {
     const int lev = b * M + m;
     if (!ewind) return ld(rEA, vb, m);
     const double x0 = ld(rEA, vb, m);
-    const double x1 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rEA, vob + (uint32_t)(b * M) * PB,
-                                                                                       (uint32_t)m * PB, 0));
+    const double x1 = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rEA, vob + (uint32_t)(b * M + m) * PB, 0, 0));
     return lev == 0 ? x0 : 0.5 * (x1 + x0);
   };
   auto T = [&](int k) -> double {
@@ -1284,7 +1283,7 @@ __global__ void __launch_bounds__(64 * RB_WAVES) remap_blk_k(RemapArgs a) {
     const double num = o0 == o1 ? q1 - q0 : (loff[wv][cl][o1] - loff[wv][cl][o0]) + (q1 - q0);
     const double v = num / (lt[wv][cl][kk + 1] - lt[wv][cl][kk]);
     if (valid)
-      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), rOUT, vb, (uint32_t)m * PB, 0);
+      __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), rOUT, vb + (uint32_t)m * PB, 0, 0);
     neg = neg || v < 0.0;
   }
   if constexpr (JK == JK_Q) {
@@ -1344,6 +1343,12 @@ __global__ void __launch_bounds__(64 * RB_WAVES, 2) remap_blkq_k(RemapArgs a) {
   auto rsrc = [&](const double* base, int nk) {
     return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(nk * PB), 0x00020000);
   };
+  // the level in the scalar offset (no VGPRs: the vector-offset form, or a per-level select of
+  // an out-of-range vector offset, runs this kernel out of them).  The scalar offset is outside
+  // the descriptor's range check, so a partial block's loads past the bottom read the planes
+  // that follow (the next sub-domain's, or the field allocation's tail pad of kFieldTailPlanes
+  // planes, Dycore::field): values replaced below (virtual layers), never a fault; its stores
+  // are guarded by the level (kk < km).
   auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t v, int lev) {
     return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, v, (uint32_t)lev * PB, 0));
   };

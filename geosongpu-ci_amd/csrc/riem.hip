@@ -316,10 +316,12 @@ __global__ void __launch_bounds__(BLOCK) riem_col_k(RiemArgs a) {
 //   * the p1 recurrence (bottom-up affine) and the dz_min clamp (bottom-up max recurrence,
 //     speculative per block, repeated only where a block below changed its bottom interface).
 // The w system is nearly singular (the acoustic coupling aa ~ 1e8 against layer masses ~ 1e2):
-// its incoming pivots carry the cancellation of the matrix products (~1e-13 relative), so its
-// solve takes one step of iterative refinement (residual from the DPP-neighbour values, the
-// same factors), which brings the error back to the sequential sweep's (~3e-14 of the mean
-// |w| in a numpy model of the solve, against 1e-14 for the column sweep).
+// scanned (Moebius-product) pivots would carry the cancellation of the matrix products
+// (~1e-13 relative), so the w solve hands its pivots block to block serially
+// (tri_solve<M, NB, false>: block b eliminates from block b-1's last pivot, NB dependent DPP
+// steps) -- the column sweep's pivot sequence -- and only the right-hand side and the back
+// substitution are scanned; no refinement step.  Measured against the oracle's column solve:
+// w within 1e-11 of its scale at L7 .. L137 (tests/test_gpu_riem.py).
 // Sums and products are associated differently from the column sweep (riem_col_k): the
 // results agree with it and with the oracle to rounding (tests/test_gpu_riem.py), not bit for
 // bit.  Transcendentals and divisions come from fastmath.hpp (~1 ulp; a third of ocml's log).
@@ -367,9 +369,10 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
   const double capa1 = KAPPA - 1.0;
 
   // Memory: one buffer descriptor per array and sub-domain (wave-uniform SGPRs), a 32-bit
-  // per-lane byte offset (the block's first level) and the level as the scalar offset.  Levels
-  // past the bottom (a partial block's) fall outside the descriptor's range: their loads read
-  // zero and their stores are dropped by the hardware range check.
+  // per-lane byte offset (the block's first level) and the level as the scalar offset.  The
+  // scalar offset is excluded from the descriptor's range check, so the levels past the
+  // bottom (a partial block's) take an out-of-range per-lane offset instead: their loads read
+  // zero and their stores are dropped, whatever the level offset.
   const uint32_t PB = (uint32_t)P * 8u;
   const uint32_t lo = (uint32_t)((o + (long)(b * M) * P) * 8);
   const uint32_t o8 = (uint32_t)o * 8u;
@@ -378,11 +381,18 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
     const long so = (long)s * (itf ? km + 1 : km) * P;
     return __builtin_amdgcn_make_buffer_rsrc((void*)(p + so), 0, itf ? li : ll, 0x00020000);
   };
+  constexpr uint32_t OOB = 0x80000000u;
+  auto lom = [&](int m) { return real(m) ? lo : OOB; };
   auto ld = [&](__amdgpu_buffer_rsrc_t r, int m) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lo, (uint32_t)m * PB, 0));
+    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, lom(m), (uint32_t)m * PB, 0));
   };
-  auto st = [&](__amdgpu_buffer_rsrc_t r, int m, double v) {
-    if (valid) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), r, lo, (uint32_t)m * PB, 0);
+  auto st = [&](__amdgpu_buffer_rsrc_t r, int m, double v) {  // layer m of the block
+    if (valid) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), r, lom(m), (uint32_t)m * PB, 0);
+  };
+  // interface m of the block: real up to the block's bottom interface (m <= nv)
+  auto loi = [&](int m) { return m == 0 || real(m - 1) ? lo : OOB; };
+  auto sti = [&](__amdgpu_buffer_rsrc_t r, int m, double v) {
+    if (valid) __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RbU2, v), r, loi(m), (uint32_t)m * PB, 0);
   };
   // the column's bottom interface (level km), written by the last block
   auto st_bot = [&](__amdgpu_buffer_rsrc_t r, double v) {
@@ -394,7 +404,8 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
   // ---- loads (W1 after the pp solve)
   double G[M + 1], DP[M], PT[M];
 #pragma unroll
-  for (int m = 0; m <= M; ++m) G[m] = ld(rG, m);
+  for (int m = 0; m <= M; ++m)  // G[M] is the block's bottom interface: real when its top layer is
+    G[m] = __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(rG, loi(m), (uint32_t)m * PB, 0));
 #pragma unroll
   for (int m = 0; m < M; ++m) DP[m] = ld(rDP, m);
 #pragma unroll
@@ -468,11 +479,11 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
       for (int m = 0; m <= M; ++m) {
         if (m > 0 || b == 0) {  // interface 0 of block b > 0 is written by block b - 1
           const double pkk = fm_exp(KAPPA * pln[m]);
-          st(rK3, m, pkk);
+          sti(rK3, m, pkk);
           if (a.last_call) {
-            st(rs(a.pe, true), m, pem[m]);
-            st(rs(a.peln, true), m, pln[m]);
-            st(rs(a.pk, true), m, pkk);
+            sti(rs(a.pe, true), m, pem[m]);
+            sti(rs(a.peln, true), m, pln[m]);
+            sti(rs(a.pk, true), m, pkk);
           }
         }
       }
@@ -645,11 +656,11 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
       dump(11, m, gz);
     }
 #pragma unroll
-    for (int m = 0; m < M; ++m) st(rG, m, gzo[m]);
+    for (int m = 0; m < M; ++m) sti(rG, m, gzo[m]);
     st_bot(rG, base);
     if constexpr (CG) {
 #pragma unroll
-      for (int m = 0; m < M; ++m) st(rPO, m, b == 0 && m == 0 ? a.ptop : pe[m] + pem[m]);
+      for (int m = 0; m < M; ++m) sti(rPO, m, b == 0 && m == 0 ? a.ptop : pe[m] + pem[m]);
       double peb = pe[M] + pem[M];
       if constexpr (PART) {
 #pragma unroll
@@ -662,7 +673,7 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
 #pragma unroll
       for (int m = 0; m < M; ++m) {
         st(rDZ, m, dz2[m]);
-        st(rPO, m, pe[m]);
+        sti(rPO, m, pe[m]);
       }
       double peb = pe[M];
       if constexpr (PART) {

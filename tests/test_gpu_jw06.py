@@ -7,11 +7,13 @@ n_split 6) for five days.
 
 Checked, on the D-grid edge winds u and v (the jet projected onto each edge's direction):
   * the dp-weighted l2 norm of (wind - initial wind) over every edge and level (JW06 eq. 14's
-    l2(u) restated on the edges) stays <= 1 m/s after 5 days, and grows by at most 4x from
-    day 1 to day 5 (measured on MI355X: 0.22, 0.26, 0.35, 0.47, 0.58 m/s on days 1-5);
-  * ps stays within 3 hPa of 1000 hPa (measured max |ps - 1000 hPa|: 73, 44, 62, 115,
-    170 Pa -- the synthetic hybrid levels with a 1 Pa top and no sponge, not JW06's eta
-    levels, so the first day's adjustment is larger than on their grid);
+    l2(u) restated on the edges) stays <= 0.65 m/s after 5 days, and grows by at most 3x from
+    day 1 to day 5 (measured on MI355X with the sponge layers of the namelist, round 5: 0.218,
+    0.256, 0.350, 0.470, 0.574 m/s on days 1-5; 0.22 .. 0.58 without them, round 4);
+  * ps stays within 2 hPa of 1000 hPa (measured max |ps - 1000 hPa|: 72.7, 45.0, 62.1, 113.4,
+    170.5 Pa with the sponge, 73 .. 170 without: the drift is not the model top's -- the
+    sponge (the three top layers, between 1.0 and 1.17 Pa) leaves it unchanged -- but the synthetic hybrid levels,
+    not JW06's eta levels, so the first day's adjustment is larger than on their grid);
   * everything finite.
 JW06's own error norms for the FV core are not available offline here; the bars are this
 core's measured drift with headroom, as a regression pin on the whole step's balance (a
@@ -59,7 +61,7 @@ def test_jw06_steady_state_five_days(pkg, require_gpu):
             hist.append((day, eu, float(np.abs(ps - 1.0e5).max())))
             print(f"JW06 steady state day {day}: l2(wind - wind0) {eu:.4f} m/s, max |ps - 1000 hPa| "
                   f"{hist[-1][2]:.2f} Pa", flush=True)
-        assert hist[-1][1] <= 1.0 and hist[-1][1] <= 4.0 * hist[0][1], hist
-        assert max(h[2] for h in hist) <= 300.0, hist
+        assert hist[-1][1] <= 0.65 and hist[-1][1] <= 3.0 * hist[0][1], hist
+        assert max(h[2] for h in hist) <= 200.0, hist
     finally:
         d.close()
