@@ -56,13 +56,15 @@ def families(kstats):
 
 
 def march_ex_fraction(nx, subs, mout=58):
-    """share of the column marches' output columns in strips that reach a tile edge (tp.hip
-    ex_fraction: the tile-edge kernel's part of each march, strips weighted by their outputs)"""
-    nstrip = (nx + 1 + mout - 1) // mout
-    outs = [min(mout, nx + 1 - st * mout) for st in range(nstrip)]
-    nex = sum(outs[st] for s in subs for st in range(nstrip)
-              if not (st * mout + s["ioff"] - 1 >= 2 and st * mout + s["ioff"] + mout + 1 <= s["N"] - 2))
-    return nex / (len(subs) * sum(outs))
+    """share of the column marches' outputs (columns 0 .. nx of every sub-domain) in tile-edge
+    spans (tp.hip plan_spans: [0, 2] at a west tile edge, [nx-3, nx] at an east one, all of a
+    sub-domain too narrow for both), the tile-edge kernel's part of the thermo march"""
+    nex = 0
+    for s in subs:
+        we, ee = s["ioff"] == 0, s["ioff"] + nx == s["N"]
+        lo, hi = (3 if we else 0), (nx - 4 if ee else nx)
+        nex += nx + 1 if hi < lo else (3 if we else 0) + (4 if ee else 0)
+    return nex / (len(subs) * (nx + 1))
 
 
 def manifest_step_bytes(nx, ny, nsub, npz, nq, n_split, pitch, nj, fex=0.5, alternatives=False):

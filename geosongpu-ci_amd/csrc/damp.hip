@@ -618,6 +618,9 @@ void w_damping0_fused(const Ctx& c, int npz, int k0, int nk, const LevelDamp* lv
   GT_LAUNCH(dl_wdamp0_k, g2(L, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, k0, nk, lv, ke_dt, w, w_new,
             hw);
   HIP_LAUNCH_CHECK();
+  // w read, w_new read and written (hw written) per level; seven metric planes
+  const Ext e = ext(d);
+  gt_bytes(nk * (hw ? 4.0 : 3.0) * e.C + 7.0 * e.C);
 }
 
 void w_damping_add(const Ctx& c, int npz, int k0, int nk, const double* dw, double* w) {

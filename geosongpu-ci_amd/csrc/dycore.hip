@@ -65,15 +65,15 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
   HIP_CHECK(hipMalloc(&dcornerw, sizeof(double) * hm.corner_w.size()));
   HIP_CHECK(hipMemcpy(dcornerw, hm.corner_w.data(), sizeof(double) * hm.corner_w.size(), hipMemcpyHostToDevice));
   {
-    // the cell area twice per sub-domain, so a march wave whose two halves run two levels
-    // addresses it with the level fields' per-lane offset (tp.hip paired strips)
-    std::vector<double> a2(2 * (size_t)d.nsub * d.plane);
+    // the cell area four times per sub-domain, so a march wave whose lane groups run two or
+    // four levels addresses it with the level fields' per-lane offset (tp.hip output spans)
+    std::vector<double> a4(4 * (size_t)d.nsub * d.plane);
     for (int s = 0; s < d.nsub; ++s)
-      for (int h = 0; h < 2; ++h)
-        std::memcpy(a2.data() + ((size_t)s * 2 + h) * d.plane, hm.m.data() + ((size_t)M_AREA * d.nsub + s) * d.plane,
+      for (int h = 0; h < 4; ++h)
+        std::memcpy(a4.data() + ((size_t)s * 4 + h) * d.plane, hm.m.data() + ((size_t)M_AREA * d.nsub + s) * d.plane,
                     sizeof(double) * d.plane);
-    HIP_CHECK(hipMalloc(&darea2, sizeof(double) * a2.size()));
-    HIP_CHECK(hipMemcpy(darea2, a2.data(), sizeof(double) * a2.size(), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMalloc(&darea4, sizeof(double) * a4.size()));
+    HIP_CHECK(hipMemcpy(darea4, a4.data(), sizeof(double) * a4.size(), hipMemcpyHostToDevice));
   }
   debug_canary("subs", dsubs, hsubs.data(), sizeof(SubInfo) * d.nsub);
   debug_canary("metrics", dmet, hm.m.data(), sizeof(double) * hm.m.size());
@@ -112,7 +112,7 @@ Dycore::~Dycore() {
   if (dlevel) (void)hipFree(dlevel);
   if (dmet) (void)hipFree(dmet);
   if (dcornerw) (void)hipFree(dcornerw);
-  if (darea2) (void)hipFree(darea2);
+  if (darea4) (void)hipFree(darea4);
   for (hipEvent_t e : {ev_fork, ev_b, ev_c})
     if (e) (void)hipEventDestroy(e);
   for (auto& set : ev_ph)
@@ -165,7 +165,7 @@ Ctx Dycore::ctx() const {
   c.hsubs = hsubs.data();
   c.met = dmet;
   c.cornerw = dcornerw;
-  c.area2 = darea2;
+  c.area4 = darea4;
   c.da_min = hm.da_min;
   c.da_min_c = hm.da_min_c;
   c.st = st;

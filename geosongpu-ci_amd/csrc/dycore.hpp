@@ -40,7 +40,7 @@ class Dycore {
   SubInfo* dsubs = nullptr;
   double* dmet = nullptr;
   double* dcornerw = nullptr;
-  double* darea2 = nullptr;
+  double* darea4 = nullptr;
   HaloExchanger halo;
   hipStream_t st = nullptr;
   // side streams of the acoustic sub-step: d_sw's wind stage and update_dz_d run beside

@@ -29,7 +29,7 @@ struct Ctx {
   const SubInfo* hsubs;    // host copy
   const double* met;       // device [NMETRIC][nsub][plane]
   const double* cornerw;   // device [nsub][12]
-  const double* area2;     // device [nsub][2][plane]: the cell area twice (paired tp_march strips)
+  const double* area4;     // device [nsub][4][plane]: the cell area four times (tp_march lane groups)
   double da_min, da_min_c;
   hipStream_t st;
 };

@@ -39,13 +39,28 @@ constexpr int ZMAX = 65535;
 // (An LDS-tiled form with 64 x 8 tiles, the first fused version, gave bit-identical
 // results and ran 1.9x slower at C180; removed with the ra_x / ra_y planes it read.)
 constexpr int MW = 64, MOUT = MW - 6, MWAVES = 4;
-// Paired last strip (the thermo march's split launches): when the last strip of a row has at
-// most MOUT_H outputs (C180: 181 edges = 3 x 58 + 7), one wave runs it for two levels at
-// once -- lanes 0-31 level k, lanes 32-63 level k+1, each half a 32-lane strip with three
-// halo lanes on either side (the DPP shifts that cross the halves only reach halo lanes) --
-// instead of one wave per level: the tile-edge kernel 460 -> 393 us per launch at C180.
-constexpr int MOUT_H = 32 - 6;
-constexpr int MAXPAIR = 192;
+// Output spans (round 5).  A row of a sub-domain's outputs (x-edges / columns 0 .. nx) is cut
+// into spans, each one wave's strip of lanes: the tile-edge PPM forms (ppm_al at g = -1, 0, 1
+// and N-1, N, N+1) reach only the outputs 0 .. 2 and N-3 .. N of a tile (edges g - 1 .. g + 1,
+// cells through their two edges), so a sub-domain at a west tile edge has a 3-output tile-edge
+// span [0, 2], one at an east tile edge a 4-output span [nx-3, nx], and everything between is
+// cut into interior strips of MOUT outputs (C180: 3 + 3 x 58 + 4 = 181, no short strip).  A
+// span of at most 26 outputs runs two levels per wave (lanes 0-31 level k, 32-63 level k+1),
+// one of at most 10 four levels (16-lane groups): each group is a strip with three halo lanes
+// on either side, so the DPP shifts that cross groups reach only halo lanes.  Round 4 cut
+// rows at multiples of 58 (C180: 58 58 58 7), which ran two of four strips per level in the
+// tile-edge form and one with 7 outputs.
+constexpr int MAXSPAN = 192;
+// span entry: sub-domain, tile-edge form, first output column, output count (1 .. MOUT)
+__host__ __device__ constexpr int span_enc(int s, bool ex, int a0, int nout) {
+  return (s << 19) | ((ex ? 1 : 0) << 18) | (a0 << 6) | (nout - 1);
+}
+__host__ __device__ inline int span_s(int e) { return e >> 19; }
+__host__ __device__ inline bool span_ex(int e) { return ((e >> 18) & 1) != 0; }
+__host__ __device__ inline int span_a0(int e) { return (e >> 6) & 4095; }
+__host__ __device__ inline int span_nout(int e) { return (e & 63) + 1; }
+// levels per wave of a span: class 0 one (> 26 outputs), 1 two (<= 26), 2 four (<= 10)
+inline int span_class(int nout) { return nout <= MW / 4 - 6 ? 2 : (nout <= MW / 2 - 6 ? 1 : 0); }
 // DXL (the thermo march's tile-edge strips): the dxa of the <= 8 tile-edge columns a strip
 // can hold (I = -2 .. 1, N-2 .. N+1) for the segment's rows live in LDS, one region per wave,
 // instead of two dxa loads per row step in the prefetch buffers: 8 fewer VGPRs, which puts
@@ -59,7 +74,7 @@ struct TpM {
   Dims d;
   const SubInfo* subs;
   const double* M;
-  const double* area2;  // [nsub][2][plane]
+  const double* area4;  // [nsub][4][plane]: the cell area once per level group of a wave
   const double* qf[3];
   double* qo[3];  // TM = 1: the updated delp, w, pt; TM = 2: the updated tracers
   // TM = 2 (tracer_2d_1l update fused): dp1 in, dp2 out (written by field group 0), the
@@ -72,15 +87,12 @@ struct TpM {
   const double *crx, *cry, *xfx, *yfx, *mx, *my;
   double* fxf[3];
   double* fyf[3];
-  int nz, nstrip, nseg, seg;
-  // split launches (EXS != 0): the (sub-domain, strip) pairs of this launch's kind, as
-  // s * 256 + strip; a wave's pair index runs fastest, so the four waves of a workgroup
-  // all have work (a workgroup holds its CU slots until its last wave ends)
-  int npair;
-  int pairs[MAXPAIR];
-  // paired last strips (split launches, pairlast set): the paired (sub-domain, strip) entries
-  // follow the npair full ones
-  int pairlast, npairh;
+  int nz, nseg, seg;
+  // the launch's spans (span_enc), by class: nspan[0] one-level spans, then nspan[1] two-level
+  // and nspan[2] four-level ones; a wave's span index runs fastest, so the four waves of a
+  // workgroup all have work (a workgroup holds its CU slots until its last wave ends)
+  int nspan[3];
+  int spans[MAXSPAN];
   // TM = 3 (d_sw's ds_uv fused): corner kinetic energy; u, v updated in place
   const double* ke;
   double *uu, *vv;
@@ -200,17 +212,20 @@ struct YRoll {
 // TM = 3: d_sw's vorticity transport with ds_uv fused (NF = 1, no mass fluxes): u on row
 //   r-2 takes the outer y flux of that edge, v on row r-3 the outer x flux of that row, with
 //   the corner kinetic energy of rows r-3 / r-2 (ds_uv's expressions); no flux plane.
-// pair: 0 one level per wave; 1 the wave's upper half runs level k+1; 2 paired strip without
-// a level k+1 (odd level count: the upper half repeats level k and stores nothing)
+// lv: levels per wave (1, 2, 4: lane group gi of MW / lv lanes runs level k + gi); nvl of
+// them exist (a group past the last level repeats level k and stores nothing); the span's
+// outputs are columns a0 .. a0 + nout - 1 of every group
 template <int ORD, bool EX, bool AHEAD2, bool MF, int NF, int TM>
-__device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, int pair) {
+__device__ void tp_march_strip(const TpM& a, int z, int a0, int nout, int j0, int j1, int lv, int nvl) {
   static_assert(TM == 0 || (TM == 1 && NF == 3 && MF) || (TM == 2 && MF) || ((TM == 3 || TM == 4) && NF == 1 && !MF),
                 "thermo march: delp, w, pt with the accumulators as MX / MY; tracer march: mass fluxes; "
                 "ds_uv and height marches: one field, no mass fluxes");
   const Dims& d = a.d;
   const int lane = threadIdx.x & (MW - 1);
-  const int hl = pair ? (lane & 31) : lane;  // lane within the strip
-  const bool upper = pair && lane >= 32;
+  const int gw = MW / lv;                     // lanes per level group
+  const int gi = lane / gw, hl = lane % gw;   // group, lane within the group's strip
+  const bool lvl_ok = gi < nvl;
+  const int gl = lvl_ok ? gi : 0;             // the group's level offset
   // z: (sub-domain, level, field group), the field group fastest: the groups of one level
   // share the Courant numbers and fluxes (loaded once per wave for its NF fields), and with
   // the groups of a level adjacent in launch order those planes are re-read from the
@@ -219,7 +234,7 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
   const SubInfo sub = a.subs[s];
   const int nx = d.nx, ny = d.ny, N = sub.N;
   const bool last = j1 >= ny;
-  const int x = strip * MOUT - NG + hl;
+  const int x = a0 - NG + hl;
   const int I = x + sub.ioff;
   const int xc = x < -NG ? -NG : (x > nx + NG ? nx + NG : x);  // addressable column
   const long pitch = d.pitch;
@@ -227,15 +242,15 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
   const double* dxa = met(a.M, d, M_DXA, s);
   const double* dya = met(a.M, d, M_DYA, s);
   const bool cin = x >= -NG && x < nx + NG;              // q exists (cell halo)
-  // owns an output edge / column (the upper half of an unpaired odd tail owns nothing)
-  const bool out_lane = hl >= NG && hl < NG + (pair ? MOUT_H : MOUT) && !(upper && pair == 2);
+  // owns an output edge / column (a group past the last level owns nothing)
+  const bool out_lane = lvl_ok && hl >= NG && hl < NG + nout;
   const long xo = xc + NG;
   // Buffer descriptors (wave-uniform) for every plane the march reads or writes; a lane
   // addresses column xo of row r with the constant voffset vx and the row offset as the
   // scalar offset, so the loads of a row step cost no vector address arithmetic.
   const int PBy = (int)(d.plane * 8);
-  // metric planes: one plane; level fields: two planes when the upper half runs level k+1
-  const int PBf = pair == 1 ? 2 * PBy : PBy;
+  // metric planes: one plane; level fields: the wave's nvl planes
+  const int PBf = nvl * PBy;
   auto rsrc = [&](const double* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, PBy, 0x00020000); };
   auto rsrcf = [&](const double* p) { return __builtin_amdgcn_make_buffer_rsrc((void*)p, 0, PBf, 0x00020000); };
   __amdgpu_buffer_rsrc_t rQ[NF];
@@ -243,18 +258,21 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
   for (int f = 0; f < NF; ++f) rQ[f] = rsrcf(a.qf[f] + zo);
   const auto rCRX = rsrcf(a.crx + fo), rCRY = rsrcf(a.cry + fo), rXFX = rsrcf(a.xfx + fo);
   const auto rYFX = rsrcf(a.yfx + fo);
-  // the area through the level fields' offset: a2 holds it twice, for both halves
+  // the area through the level fields' offset: area4 holds it once per level group
   const auto rMX = rsrcf(a.mx + fo), rMY = rsrcf(a.my + fo), rDXA = rsrc(dxa);
-  const auto rAR = __builtin_amdgcn_make_buffer_rsrc((void*)(a.area2 + (long)s * 2 * d.plane), 0, 2 * PBy, 0x00020000);
+  const auto rAR = __builtin_amdgcn_make_buffer_rsrc((void*)(a.area4 + (long)s * 4 * d.plane), 0, 4 * PBy, 0x00020000);
   const auto rDP1 = rsrcf(TM == 2 ? a.dp1 + fo : a.mx + fo);
   const auto rDP2 = rsrcf(TM == 2 ? a.dp2o + fo : a.mx + fo);
   const bool dp2_group = TM == 2 && tg == 0;  // one field group writes dp2
+  // TM = 2, several levels per wave: a group whose level has had its sub-steps carries its
+  // tracers (and dp1 as dp2) over unchanged -- the march's own copy of the old values
+  const bool tdone = TM == 2 && lv > 1 && a.it >= a.nsplt[k + gl];
   // TM = 3: ke, u, v (level fields), dx, dy (metric planes)
   const auto rKE = rsrcf(TM == 3 ? a.ke + fo : a.crx + fo), rU = rsrcf(TM == 3 ? a.uu + fo : a.crx + fo);
   const auto rV = rsrcf(TM == 3 ? a.vv + fo : a.crx + fo);
   const auto rDX = rsrc(met(a.M, d, M_DX, s)), rDY = rsrc(met(a.M, d, M_DY, s));
   const uint32_t vx = (uint32_t)xo * 8u;  // metric planes
-  const uint32_t vf = vx + (upper && pair == 1 ? (uint32_t)PBy : 0u);  // level fields
+  const uint32_t vf = vx + (uint32_t)gl * (uint32_t)PBy;  // level fields
   // dxa only enters the tile-edge interface values (ppm_al at g = 0, N reads the four
   // cells g-2 .. g+1): the other lanes read one shared word instead of their own column
   const bool dx_lane = (I >= -2 && I <= 1) || (I >= N - 2 && I <= N + 1);
@@ -615,18 +633,21 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
           const double dp2 = dp1 + (cur.mx - dpp_next(cur.mx) + my_prev - cur.my) * ra;
           double qn[NF];
 #pragma unroll
-          for (int f = 0; f < NF; ++f)
+          for (int f = 0; f < NF; ++f) {
             qn[f] = (qyw[f][0] * dp1 + (fxo[f] - dpp_next(fxo[f]) + fyo_prev[f] - fyo[f]) * ra) / dp2;
+            if (tdone) qn[f] = qyw[f][0];
+          }
+          const double dp2o = tdone ? dp1 : dp2;
           if (GEN) {
             if (s_fy && mrow < j1) {
 #pragma unroll
               for (int f = 0; f < NF; ++f) bst(rFX[f], se - rowb, qn[f]);
-              if (dp2_group) bst(rDP2, se - rowb, dp2);
+              if (dp2_group) bst(rDP2, se - rowb, dp2o);
             }
           } else {
 #pragma unroll
             for (int f = 0; f < NF; ++f) bstv(rFX[f], vfy, se - rowb, qn[f]);
-            if (dp2_group) bstv(rDP2, vfy, se - rowb, dp2);
+            if (dp2_group) bstv(rDP2, vfy, se - rowb, dp2o);
           }
         }
 #pragma unroll
@@ -707,12 +728,12 @@ __device__ void tp_march_strip(const TpM& a, int z, int strip, int j0, int j1, i
 // waves per SIMD); otherwise one row ahead (two buffers, <= 128 VGPRs, four waves)
 // copy of the strip's output cells of rows [j0, j1) from the tracers to qo (and dp1 to dp2)
 template <int NF>
-__device__ void tracer_carry(const TpM& a, int z, int strip, int j0, int j1) {
+__device__ void tracer_carry(const TpM& a, int z, int a0, int nout, int j0, int j1) {
   const Dims& d = a.d;
   const int lane = threadIdx.x & (MW - 1);
   const int tg = z % a.ntg, k = (z / a.ntg) % a.nk, s = z / a.ntg / a.nk;
-  const int x = strip * MOUT - NG + lane;
-  if (!(lane >= NG && lane < NG + MOUT && x < d.nx)) return;
+  const int x = a0 - NG + lane;
+  if (!(lane >= NG && lane < NG + nout && x < d.nx)) return;
   const long zo = ((long)(s * a.nt + tg * NF) * a.nk + k) * d.plane, fo = ((long)s * a.nk + k) * d.plane;
   const long tstride = (long)a.nk * d.plane;
   const double* __restrict__ qi = a.qf[0] + zo;
@@ -748,125 +769,124 @@ __global__ void __launch_bounds__(MW * MWAVES, OCC ? OCC : (AHEAD2 ? 1 : 4)) tp_
   // wave index through readfirstlane: everything derived from it (plane, strip, segment,
   // buffer descriptors, row offsets) is then provably wave-uniform (SGPRs, no waterfalls)
   const int wv = __builtin_amdgcn_readfirstlane(threadIdx.x / MW);
-  const unsigned w = blockIdx.x * MWAVES + wv;  // < 2^31 (launch_tp checks)
-  int strip, seg, z, pair = 0;
-  const int kh = (a.nk + 1) / 2;  // level pairs of a paired strip
-  // paired-strip wave: (level pair kk, field group tg) of sub-domain s, tg fastest
-  auto paired_z = [&](int s_, unsigned zz) {
-    const int tg = (int)(zz % (unsigned)a.ntg), k = 2 * (int)(zz / (unsigned)a.ntg);
-    pair = k + 1 < a.nk ? 1 : 2;
-    return (s_ * a.nk + k) * a.ntg + tg;
-  };
-  if constexpr (EXS == 0) {
-    // field group fastest: the groups of one (strip, segment, level) are neighbouring waves
-    // of one workgroup, so the Courant / flux rows they all read come from HBM once (one
-    // CU's L1, one XCD's L2) instead of once per group on different XCDs
-    const unsigned tg = w % (unsigned)a.ntg;
-    unsigned t = w / (unsigned)a.ntg;
-    strip = (int)(t % (unsigned)a.nstrip);
-    t = t / (unsigned)a.nstrip;
-    seg = (int)(t % (unsigned)a.nseg);
-    z = (int)((t / (unsigned)a.nseg) * (unsigned)a.ntg + tg);
-    if (z >= a.nz) return;  // whole wavefront leaves; no workgroup barrier follows
-  } else {
-    // pair p = (sub-domain, strip) of this kind; then segment; then (field group, level);
-    // the paired entries (pairs[npair ..]) after the full ones
-    const unsigned nfull = (unsigned)a.npair * (unsigned)a.nseg * (unsigned)(a.ntg * a.nk);
-    if (w < nfull) {
-      const unsigned p = w % (unsigned)a.npair;
-      const unsigned t = w / (unsigned)a.npair;
-      seg = (int)(t % (unsigned)a.nseg);
-      const int zz = (int)(t / (unsigned)a.nseg);
-      const int pr = a.pairs[p];
-      strip = pr & 255;
-      z = (pr >> 8) * a.ntg * a.nk + zz;
-    } else {
-      if (a.npairh == 0) return;
-      const unsigned w2 = w - nfull;
-      const unsigned p = (unsigned)a.npair + w2 % (unsigned)a.npairh;
-      const unsigned t = w2 / (unsigned)a.npairh;
-      seg = (int)(t % (unsigned)a.nseg);
-      const unsigned zz = t / (unsigned)a.nseg;
-      if (zz >= (unsigned)(kh * a.ntg)) return;
-      const int pr = a.pairs[p];
-      strip = pr & 255;
-      z = paired_z(pr >> 8, zz);
-    }
+  unsigned w = blockIdx.x * MWAVES + wv;  // < 2^31 (launch_tp checks)
+  // span class (levels per wave 1, 2, 4), then field group (fastest), span, segment, level
+  // slot: the groups of one (span, segment, level) are neighbouring waves of one workgroup, so
+  // the Courant / flux rows they all read come from HBM once (one CU's L1, one XCD's L2)
+  // instead of once per group on different XCDs
+  // (the four-level spans first: their waves take the longest, so they start in the first
+  // round instead of trailing the launch)
+  int cls = 2, first = a.nspan[0] + a.nspan[1];
+  for (; cls >= 0; --cls) {
+    const unsigned slots = (unsigned)((a.nk + (1 << cls) - 1) >> cls);
+    const unsigned nw = (unsigned)a.nspan[cls] * (unsigned)a.nseg * (unsigned)a.ntg * slots;
+    if (w < nw) break;
+    w -= nw;
+    if (cls > 0) first -= a.nspan[cls - 1];
   }
-  const int s = z / a.nk / a.ntg;
-  const SubInfo& sub = a.subs[s];
+  if (cls < 0) return;  // whole wavefront leaves; no workgroup barrier follows
+  const int tg = (int)(w % (unsigned)a.ntg);
+  unsigned t = w / (unsigned)a.ntg;
+  const unsigned p = t % (unsigned)a.nspan[cls];
+  t /= (unsigned)a.nspan[cls];
+  const int seg = (int)(t % (unsigned)a.nseg);
+  const int k = (int)(t / (unsigned)a.nseg) << cls;
+  const int e = a.spans[first + (int)p];
+  const int s = span_s(e), a0 = span_a0(e), nout = span_nout(e);
+  const bool ex = span_ex(e);
+  const int lv = 1 << cls, nvl = a.nk - k < lv ? a.nk - k : lv;
+  const int z = (s * a.nk + k) * a.ntg + tg;
   const int j0 = seg * a.seg;
   const int j1 = j0 + a.seg < a.d.ny ? j0 + a.seg : a.d.ny;
   if constexpr (TM == 2) {
     // tracer sub-steps past this level's count: the level's tracers carry over unchanged
-    const int k = (z / a.ntg) % a.nk;
-    if (a.it >= a.nsplt[k]) {
-      tracer_carry<NF>(a, z, strip, j0, j1);
+    // (several levels per wave: per group, inside the march)
+    if (lv == 1 && a.it >= a.nsplt[k]) {
+      tracer_carry<NF>(a, z, a0, nout, j0, j1);
       return;
     }
   }
-  const int A = strip * MOUT + sub.ioff;
-  const bool ex = !(A - 1 >= 2 && A + MOUT + 1 <= sub.N - 2);
   if constexpr (EXS == 1) {
-    if (ex) tp_march_strip<ORD, true, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1, pair);
+    if (ex) tp_march_strip<ORD, true, AHEAD2, MF, NF, TM>(a, z, a0, nout, j0, j1, lv, nvl);
   } else if constexpr (EXS == 2) {
-    if (!ex) tp_march_strip<ORD, false, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1, pair);
+    if (!ex) tp_march_strip<ORD, false, AHEAD2, MF, NF, TM>(a, z, a0, nout, j0, j1, lv, nvl);
   } else {
-    if (ex) tp_march_strip<ORD, true, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1, pair);
-    else tp_march_strip<ORD, false, AHEAD2, MF, NF, TM>(a, (int)z, strip, j0, j1, pair);
+    if (ex) tp_march_strip<ORD, true, AHEAD2, MF, NF, TM>(a, z, a0, nout, j0, j1, lv, nvl);
+    else tp_march_strip<ORD, false, AHEAD2, MF, NF, TM>(a, z, a0, nout, j0, j1, lv, nvl);
   }
 }
 
-// whether the last strip of a row has at most MOUT_H outputs (edges 0 .. nx), so that one
-// wave runs it for two levels
-bool pair_last_strip(const Dims& d, int nstrip) {
-  if (nstrip < 2) return false;
-  const int rem = d.nx + 1 - (nstrip - 1) * MOUT;
-  if (getenv("GTFV3_TP_NOPAIR")) return false;
-  return rem >= 1 && rem <= MOUT_H;
-}
-
-// Fraction of the (sub-domain, strip) pairs of a launch whose strip reaches a tile edge
-// (same test as the kernel): the EX kernel's share of the launch's algorithmic bytes.
-// `pex` / `pin` receive the (sub-domain, strip) pairs of each kind (s * 256 + strip).
-// Weighted by the strips' output columns (the last strip of a row is short: C180 has strips
-// of 58, 58, 58 and 7 edges), so each kernel is charged the bytes of the columns it writes.
-double ex_fraction(const Ctx& c, int nstrip, std::vector<int>* pex = nullptr, std::vector<int>* pin = nullptr) {
+// The output spans of every local sub-domain (see MAXSPAN): tile-edge spans [0, 2] at a west
+// tile edge and [nx-3, nx] at an east one, interior strips of MOUT outputs between them (a
+// sub-domain too narrow for both runs one tile-edge span over all its outputs).  `ex` /
+// `in` receive the spans of each form.  Returns the tile-edge spans' share of the outputs.
+double plan_spans(const Ctx& c, std::vector<int>& ex, std::vector<int>& in) {
+  const Dims& d = c.d;
   long nex = 0, nall = 0;
-  for (int s = 0; s < c.d.nsub; ++s)
-    for (int st = 0; st < nstrip; ++st) {
-      const int A = st * MOUT + c.hsubs[s].ioff;
-      const bool ex = !(A - 1 >= 2 && A + MOUT + 1 <= c.hsubs[s].N - 2);
-      const int outs = std::min(MOUT, c.d.nx + 1 - st * MOUT);
-      nex += ex ? outs : 0;
-      nall += outs;
-      std::vector<int>* v = ex ? pex : pin;
-      if (v) v->push_back(s * 256 + st);
+  if (d.nx + 1 > 4095) throw std::runtime_error("fv_tp_2d: sub-domain too wide for the span encoding");
+  for (int s = 0; s < d.nsub; ++s) {
+    const SubInfo& h = c.hsubs[s];
+    const bool we = h.ioff == 0, ee = h.ioff + d.nx == h.N;
+    int lo = we ? 3 : 0, hi = ee ? d.nx - 4 : d.nx;
+    nall += d.nx + 1;
+    if (hi < lo) {
+      if (d.nx + 1 > MOUT) throw std::runtime_error("fv_tp_2d: no span plan for this sub-domain");
+      ex.push_back(span_enc(s, true, 0, d.nx + 1));
+      nex += d.nx + 1;
+      continue;
     }
+    if (we) {
+      ex.push_back(span_enc(s, true, 0, 3));
+      nex += 3;
+    }
+    for (int a0 = lo; a0 <= hi; a0 += MOUT) in.push_back(span_enc(s, false, a0, std::min(MOUT, hi - a0 + 1)));
+    if (ee) {
+      ex.push_back(span_enc(s, true, d.nx - 3, 4));
+      nex += 4;
+    }
+  }
   return (double)nex / (double)nall;
 }
 
-// One march as two kernels: the tile-edge strips (EX forms, AHEAD2, their register count)
-// and the interior strips (A2_IN prefetch depth, OCC_IN workgroups per CU).  Each launch
-// registers its share of the algorithmic bytes.
+// fill m's span list from `spans` (any order; sorted into the three classes); returns the
+// launch's wave count
+long set_spans(TpM& m, const std::vector<int>& spans) {
+  if ((int)spans.size() > MAXSPAN) throw std::runtime_error("fv_tp_2d: too many spans for one launch");
+  auto cls_of = [](int e) { return span_class(span_nout(e)); };
+  int n = 0;
+  for (int cls = 0; cls < 3; ++cls) {
+    m.nspan[cls] = 0;
+    for (int e : spans)
+      if (cls_of(e) == cls) {
+        m.spans[n++] = e;
+        ++m.nspan[cls];
+      }
+  }
+  long waves = 0;
+  for (int cls = 0; cls < 3; ++cls)
+    waves += (long)m.nspan[cls] * m.nseg * m.ntg * ((m.nk + (1 << cls) - 1) >> cls);
+  if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
+  return waves;
+}
+
+// waves per (sub-domain, level, field group) plane of a span list: the segment heuristic's
+// strip count
+double span_waves_per_plane(const std::vector<int>& spans, int nsub) {
+  double w = 0.0;
+  for (int e : spans) w += 1.0 / (1 << span_class(span_nout(e)));
+  return w / nsub;
+}
+
+// One march as two kernels: the tile-edge spans (EX forms, their register count) and the
+// interior strips (A2_IN prefetch depth, OCC_IN workgroups per CU).  Each launch registers its
+// share of the algorithmic bytes (by output columns).
 template <int ORD, bool MF, int NF, int TM, int OCC_IN, bool A2_IN, int OCC_EX = 0, bool A2_EX = true>
 void march2(const Ctx& c, const TpM& m0, double bytes, const char* name_ex, const char* name_in) {
   std::vector<int> pex, pin;
-  const double fex = ex_fraction(c, m0.nstrip, &pex, &pin);
-  if ((int)pex.size() > MAXPAIR || (int)pin.size() > MAXPAIR || c.d.nsub > 128)
-    throw std::runtime_error("fv_tp_2d: too many (sub-domain, strip) pairs for one launch");
+  const double fex = plan_spans(c, pex, pin);
   auto go = [&](const std::vector<int>& pr, bool ex) {
     TpM m = m0;
-    // full strips first, then the paired last strips
-    std::vector<int> full, half;
-    for (int v : pr) ((m0.pairlast && (v & 255) == m0.nstrip - 1) ? half : full).push_back(v);
-    m.npair = (int)full.size();
-    m.npairh = (int)half.size();
-    for (int q = 0; q < m.npair; ++q) m.pairs[q] = full[q];
-    for (int q = 0; q < m.npairh; ++q) m.pairs[m.npair + q] = half[q];
-    const long kh = (m.nk + 1) / 2;
-    const long waves = (long)m.ntg * m.nseg * ((long)m.nk * m.npair + kh * m.npairh);
-    if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
+    const long waves = set_spans(m, pr);
     const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
     if (ex) GT_LAUNCH_N(name_ex, (tp_march<ORD, A2_EX, MF, NF, TM, OCC_EX, 1>), g, b, 0, c.st, m);
     else GT_LAUNCH_N(name_in, (tp_march<ORD, A2_IN, MF, NF, TM, OCC_IN, 2>), g, b, 0, c.st, m);
@@ -1038,7 +1058,7 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     m.d = d;
     m.subs = c.subs;
     m.M = c.met;
-  m.area2 = c.area2;
+  m.area4 = c.area4;
     const long tstride = (long)a.nk * d.plane;  // next tracer of the same sub-domain
     // field f of a group at slot f (the group's plane offset is added in the kernel); every
     // slot below NFw must be set: a null or stale slot is an out-of-bounds access
@@ -1092,16 +1112,17 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     // Default: segments of <= 45 rows, more (down to 15 rows) when the launch would
     // otherwise have fewer than ~6900 field-waves (the C180 count on one GPU; small
     // sub-domains, as on 4-8 GPUs, need the shorter segments to fill the chip).
-    const int nstrip = (d.nx + 1 + MOUT - 1) / MOUT;
+    std::vector<int> spans;
+    plan_spans(c, spans, spans);
+    const double wpp = span_waves_per_plane(spans, d.nsub);
     int seg = a.cfg >= 8 ? a.cfg : seg_env;
     if (seg < 8) {
-      const long fw = nz * NFw * nstrip;
+      const long fw = std::max<long>(1, (long)(nz * NFw * wpp));
       const long want = (6912 + fw - 1) / fw;
       const long nseg = std::max<long>((d.ny + 44) / 45, std::min<long>((d.ny + 14) / 15, want));
       seg = (int)((d.ny + nseg - 1) / nseg);
     }
     m.seg = seg;
-    m.nstrip = nstrip;
     m.nseg = (d.ny + seg - 1) / seg;
     // algorithmic bytes: q read + fx, fy written per field plane; crx cry xfx yfx (+ mfx mfy)
     // read once per (sub-domain, level) however many fields share them (ra_x, ra_y are
@@ -1118,8 +1139,7 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     // MF: separate mass fluxes (w, pt and the tracers) or xfx / yfx themselves
     // (the paired last strip of the split thermo march measured 7 us slower per launch here,
     // 242 -> 249 us at C180, in either wave order: single-kernel marches keep one level per wave)
-    const long waves = (long)m.nseg * nz * m.nstrip;
-    if (waves >= (1L << 31)) throw std::runtime_error("fv_tp_2d: too many strips for one launch");
+    const long waves = set_spans(m, spans);
     const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
 #define TP_GO(O, M_, F_)                                                                           \
   do {                                                                                             \
@@ -1174,7 +1194,7 @@ void d_sw_thermo_march(const Ctx& c, const ThermoArgs& a) {
   m.d = d;
   m.subs = c.subs;
   m.M = c.met;
-  m.area2 = c.area2;
+  m.area4 = c.area4;
   m.qf[0] = a.delp; m.qf[1] = a.w; m.qf[2] = a.pt;
   m.qo[0] = a.delp_o; m.qo[1] = a.w_o; m.qo[2] = a.pt_o;
   m.nt = 1;
@@ -1185,8 +1205,10 @@ void d_sw_thermo_march(const Ctx& c, const ThermoArgs& a) {
   m.my = a.mfy;
   const long nz = (long)d.nsub * a.npz;
   m.nz = (int)nz;
-  const int nstrip = (d.nx + 1 + MOUT - 1) / MOUT;
-  const long fw = nz * 3 * nstrip;
+  std::vector<int> pex, pin;
+  plan_spans(c, pex, pin);
+  pex.insert(pex.end(), pin.begin(), pin.end());
+  const long fw = std::max<long>(1, (long)(nz * 3 * span_waves_per_plane(pex, d.nsub)));
   const long want = (6912 + fw - 1) / fw;
   const long nseg = std::max<long>((d.ny + 44) / 45, std::min<long>((d.ny + 14) / 15, want));
   m.seg = (int)((d.ny + nseg - 1) / nseg);
@@ -1195,10 +1217,8 @@ void d_sw_thermo_march(const Ctx& c, const ThermoArgs& a) {
     return e ? atoi(e) : 0;
   }();
   if (seg_env >= 8) m.seg = seg_env;
-  m.nstrip = nstrip;
   m.nseg = (d.ny + m.seg - 1) / m.seg;
   if (m.seg + 10 > DXL_ROWS) throw std::runtime_error("d_sw thermo march: segment longer than the LDS dxa rows");
-  m.pairlast = pair_last_strip(d, nstrip) ? 1 : 0;
   // delp w pt read and written, crx cry xfx yfx read, mfx mfy read and written; the
   // interior strips prefetch one row ahead to fit two waves per SIMD (233 VGPRs; the
   // tile-edge form takes 292 with the two-ahead prefetch)
