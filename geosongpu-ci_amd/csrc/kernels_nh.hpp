@@ -45,7 +45,6 @@ void riem_solver3(const Ctx& c, const Riem3Args& a, const NhScratch& sc);
 // Riemann kernel form: 0 = register-resident level blocks (default), 1 = column sweeps
 // through scratch planes (riem_col_k, kept as the bitwise reference of the blocked form)
 void set_riem_variant(int v);
-void riem_debug(double* buf, int col);  // debug: dump one column's intermediates (scan form)
 int riem_variant();
 void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* delp, double* pk3, double* pe);
 void a2b_ord4(const Ctx& c, int nk, const double* q, double* qout, double* qx, double* qy);
@@ -74,9 +73,9 @@ struct RemapScratch {
 };
 int remap_jobs(int nq);
 int remap_scratch_slots(int nq);  // scratch column sets (jobs run in chunks of this many)
-// variant: 0 = the level-block form (remap_blk_k) where a shape is instantiated, else the
-// register-resident columns (L10/12/20/72) or the scratch-column jobs; 2 = the register
-// columns; 1 = the scratch-column jobs (remap_job_k)
+// variant: 0 = the level-block form (remap_blkq_k tracers) where a shape is instantiated, else
+// the scratch-column jobs (remap_job_k, the generic form for any level count); 3 = the level
+// blocks one tracer per wave; 1 = the scratch-column jobs
 int remap_variant();  // GTFV3_REMAP (default 0: the level-block form where instantiated)
 void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fill, const double* ak_dev,
                             const double* bk_dev, const RemapState& S, const RemapScratch& R, int variant = 0,

@@ -7,11 +7,11 @@
 // columns x jobs lanes instead of one lane doing every field in series.  Lanes are
 // consecutive i, so every k-plane access of a wave is coalesced.
 //
-// Two forms, bit-identical: remap_reg_k (default at L10/12/20/72: the column in
-// registers + LDS, see below) and remap_job_k (any level count: per job the edge values
+// Two forms, bit-identical, both with the expressions of oracle/fv_mapz.py: the level-block
+// form (remap_blk_k / remap_blkq_k, default where a block shape covers the level count,
+// see below) and remap_job_k (the generic form for any level count: per job the edge values
 // q, the tridiagonal gam and a copy of the source means live in HBM scratch columns; the
-// per-layer coefficients are recomputed on the fly in the integration walk), both with
-// the expressions of oracle/fv_mapz.py.
+// per-layer coefficients are recomputed on the fly in the integration walk).
 #include <cstdlib>
 #include <type_traits>
 #include <utility>
@@ -319,7 +319,7 @@ __device__ void map1(const Edges& E, const Col& A, const Targets& T, const Col& 
 }
 
 // map1_ppm as ONE streaming sweep over the source layers with the target pointer dynamic
-// (the register form's walk, remap_reg_k below): per source layer the PPM coefficients from
+// (remap_job_k's walk): per source layer the PPM coefficients from
 // a sliding window of means A[l-2 .. l+2] and edges q[l], q[l+1], then every target piece
 // inside the layer.  The loads of a layer are issued two layers ahead, independent of the
 // data-dependent walk, instead of the two-pointer search's chain of dependent HBM round
@@ -573,383 +573,10 @@ __global__ void __launch_bounds__(BLOCK) remap_job_k(RemapArgs a) {
   if (job >= J_Q0 && a.fill && neg) fillz_col(OUT, [&](int k) { return T(k + 1) - T(k); }, km);
 }
 
-// ---------------- register-resident column form (default for the instantiated level counts) ----------------
-//
-// One lane per (column, job) as in remap_job_k, one kernel instantiation per job kind
-// (T_v, delz, w, winds, tracers; a single kernel for all kinds was unswitched by the
-// compiler into 90-170 KB of code).  The job's column stays on chip: the source means
-// A[KM] and the forward-elimination values in VGPRs (AGPRs take the overflow), the
-// tridiagonal factors gam in LDS (one column per lane at [e][lane]: conflict-free 8-byte
-// accesses) and, once the back substitution has consumed each factor, the constrained
-// edge value in its slot; the ak / bk table in LDS.  map1_ppm runs as ONE top-down sweep
-// over the source layers with the target pointer k dynamic: a target layer is opened in
-// the source layer holding its top, accumulates whole layers and is closed in the layer
-// holding its bottom — the same terms added in the same order as the two-pointer walk of
-// remap_job_k (oracle/fv_mapz.py map1_ppm), so the results are bit-identical
-// (tests/test_gpu_remap.py).  Per job the field is read once and written once (in place:
-// A is in registers before the first output is stored); the edge pressures are re-read
-// from cache PF levels / one chunk ahead of their use.  No HBM scratch: remap_job_k moved
-// ~8x its algorithmic bytes through its edge / factor / source-copy scratch columns.
-// Measured C180 L72 (one MI355X): the nine jobs 2.6 ms per step against 4.4 ms; SQ
-// counters: ~207 VALU instructions per level and lane, one wave per SIMD (LDS-bound:
-// 38.5 KB per 64-lane workgroup), 58 % of wave cycles issuing — arithmetic-bound at that
-// occupancy, not memory-bound.
-typedef unsigned int RmU2 __attribute__((ext_vector_type(2)));
-// a scheduling fence every few levels: left alone the scheduler hoists the edge-pressure
-// loads of all 73 interfaces ahead of the recurrences and runs out of registers
-#define RM_FENCE() __builtin_amdgcn_sched_barrier(0)
-constexpr int PF = 8;  // prefetch distance (levels) of the edge-pressure loads
-// job kinds of the register form: one kernel instantiation per kind, so no branch on the
-// kind is left in the body (a single kernel for all kinds was unswitched by the compiler
-// into one copy of the column code per kind: 90-170 KB of code)
+// job kinds of the level-block form: one kernel instantiation per kind, so no branch on the
+// kind is left in the body (a single kernel for all kinds was unswitched by the compiler into
+// one copy of the column code per kind: 90-170 KB of code)
 enum { JK_PT = 0, JK_DZ = 1, JK_W = 2, JK_UV = 3, JK_Q = 4 };
-template <int KM, int JK, int CHK = 8>
-__global__ void __launch_bounds__(64) remap_reg_k(RemapArgs a) {
-  __shared__ double lg[(KM + 1) * 64];  // gam of lane l at lg[e * 64 + l]
-  __shared__ double lab[2 * (KM + 1)];  // ak | bk
-  const int lane = threadIdx.x;
-  for (int k = lane; k <= KM; k += 64) {
-    lab[k] = a.ak[k];
-    lab[KM + 1 + k] = a.bk[k];
-  }
-  __syncthreads();
-  // everything the lambdas below use is copied out of the kernel argument first (a lambda
-  // capturing `a` would take its address and put the whole argument struct in scratch)
-  const Dims d = a.d;
-  const double ptop = a.ptop;
-  const int fill = a.fill;
-  const int job = JK == JK_PT ? J_PT : JK == JK_DZ ? J_DZ : JK == JK_W ? J_W
-                : JK == JK_UV ? J_U + (int)blockIdx.y : J_Q0 + (int)blockIdx.y;
-  const int s = blockIdx.z;
-  const int nxe = d.nx + 1;
-  const int c = blockIdx.x * 64 + lane;
-  if (c >= nxe * (d.ny + 1)) return;  // no barrier follows
-  const int i = c % nxe, j = c / nxe;
-  if (job == J_U) {
-    if (i >= d.nx) return;
-  } else if (job == J_V) {
-    if (j >= d.ny) return;
-  } else if (i >= d.nx || j >= d.ny) {
-    return;
-  }
-  const long P = d.plane, o = pidx(d, i, j);
-  // Memory through buffer descriptors (wave-uniform base of the sub-domain's field) with the
-  // lane's column plus the level as the 32-bit vector offset (the range check covers it; the
-  // scalar offset would not be checked), so the 73 level addresses cost no 64-bit VGPR pairs
-  const uint32_t PB = (uint32_t)P * 8u, vo = (uint32_t)o * 8u;
-  auto rsrc = [&](const double* base, int nk) {
-    return __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, (int)(nk * PB), 0x00020000);
-  };
-  auto ld = [&](__amdgpu_buffer_rsrc_t r, uint32_t v, int lev) {
-    return __builtin_bit_cast(double, __builtin_amdgcn_raw_buffer_load_b64(r, v + (uint32_t)lev * PB, 0, 0));
-  };
-  const double* pe_s = a.S.pe + (long)s * (KM + 1) * P;
-  const auto rPE = rsrc(pe_s, KM + 1);
-  // source edges E(l): own column (pe, or peln for T_v) or the average of two (winds);
-  // target edges T(k): 0 ak + bk ps, 1 log of that, 2 ak + bk/2 (ps_left + ps_right)
-  auto rEA = rPE;
-  uint32_t vob = vo;
-  constexpr bool ewind = JK == JK_UV;
-  constexpr int tkind = JK == JK_PT ? 1 : (JK == JK_UV ? 2 : 0);
-  constexpr int iv = JK == JK_W ? -2 : (JK == JK_UV ? -1 : (JK == JK_Q ? 0 : 1));
-  const double ps = ld(rPE, vo, KM);
-  double lntop = 0.0, lnbot = 0.0, pb = 0.0;
-  const double* src;
-  double* out;
-  double qs = 0.0;
-  const long slot = ((long)s * a.nslot + job) * (KM + 1) * P;  // (T_v, delz only: job < 2)
-  if (JK == JK_PT) {
-    rEA = rsrc(a.S.peln + (long)s * (KM + 1) * P, KM + 1);
-    lntop = ld(rEA, vo, 0);
-    lnbot = ld(rEA, vo, KM);
-    src = a.src + slot;
-    out = a.S.pt + (long)s * KM * P;
-  } else if (JK == JK_DZ) {
-    src = a.src + slot;
-    out = a.S.delz + (long)s * KM * P;
-  } else {
-    double* f;
-    if (JK == JK_W) {
-      f = a.S.w + (long)s * KM * P;
-      qs = a.S.ws[(long)s * P + o];
-    } else if (JK == JK_UV) {
-      f = (job == J_U ? a.S.u : a.S.v) + (long)s * KM * P;
-      const long w = job == J_U ? -d.pitch : -1;
-      vob = (uint32_t)(o + w) * 8u;
-      pb = ld(rPE, vob, KM) + ps;
-    } else {
-      f = a.S.q + ((long)s * a.nq + (job - J_Q0)) * KM * P;
-    }
-    src = f;
-    out = f;
-  }
-  const auto rSRC = rsrc(src, KM), rOUT = rsrc(out, KM);
-  auto E = [&](int l) -> double {
-    if (!ewind) return ld(rEA, vo, l);
-    return l == 0 ? ld(rEA, vo, 0) : 0.5 * (ld(rEA, vob, l) + ld(rEA, vo, l));
-  };
-  auto T = [&](int k) -> double {
-    if (tkind == 0) return k == 0 ? ptop : (k == KM ? ps : lab[k] + lab[KM + 1 + k] * ps);
-    if (tkind == 1) return k == 0 ? lntop : (k == KM ? lnbot : log(lab[k] + lab[KM + 1 + k] * ps));
-    return lab[k] + 0.5 * lab[KM + 1 + k] * pb;
-  };
-  auto put = [&](int k, double v) {
-    __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(RmU2, v), rOUT, vo + (uint32_t)k * PB, 0, 0);
-  };
-  auto G = [&](int e) -> double& { return lg[e * 64 + lane]; };
-
-  double A[KM];
-#pragma unroll
-  for (int k = 0; k < KM; ++k) A[k] = ld(rSRC, vo, k);
-  // clamped static index (the out-of-range reads sit in branches folded away per level)
-  auto Aa = [&](int e) { return A[e < 0 ? 0 : (e > KM - 1 ? KM - 1 : e)]; };
-  // large-scale constraint of edge e (same expressions as cs_edges)
-  auto constrain = [&](int e, double v) {
-    if (e == 1 || e == KM - 1) {
-      v = fmin(v, fmax(Aa(e - 1), Aa(e)));
-      return fmax(v, fmin(Aa(e - 1), Aa(e)));
-    }
-    if (e >= 2 && e <= KM - 2) {
-      const double g0 = Aa(e - 1) - Aa(e - 2), g1 = Aa(e + 1) - Aa(e);
-      if (g0 * g1 > 0.0) {
-        v = fmin(v, fmax(Aa(e - 1), Aa(e)));
-        v = fmax(v, fmin(Aa(e - 1), Aa(e)));
-      } else if (g0 > 0.0) {
-        v = fmax(v, fmin(Aa(e - 1), Aa(e)));
-      } else {
-        v = fmin(v, fmax(Aa(e - 1), Aa(e)));
-        if (iv == 0) v = fmax(0.0, v);
-      }
-    }
-    return v;
-  };
-
-  // ---- constrained edge values (kord = 9 cs_profile), forward elimination + back substitution.
-  // The forward values qp stay in VGPRs, the factors gam go to LDS; the back substitution
-  // reads gam[e] and puts the final edge value in the slot it just freed (iv = -2: q[e] in
-  // slot e+1, q[km] = qs in a register), so the sweep below holds only A in registers.
-  double qp[KM];
-  double qtop = 0.0;  // q[km]
-  if constexpr (iv == -2) {
-    double gp = 0.5;  // gam[1]
-    G(1) = gp;
-    double qv = 1.5 * A[0];
-    qp[0] = qv;
-    // edge pressures loaded PF levels ahead of their use (the fences below stop the
-    // scheduler from hoisting them itself)
-    double Ev[KM + 1];
-#pragma unroll
-    for (int e = 0; e <= PF && e <= KM; ++e) Ev[e] = E(e);
-    double el = Ev[1];
-    double dprev = el - Ev[0];  // DP(0)
-#pragma unroll
-    for (int e = 1; e < KM - 1; ++e) {
-      if (e + PF <= KM) Ev[e + PF] = E(e + PF);
-      const double en = Ev[e + 1];
-      const double dcur = en - el;  // DP(e)
-      const double grat = dprev / dcur;
-      const double bet = 2.0 + grat + grat - gp;
-      qv = (3.0 * (A[e - 1] + A[e]) - qv) / bet;
-      qp[e] = qv;
-      gp = grat / bet;
-      G(e + 1) = gp;
-      dprev = dcur;
-      el = en;
-      if ((e & 3) == 3) RM_FENCE();
-    }
-    const double grat = dprev / (Ev[KM] - el);  // DP(km-2) / DP(km-1)
-    double x = (3.0 * (A[KM - 2] + A[KM - 1]) - grat * qs - qv) / (2.0 + grat + grat - gp);
-    qtop = qs;
-    G(KM) = constrain(KM - 1, x);
-#pragma unroll
-    for (int e = KM - 2; e >= 0; --e) {
-      x = qp[e] - G(e + 1) * x;
-      G(e + 1) = constrain(e, x);
-      if ((e & 3) == 0) RM_FENCE();
-    }
-  } else {
-    double Ev[KM + 1];
-#pragma unroll
-    for (int e = 0; e <= PF && e <= KM; ++e) Ev[e] = E(e);
-    const double e0 = Ev[0], e1 = Ev[1];
-    double dprev = e1 - e0;  // DP(0)
-    const double grat = (Ev[2] - e1) / dprev;
-    double bet = grat * (grat + 0.5);
-    double qv = ((grat + grat) * (grat + 1.0) * A[0] + A[1]) / bet;
-    qp[0] = qv;
-    double gp = (1.0 + grat * (grat + 1.5)) / bet;
-    G(0) = gp;
-    double d4 = grat;
-    double el = e1;
-#pragma unroll
-    for (int e = 1; e < KM; ++e) {
-      if (e + PF <= KM) Ev[e + PF] = E(e + PF);
-      const double en = Ev[e + 1];
-      const double dcur = en - el;  // DP(e)
-      d4 = dprev / dcur;
-      bet = 2.0 + d4 + d4 - gp;
-      qv = (3.0 * (A[e - 1] + d4 * A[e]) - qv) / bet;
-      qp[e] = qv;
-      gp = d4 / bet;
-      G(e) = gp;
-      dprev = dcur;
-      el = en;
-      if ((e & 3) == 3) RM_FENCE();
-    }
-    const double a_bot = 1.0 + d4 * (d4 + 1.5);
-    double x = (2.0 * d4 * (d4 + 1.0) * A[KM - 1] + A[KM - 2] - a_bot * qv) / (d4 * (d4 + 0.5) - a_bot * gp);
-    qtop = x;
-#pragma unroll
-    for (int e = KM - 1; e >= 0; --e) {
-      x = qp[e] - G(e) * x;
-      G(e) = constrain(e, x);
-      if ((e & 3) == 0) RM_FENCE();
-    }
-  }
-  // the sweep re-reads the edge pressures (cache hits) instead of keeping the forward
-  // sweep's 73 values live across the back substitution
-  asm volatile("" ::: "memory");
-  // final edge value e (static e)
-  constexpr int qo = iv == -2 ? 1 : 0;
-  auto Q = [&](int e) -> double { return e == KM ? qtop : lg[(e + qo) * 64 + lane]; };
-
-  // ---- map1_ppm as one sweep over the source layers, in chunks of CH layers: the chunk
-  // body is instantiated once (static_for over the layer offset lo, so its indices into A
-  // are constants) and the chunk loop stays rolled; after a chunk the register array A is
-  // shifted down by CH (static moves), so layer l = base + lo always finds its means at
-  // A[lo - 2 .. lo + 2] (the two before the chunk in Ap).  A fully unrolled 72-layer
-  // sweep was ~300 KB of code: instruction fetch, not arithmetic, bounded it.
-  constexpr int CH = KM % CHK == 0 ? CHK : KM;
-  double Ap[2] = {0.0, 0.0};  // A[base-2], A[base-1]
-  auto Aw = [&](int i) -> double { return i < 0 ? Ap[i + 2] : A[i > KM - 1 ? KM - 1 : i]; };
-  // PPM coefficients of source layer l = base + lo (kord = 9 cs_profile + cs_limiters)
-  auto coef = [&](int lo, int l, double& AL, double& AR, double& A6) {
-    auto gm = [&](int e) { return Aw(e) - Aw(e - 1); };  // local index e
-    auto extm = [&](int e) { return gm(e) * gm(e + 1) < 0.0; };
-    const double av = Aw(lo);
-    AL = Q(l);
-    AR = Q(l + 1);
-    if (l == 0) {
-      if (iv == 0) AL = fmax(0.0, AL);
-      else if (iv == -1 && AL * av <= 0.0) AL = 0.0;
-      A6 = 3.0 * (2.0 * av - (AL + AR));
-      lim(av, AL, AR, A6, false, 1);
-    } else if (l == 1) {
-      A6 = 3.0 * (2.0 * av - (AL + AR));
-      lim(av, AL, AR, A6, extm(lo), 2);
-    } else if (l < KM - 2) {
-      const bool el = extm(lo);
-      if ((el && extm(lo - 1)) || (el && extm(lo + 1))) {
-        AL = av; AR = av; A6 = 0.0;
-      } else {
-        A6 = 6.0 * av - 3.0 * (AL + AR);
-        if (fabs(A6) > fabs(AL - AR)) {
-          double pmp_1 = av - 2.0 * gm(lo + 1);
-          double lac_1 = pmp_1 + 1.5 * gm(lo + 2);
-          AL = fmin(fmax(AL, fmin(fmin(av, pmp_1), lac_1)), fmax(fmax(av, pmp_1), lac_1));
-          double pmp_2 = av + 2.0 * gm(lo);
-          double lac_2 = pmp_2 - 1.5 * gm(lo - 1);
-          AR = fmin(fmax(AR, fmin(fmin(av, pmp_2), lac_2)), fmax(fmax(av, pmp_2), lac_2));
-          A6 = 6.0 * av - 3.0 * (AL + AR);
-        }
-      }
-      if (iv == 0) lim(av, AL, AR, A6, el, 0);
-    } else if (l == KM - 2) {
-      A6 = 3.0 * (2.0 * av - (AL + AR));
-      lim(av, AL, AR, A6, extm(lo), 2);
-    } else {
-      if (iv == 0) AR = fmax(0.0, AR);
-      else if (iv == -1 && AR * av <= 0.0) AR = 0.0;
-      A6 = 3.0 * (2.0 * av - (AL + AR));
-      lim(av, AL, AR, A6, false, 1);
-    }
-  };
-
-  int k = 0;            // next target layer to finish
-  bool open = false;    // target k started in an earlier source layer
-  double qsum = 0.0, topk = 0.0, bot = 0.0;
-  double topv = T(0);   // top of target k when not open
-  // target edges one target ahead: tb1 = T(k+1), tb2 = T(k+2) (the LDS read and, for T_v,
-  // the log of the next target's bottom overlap the current target's work)
-  double tb1 = T(1), tb2 = T(KM >= 2 ? 2 : 1);
-  auto advance = [&]() {
-    ++k;
-    tb1 = tb2;
-    tb2 = T(k + 2 <= KM ? k + 2 : KM);
-  };
-  bool neg = false;     // a remapped value < 0 (fillz has work only then)
-  double e0 = E(0);
-  // this chunk's lower edges eb and the next chunk's nb, loaded one chunk ahead
-  double eb[CH], nb[CH];
-#pragma unroll
-  for (int m = 0; m < CH; ++m) eb[m] = E(1 + m);
-#pragma unroll 1
-  for (int base = 0; base < KM; base += CH) {
-    static_for<CH>([&](auto LC) {
-      constexpr int lo = decltype(LC)::value;
-      const int l = base + lo;
-      const double e1 = eb[lo];
-      if (base + CH + 1 + lo <= KM) nb[lo] = E(base + CH + 1 + lo);
-      double AL, AR, A6;
-      coef(lo, l, AL, AR, A6);
-      const double dpl = e1 - e0;
-      const double al = Aw(lo);
-      while (k < KM) {
-        if (open) {
-          if (bot > e1) {  // whole layer
-            qsum = qsum + dpl * al;
-            break;
-          }
-          const double dp = bot - e0;  // last (partial) piece
-          const double esl = dp / dpl;
-          qsum = qsum + dp * (AL + 0.5 * esl * (AR - AL + A6 * (1.0 - R23 * esl)));
-          const double v = qsum / (bot - topk);
-          put(k, v);
-          neg = neg || v < 0.0;
-          advance();
-          open = false;
-          topv = bot;
-          continue;
-        }
-        if (!(topv >= e0 && topv <= e1)) break;
-        bot = tb1;
-        const double pl = (topv - e0) / dpl;
-        if (bot <= e1) {  // target inside this layer
-          const double pr = (bot - e0) / dpl;
-          const double v = AL + 0.5 * (A6 + AR - AL) * (pr + pl) - A6 * R3 * (pr * (pr + pl) + pl * pl);
-          put(k, v);
-          neg = neg || v < 0.0;
-          advance();
-          topv = bot;
-          continue;
-        }
-        // first (partial) piece; the target continues below
-        qsum = (e1 - topv) * (AL + 0.5 * (A6 + AR - AL) * (1.0 + pl) - A6 * (R3 * (1.0 + pl * (1.0 + pl))));
-        topk = topv;
-        open = true;
-        break;
-      }
-      e0 = e1;
-    });
-    // next chunk: its layers' means move to the front of A, its edges into eb
-#pragma unroll
-    for (int m = 0; m < CH; ++m) eb[m] = nb[m];
-    Ap[0] = A[CH - 2];
-    Ap[1] = A[CH - 1];
-#pragma unroll
-    for (int m = 0; m + CH < KM; ++m) A[m] = A[m + CH];
-  }
-  if (open) {  // bottom beyond the last source edge (the walk ran out of layers)
-    const double v = qsum / (bot - topk);
-    put(k, v);
-    neg = neg || v < 0.0;
-  }
-  if (JK == JK_Q && fill && neg) {
-    // the buffer stores above must land before fillz reads the column back
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    fillz_col(Col{out + o, P}, [&](int kk) { return T(kk + 1) - T(kk); }, KM);
-  }
-}
 
 // ---------------- level-block form (default where instantiated) ----------------
 //
@@ -1637,8 +1264,8 @@ __global__ void __launch_bounds__(BLOCK) remap_finish_k(RemapArgs a) {
 
 int remap_jobs(int nq) { return nq + J_Q0; }
 
-// the step's remap form: GTFV3_REMAP (0 the level-block form, 2 the register columns, 1 the
-// scratch-column jobs; see lagrangian_to_eulerian)
+// the step's remap form: GTFV3_REMAP (0 the level-block form, 1 the scratch-column jobs, 3 the
+// level-block form one tracer per wave; see lagrangian_to_eulerian)
 int remap_variant() {
   static const int env = [] {
     const char* e = std::getenv("GTFV3_REMAP");
@@ -1685,8 +1312,9 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
     gt_bytes(L * 5 * e.C);  // delp delz pt read, T_v and -delz/delp source columns written
   }
   // variant 0: the level-block form where a shape is instantiated ((NB - 1) M < npz <= NB M),
-  // tracers RB_NT per wave (remap_blkq_k); 3: the same with one tracer per wave (remap_blk_k);
-  // 2: the register-resident columns (L10 / 12 / 20 / 72); 1 (or no shape): the scratch-column jobs
+  // tracers RB_NT per wave (remap_blkq_k); 3: the same with one tracer per wave (remap_blk_k,
+  // the bit-identity reference of the shared-pivot form); 1 (or a level count no block shape
+  // covers: 6, 9, 13-15, 21-63, 73-90, 97-135, > 144): the scratch-column jobs, the generic form
   auto fits = [&](int m, int nb) { return (nb - 1) * m < npz && npz <= nb * m; };
   auto blk = [&](auto Mc, auto NBc, auto PARTc) {
     constexpr int M = decltype(Mc)::value, NB = decltype(NBc)::value;
@@ -1729,31 +1357,6 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
     blk(integral_constant<int, 3>{}, integral_constant<int, 4>{}, std::true_type{});
   } else if (b0 && fits(2, 4)) {
     blk(integral_constant<int, 2>{}, integral_constant<int, 4>{}, std::true_type{});
-  } else if (variant != 1 && (npz == 72 || npz == 10 || npz == 12 || npz == 20)) {
-    const unsigned gx = cdiv(nce, 64);
-    auto go = [&](auto KMc, auto CHc) {
-      constexpr int KM = decltype(KMc)::value, CH = decltype(CHc)::value;
-      // per launch: each job's source column read and its field written (L levels), the
-      // source pressures (pe, + peln for T_v; winds: pe of both neighbours) read once
-      if (p1) {
-        GT_LAUNCH((remap_reg_k<KM, JK_PT, CH>), dim3(gx, 1, d.nsub), dim3(64), 0, c.st, a);
-        gt_bytes(L * 2 * e.C + L1 * 2 * e.C);
-        GT_LAUNCH((remap_reg_k<KM, JK_DZ, CH>), dim3(gx, 1, d.nsub), dim3(64), 0, c.st, a);
-        gt_bytes(L * 2 * e.C + L1 * e.C);
-        GT_LAUNCH((remap_reg_k<KM, JK_W, CH>), dim3(gx, 1, d.nsub), dim3(64), 0, c.st, a);
-        gt_bytes(L * 2 * e.C + L1 * e.C + e.C);
-        GT_LAUNCH((remap_reg_k<KM, JK_UV, CH>), dim3(gx, 2, d.nsub), dim3(64), 0, c.st, a);
-        gt_bytes(L * 2 * (e.X + e.Y) + L1 * e.C);
-      }
-      if (p2 && nq > 0) {
-        GT_LAUNCH((remap_reg_k<KM, JK_Q, CH>), dim3(gx, nq, d.nsub), dim3(64), 0, c.st, a);
-        gt_bytes(nq * L * 2 * e.C + L1 * e.C);
-      }
-    };
-    if (npz == 72) go(std::integral_constant<int, 72>{}, std::integral_constant<int, 8>{});
-    else if (npz == 10) go(std::integral_constant<int, 10>{}, std::integral_constant<int, 8>{});
-    else if (npz == 12) go(std::integral_constant<int, 12>{}, std::integral_constant<int, 8>{});
-    else go(std::integral_constant<int, 20>{}, std::integral_constant<int, 8>{});
   } else {
     // every job reads its source column and writes its field (L each), pe + peln once, ws;
     // each chunk registers its jobs' share

@@ -39,11 +39,7 @@ struct RiemArgs {
   double *pk3, *pe, *peln, *pk;  // D-grid only (pe/peln/pk on the last call)
   double* ws_out;  // D-grid: surface w for the remap (may be null)
   double *gam, *pp, *w2;  // scratch, L+1 planes each
-  double* dbg = nullptr;   // debug: intermediates of column dbg_col of sub-domain 0 (scan form)
-  int dbg_col = -1;
 };
-double* g_riem_dbg = nullptr;
-int g_riem_dbg_col = -1;
 
 // The column body takes every array as a distinct __restrict__ pointer: the arrays never
 // alias, and saying so lets the compiler hoist the loads of an unrolled group of levels
@@ -354,15 +350,6 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
   const int i = c % ni - a.ring, j = c / ni - a.ring;
   const long P = d.plane;
   const long o = pidx(d, i, j);
-  // debug build only (-DGTFV3_RIEM_DEBUG, tools/dbg_riem_replay.py): one column's intermediates
-#ifdef GTFV3_RIEM_DEBUG
-  const bool dbg = a.dbg && s == 0 && c0 + lane / NB == a.dbg_col;
-  auto dump = [&](int phase, int m, double v) {
-    if (dbg) a.dbg[(phase * NB + b) * M + m] = v;
-  };
-#else
-  auto dump = [](int, int, double) {};
-#endif
   const double dt = a.dt, rdt = 1.0 / dt;
   const double gama = 1.0 / (1.0 - KAPPA);
   const double t1g = gama * 2.0 * dt * dt;
@@ -455,8 +442,6 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
       carry = b == r + 1 ? nx : carry;
     }
   }
-#pragma unroll
-  for (int m = 0; m < M; ++m) { dump(0, m, pem[m]); dump(13, m, gl[m]); dump(14, m, G[m]); }
 
   // ---- S1b: pointwise layer quantities (and pk3 / pe / peln / pk on the D grid)
   // per-layer values that live from the first sweep to the last, in LDS: pm, q = dm RDGAS pt
@@ -499,7 +484,6 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
       Spm[m][lane] = real(m) ? pmv : 0.0;
       Sq[m][lane] = dm[m] * RDGAS * PT[m];
       pl[m] = real(m) ? plv : 0.0;
-      dump(1, m, dz[m]); dump(2, m, pmv); dump(3, m, pl[m]);
     }
   }
 
@@ -528,8 +512,6 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
       cm = gv;
     };
     tri_solve<M, NB, true>(row, [&](int m) { return dd[m]; }, pp, b, last);
-#pragma unroll
-    for (int m = 0; m < M; ++m) { dump(4, m, Sg[m][lane]); dump(5, m, pp[m]); dump(15, m, dd[m]); }
   }
 
   // ---- S3/S4: the w system
@@ -577,12 +559,7 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
       const double v = dm[m] * W1[m] + dt * (pp[m] - ppi(m));
       return isbot(m) ? v - p1 * ws : (real(m) ? v : 0.0);
     };
-#pragma unroll
-    for (int m = 0; m < M; ++m) { dump(6, m, aat[m]); dump(16, m, rhs(m)); }
-    dump(17, 0, p1);
     tri_solve<M, NB, false>(row, rhs, w2, b, last);
-#pragma unroll
-    for (int m = 0; m < M; ++m) dump(7, m, w2[m]);
   }
 
   // ---- S5: pe prefix (top-down); w out
@@ -598,8 +575,6 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
     pe[0] = b == 0 ? 0.0 : ex;
 #pragma unroll
     for (int m = 0; m < M; ++m) pe[m + 1] = pe[m] + num[m];
-#pragma unroll
-    for (int m = 0; m < M; ++m) dump(8, m, pe[m]);
     if (a.w_out) {
       const auto rW = rs(a.w_out, false);
 #pragma unroll
@@ -640,7 +615,6 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
       const double pmk = Spm[m][lane];
       const double v = -Sq[m][lane] * fm_exp(capa1 * fm_log(fmax(a.p_fac * pmk, p1v[m] + pmk)));
       dz2[m] = real(m) ? v : 0.0;
-      dump(9, m, p1v[m]); dump(10, m, dz2[m]);
       tot += CG ? dz2[m] * GRAV : dz2[m];
     }
     // heights bottom-up from the surface
@@ -653,7 +627,6 @@ __global__ void __launch_bounds__(64 * RS_WAVES, 2) riem_scan_k(RiemArgs a) {
     for (int m = M - 1; m >= 0; --m) {
       gz = CG ? gz - dz2[m] * GRAV : gz - dz2[m];
       gzo[m] = gz;
-      dump(11, m, gz);
     }
 #pragma unroll
     for (int m = 0; m < M; ++m) sti(rG, m, gzo[m]);
@@ -698,9 +671,6 @@ void launch_riem(const Ctx& c, const RiemArgs& a) {
     return dim3(xcd_pad(cdiv(cdiv(ncol, 64 / nb), RS_WAVES)), c.d.nsub);
   };
   const bool scan = riem_variant() != 1;
-  RiemArgs& am = const_cast<RiemArgs&>(a);
-  am.dbg = g_riem_dbg;
-  am.dbg_col = g_riem_dbg_col;
 #define RIEM_SCAN(M_, NB_, PART_)                                                                   \
   do {                                                                                              \
     if (a.cgrid) GT_LAUNCH((riem_scan_k<M_, NB_, PART_, true>), grid(NB_), tb, 0, c.st, a);        \
@@ -726,10 +696,6 @@ void launch_riem(const Ctx& c, const RiemArgs& a) {
 }  // namespace
 
 void set_riem_variant(int v) { g_riem_variant = v; }
-void riem_debug(double* buf, int col) {
-  g_riem_dbg = buf;
-  g_riem_dbg_col = col;
-}
 // GTFV3_RIEM=1: the column sweeps on the step (A/B and fault isolation); the stencil
 // interface's explicit variant parameter overrides it
 int riem_variant() {

@@ -207,7 +207,7 @@ std::map<std::string, Fn>& reg() {
       // geopotential out.  params: dt2, ptop, p_fac, dz_min[, variant (0 blocked, 1 column)]
       {"riem_solver_c",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
-         if (f.size() != 6 && f.size() != 7) need(f, 6, "riem_solver_c");
+         need(f, 6, "riem_solver_c");
          const int npz = F(dy, f[0]).nk;
          if (F(dy, f[4]).nk != npz + 1 || F(dy, f[3]).nk != 1) throw std::runtime_error("riem_solver_c: field shapes");
          NhScratch sc{};
@@ -216,10 +216,8 @@ std::map<std::string, Fn>& reg() {
          sc.s[13] = dy.field("_riem_w2", npz + 1).p;
          const int v0 = riem_variant();
          set_riem_variant(p.size() > 4 ? (int)p[4] : v0);
-         if (f.size() > 6) riem_debug(dy.field(f[6], 32).p, (int)p.at(5));  // debug dump of one column
          riem_solver_c(dy.ctx(), npz, p.at(0), p.at(1), p.at(2), p.at(3), F(dy, f[0]).p, F(dy, f[1]).p,
                        F(dy, f[2]).p, F(dy, f[3]).p, F(dy, f[4]).p, dy.field(f[5], npz + 1).p, sc);
-         riem_debug(nullptr, -1);
          set_riem_variant(v0);
        }},
       // riem_solver3(delp, pt, w, phis, zh | delz, ppe, pk3, pe, peln, pk, ws): w and zh in place.

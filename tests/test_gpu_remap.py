@@ -75,25 +75,6 @@ def test_remap_vs_oracle(pkg, require_gpu, npz, nq, variant):
             assert worst <= 1e-11, f"sub{s} {k}: max scaled error {worst:.3e}"
 
 
-@pytest.mark.parametrize("npz,nq", [(72, 4), (10, 3), (20, 2)])
-def test_remap_register_columns_bitwise(pkg, require_gpu, npz, nq):
-    """The register-resident column remap (remap_reg_k<L>, variant 2) gives bit for bit the
-    scratch-column job form (remap_job_k, variant 1) on the same displaced state."""
-    outs = []
-    for variant in (2, 1):
-        d = pkg.Domain(npx=13, npz=npz, nq=nq)
-        r = rng(700 + npz)
-        st, ak, bk, ks = lagrangian_state(pkg, d, npz, nq, r)
-        d.set_vertical(ak, bk, ks)
-        for k, v in st.items():
-            d.upload(k, v)
-        d.stencil("lagrangian_to_eulerian", [], [1, variant])
-        outs.append({k: d.download(k) for k in FIELDS})
-        d.close()
-    for k in FIELDS:
-        assert np.array_equal(outs[0][k], outs[1][k]), f"{k}: register columns differ from the job form"
-
-
 @pytest.mark.parametrize("npz,nq", [(72, 11), (137, 5), (10, 3)])
 def test_remap_shared_tracer_pivots_bitwise(pkg, require_gpu, npz, nq):
     """The tracer jobs with the pressure part shared by four tracers per wave (remap_blkq_k,
