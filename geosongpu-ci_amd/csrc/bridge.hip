@@ -4,6 +4,7 @@
 #include <dlfcn.h>
 #include <unistd.h>
 
+#include <algorithm>
 #include <chrono>
 #include <cstdint>
 #include <cstdio>
@@ -43,105 +44,100 @@ struct FDesc {
   int order;                 // 0: (i,j,k)  1: (i,k,j)
 };
 
-template <typename T>
-__global__ void fort_to_dev(const T* __restrict__ f, double* __restrict__ dev, Dims d, int s, int nk_dev, FDesc fd,
-                            long t0, long n) {
-  long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n) return;
-  const long t = t0 + c;  // flat Fortran index of the element (this chunk starts at t0)
-  int i = (int)(t % fd.ni), j, k;
-  if (fd.order == 0) {
-    j = (int)((t / fd.ni) % fd.nj);
-    k = (int)(t / ((long)fd.ni * fd.nj));
-  } else {
-    k = (int)((t / fd.ni) % fd.nk);
-    j = (int)(t / ((long)fd.ni * fd.nk));
-  }
-  dev[((long)s * nk_dev + k) * d.plane + pidx(d, fd.ilo + i, fd.jlo + j)] = (double)f[c];
+// Host <-> HBM movement of one run call.  The Fortran arrays are page-locked and mapped once
+// (hipHostRegister: GEOS keeps them for the whole run).  Two transfer forms, both through one
+// kernel (fort_move) that converts layout and precision:
+//  * zero-copy: the kernel reads / writes the mapped Fortran array itself over PCIe -- one
+//    launch per array (or section), no staging buffer, no DMA;
+//  * staged: the array (in pieces of at most the staging buffer) by DMA into an HBM staging
+//    buffer and scattered from there, or gathered there and sent by DMA, in one stream's order.
+// GTFV3_BRIDGE_ZC (bit mask) picks zero-copy for: 1 the uploads before the step, 2 the uploads
+// beside it, 4 the copies back.  Default 1: a zero-copy transfer beside the step slows it (its
+// PCIe traffic goes through the CUs' memory path: gathers held the remap's kernels up ~10x,
+// 32-workgroup uploads the first acoustic sub-step by ~25 %), the DMA engine's does not; before
+// the step nothing else runs and the kernel form saves the DMA queue's per-copy latency.
+// Arrays that could not be mapped (or GTFV3_BRIDGE_PIN=0) always go staged.
+// Ordering (bridge_run): the arrays the step reads first go up before it; tracers 1.. and
+// omga's halo go up on the side stream beside the acoustic sub-steps (the step waits for them
+// before tracer_2d / fv_wrapup); each output group comes back on the side stream as soon as
+// the step marks it final (Dycore::StepMark), while the rest of the step runs.  The runtime
+// maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES, 4 by default) in creation order,
+// and two streams sharing a queue run in enqueue order: the step's three streams plus the side
+// stream fit, so side traffic queued ahead of the step never holds up a step kernel.
+enum { ZC_CRIT = 1, ZC_SIDE = 2, ZC_DOWN = 4 };
+int zc_mode() {
+  const char* e = std::getenv("GTFV3_BRIDGE_ZC");
+  return e && *e ? std::atoi(e) : ZC_CRIT;
 }
-
-template <typename T>
-__global__ void dev_to_fort(T* __restrict__ f, const double* __restrict__ dev, Dims d, int s, int nk_dev, FDesc fd,
-                            long t0, long n) {
-  long c = (long)blockIdx.x * blockDim.x + threadIdx.x;
-  if (c >= n) return;
-  const long t = t0 + c;
-  int i = (int)(t % fd.ni), j, k;
-  if (fd.order == 0) {
-    j = (int)((t / fd.ni) % fd.nj);
-    k = (int)(t / ((long)fd.ni * fd.nj));
-  } else {
-    k = (int)((t / fd.ni) % fd.nk);
-    j = (int)(t / ((long)fd.ni * fd.nk));
-  }
-  f[c] = (T)dev[((long)s * nk_dev + k) * d.plane + pidx(d, fd.ilo + i, fd.jlo + j)];
-}
-
-// Host <-> HBM pipeline of one run call (the reference alternates two CUDA streams for its
-// uploads, data_conversion.py:42-44,113-132).  The Fortran arrays are page-locked once
-// (hipHostRegister: GEOS keeps them for the whole run), so every copy is a DMA straight from
-// or to them.  Each array travels in chunks through a ring of staging buffers: the DMA of
-// chunk n+1 on the copy stream overlaps the scatter (fort_to_dev) or gather (dev_to_fort)
-// kernel of chunk n on the compute stream, events handing each buffer back and forth.
-constexpr int kRing = 3;
-constexpr size_t kChunkBytes = size_t(32) << 20;
-// chunk of one DMA (GTFV3_BRIDGE_CHUNK_KB, at most the 32 MiB staging buffer; tests use
-// small chunks to run the ring through many wrap-arounds)
-size_t chunk_bytes() {
-  const char* e = std::getenv("GTFV3_BRIDGE_CHUNK_KB");
+// staging buffer bytes (GTFV3_BRIDGE_STAGE_KB; tests use a small one to cut arrays into many
+// pieces): one C180 L72 array of four tracers fits the default
+size_t stage_bytes() {
+  const char* e = std::getenv("GTFV3_BRIDGE_STAGE_KB");
   const long kb = e ? std::atol(e) : 0;
-  return kb > 0 ? std::min(kChunkBytes, (size_t)kb << 10) : kChunkBytes;
+  return kb > 0 ? (size_t)kb << 10 : size_t(512) << 20;
+}
+// workgroups of a zero-copy launch beside the acoustic sub-steps (GTFV3_BRIDGE_ZC_BLOCKS):
+// enough lanes in flight to cover the PCIe round trip, few enough to leave the CUs to the step
+int zc_blocks(const char* env, int dflt) {
+  const char* e = std::getenv(env);
+  const int b = e ? std::atoi(e) : 0;
+  return b > 0 ? b : dflt;
 }
 
 struct BridgeIO {
-  hipStream_t cp = nullptr;  // DMA stream
-  hipStream_t tr = nullptr;  // scatters of the tracers that upload beside the step
-  void* ring[kRing] = {};
-  hipEvent_t landed[kRing] = {}, freed[kRing] = {};
-  bool used[kRing] = {};
-  int next = 0;
-  hipEvent_t ev_t[4] = {};     // call start, state scattered, step done, last copy back
-  hipEvent_t ev_tracers = nullptr;
-  std::map<const void*, size_t> pinned;  // registered Fortran arrays (pointer -> bytes)
-  double ms[3] = {0, 0, 0};    // last call: upload (critical path), step, download
+  hipStream_t side = nullptr;
+  void* stage = nullptr;  // staged form (reuse is ordered by the stream)
+  size_t stage_cap = 0;
+  hipEvent_t ev_t[4] = {};  // call start, state scattered, step done, last copy back
+  hipEvent_t ev_tracers = nullptr, ev_exit = nullptr, ev_crit = nullptr;
+  hipEvent_t marks[Dycore::SM_COUNT] = {};
+  struct Pinned {
+    size_t bytes;
+    void* dev;  // mapped device address (null: page-locked only)
+  };
+  std::map<const void*, Pinned> pinned;  // registered Fortran arrays
+  double ms[3] = {0, 0, 0};    // last call: upload before the step, step, copy-back tail
   double bytes[2] = {0, 0};    // last call: host bytes uploaded / downloaded
 
   void init() {
-    if (cp) return;
-    HIP_CHECK(hipStreamCreateWithFlags(&cp, hipStreamNonBlocking));
-    HIP_CHECK(hipStreamCreateWithFlags(&tr, hipStreamNonBlocking));
-    for (int b = 0; b < kRing; ++b) {
-      HIP_CHECK(hipMalloc(&ring[b], kChunkBytes));
-      HIP_CHECK(hipEventCreateWithFlags(&landed[b], hipEventDisableTiming));
-      HIP_CHECK(hipEventCreateWithFlags(&freed[b], hipEventDisableTiming));
-    }
+    if (side) return;
+    HIP_CHECK(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
     for (auto& e : ev_t) HIP_CHECK(hipEventCreate(&e));
-    HIP_CHECK(hipEventCreateWithFlags(&ev_tracers, hipEventDisableTiming));
+    for (hipEvent_t* e : {&ev_tracers, &ev_exit, &ev_crit}) HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+    for (auto& e : marks) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  }
+  void* staging() {
+    const size_t want = stage_bytes();
+    if (stage && stage_cap != want) {
+      // nothing queued may still use the old buffer
+      HIP_CHECK(hipDeviceSynchronize());
+      HIP_CHECK(hipFree(stage));
+      stage = nullptr;
+    }
+    if (!stage) {
+      HIP_CHECK(hipMalloc(&stage, want));
+      stage_cap = want;
+    }
+    return stage;
   }
   void release() {
-    if (!cp) return;
-    (void)hipStreamSynchronize(cp);
-    (void)hipStreamSynchronize(tr);
+    if (!side) return;
+    (void)hipStreamSynchronize(side);
     unpin_except({});
-    for (int b = 0; b < kRing; ++b) {
-      (void)hipFree(ring[b]);
-      (void)hipEventDestroy(landed[b]);
-      (void)hipEventDestroy(freed[b]);
-      ring[b] = nullptr;
-      used[b] = false;
-    }
+    if (stage) (void)hipFree(stage);
+    stage = nullptr;
     for (auto& e : ev_t) (void)hipEventDestroy(e);
-    (void)hipEventDestroy(ev_tracers);
-    (void)hipStreamDestroy(cp);
-    (void)hipStreamDestroy(tr);
-    cp = tr = nullptr;
+    for (hipEvent_t e : {ev_tracers, ev_exit, ev_crit}) (void)hipEventDestroy(e);
+    for (auto& e : marks) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(side);
+    side = nullptr;
   }
   // page-lock this call's arrays; arrays of earlier calls that are not among them are
   // released first (a caller that reallocates between calls keeps only one set pinned)
   void unpin_except(const std::vector<std::pair<const void*, size_t>>& keep) {
     for (auto it = pinned.begin(); it != pinned.end();) {
       bool k = false;
-      for (auto& p : keep) k = k || (p.first == it->first && p.second == it->second);
+      for (auto& p : keep) k = k || (p.first == it->first && p.second == it->second.bytes);
       if (!k) {
         (void)hipHostUnregister(const_cast<void*>(it->first));
         it = pinned.erase(it);
@@ -160,75 +156,153 @@ struct BridgeIO {
     for (auto& p : arrays) {
       if (pinned.count(p.first)) continue;
       // a range another array already pinned (or memory HIP allocated) stays pageable here
-      if (hipHostRegister(const_cast<void*>(p.first), p.second, hipHostRegisterDefault) == hipSuccess)
-        pinned[p.first] = p.second;
-      else
+      void* h = const_cast<void*>(p.first);
+      if (hipHostRegister(h, p.second, hipHostRegisterMapped) != hipSuccess) {
         (void)hipGetLastError();
+        continue;
+      }
+      void* dev = nullptr;
+      if (hipHostGetDevicePointer(&dev, h, 0) != hipSuccess) {
+        (void)hipGetLastError();
+        dev = nullptr;
+      }
+      pinned[p.first] = Pinned{p.second, dev};
     }
   }
-  // a staging buffer whose previous consumer (scatter kernel or DMA) has finished
-  int acquire(hipStream_t waiter) {
-    const int b = next;
-    next = (next + 1) % kRing;
-    if (used[b]) HIP_CHECK(hipStreamWaitEvent(waiter, freed[b], 0));
-    used[b] = true;
-    return b;
+  // the mapped device address of a registered array when this kind of transfer (ZC_*) goes
+  // zero-copy, else null
+  void* mapped(const void* host, int kind) const {
+    if (!(zc_mode() & kind)) return nullptr;
+    auto it = pinned.find(host);
+    return it == pinned.end() ? nullptr : it->second.dev;
   }
 };
 
 BridgeIO g_io;
 
-// Fortran array (all local sub-domains, tile-major) -> device field, chunked through the ring;
-// the scatter kernels run on `sst`
-template <typename T>
-double copy_in(Dycore& dy, const char* name, int nk_dev, const T* host, const FDesc& fd, hipStream_t sst,
-               int s_lo = 0, int s_hi = -1, long t_lo = 0, long t_hi = -1) {
-  Field& f = dy.field(name, nk_dev);
-  const long n = (long)fd.ni * fd.nj * fd.nk;
-  const long per = (long)(chunk_bytes() / sizeof(T));
-  if (s_hi < 0) s_hi = g_tiles_per_rank;
-  if (t_hi < 0) t_hi = n;
-  double bytes = 0;
-  for (int s = s_lo; s < s_hi; ++s) {
-    for (long t0 = t_lo; t0 < t_hi; t0 += per) {
-      const long m = std::min(per, t_hi - t0);
-      const int b = g_io.acquire(g_io.cp);
-      HIP_CHECK(hipMemcpyAsync(g_io.ring[b], host + (size_t)s * n + t0, sizeof(T) * m, hipMemcpyHostToDevice,
-                               g_io.cp));
-      HIP_CHECK(hipEventRecord(g_io.landed[b], g_io.cp));
-      HIP_CHECK(hipStreamWaitEvent(sst, g_io.landed[b], 0));
-      GT_LAUNCH(fort_to_dev<T>, dim3(cdiv(m, 256)), dim3(256), 0, sst, (const T*)g_io.ring[b], f.p, dy.d, s, nk_dev,
-                fd, t0, m);
-      HIP_LAUNCH_CHECK();
-      HIP_CHECK(hipEventRecord(g_io.freed[b], sst));
-      bytes += sizeof(T) * (double)m;
+// the device plane offset of element t (flat Fortran index within one tile's section)
+__device__ __forceinline__ long fort_dev_index(const Dims& d, int s, int nk_dev, const FDesc& fd, long t) {
+  const int i = (int)(t % fd.ni);
+  int j, k;
+  if (fd.order == 0) {
+    j = (int)((t / fd.ni) % fd.nj);
+    k = (int)(t / ((long)fd.ni * fd.nj));
+  } else {
+    k = (int)((t / fd.ni) % fd.nk);
+    j = (int)(t / ((long)fd.ni * fd.nk));
+  }
+  return ((long)s * nk_dev + k) * d.plane + pidx(d, fd.ilo + i, fd.jlo + j);
+}
+
+// Elements [t_lo, t_lo + span) of tiles s0, s0 + 1, ... of one Fortran array (`total` = tiles
+// x span) between the device field and `f`, where element t of tile s sits at
+// f[(s - s_base) * stride + t - t_base]: the mapped Fortran array itself (zero-copy: s_base =
+// t_base = 0, stride = the tile's element count) or a staging piece.  Consecutive lanes take
+// consecutive Fortran elements (full PCIe packets); ZC_U elements per lane are in flight per
+// iteration of the grid-stride loop (a PCIe round trip is microseconds long).
+constexpr int ZC_U = 4;
+template <typename T, bool UP>
+__global__ void __launch_bounds__(256) fort_move(T* __restrict__ f, double* __restrict__ dev, Dims d, int s0,
+                                                 int nk_dev, FDesc fd, int s_base, long stride, long t_base,
+                                                 long t_lo, long span, long total) {
+  const long step = (long)gridDim.x * blockDim.x;
+  for (long e0 = (long)blockIdx.x * blockDim.x + threadIdx.x; e0 < total; e0 += step * ZC_U) {
+    long hi[ZC_U], di[ZC_U];
+#pragma unroll
+    for (int u = 0; u < ZC_U; ++u) {
+      const long e = e0 + u * step;
+      const long ee = e < total ? e : 0;
+      const int s = s0 + (int)(ee / span);
+      const long t = t_lo + ee % span;
+      hi[u] = (long)(s - s_base) * stride + t - t_base;
+      di[u] = fort_dev_index(d, s, nk_dev, fd, t);
+    }
+    if constexpr (UP) {
+      T v[ZC_U];
+#pragma unroll
+      for (int u = 0; u < ZC_U; ++u) v[u] = e0 + u * step < total ? f[hi[u]] : T(0);
+#pragma unroll
+      for (int u = 0; u < ZC_U; ++u)
+        if (e0 + u * step < total) dev[di[u]] = (double)v[u];
+    } else {
+      double v[ZC_U];
+#pragma unroll
+      for (int u = 0; u < ZC_U; ++u) v[u] = e0 + u * step < total ? dev[di[u]] : 0.0;
+#pragma unroll
+      for (int u = 0; u < ZC_U; ++u)
+        if (e0 + u * step < total) f[hi[u]] = (T)v[u];
     }
   }
+}
+
+template <typename T, bool UP>
+void launch_move(T* f, double* dev, const Dims& d, int s_lo, int s_hi, int nk_dev, const FDesc& fd, int s_base,
+                 long stride, long t_base, long t_lo, long t_hi, hipStream_t st, int max_blocks) {
+  const long span = t_hi - t_lo, total = span * (s_hi - s_lo);
+  if (total <= 0) return;
+  const int blocks = (int)std::min<long>(max_blocks, cdiv(total, 256L * ZC_U));
+  GT_LAUNCH((fort_move<T, UP>), dim3(blocks), dim3(256), 0, st, f, dev, d, s_lo, nk_dev, fd, s_base, stride, t_base,
+            t_lo, span, total);
+  HIP_LAUNCH_CHECK();
+}
+
+// the staged pieces of tiles [s_lo, s_hi) x elements [t_lo, t_hi): whole tiles together while
+// they fit the staging buffer and the range is the whole tile (one contiguous host block),
+// else one tile at a time, cut to the buffer
+template <typename F>
+void staged_pieces(int s_lo, int s_hi, long n, long t_lo, long t_hi, long cap, F&& fn) {
+  if (t_lo == 0 && t_hi == n && n <= cap) {
+    const int per = (int)std::max<long>(1, cap / n);
+    for (int s = s_lo; s < s_hi; s += per) fn(s, std::min(s + per, s_hi), t_lo, t_hi);
+    return;
+  }
+  for (int s = s_lo; s < s_hi; ++s)
+    for (long t = t_lo; t < t_hi; t += cap) fn(s, s + 1, t, std::min(t + cap, t_hi));
+}
+
+// Fortran array (all local sub-domains, tile-major) -> device field: elements [t_lo, t_hi) of
+// each tile in [s_lo, s_hi), on stream `st`; `kind` the transfer's ZC_* class
+template <typename T>
+double copy_in(Dycore& dy, const char* name, int nk_dev, const T* host, const FDesc& fd, hipStream_t st, int kind,
+               int zc_grid, int s_lo = 0, int s_hi = -1, long t_lo = 0, long t_hi = -1) {
+  Field& f = dy.field(name, nk_dev);
+  const long n = (long)fd.ni * fd.nj * fd.nk;
+  if (s_hi < 0) s_hi = g_tiles_per_rank;
+  if (t_hi < 0) t_hi = n;
+  const double bytes = sizeof(T) * (double)(t_hi - t_lo) * (s_hi - s_lo);
+  if (void* m = g_io.mapped(host, kind)) {
+    launch_move<T, true>((T*)m, f.p, dy.d, s_lo, s_hi, nk_dev, fd, 0, n, 0, t_lo, t_hi, st, zc_grid);
+    return bytes;
+  }
+  T* buf = (T*)g_io.staging();
+  const long cap = (long)(g_io.stage_cap / sizeof(T));
+  staged_pieces(s_lo, s_hi, n, t_lo, t_hi, cap, [&](int a, int b, long ta, long tb) {
+    const long m = (tb - ta) * (b - a);  // contiguous on the host (whole tiles, or one tile's range)
+    HIP_CHECK(hipMemcpyAsync(buf, host + (size_t)a * n + ta, sizeof(T) * m, hipMemcpyHostToDevice, st));
+    launch_move<T, true>(buf, f.p, dy.d, a, b, nk_dev, fd, a, tb - ta, ta, ta, tb, st, 1024);
+  });
   return bytes;
 }
 
+// device field -> Fortran array, on stream `st` (which the caller has made wait for the
+// field's last writer)
 template <typename T>
-double copy_out(Dycore& dy, const char* name, T* host, const FDesc& fd) {
+double copy_out(Dycore& dy, const char* name, T* host, const FDesc& fd, hipStream_t st, int zc_grid) {
   Field* f = dy.find(name);
   if (!f) throw std::runtime_error(std::string("bridge: missing field ") + name);
   const long n = (long)fd.ni * fd.nj * fd.nk;
-  const long per = (long)(chunk_bytes() / sizeof(T));
-  double bytes = 0;
-  for (int s = 0; s < g_tiles_per_rank; ++s) {
-    for (long t0 = 0; t0 < n; t0 += per) {
-      const long m = std::min(per, n - t0);
-      const int b = g_io.acquire(dy.st);
-      GT_LAUNCH(dev_to_fort<T>, dim3(cdiv(m, 256)), dim3(256), 0, dy.st, (T*)g_io.ring[b], f->p, dy.d, s, f->nk,
-                fd, t0, m);
-      HIP_LAUNCH_CHECK();
-      HIP_CHECK(hipEventRecord(g_io.landed[b], dy.st));
-      HIP_CHECK(hipStreamWaitEvent(g_io.cp, g_io.landed[b], 0));
-      HIP_CHECK(hipMemcpyAsync(host + (size_t)s * n + t0, g_io.ring[b], sizeof(T) * m, hipMemcpyDeviceToHost,
-                               g_io.cp));
-      HIP_CHECK(hipEventRecord(g_io.freed[b], g_io.cp));
-      bytes += sizeof(T) * (double)m;
-    }
+  const double bytes = sizeof(T) * (double)n * g_tiles_per_rank;
+  if (void* m = g_io.mapped(host, ZC_DOWN)) {
+    launch_move<T, false>((T*)m, f->p, dy.d, 0, g_tiles_per_rank, f->nk, fd, 0, n, 0, 0, n, st, zc_grid);
+    return bytes;
   }
+  T* buf = (T*)g_io.staging();
+  const long cap = (long)(g_io.stage_cap / sizeof(T));
+  staged_pieces(0, g_tiles_per_rank, n, 0, n, cap, [&](int a, int b, long ta, long tb) {
+    const long m = (tb - ta) * (b - a);
+    launch_move<T, false>(buf, f->p, dy.d, a, b, f->nk, fd, a, tb - ta, ta, ta, tb, st, 1024);
+    HIP_CHECK(hipMemcpyAsync(host + (size_t)a * n + ta, buf, sizeof(T) * m, hipMemcpyDeviceToHost, st));
+  });
   return bytes;
 }
 
@@ -481,17 +555,19 @@ void bridge_run(const BridgeArgs<T>& a) {
   // What a call has to move.  Up: an inout the step overwrites over the whole Fortran extent
   // before reading it needs no upload -- mfx, mfy, cx, cy (zeroed at the step's start), pkz
   // (fv_prep writes the compute domain first), ua, va, uc, vc (d2a2c_vect writes the whole
-  // data domain each sub-step), diss_est (zeroed with d_con, else untouched) -- and q_con,
-  // which the step never touches, moves neither way (its Fortran values stay as they were, as
-  // after a copy round trip).  Down: diss_est only with d_con (phis comes back: the step
-// fills its halo).
-  // GTFV3_BRIDGE_SKIP=0 moves every array both ways.
+  // data domain each sub-step), pe, peln, pk (riem_solver3's last call writes every level of
+  // the compute domain and pk3_pe_halo pe's ring of one), diss_est (zeroed with d_con, else
+  // untouched) -- and q_con, which the step never touches, moves neither way (its Fortran
+  // values stay as they were, as after a copy round trip).  Down: diss_est only with d_con
+  // (phis comes back: the step fills its halo).  GTFV3_BRIDGE_SKIP=0 moves every array both
+  // ways, all of them before / after the step.
   const char* skip_env = std::getenv("GTFV3_BRIDGE_SKIP");
   const bool skip = !(skip_env && skip_env[0] == '0');
   const bool dcon = dy.nl.d_con > 1e-5;
   auto up = [&](const std::string& n) {
     if (!skip) return true;
-    for (const char* x : {"mfx", "mfy", "cx", "cy", "pkz", "q_con", "ua", "va", "uc", "vc", "diss_est"})
+    for (const char* x : {"mfx", "mfy", "cx", "cy", "pkz", "q_con", "ua", "va", "uc", "vc", "pe", "peln", "pk",
+                          "diss_est"})
       if (n == x) return false;
     return true;
   };
@@ -506,40 +582,91 @@ void bridge_run(const BridgeArgs<T>& a) {
   for (auto& it : items)
     arrays.push_back({it.p, sizeof(T) * (size_t)it.fd.ni * it.fd.nj * it.fd.nk * g_tiles_per_rank});
   g_io.pin(arrays);
-  HIP_CHECK(hipEventRecord(g_io.ev_t[0], g_io.cp));
+  const int up_blocks = zc_blocks("GTFV3_BRIDGE_ZC_BLOCKS", 32);
+  const int down_blocks = zc_blocks("GTFV3_BRIDGE_ZC_DOWN_BLOCKS", 1024);
+  HIP_CHECK(hipEventRecord(g_io.ev_t[0], dy.st));
   double up_bytes = 0, down_bytes = 0;
-  // the state the step reads first; tracers 1.. are first read by tracer_2d, after the
-  // acoustic sub-steps, so they upload and scatter beside those (on their own stream) and
-  // the step waits for them only there
+  // the state the step reads first goes up before it (small arrays first); tracers 1.. are
+  // first read by tracer_2d, after the acoustic sub-steps, and omga only by fv_wrapup (its
+  // compute domain is overwritten there, the halo must come back as it went), so those go up
+  // beside the step on the side stream and the step waits for them only there
   const long q0 = (long)(ied - isd + 1) * (jed - jsd + 1) * npz;  // tracer 0's share of a tile
-  const bool defer = nq > 1 && skip;
+  const bool defer = skip;
+  auto find = [&](const char* n) -> Item& {
+    for (auto& it : items)
+      if (std::string(it.name) == n) return it;
+    throw std::runtime_error(std::string("bridge: no item ") + n);
+  };
+  const char* first[] = {"ps", "phis", "delp", "delz", "pt", "q", "u", "v", "w"};
+  for (const char* n : first) {
+    Item& it = find(n);
+    const bool qpart = defer && std::string(n) == "q";
+    up_bytes += copy_in<T>(dy, it.name, it.nk_dev, it.p, it.fd, dy.st, ZC_CRIT, 1024, 0, -1, 0, qpart ? q0 : -1);
+  }
   for (auto& it : items) {
-    if (!up(it.name)) continue;
-    if (defer && std::string(it.name) == "q")
-      up_bytes += copy_in<T>(dy, it.name, it.nk_dev, it.p, it.fd, dy.st, 0, -1, 0, q0);
-    else
-      up_bytes += copy_in<T>(dy, it.name, it.nk_dev, it.p, it.fd, dy.st);
+    bool listed = false;
+    for (const char* n : first) listed = listed || std::string(it.name) == n;
+    if (listed || !up(it.name) || (defer && std::string(it.name) == "omga")) continue;
+    up_bytes += copy_in<T>(dy, it.name, it.nk_dev, it.p, it.fd, dy.st, ZC_CRIT, 1024);
   }
   HIP_CHECK(hipEventRecord(g_io.ev_t[1], dy.st));
-  dy.tracer_wait = nullptr;
+  dy.tracer_wait = dy.exit_wait = nullptr;
   if (defer) {
-    // the deferred scatters write into q, which the first call allocates and zeroes on dy.st:
-    // the tracer stream starts behind everything queued on dy.st so far (the step itself starts
-    // at ev_t[1] as well, so this costs no overlap)
-    HIP_CHECK(hipStreamWaitEvent(g_io.tr, g_io.ev_t[1], 0));
-    for (auto& it : items)
-      if (std::string(it.name) == "q")
-        up_bytes += copy_in<T>(dy, it.name, it.nk_dev, it.p, it.fd, g_io.tr, 0, -1, q0, -1);
-    HIP_CHECK(hipEventRecord(g_io.ev_tracers, g_io.tr));
-    dy.tracer_wait = g_io.ev_tracers;
+    // the deferred scatters write into q and omga, which the first call allocates and zeroes
+    // on dy.st: the side stream starts behind everything queued there so far (the step itself
+    // starts at ev_t[1] as well, so this costs no overlap)
+    HIP_CHECK(hipEventRecord(g_io.ev_crit, dy.st));
+    HIP_CHECK(hipStreamWaitEvent(g_io.side, g_io.ev_crit, 0));
+    if (nq > 1) {
+      Item& it = find("q");
+      up_bytes += copy_in<T>(dy, it.name, it.nk_dev, it.p, it.fd, g_io.side, ZC_SIDE, up_blocks, 0, -1, q0, -1);
+      HIP_CHECK(hipEventRecord(g_io.ev_tracers, g_io.side));
+      dy.tracer_wait = g_io.ev_tracers;
+    }
+    Item& om = find("omga");
+    up_bytes += copy_in<T>(dy, om.name, om.nk_dev, om.p, om.fd, g_io.side, ZC_SIDE, up_blocks);
+    HIP_CHECK(hipEventRecord(g_io.ev_exit, g_io.side));
+    dy.exit_wait = g_io.ev_exit;
+    dy.marks = g_io.marks;
   }
   dy.step();
-  dy.tracer_wait = nullptr;
+  dy.tracer_wait = dy.exit_wait = nullptr;
+  dy.marks = nullptr;
   HIP_CHECK(hipEventRecord(g_io.ev_t[2], dy.st));
-  for (auto& it : items)
-    if (down(it.name)) down_bytes += copy_out<T>(dy, it.name, it.p, it.fd);
-  HIP_CHECK(hipEventRecord(g_io.ev_t[3], g_io.cp));
-  HIP_CHECK(hipStreamSynchronize(g_io.cp));
+  // copy back: each group once the step has marked it final (Dycore::StepMark), the rest
+  // after the step; all on one stream, in the order the step finishes them
+  struct Group {
+    hipEvent_t ev;
+    std::vector<const char*> names;
+  };
+  std::vector<Group> groups;
+  if (defer) {
+    groups = {{g_io.marks[Dycore::SM_CWINDS], {"uc", "vc"}},
+              {g_io.marks[Dycore::SM_ACOUSTIC], {"phis", "diss_est"}},
+              {g_io.marks[Dycore::SM_FLUXES], {"mfx", "mfy", "cx", "cy"}},
+              {g_io.marks[Dycore::SM_REMAP], {"w", "delz", "delp", "q", "pe", "peln", "pk", "pkz", "ps"}},
+              {g_io.marks[Dycore::SM_WRAPUP], {"pt", "omga"}},
+              {g_io.marks[Dycore::SM_WINDS], {"u", "v"}},
+              {g_io.ev_t[2], {"ua", "va"}}};
+  } else {
+    groups = {{g_io.ev_t[2], {}}};
+    for (auto& it : items) groups[0].names.push_back(it.name);
+  }
+  int ncopied = 0;
+  for (auto& g : groups) {
+    HIP_CHECK(hipStreamWaitEvent(g_io.side, g.ev, 0));
+    for (const char* n : g.names) {
+      Item& it = find(n);
+      if (!down(it.name)) continue;
+      down_bytes += copy_out<T>(dy, it.name, it.p, it.fd, g_io.side, down_blocks);
+      ++ncopied;
+    }
+  }
+  if (ncopied != (int)std::count_if(items.begin(), items.end(), [&](const Item& it) { return down(it.name); }))
+    throw std::runtime_error("bridge: copy-back groups do not cover the outputs");
+  HIP_CHECK(hipEventRecord(g_io.ev_t[3], g_io.side));
+  HIP_CHECK(hipStreamSynchronize(g_io.side));
+  HIP_CHECK(hipStreamSynchronize(dy.st));
   for (int n = 0; n < 3; ++n) {
     float ms = 0;
     HIP_CHECK(hipEventElapsedTime(&ms, g_io.ev_t[n], g_io.ev_t[n + 1]));

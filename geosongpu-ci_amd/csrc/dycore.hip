@@ -241,6 +241,10 @@ void Dycore::allreduce_max(double* dev, int n) {
 }
 
 void Dycore::set_vertical(const double* ak_, const double* bk_, int ks_) {
+  // a caller that passes the same table every step (the bridge) uploads it once
+  const bool same = (int)ak.size() == nl.npz + 1 && std::equal(ak.begin(), ak.end(), ak_) &&
+                    std::equal(bk.begin(), bk.end(), bk_);
+  if (same && ks == ks_) return;
   ak.assign(ak_, ak_ + nl.npz + 1);
   bk.assign(bk_, bk_ + nl.npz + 1);
   ks = ks_;
@@ -660,6 +664,7 @@ void Dycore::step() {
   // second set the halo ring of the first, so a halo point no exchange fills (the cube-corner
   // regions) holds the same value whichever set is current -- the in-place update's semantics
   copy_halo_ring(c, d.nsub * k1, zh, za.zh_out);
+  bool in_graph = false;  // the loop is being captured: no event records inside
   auto acoustic = [&]() {
   for (int it = 0; it < nl.n_split; ++it) {
     const bool last = it == nl.n_split - 1;
@@ -689,6 +694,7 @@ void Dycore::step() {
     // as one exchange (H_CSC, bit-identical to 'S' then 'C')
     if (nl.nord > 0) halo_update({{"uc", 'X'}, {"vc", 'X'}, {"divgd", 'b'}});
     else halo_update({{"uc", 'X'}, {"vc", 'X'}});
+    if (last && marks && !in_graph) HIP_CHECK(hipEventRecord(marks[SM_CWINDS], st));
     // fork: after the Courant numbers, the wind stage of d_sw (stream b) and update_dz_d
     // (stream c) run beside the mass / thermodynamic transport (and the wind stage on beside
     // riem_solver3 and the exchange of delp, pt, zh, ppe, w).  Default on (GTFV3_STREAMS=0: one
@@ -761,7 +767,9 @@ void Dycore::step() {
       ac_exec = nullptr;
       hipGraph_t g = nullptr;
       HIP_CHECK(hipStreamBeginCapture(st, hipStreamCaptureModeRelaxed));
+      in_graph = true;
       acoustic();
+      in_graph = false;
       HIP_CHECK(hipStreamEndCapture(st, &g));
       HIP_CHECK(hipGraphInstantiate(&ac_exec, g, nullptr, nullptr, 0));
       HIP_CHECK(hipGraphDestroy(g));
@@ -787,6 +795,11 @@ void Dycore::step() {
     damping_heat_apply(c, npz, n_con, std::fabs(bdt * nl.delt_max), da.heat, delp.p, delz.p, pt.p);
   }
   HIP_CHECK(hipEventRecord(ev[1], st));
+  auto mark = [&](int m) {
+    if (marks) HIP_CHECK(hipEventRecord(marks[m], st));
+  };
+  if (graph) mark(SM_CWINDS);  // (not recorded inside the replayed loop)
+  mark(SM_ACOUSTIC);
 
   // ---- tracer transport with the accumulated mass fluxes, beside the remap of T_v, delz,
   // w and the winds (which touch none of the tracer step's fields); the tracer remap and
@@ -799,6 +812,7 @@ void Dycore::step() {
     std::swap(st, st_b);  // tracer_2d enqueues (kernels, halo updates, copies) on the side stream
     if (tracer_wait) HIP_CHECK(hipStreamWaitEvent(st, tracer_wait, 0));
     tracer_2d(nq, mdt);
+    mark(SM_FLUXES);
     std::swap(st, st_b);
     HIP_CHECK(hipEventRecord(ev_b, st_b));
     RemapState rs1{pe, peln, pk, pkz, delp.p, delz.p, pt.p, w.p, q.p, u.p, v.p, ps, ws};
@@ -807,6 +821,7 @@ void Dycore::step() {
   } else {
     if (tracer_wait) HIP_CHECK(hipStreamWaitEvent(st, tracer_wait, 0));
     tracer_2d(nq, mdt);
+    mark(SM_FLUXES);
   }
   HIP_CHECK(hipEventRecord(ev[2], st));
 
@@ -814,10 +829,14 @@ void Dycore::step() {
   RemapState rs{pe, peln, pk, pkz, delp.p, delz.p, pt.p, w.p, q.p, u.p, v.p, ps, ws};
   lagrangian_to_eulerian(c, npz, nq, ptop, nl.fill != 0, ak_dev, bk_dev, rs, rsc, remap_variant(), fork_substep ? 2 : 0);
   HIP_CHECK(hipEventRecord(ev[3], st));
+  mark(SM_REMAP);
 
   // ---- exit: T, omega, A-grid winds ----
+  if (exit_wait) HIP_CHECK(hipStreamWaitEvent(st, exit_wait, 0));
   fv_wrapup(c, npz, nq, zvir, q.p, delp.p, delz.p, w.p, pt.p, omga);
+  mark(SM_WRAPUP);
   halo_update({{"u", 'd'}, {"v", 'd'}});
+  mark(SM_WINDS);
   c2l_ord4(c, npz, u.p, v.p, ua, va);
   HIP_CHECK(hipEventRecord(ev[4], st));
   ev_pending[slot] = true;

@@ -71,6 +71,21 @@ class Dycore {
   // when set, the step's tracer transport waits for this event (the bridge uploads tracers
   // 1.. beside the acoustic sub-steps)
   hipEvent_t tracer_wait = nullptr;
+  // when set, the exit phase (fv_wrapup's omega) waits for this event (the bridge uploads
+  // omga's halo beside the step)
+  hipEvent_t exit_wait = nullptr;
+  // when set, the step records mark[m] as the fields of StepMark m are final (the bridge
+  // starts copying each group back while the rest of the step runs)
+  enum StepMark {
+    SM_CWINDS,      // uc, vc (after the last acoustic sub-step's C-grid exchange)
+    SM_ACOUSTIC,    // diss_est, phis (after the acoustic sub-steps and the heating)
+    SM_FLUXES,      // mfx, mfy, cx, cy (after tracer_2d's split scaling; recorded on its stream)
+    SM_REMAP,       // w, delz, delp, q, pe, peln, pk, pkz, ps (after the vertical remap)
+    SM_WRAPUP,      // pt, omga
+    SM_WINDS,       // u, v (after their final halo update)
+    SM_COUNT
+  };
+  hipEvent_t* marks = nullptr;
   // the acoustic sub-steps as one HIP graph (GTFV3_GRAPH, Dycore::step): captured on the
   // second step (the first allocates every field and table), replayed while the key (field
   // generation, state planes, step constants) is unchanged

@@ -173,7 +173,7 @@ def test_bridge_adiabatic_is_dry_dynamics(pkg, require_gpu):
 
 # inouts the bridge does not upload (the step overwrites them over their whole Fortran
 # extent before reading them) and q_con, which moves neither way (bridge.hip bridge_run)
-SKIPPED_UP = ("mfx", "mfy", "cx", "cy", "pkz", "ua", "va", "uc", "vc", "diss_est", "q_con")
+SKIPPED_UP = ("mfx", "mfy", "cx", "cy", "pkz", "ua", "va", "uc", "vc", "pe", "peln", "pk", "diss_est", "q_con")
 
 
 def _garbage_call(pkg, d, st, ak, bk, ks, npx, npz, nq, env):
@@ -184,8 +184,9 @@ def _garbage_call(pkg, d, st, ak, bk, ks, npx, npz, nq, env):
     try:
         rng = np.random.default_rng(7)
         st = dict(st)
+        shapes = _shapes(npx - 1, npz, nq)
         for name in SKIPPED_UP:
-            st[name] = rng.standard_normal((d.nsub, npz, d.nj, d.pitch))
+            st[name] = rng.standard_normal((d.nsub, shapes[name][4], d.nj, d.pitch))
         return _bridge_call(pkg, st, d, ak, bk, ks, npx, npz, nq)
     finally:
         for k, v in old.items():
@@ -196,30 +197,39 @@ def _garbage_call(pkg, d, st, ak, bk, ks, npx, npz, nq, env):
 
 
 def test_bridge_copy_pipeline_equivalent(pkg, require_gpu):
-    """The pipelined copies (page-locked arrays, chunks through the staging ring, tracers
-    1.. uploaded beside the acoustic sub-steps, inouts the step overwrites not uploaded) give
-    bit for bit what moving every array both ways gives, with garbage in those inouts; q_con
-    and phis come back untouched.  Small chunks run the ring through many wrap-arounds."""
+    """The overlapped copies (page-locked mapped arrays; tracers 1.. and omga's halo uploaded
+    beside the acoustic sub-steps; each output group copied back once the step marks it final;
+    inouts the step overwrites not uploaded) give bit for bit what moving every array both
+    ways before / after the step gives, with garbage in those inouts, in both transfer forms:
+    zero-copy kernels (GTFV3_BRIDGE_ZC=7, few workgroups so the grid-stride loops wrap),
+    staged DMA (GTFV3_BRIDGE_ZC=0, a 4 KiB staging buffer cutting every array into many
+    pieces) and the default mix (zero-copy before the step, staged beside and after it);
+    q_con comes back untouched."""
     npx, npz, nq = 13, 10, 3
     d, st, ak, bk, ks = _setup(pkg, npx, npz, nq)
     full, shapes = _garbage_call(pkg, d, st, ak, bk, ks, npx, npz, nq,
                                  {"GTFV3_BRIDGE_SKIP": "0", "GTFV3_BRIDGE_PIN": "0"})
-    piped, _ = _garbage_call(pkg, d, st, ak, bk, ks, npx, npz, nq,
-                             {"GTFV3_BRIDGE_SKIP": "1", "GTFV3_BRIDGE_PIN": "1", "GTFV3_BRIDGE_CHUNK_KB": "4"})
+    dma, _ = _garbage_call(pkg, d, st, ak, bk, ks, npx, npz, nq,
+                           {"GTFV3_BRIDGE_SKIP": "1", "GTFV3_BRIDGE_ZC": "0", "GTFV3_BRIDGE_STAGE_KB": "4"})
+    zc, _ = _garbage_call(pkg, d, st, ak, bk, ks, npx, npz, nq,
+                          {"GTFV3_BRIDGE_SKIP": "1", "GTFV3_BRIDGE_ZC": "7", "GTFV3_BRIDGE_ZC_BLOCKS": "3",
+                           "GTFV3_BRIDGE_ZC_DOWN_BLOCKS": "5"})
     ref, _ = _garbage_call(pkg, d, st, ak, bk, ks, npx, npz, nq, {"GTFV3_BRIDGE_SKIP": "1"})
     d.close()
     for name in shapes:
         if name == "q_con":
             continue
-        assert np.array_equal(full[name], piped[name]), f"{name}: pipelined bridge differs from full copies"
-        assert np.array_equal(full[name], ref[name]), f"{name}: default chunks differ from full copies"
+        assert np.array_equal(full[name], dma[name]), f"{name}: staged DMA copies differ from full copies"
+        assert np.array_equal(full[name], zc[name]), f"{name}: zero-copy (3 / 5 workgroups) differs from full copies"
+        assert np.array_equal(full[name], ref[name]), f"{name}: default copies differ from full copies"
     # q_con never moves: the caller's values stay
     rng = np.random.default_rng(7)
     for name in SKIPPED_UP:
-        g = rng.standard_normal((d.nsub, npz, d.nj, d.pitch))
+        g = rng.standard_normal((d.nsub, shapes[name][4], d.nj, d.pitch))
         if name == "q_con":
             li, hi, lj, hj, nk, kj = shapes[name]
-            assert np.array_equal(piped[name], to_fortran(g, li, hi, lj, hj, kj)), "q_con must stay untouched"
+            for got in (dma, zc):
+                assert np.array_equal(got[name], to_fortran(g, li, hi, lj, hj, kj)), "q_con must stay untouched"
     # the bridge reports what it moved (the last call: default chunks)
     import ctypes
     out = (ctypes.c_double * 6)()

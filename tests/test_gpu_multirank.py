@@ -72,3 +72,67 @@ def test_multirank_step_matches_single_rank(pkg, require_gpu, nranks, layout, np
             a = got[r][k][..., NG:NG + ny, NG:NG + nx]
             b = want[k][r * nper:(r + 1) * nper, ..., NG:NG + ny, NG:NG + nx]
             assert np.array_equal(a, b), f"rank {r} field {k} differs from the single-rank step"
+
+
+MOIST_FIELDS = FIELDS + ("clls", "clcn", "qlcn", "qicn", "prec_rain", "prec_snow", "prec_graupel", "prec_ice",
+                         "rad_cf", "rad_rl", "rad_ri")
+
+
+def test_multirank_aquaplanet_step_matches_single_rank(pkg, require_gpu):
+    """Config 4's coupled step (aquaplanet.py:99-178: fv_dynamics, then GEOS's moist physics)
+    on the 8-GPU layout bench.py runs -- 8 ranks of bands 1x4 (three sub-domains each) --
+    through the loopback transport at C48 L72 with the six moist tracers: every rank's state,
+    condensate, cloud fractions, precipitation and radiation inputs after one coupled step
+    equal the single-rank step of the same global state bit for bit.  The global state is
+    made once (aquaplanet_tracers draws its humidity noise per sub-domain) and each rank gets
+    its three sub-domains of it."""
+    state = importlib.import_module(pkg.__name__ + ".state")
+    npx, npz, nq, dt, nranks, layout = 49, 72, 6, 450.0, 8, (1, 4)
+    ak, bk, ks = state.hybrid_levels(npz)
+    ref = pkg.Domain(npx=npx, npz=npz, nq=nq, layout_x=layout[0], layout_y=layout[1], dt=dt)
+    st = state.jablonowski_williamson(ref, ak, bk)
+    state.aquaplanet_tracers(ref, st, ak, bk)
+    ref.set_vertical(ak, bk, ks)
+    for k, v in st.items():
+        ref.upload(k, v)
+    ref.step(1)
+    ref.stencil("aquaplanet_physics", [], [dt])
+    want = {k: ref.download(k) for k in MOIST_FIELDS}
+    nx, ny = ref.nx, ref.ny
+    ref.close()
+    gid = next(_gid)
+    doms = [pkg.Domain(r, nranks, None, npx=npx, npz=npz, nq=nq, layout_x=layout[0], layout_y=layout[1], dt=dt,
+                       loopback=gid) for r in range(nranks)]
+    nper = doms[0].nsub
+    assert nper * nranks == 6 * layout[0] * layout[1]
+    for r, d in enumerate(doms):
+        d.set_vertical(ak, bk, ks)
+        for k, v in st.items():
+            d.upload(k, np.ascontiguousarray(v[r * nper:(r + 1) * nper]))
+    del st
+    errors = []
+
+    def work(d):
+        try:
+            d.step(1)
+            d.stencil("aquaplanet_physics", [], [dt])
+        except Exception as e:  # surfaced below
+            errors.append(repr(e))
+
+    threads = [threading.Thread(target=work, args=(d,), daemon=True) for d in doms]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join(timeout=120)
+    assert not errors, errors
+    assert not any(t.is_alive() for t in threads), "a rank did not finish (loopback barrier)"
+    try:
+        for r, d in enumerate(doms):
+            for k in MOIST_FIELDS:
+                a = d.download(k)[..., NG:NG + ny, NG:NG + nx]
+                b = want[k][r * nper:(r + 1) * nper, ..., NG:NG + ny, NG:NG + nx]
+                assert np.all(np.isfinite(b)), f"{k}: single-rank step not finite"
+                assert np.array_equal(a, b), f"rank {r} field {k} differs from the single-rank coupled step"
+    finally:
+        for d in doms:
+            d.close()

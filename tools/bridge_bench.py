@@ -1,8 +1,10 @@
 #!/usr/bin/env python3
 """PCIe-inclusive time of the drop-in boundary: geos_gtfv3_run_f64_c (through the Python
 hook mirror) on Fortran-layout host buffers, C180 L72 nq=4, all six tiles on one GPU.
-Each call copies the 24 state arrays host -> device (fused transpose), runs one
-fv_dynamics step and copies them back in place.  The device-resident step
+Each call moves the state arrays host -> device (fused transpose), runs one fv_dynamics
+step and copies them back in place, the uploads the step reads late and the copies back of
+the groups it finishes early overlapped with it.  GTFV3_BRIDGE_ZC selects the
+transfer forms (bridge.hip).  The device-resident step
 alone is what bench.py reports.
 
     python tools/bridge_bench.py [--npx 181] [--npz 72] [--steps 3]
@@ -87,11 +89,10 @@ def main():
     print(json.dumps({"what": f"{fn} incl. host<->device copies", "dtype": a.dtype, "npx": npx, "npz": npz,
                       "nq": nq, "ms_per_call": 1e3 * el, "cell_updates_per_s": cells / el,
                       "host_bytes_of_the_arrays": nbytes,
-                      "median_phases_ms": {"upload_before_step": ph[0], "step_incl_tracer_wait": ph[1],
-                                           "download": ph[2]},
-                      "bytes_up": ph[3], "bytes_down": ph[4],
-                      "up_GBps": ph[3] / ph[0] / 1e6, "down_GBps": ph[4] / ph[2] / 1e6,
-                      "arrays_pinned": int(ph[5])}))
+                      "transfer_zc_mask": int(os.environ.get("GTFV3_BRIDGE_ZC", "1")),
+                      "median_phases_ms": {"upload_before_step": ph[0], "step_incl_waits": ph[1],
+                                           "copy_back_after_step": ph[2]},
+                      "bytes_up": ph[3], "bytes_down": ph[4], "arrays_pinned": int(ph[5])}))
 
 
 if __name__ == "__main__":
