@@ -1,4 +1,5 @@
 // halo.hip — table construction (host) and halo gather / pack / unpack kernels.
+#include <cstdlib>
 #include <algorithm>
 #include <stdexcept>
 
@@ -292,8 +293,7 @@ __device__ __forceinline__ HaloSel halo_sel(const HaloBatch b, int f) {  // by v
 // tiles: C180 halo_local 0.93 -> 0.90 ms/step); HK = 1 for the smaller per-rank exchanges
 // (8-rank share: pack / unpack 0.29 -> 0.34-0.36 ms/step with HK = 8, too few threads).
 template <int HK>
-__global__ void halo_local_kernel(HaloBatch b, long plane) {
-  const HaloSel F = halo_sel(b, blockIdx.z);
+__device__ __forceinline__ void halo_local_body(const HaloSel& F, long plane) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int k0 = blockIdx.y * HK;
   if (e >= F.n || k0 >= F.nk) return;
@@ -314,8 +314,7 @@ __global__ void halo_local_kernel(HaloBatch b, long plane) {
 }
 
 template <int HK>
-__global__ void halo_pack_kernel(HaloBatch b, long plane, double* __restrict__ buf) {
-  const HaloSel F = halo_sel(b, blockIdx.z);
+__device__ __forceinline__ void halo_pack_body(const HaloSel& F, long plane, double* __restrict__ buf) {
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   const int k0 = blockIdx.y * HK;
   if (e >= F.n || k0 >= F.nk) return;
@@ -328,6 +327,25 @@ __global__ void halo_pack_kernel(HaloBatch b, long plane, double* __restrict__ b
       buf[F.boff + (long)h.pstart * F.nk + (long)k * h.pcount + (e - h.pstart)] =
           h.sign * src[((long)h.sub * F.nk + k) * plane + h.off];
   }
+}
+
+template <int HK>
+__global__ void halo_local_kernel(HaloBatch b, long plane) {
+  halo_local_body<HK>(halo_sel(b, blockIdx.z), plane);
+}
+
+template <int HK>
+__global__ void halo_pack_kernel(HaloBatch b, long plane, double* __restrict__ buf) {
+  halo_pack_body<HK>(halo_sel(b, blockIdx.z), plane, buf);
+}
+
+// a remote exchange's pack and same-rank gather in one launch (grid z: the np packed fields,
+// then the local ones): the gather writes halo points only, the pack reads owned points only
+template <int HK>
+__global__ void halo_pack_local_kernel(HaloBatch pk, int np, HaloBatch lc, long plane, double* __restrict__ buf) {
+  const int z = blockIdx.z;
+  if (z < np) halo_pack_body<HK>(halo_sel(pk, z), plane, buf);
+  else halo_local_body<HK>(halo_sel(lc, z - np), plane);
 }
 
 template <int HK>
@@ -361,56 +379,78 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
     if (off > buf_elems_) throw std::runtime_error("halo: exchange buffer too small");
     if (!tr_) throw std::runtime_error("halo: multi-rank exchange without a transport");
   }
-  // one launch per stage for (up to HB) fields; stage 0 local gather, 1 pack, 2 unpack
+  // one launch per stage for (up to HB) fields; stage 0 local gather, 1 pack, 2 unpack,
+  // 3 pack + local gather together
+  auto batch = [&](int stage, int f0, HaloBatch& b, int& maxn, int& maxk) {
+    b = HaloBatch{};
+    int nb = 0;
+    for (int f = f0; f < nf && f < f0 + HB; ++f) {
+      const HaloField& F = fields[f];
+      const int n = stage == 0 ? n_local_[F.kind] : (stage == 1 ? n_send_[F.kind] : n_recv_[F.kind]);
+      if (!n) continue;
+      b.tab[nb] = stage == 0 ? (const void*)d_local_[F.kind]
+                             : (stage == 1 ? (const void*)d_send_[F.kind] : (const void*)d_recv_[F.kind]);
+      b.n[nb] = n;
+      b.nk[nb] = F.nk;
+      b.p0[nb] = F.p[0];
+      b.p1[nb] = F.p[1] ? F.p[1] : F.p[0];
+      b.boff[nb] = stage ? (long)foff[f] : 0;
+      maxn = std::max(maxn, n);
+      maxk = std::max(maxk, F.nk);
+      ++nb;
+    }
+    return nb;
+  };
   auto launch = [&](int stage) {
     for (int f0 = 0; f0 < nf; f0 += HB) {
-      HaloBatch b{};
-      int nb = 0, maxn = 0, maxk = 0;
-      for (int f = f0; f < nf && f < f0 + HB; ++f) {
-        const HaloField& F = fields[f];
-        const int n = stage == 0 ? n_local_[F.kind] : (stage == 1 ? n_send_[F.kind] : n_recv_[F.kind]);
-        if (!n) continue;
-        b.tab[nb] = stage == 0 ? (const void*)d_local_[F.kind]
-                               : (stage == 1 ? (const void*)d_send_[F.kind] : (const void*)d_recv_[F.kind]);
-        b.n[nb] = n;
-        b.nk[nb] = F.nk;
-        b.p0[nb] = F.p[0];
-        b.p1[nb] = F.p[1] ? F.p[1] : F.p[0];
-        b.boff[nb] = stage ? (long)foff[f] : 0;
-        maxn = std::max(maxn, n);
-        maxk = std::max(maxk, F.nk);
-        ++nb;
-      }
-      if (!nb) continue;
-      if ((long)cdiv(maxn, 256) * cdiv(maxk, 8) * nb >= 2048) {  // >= 8 workgroups per CU at HK = 8
-        const dim3 g(cdiv(maxn, 256), cdiv(maxk, 8), nb);
+      HaloBatch b{}, bl{};
+      int maxn = 0, maxk = 0;
+      const int nb = batch(stage == 3 ? 1 : stage, f0, b, maxn, maxk);
+      const int nl = stage == 3 ? batch(0, f0, bl, maxn, maxk) : 0;
+      if (!nb && !nl) continue;
+      if ((long)cdiv(maxn, 256) * cdiv(maxk, 8) * (nb + nl) >= 2048) {  // >= 8 workgroups per CU at HK = 8
+        const dim3 g(cdiv(maxn, 256), cdiv(maxk, 8), nb + nl);
         if (stage == 0) GT_LAUNCH_N("halo_local_kernel", halo_local_kernel<8>, g, dim3(256), 0, stream, b, d_.plane);
         else if (stage == 1) GT_LAUNCH_N("halo_pack_kernel", halo_pack_kernel<8>, g, dim3(256), 0, stream, b, d_.plane, sendbuf_);
-        else GT_LAUNCH_N("halo_unpack_kernel", halo_unpack_kernel<8>, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
+        else if (stage == 2) GT_LAUNCH_N("halo_unpack_kernel", halo_unpack_kernel<8>, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
+        else GT_LAUNCH_N("halo_pack_local_kernel", halo_pack_local_kernel<8>, g, dim3(256), 0, stream, b, nb, bl, d_.plane, sendbuf_);
       } else {
-        const dim3 g(cdiv(maxn, 256), maxk, nb);
+        const dim3 g(cdiv(maxn, 256), maxk, nb + nl);
         if (stage == 0) GT_LAUNCH_N("halo_local_kernel", halo_local_kernel<1>, g, dim3(256), 0, stream, b, d_.plane);
         else if (stage == 1) GT_LAUNCH_N("halo_pack_kernel", halo_pack_kernel<1>, g, dim3(256), 0, stream, b, d_.plane, sendbuf_);
-        else GT_LAUNCH_N("halo_unpack_kernel", halo_unpack_kernel<1>, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
+        else if (stage == 2) GT_LAUNCH_N("halo_unpack_kernel", halo_unpack_kernel<1>, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
+        else GT_LAUNCH_N("halo_pack_local_kernel", halo_pack_local_kernel<1>, g, dim3(256), 0, stream, b, nb, bl, d_.plane, sendbuf_);
       }
       HIP_LAUNCH_CHECK();
       // every halo point of every level: one value read, one written
       double pts = 0.0;
       for (int q = 0; q < nb; ++q) pts += (double)b.n[q] * b.nk[q];
+      for (int q = 0; q < nl; ++q) pts += (double)bl.n[q] * bl.nk[q];
       ktimer_bytes(16.0 * pts);
     }
   };
   if (remote) {
-    // pack on the compute stream, messages on the comm stream (after the pack), the
-    // same-rank gather on the compute stream meanwhile, then the unpack after the
+    // pack (with the same-rank gather, one launch) on the compute stream, messages on the comm
+    // stream after it, then the unpack after the
     // messages.  The next exchange's pack follows this unpack in stream order, so the
     // pack buffers are never rewritten while a send may still read them.  The gather is
     // enqueued before the messages are posted (it writes halo points only, the pack reads
     // owned points only), so the device runs it while the host posts them (an 8-rank trace
     // had the device idle ~10 us between pack and gather at every exchange).
-    launch(1);
-    HIP_CHECK(hipEventRecord(ev_packed_, stream));
-    launch(0);
+    // GTFV3_HALO_FUSE=0: the pack and the gather as two launches (the messages then start
+    // after the pack alone)
+    static const bool fuse = [] {
+      const char* e = std::getenv("GTFV3_HALO_FUSE");
+      return !(e && e[0] == '0');
+    }();
+    if (fuse) {
+      launch(3);
+      HIP_CHECK(hipEventRecord(ev_packed_, stream));
+    } else {
+      launch(1);
+      HIP_CHECK(hipEventRecord(ev_packed_, stream));
+      launch(0);
+    }
     HIP_CHECK(hipStreamWaitEvent(comm_st_, ev_packed_, 0));
     tr_->group_start();
     for (int f = 0; f < nf; ++f) {
