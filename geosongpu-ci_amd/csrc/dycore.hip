@@ -289,6 +289,8 @@ void Dycore::tracer_2d(int nq, double /*dt*/, int fused_mode, int nf) {
   HIP_CHECK(hipMemcpyAsync(h_cmax, cmax.p, sizeof(double) * npz, hipMemcpyDeviceToHost, st));
   HIP_CHECK(hipEventRecord(ev_cmax, st));
   tracer_split(c, npz, dns, cx.p, cy.p, xfx.p, yfx.p, mfx.p, mfy.p);
+  // the last writer of cx, cy, mfx, mfy (the bridge copies them back from here on)
+  if (marks) HIP_CHECK(hipEventRecord(marks[SM_FLUXES], st));
   int nmax = -1;
   auto sub_steps = [&]() {
     if (nmax < 0) {
@@ -811,8 +813,7 @@ void Dycore::step() {
     HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
     std::swap(st, st_b);  // tracer_2d enqueues (kernels, halo updates, copies) on the side stream
     if (tracer_wait) HIP_CHECK(hipStreamWaitEvent(st, tracer_wait, 0));
-    tracer_2d(nq, mdt);
-    mark(SM_FLUXES);
+    tracer_2d(nq, mdt);  // records SM_FLUXES
     std::swap(st, st_b);
     HIP_CHECK(hipEventRecord(ev_b, st_b));
     RemapState rs1{pe, peln, pk, pkz, delp.p, delz.p, pt.p, w.p, q.p, u.p, v.p, ps, ws};
@@ -820,8 +821,7 @@ void Dycore::step() {
     HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
   } else {
     if (tracer_wait) HIP_CHECK(hipStreamWaitEvent(st, tracer_wait, 0));
-    tracer_2d(nq, mdt);
-    mark(SM_FLUXES);
+    tracer_2d(nq, mdt);  // records SM_FLUXES
   }
   HIP_CHECK(hipEventRecord(ev[2], st));
 

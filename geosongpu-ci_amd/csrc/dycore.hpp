@@ -79,7 +79,7 @@ class Dycore {
   enum StepMark {
     SM_CWINDS,      // uc, vc (after the last acoustic sub-step's C-grid exchange)
     SM_ACOUSTIC,    // diss_est, phis (after the acoustic sub-steps and the heating)
-    SM_FLUXES,      // mfx, mfy, cx, cy (after tracer_2d's split scaling; recorded on its stream)
+    SM_FLUXES,      // mfx, mfy, cx, cy (after tracer_2d's split scaling, on its stream)
     SM_REMAP,       // w, delz, delp, q, pe, peln, pk, pkz, ps (after the vertical remap)
     SM_WRAPUP,      // pt, omga
     SM_WINDS,       // u, v (after their final halo update)
