@@ -629,39 +629,55 @@ void bridge_run(const BridgeArgs<T>& a) {
     dy.exit_wait = g_io.ev_exit;
     dy.marks = g_io.marks;
   }
-  dy.step();
-  dy.tracer_wait = dy.exit_wait = nullptr;
-  dy.marks = nullptr;
-  HIP_CHECK(hipEventRecord(g_io.ev_t[2], dy.st));
-  // copy back: each group once the step has marked it final (Dycore::StepMark), the rest
-  // after the step; all on one stream, in the order the step finishes them
+  // copy back: each group once the step has marked it final (Dycore::StepMark), queued on the
+  // side stream as the step records the mark (the step's host thread waits mid-way, in
+  // tracer_2d, so groups queued after step() returns would start late), the rest after the step
   struct Group {
-    hipEvent_t ev;
+    int mark;  // Dycore::StepMark, or -1: after the step
     std::vector<const char*> names;
+    bool queued;
   };
   std::vector<Group> groups;
   if (defer) {
-    groups = {{g_io.marks[Dycore::SM_CWINDS], {"uc", "vc"}},
-              {g_io.marks[Dycore::SM_ACOUSTIC], {"phis", "diss_est"}},
-              {g_io.marks[Dycore::SM_FLUXES], {"mfx", "mfy", "cx", "cy"}},
-              {g_io.marks[Dycore::SM_REMAP], {"w", "delz", "delp", "q", "pe", "peln", "pk", "pkz", "ps"}},
-              {g_io.marks[Dycore::SM_WRAPUP], {"pt", "omga"}},
-              {g_io.marks[Dycore::SM_WINDS], {"u", "v"}},
-              {g_io.ev_t[2], {"ua", "va"}}};
+    groups = {{Dycore::SM_CWINDS, {"uc", "vc"}, false},
+              {Dycore::SM_ACOUSTIC, {"phis", "diss_est"}, false},
+              {Dycore::SM_FLUXES, {"mfx", "mfy", "cx", "cy"}, false},
+              {Dycore::SM_REMAP, {"w", "delz", "delp", "q", "pe", "peln", "pk", "pkz", "ps"}, false},
+              {Dycore::SM_WRAPUP, {"pt", "omga"}, false},
+              {Dycore::SM_WINDS, {"u", "v"}, false},
+              {-1, {"ua", "va"}, false}};
   } else {
-    groups = {{g_io.ev_t[2], {}}};
+    groups = {{-1, {}, false}};
     for (auto& it : items) groups[0].names.push_back(it.name);
   }
   int ncopied = 0;
-  for (auto& g : groups) {
-    HIP_CHECK(hipStreamWaitEvent(g_io.side, g.ev, 0));
+  auto queue = [&](Group& g, hipEvent_t ev) {
+    HIP_CHECK(hipStreamWaitEvent(g_io.side, ev, 0));
     for (const char* n : g.names) {
       Item& it = find(n);
       if (!down(it.name)) continue;
       down_bytes += copy_out<T>(dy, it.name, it.p, it.fd, g_io.side, down_blocks);
       ++ncopied;
     }
-  }
+    g.queued = true;
+  };
+  struct Unhook {  // the hooks reference this frame: cleared however step() ends
+    Dycore& d;
+    ~Unhook() {
+      d.on_mark = nullptr;
+      d.marks = nullptr;
+      d.tracer_wait = d.exit_wait = nullptr;
+    }
+  } unhook{dy};
+  if (defer)
+    dy.on_mark = [&](int m) {
+      for (auto& g : groups)
+        if (g.mark == m && !g.queued) queue(g, g_io.marks[m]);
+    };
+  dy.step();
+  HIP_CHECK(hipEventRecord(g_io.ev_t[2], dy.st));
+  for (auto& g : groups)
+    if (!g.queued) queue(g, g_io.ev_t[2]);
   if (ncopied != (int)std::count_if(items.begin(), items.end(), [&](const Item& it) { return down(it.name); }))
     throw std::runtime_error("bridge: copy-back groups do not cover the outputs");
   HIP_CHECK(hipEventRecord(g_io.ev_t[3], g_io.side));

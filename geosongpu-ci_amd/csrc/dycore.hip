@@ -53,10 +53,13 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
   HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&st_b, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&st_c, hipStreamNonBlocking));
-  for (hipEvent_t* e : {&ev_fork, &ev_b, &ev_c}) HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
+  for (hipEvent_t* e : {&ev_fork, &ev_b, &ev_c, &ev_s, &ev_v, &ev_ut})
+    HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   {
     const char* e = std::getenv("GTFV3_STREAMS");
     fork_substep = e ? e[0] == '1' : true;
+    const char* w = std::getenv("GTFV3_EARLY_WINDS");
+    early_winds = !(w && w[0] == '0');
   }
   HIP_CHECK(hipMalloc(&dsubs, sizeof(SubInfo) * d.nsub));
   HIP_CHECK(hipMemcpy(dsubs, hsubs.data(), sizeof(SubInfo) * d.nsub, hipMemcpyHostToDevice));
@@ -113,7 +116,7 @@ Dycore::~Dycore() {
   if (dmet) (void)hipFree(dmet);
   if (dcornerw) (void)hipFree(dcornerw);
   if (darea4) (void)hipFree(darea4);
-  for (hipEvent_t e : {ev_fork, ev_b, ev_c})
+  for (hipEvent_t e : {ev_fork, ev_b, ev_c, ev_s, ev_v, ev_ut})
     if (e) (void)hipEventDestroy(e);
   for (auto& set : ev_ph)
     for (hipEvent_t e : set)
@@ -290,7 +293,7 @@ void Dycore::tracer_2d(int nq, double /*dt*/, int fused_mode, int nf) {
   HIP_CHECK(hipEventRecord(ev_cmax, st));
   tracer_split(c, npz, dns, cx.p, cy.p, xfx.p, yfx.p, mfx.p, mfy.p);
   // the last writer of cx, cy, mfx, mfy (the bridge copies them back from here on)
-  if (marks) HIP_CHECK(hipEventRecord(marks[SM_FLUXES], st));
+  record_mark(SM_FLUXES, st);
   int nmax = -1;
   auto sub_steps = [&]() {
     if (nmax < 0) {
@@ -343,6 +346,12 @@ void Dycore::tracer_2d(int nq, double /*dt*/, int fused_mode, int nf) {
       halo_update({{"q", 'c'}});
     }
   }
+}
+
+void Dycore::record_mark(int m, hipStream_t s) {
+  if (!marks) return;
+  HIP_CHECK(hipEventRecord(marks[m], s));
+  if (on_mark) on_mark(m);
 }
 
 Field& Dycore::need(const std::string& name, int nk) {
@@ -668,8 +677,20 @@ void Dycore::step() {
   copy_halo_ring(c, d.nsub * k1, zh, za.zh_out);
   bool in_graph = false;  // the loop is being captured: no event records inside
   auto acoustic = [&]() {
+  const bool early = fork_substep && early_winds;
   for (int it = 0; it < nl.n_split; ++it) {
     const bool last = it == nl.n_split - 1;
+    if (early) {
+      // d_sw's cell vorticity needs only this sub-step's starting u, v (final here: the last
+      // sub-step's exchange, or the step's first): formed on stream c beside c_sw, so the
+      // wind stage after the fork is the kinetic energy and the vorticity march alone
+      HIP_CHECK(hipEventRecord(ev_s, st));
+      HIP_CHECK(hipStreamWaitEvent(st_c, ev_s, 0));
+      Ctx cc = c;
+      cc.st = st_c;
+      d_sw_vort(cc, da);
+      HIP_CHECK(hipEventRecord(ev_v, st_c));
+    }
     c_sw_transport(c, ca);
     // nord > 0: c_sw's divergence_corner from the D-grid winds and d2a2c's ua, va
     if (nl.nord > 0) divergence_corner(c, npz, u.p, v.p, ua, va, const_cast<double*>(da.divg));
@@ -696,13 +717,13 @@ void Dycore::step() {
     // as one exchange (H_CSC, bit-identical to 'S' then 'C')
     if (nl.nord > 0) halo_update({{"uc", 'X'}, {"vc", 'X'}, {"divgd", 'b'}});
     else halo_update({{"uc", 'X'}, {"vc", 'X'}});
-    if (last && marks && !in_graph) HIP_CHECK(hipEventRecord(marks[SM_CWINDS], st));
+    if (last && !in_graph) record_mark(SM_CWINDS, st);
     // fork: after the Courant numbers, the wind stage of d_sw (stream b) and update_dz_d
     // (stream c) run beside the mass / thermodynamic transport (and the wind stage on beside
     // riem_solver3 and the exchange of delp, pt, zh, ppe, w).  Default on (GTFV3_STREAMS=0: one
     // stream): with the thermo march at one or two waves per SIMD the side streams fill
     // the chip -- C180 on one GPU 43.8 -> 42.4 ms per step.
-    d_sw_courant(c, da);
+    d_sw_courant(c, da, early ? ev_ut : nullptr);
     if (!fork_substep) {
       d_sw_thermo(c, da);
       if (tfused) thermo_swap();
@@ -711,13 +732,21 @@ void Dycore::step() {
       zh_swap();
     } else {
     HIP_CHECK(hipEventRecord(ev_fork, st));
-    HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
     HIP_CHECK(hipStreamWaitEvent(st_c, ev_fork, 0));
     {
       Ctx cb = c, cc = c;
       cb.st = st_b;
       cc.st = st_c;
-      d_sw_winds(cb, da);
+      if (early) {
+        // the kinetic energy needs ut / vt, not the Courant numbers: it starts beside
+        // ds_courant, and the vorticity march waits for those and the vorticity
+        HIP_CHECK(hipStreamWaitEvent(st_b, ev_ut, 0));
+        const hipEvent_t before_march[2] = {ev_fork, ev_v};
+        d_sw_winds(cb, da, true, before_march, 2);
+      } else {
+        HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
+        d_sw_winds(cb, da);
+      }
       update_dz_d(cc, za);
       zh_swap();
     }
@@ -757,7 +786,7 @@ void Dycore::step() {
                                (double)nl.n_split, nl.dddmp, nl.d2_bg, nl.p_fac, nl.dz_min, nl.d4_bg, nl.vtdm4,
                                nl.d_con, (double)nl.nord, (double)nl.nord_v, (double)nl.hord_mt, (double)nl.hord_vt,
                                (double)nl.n_sponge, nl.d2_bg_k1, nl.d2_bg_k2, nl.ke_bg, (double)nl.do_vort_damp,
-                               (double)nl.hord_tm, (double)nl.hord_dp,
+                               (double)nl.hord_tm, (double)nl.hord_dp, (double)early_winds,
                                // launch-shape switches read at every launch (tests flip them in-process)
                                (double)kloop_levels(),
                                (double)riem_variant(), (double)remap_variant()};
@@ -797,9 +826,7 @@ void Dycore::step() {
     damping_heat_apply(c, npz, n_con, std::fabs(bdt * nl.delt_max), da.heat, delp.p, delz.p, pt.p);
   }
   HIP_CHECK(hipEventRecord(ev[1], st));
-  auto mark = [&](int m) {
-    if (marks) HIP_CHECK(hipEventRecord(marks[m], st));
-  };
+  auto mark = [&](int m) { record_mark(m, st); };
   if (graph) mark(SM_CWINDS);  // (not recorded inside the replayed loop)
   mark(SM_ACOUSTIC);
 

@@ -5,6 +5,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <functional>
 #include <map>
 #include <memory>
 #include <string>
@@ -47,6 +48,10 @@ class Dycore {
   // its thermodynamic transport (fork after the Courant numbers, join before riem_solver3)
   hipStream_t st_b = nullptr, st_c = nullptr;
   hipEvent_t ev_fork = nullptr, ev_b = nullptr, ev_c = nullptr;
+  // early d_sw winds (GTFV3_EARLY_WINDS, default on): the sub-step's start (u, v final), the
+  // cell vorticity formed on stream c, ut / vt written
+  hipEvent_t ev_s = nullptr, ev_v = nullptr, ev_ut = nullptr;
+  bool early_winds = true;
   bool fork_substep = true;  // GTFV3_STREAMS=0: one stream
   std::unique_ptr<Transport> comm;  // null for one rank
   std::map<std::string, Field> fields;
@@ -86,6 +91,10 @@ class Dycore {
     SM_COUNT
   };
   hipEvent_t* marks = nullptr;
+  // called on the host right after mark m is recorded (the bridge queues that group's copies
+  // back then, not after step() returns: the step's host thread waits mid-way, in tracer_2d)
+  std::function<void(int)> on_mark;
+  void record_mark(int m, hipStream_t s);
   // the acoustic sub-steps as one HIP graph (GTFV3_GRAPH, Dycore::step): captured on the
   // second step (the first allocates every field and table), replayed while the key (field
   // generation, state planes, step constants) is unchanged

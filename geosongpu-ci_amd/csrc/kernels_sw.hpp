@@ -49,9 +49,16 @@ struct DswArgs {
   double *heat = nullptr, *diss = nullptr;               // d_con: summed over the sub-steps
 };
 void d_sw(const Ctx& c, const DswArgs& a);  // the three stages in order
-void d_sw_courant(const Ctx& c, const DswArgs& a);  // ut, vt, Courant numbers and area fluxes
+// ut, vt, Courant numbers and area fluxes; utvt_done (optional) is recorded once ut / vt are
+// written (d_sw's kinetic energy needs those, not the Courant numbers)
+void d_sw_courant(const Ctx& c, const DswArgs& a, hipEvent_t utvt_done = nullptr);
 void d_sw_thermo(const Ctx& c, const DswArgs& a);   // delp / w / pt transport, flux accumulation
-void d_sw_winds(const Ctx& c, const DswArgs& a);    // kinetic energy, vorticity transport, u, v
+// kinetic energy, vorticity transport, u, v.  vort_done: the cell vorticity was formed already
+// (d_sw_vort, from the same u, v); the stream waits for the nwait events of march_wait before
+// the vorticity march (which needs the Courant numbers)
+void d_sw_winds(const Ctx& c, const DswArgs& a, bool vort_done = false, const hipEvent_t* march_wait = nullptr,
+                int nwait = 0);
+void d_sw_vort(const Ctx& c, const DswArgs& a);  // d_sw's cell vorticity of the old u, v (ds_vort)
 // after both stages (needs the updated delp): d_con heat / diss_est, vorticity-damping fluxes
 void d_sw_post(const Ctx& c, const DswArgs& a);
 bool d_sw_post_needed(const DswArgs& a);

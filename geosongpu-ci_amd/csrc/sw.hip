@@ -785,7 +785,7 @@ bool d_sw_thermo_fused(const DswArgs& a) {
   return on && !deln && a.delp_o && a.w_o && a.pt_o && a.hord_dp == a.hord_vt && a.hord_vt == a.hord_tm;
 }
 
-void d_sw_courant(const Ctx& c, const DswArgs& a) {
+void d_sw_courant(const Ctx& c, const DswArgs& a, hipEvent_t utvt_done) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
@@ -803,6 +803,7 @@ void d_sw_courant(const Ctx& c, const DswArgs& a) {
   GT_LAUNCH(ds_utvt2, dim3(cdiv(edge_line_count(-NG, d.nx + NG, -NG, d.ny + NG), 256), 1, nz), dim3(256), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.ut,
                      a.vt);
   HIP_LAUNCH_CHECK();
+  if (utvt_done) HIP_CHECK(hipEventRecord(utvt_done, c.st));
   const bool acc = d_sw_thermo_fused(a);
   GT_LAUNCH(ds_courant, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.ut, a.vt,
                      a.crx, a.cry, a.xfx, a.yfx, acc ? a.cx : nullptr, acc ? a.cy : nullptr);
@@ -904,7 +905,17 @@ void d_sw_thermo(const Ctx& c, const DswArgs& a) {
   d_sw_w_damping_add(c, a, a.w, false);
 }
 
-void d_sw_winds(const Ctx& c, const DswArgs& a) {
+void d_sw_vort(const Ctx& c, const DswArgs& a) {
+  const Dims& d = c.d;
+  const int nz = d.nsub * a.npz;
+  Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
+  GT_LAUNCH(ds_vort, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.vort);
+  HIP_LAUNCH_CHECK();
+  const Ext e = ext(d);
+  gt_bytes((double)a.npz * (e.X + e.Y + e.C) + 4 * e.C);
+}
+
+void d_sw_winds(const Ctx& c, const DswArgs& a, bool vort_done, const hipEvent_t* march_wait, int nwait) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   if (!a.lv || !a.hlv) throw std::runtime_error("d_sw: the column damping table is required");
@@ -944,10 +955,8 @@ void d_sw_winds(const Ctx& c, const DswArgs& a) {
   level_runs(a.hlv, a.npz, [](const LevelDamp& l) { return l.vt4 > 0.0 ? l.nord_v : -1; },
              [&](int k0, int nk, int nord) { deln_fluxes(c, a.npz, k0, nk, nord, a.lv, DL_VT4, a.wk, a.d2, a.fx2, a.fy2); });
   // vorticity transport
-  Launch2D Lr{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  GT_LAUNCH(ds_vort, g2(d, Lr, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v, a.vort);
-  HIP_LAUNCH_CHECK();
-  gt_bytes(L * (e.X + e.Y + e.C) + 4 * e.C);
+  if (!vort_done) d_sw_vort(c, a);
+  for (int n = 0; n < nwait; ++n) HIP_CHECK(hipStreamWaitEvent(c.st, march_wait[n], 0));
   TpArgs t = d_sw_tp(a);
   t.mfx = nullptr; t.mfy = nullptr;
   t.q = a.vort; t.fx = a.gvx; t.fy = a.gvy; t.ord = a.hord_vt;
