@@ -50,16 +50,25 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
     halo.build(*cs, dc, d, max_nk, 8, false);
     return;
   }
-  HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-  HIP_CHECK(hipStreamCreateWithFlags(&st_b, hipStreamNonBlocking));
-  HIP_CHECK(hipStreamCreateWithFlags(&st_c, hipStreamNonBlocking));
+  {
+    // GTFV3_STREAM_PRIO="a,b,c" (h: the greatest priority, anything else the default): the
+    // dispatch priority of the step's three streams (tuning; default all equal)
+    int least = 0, greatest = 0;
+    HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+    const char* e = std::getenv("GTFV3_STREAM_PRIO");
+    const std::string pr = e ? e : "";
+    auto prio = [&](int n) { return (int)pr.size() > 2 * n && pr[2 * n] == 'h' ? greatest : least; };
+    HIP_CHECK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio(0)));
+    HIP_CHECK(hipStreamCreateWithPriority(&st_b, hipStreamNonBlocking, prio(1)));
+    HIP_CHECK(hipStreamCreateWithPriority(&st_c, hipStreamNonBlocking, prio(2)));
+  }
   for (hipEvent_t* e : {&ev_fork, &ev_b, &ev_c, &ev_s, &ev_v, &ev_ut})
     HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   {
     const char* e = std::getenv("GTFV3_STREAMS");
     fork_substep = e ? e[0] == '1' : true;
     const char* w = std::getenv("GTFV3_EARLY_WINDS");
-    early_winds = !(w && w[0] == '0');
+    early_winds = w && *w ? std::atoi(w) : 1;
   }
   HIP_CHECK(hipMalloc(&dsubs, sizeof(SubInfo) * d.nsub));
   HIP_CHECK(hipMemcpy(dsubs, hsubs.data(), sizeof(SubInfo) * d.nsub, hipMemcpyHostToDevice));
@@ -677,10 +686,10 @@ void Dycore::step() {
   copy_halo_ring(c, d.nsub * k1, zh, za.zh_out);
   bool in_graph = false;  // the loop is being captured: no event records inside
   auto acoustic = [&]() {
-  const bool early = fork_substep && early_winds;
+  const bool early = fork_substep && early_winds != 0;
   for (int it = 0; it < nl.n_split; ++it) {
     const bool last = it == nl.n_split - 1;
-    if (early) {
+    if (early && early_winds == 1) {
       // d_sw's cell vorticity needs only this sub-step's starting u, v (final here: the last
       // sub-step's exchange, or the step's first): formed on stream c beside c_sw, so the
       // wind stage after the fork is the kinetic energy and the vorticity march alone
@@ -701,6 +710,10 @@ void Dycore::step() {
       HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
       Ctx cb = c;
       cb.st = st_b;
+      // (early winds, form 2: d_sw's cell vorticity here, ahead of c_sw's wind stage on the
+      // same stream -- u, v are this sub-step's starting winds until the d_sw march; measured
+      // 32.98-33.10 against form 1's 32.69-32.95 ms per step on one box: not the default)
+      if (early && early_winds == 2) d_sw_vort(cb, da);
       c_sw_winds(cb, ca);
       HIP_CHECK(hipEventRecord(ev_b, st_b));
     } else {
@@ -742,7 +755,7 @@ void Dycore::step() {
         // ds_courant, and the vorticity march waits for those and the vorticity
         HIP_CHECK(hipStreamWaitEvent(st_b, ev_ut, 0));
         const hipEvent_t before_march[2] = {ev_fork, ev_v};
-        d_sw_winds(cb, da, true, before_march, 2);
+        d_sw_winds(cb, da, true, before_march, early_winds == 1 ? 2 : 1);
       } else {
         HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
         d_sw_winds(cb, da);

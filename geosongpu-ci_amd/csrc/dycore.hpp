@@ -48,10 +48,11 @@ class Dycore {
   // its thermodynamic transport (fork after the Courant numbers, join before riem_solver3)
   hipStream_t st_b = nullptr, st_c = nullptr;
   hipEvent_t ev_fork = nullptr, ev_b = nullptr, ev_c = nullptr;
-  // early d_sw winds (GTFV3_EARLY_WINDS, default on): the sub-step's start (u, v final), the
-  // cell vorticity formed on stream c, ut / vt written
+  // early d_sw winds (GTFV3_EARLY_WINDS: 0 off, 1 (default) the cell vorticity on stream c
+  // from the sub-step's start, 2 on stream b ahead of c_sw's wind stage): the sub-step's start
+  // (u, v final), the vorticity formed on stream c, ut / vt written
   hipEvent_t ev_s = nullptr, ev_v = nullptr, ev_ut = nullptr;
-  bool early_winds = true;
+  int early_winds = 1;
   bool fork_substep = true;  // GTFV3_STREAMS=0: one stream
   std::unique_ptr<Transport> comm;  // null for one rank
   std::map<std::string, Field> fields;

@@ -236,14 +236,15 @@ def test_acoustic_graph_bitwise(pkg, require_gpu, monkeypatch, proxy):
         assert np.array_equal(out["0"][k], out["1"][k], equal_nan=bool(proxy)), f"{k}: graph replay differs"
 
 
-@pytest.mark.parametrize("mode", ["streams1", "late_winds"])
+@pytest.mark.parametrize("mode", ["streams1", "late_winds", "vort_on_b"])
 def test_stream_forms_bitwise(pkg, require_gpu, monkeypatch, mode):
     """The default three-stream step (d_sw's cell vorticity on stream c from the sub-step's
     start, its kinetic energy on stream b from ut / vt on, the vorticity march after the
-    Courant numbers: GTFV3_EARLY_WINDS) against every kernel on one stream
-    (GTFV3_STREAMS=0) and against the wind stage forked after the Courant numbers
-    (GTFV3_EARLY_WINDS=0): three C48 L20 steps with the HIP graph off and on, bit for bit on
-    every state field -- a missing cross-stream dependency shows up here as a race."""
+    Courant numbers: GTFV3_EARLY_WINDS=1) against every kernel on one stream
+    (GTFV3_STREAMS=0), the wind stage forked after the Courant numbers (GTFV3_EARLY_WINDS=0)
+    and the vorticity on stream b ahead of c_sw's wind stage (GTFV3_EARLY_WINDS=2): three C48
+    L20 steps with the HIP graph off and on, bit for bit on every state field -- a missing
+    cross-stream dependency shows up here as a race."""
     state = importlib.import_module(pkg.__name__ + ".state")
     npz = 20
     ak, bk, ks = state.hybrid_levels(npz)
@@ -252,7 +253,7 @@ def test_stream_forms_bitwise(pkg, require_gpu, monkeypatch, mode):
         for graph in ("0", "1"):
             monkeypatch.setenv("GTFV3_GRAPH", graph)
             monkeypatch.setenv("GTFV3_STREAMS", "0" if form == "streams1" else "1")
-            monkeypatch.setenv("GTFV3_EARLY_WINDS", "0" if form == "late_winds" else "1")
+            monkeypatch.setenv("GTFV3_EARLY_WINDS", {"late_winds": "0", "vort_on_b": "2"}.get(form, "1"))
             d = pkg.Domain(npx=49, npz=npz, nq=2)
             st = state.jablonowski_williamson(d, ak, bk)
             d.set_vertical(ak, bk, ks)
