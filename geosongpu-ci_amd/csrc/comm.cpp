@@ -4,6 +4,7 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include <condition_variable>
 #include <cstring>
 #include <map>
@@ -184,15 +185,26 @@ class NullTransport : public Transport {
   void recv(double* buf, size_t n, int peer, hipStream_t) override { recvs_.push_back({peer, buf, n}); }
   void group_end(hipStream_t st) override {
     std::vector<bool> used(sends_.size(), false);
+    std::vector<CopyMsg> msgs;
     for (auto& r : recvs_) {
       for (size_t i = 0; i < sends_.size(); ++i) {
         if (used[i] || sends_[i].peer != r.peer) continue;
         used[i] = true;
         const size_t n = std::min(r.n, sends_[i].n);
-        if (n) HIP_CHECK(hipMemcpyAsync(const_cast<double*>(r.p), sends_[i].p, sizeof(double) * n,
-                                        hipMemcpyDeviceToDevice, st));
+        if (n) msgs.push_back({const_cast<double*>(r.p), sends_[i].p, n});
         break;
       }
+    }
+    // the group's copies in one launch, as RCCL moves a grouped set of point-to-point
+    // messages in one kernel (GTFV3_NULL_COPIES=1: one hipMemcpyAsync per message)
+    static const bool each = [] {
+      const char* e = std::getenv("GTFV3_NULL_COPIES");
+      return e && e[0] == '1';
+    }();
+    if (each) {
+      for (auto& m : msgs) HIP_CHECK(hipMemcpyAsync(m.dst, m.src, sizeof(double) * m.n, hipMemcpyDeviceToDevice, st));
+    } else if (!msgs.empty()) {
+      batched_copy(msgs.data(), (int)msgs.size(), st);
     }
     sends_.clear();
     recvs_.clear();

@@ -26,6 +26,15 @@ class Transport {
   virtual bool capturable() const { return false; }
 };
 
+// every device-to-device copy of one message group in one launch (halo.hip), as RCCL moves a
+// grouped set of point-to-point messages in one kernel
+struct CopyMsg {
+  double* dst;
+  const double* src;
+  size_t n;
+};
+void batched_copy(const CopyMsg* msgs, int nmsg, hipStream_t st);
+
 std::unique_ptr<Transport> make_nccl_transport(int nranks, int rank, const void* nccl_id);
 // group < 0: the null transport (one rank alone, each receive answered by its own send to
 // that peer: measurement only)

@@ -367,6 +367,33 @@ __global__ void halo_unpack_kernel(HaloBatch b, long plane, const double* __rest
 
 }  // namespace
 
+namespace {
+// up to CB_MAX messages per launch (kernel-argument table); block y = message
+constexpr int CB_MAX = 96;
+struct CopyBatch {
+  CopyMsg m[CB_MAX];
+};
+__global__ void __launch_bounds__(256) batched_copy_k(CopyBatch b) {
+  const CopyMsg m = b.m[blockIdx.y];
+  for (size_t t = (size_t)blockIdx.x * 256 + threadIdx.x; t < m.n; t += (size_t)gridDim.x * 256) m.dst[t] = m.src[t];
+}
+}  // namespace
+
+void batched_copy(const CopyMsg* msgs, int nmsg, hipStream_t st) {
+  for (int m0 = 0; m0 < nmsg; m0 += CB_MAX) {
+    CopyBatch b{};
+    const int nb = std::min(CB_MAX, nmsg - m0);
+    size_t maxn = 0;
+    for (int q = 0; q < nb; ++q) {
+      b.m[q] = msgs[m0 + q];
+      maxn = std::max(maxn, msgs[m0 + q].n);
+    }
+    const unsigned gx = (unsigned)std::min<size_t>(cdiv((long)maxn, 256L), 64);
+    GT_LAUNCH(batched_copy_k, dim3(gx, nb), dim3(256), 0, st, b);
+    HIP_LAUNCH_CHECK();
+  }
+}
+
 void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream) {
   const bool remote = nranks_ > 1;
   std::vector<size_t> foff(nf);
