@@ -53,14 +53,20 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
   {
     // GTFV3_STREAM_PRIO="a,b,c" (h: the greatest priority, anything else the default): the
     // dispatch priority of the step's three streams (tuning; default all equal)
-    int least = 0, greatest = 0;
-    HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
     const char* e = std::getenv("GTFV3_STREAM_PRIO");
-    const std::string pr = e ? e : "";
-    auto prio = [&](int n) { return (int)pr.size() > 2 * n && pr[2 * n] == 'h' ? greatest : least; };
-    HIP_CHECK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio(0)));
-    HIP_CHECK(hipStreamCreateWithPriority(&st_b, hipStreamNonBlocking, prio(1)));
-    HIP_CHECK(hipStreamCreateWithPriority(&st_c, hipStreamNonBlocking, prio(2)));
+    if (e && *e) {
+      int least = 0, greatest = 0;
+      HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+      const std::string pr = e;
+      auto prio = [&](int n) { return (int)pr.size() > 2 * n && pr[2 * n] == 'h' ? greatest : least; };
+      HIP_CHECK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio(0)));
+      HIP_CHECK(hipStreamCreateWithPriority(&st_b, hipStreamNonBlocking, prio(1)));
+      HIP_CHECK(hipStreamCreateWithPriority(&st_c, hipStreamNonBlocking, prio(2)));
+    } else {
+      HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+      HIP_CHECK(hipStreamCreateWithFlags(&st_b, hipStreamNonBlocking));
+      HIP_CHECK(hipStreamCreateWithFlags(&st_c, hipStreamNonBlocking));
+    }
   }
   for (hipEvent_t* e : {&ev_fork, &ev_b, &ev_c, &ev_s, &ev_v, &ev_ut})
     HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));

@@ -848,24 +848,6 @@ double plan_spans(const Ctx& c, std::vector<int>& ex, std::vector<int>& in) {
   return (double)nex / (double)nall;
 }
 
-// The round-4 layout: strips of MOUT outputs from the sub-domain's first column, the last one
-// narrower, each strip within three columns of a tile edge in the tile-edge form (fewer
-// overlapping reads than the separate tile-edge spans: a 58-output strip reads 64 columns, a
-// 3-output span 16)
-void plan_strips(const Ctx& c, std::vector<int>& spans) {
-  const Dims& d = c.d;
-  if (d.nx + 1 > 4095) throw std::runtime_error("fv_tp_2d: sub-domain too wide for the span encoding");
-  for (int s = 0; s < d.nsub; ++s) {
-    const SubInfo& h = c.hsubs[s];
-    const bool we = h.ioff == 0, ee = h.ioff + d.nx == h.N;
-    for (int a0 = 0; a0 <= d.nx; a0 += MOUT) {
-      const int nout = std::min(MOUT, d.nx + 1 - a0);
-      const bool ex = (we && a0 < 3) || (ee && a0 + nout - 1 > d.nx - 4);
-      spans.push_back(span_enc(s, ex, a0, nout));
-    }
-  }
-}
-
 // fill m's span list from `spans` (any order; sorted into the three classes); returns the
 // launch's wave count
 long set_spans(TpM& m, const std::vector<int>& spans) {
@@ -1133,15 +1115,10 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     // otherwise have fewer than ~6900 field-waves (the C180 count on one GPU; small
     // sub-domains, as on 4-8 GPUs, need the shorter segments to fill the chip).
     std::vector<int> spans;
-    // GTFV3_TP_STRIPS (bit mask, tuning): the round-4 strip layout (plan_strips) instead of the
-    // tile-edge spans for 1 the vorticity (uv) march, 2 the height (zh) march, 4 the tracers
-    static const int strips_env = [] {
-      const char* e = getenv("GTFV3_TP_STRIPS");
-      return e ? atoi(e) : 0;
-    }();
-    const int kind = uv ? 1 : (zup ? 2 : (tupd ? 4 : 0));
-    if (strips_env & kind) plan_strips(c, spans);
-    else plan_spans(c, spans, spans);
+    // (the round-4 layout -- strips of MOUT from the first column, the tile-edge ones in the
+    // edge form -- measured 32.43 / 32.34 / 32.45 ms per step for the uv / zh / tracer marches
+    // against 32.33-32.40 with the spans: not kept)
+    plan_spans(c, spans, spans);
     const double wpp = span_waves_per_plane(spans, d.nsub);
     int seg = a.cfg >= 8 ? a.cfg : seg_env;
     if (seg < 8) {
