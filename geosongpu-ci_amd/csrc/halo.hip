@@ -457,40 +457,41 @@ void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream
     }
   };
   if (remote) {
-    // pack (with the same-rank gather, one launch) on the compute stream, messages on the comm
-    // stream after it, then the unpack after the
-    // messages.  The next exchange's pack follows this unpack in stream order, so the
-    // pack buffers are never rewritten while a send may still read them.  The gather is
-    // enqueued before the messages are posted (it writes halo points only, the pack reads
-    // owned points only), so the device runs it while the host posts them (an 8-rank trace
-    // had the device idle ~10 us between pack and gather at every exchange).
-    // GTFV3_HALO_FUSE=0: the pack and the gather as two launches (the messages then start
-    // after the pack alone)
+    // Default (GTFV3_HALO_FUSE=1): the pack and the same-rank gather in one launch, the
+    // messages and the unpack after it, all on the exchange's own stream -- with nothing left
+    // to overlap the messages with, a separate communication stream only added two cross-queue
+    // hand-offs per exchange (pack -> messages -> unpack: ~13 us each in an 8-rank trace, 0.5 ms
+    // per step).  GTFV3_HALO_FUSE=0: the round-4 form -- the pack, then the messages on the
+    // communication stream while the gather runs on the compute stream, then the unpack.
+    // Either way the next exchange's pack follows this unpack in stream order, so the pack
+    // buffers are never rewritten while a send may still read them.
     static const bool fuse = [] {
       const char* e = std::getenv("GTFV3_HALO_FUSE");
       return !(e && e[0] == '0');
     }();
+    hipStream_t mst = fuse ? stream : comm_st_;
     if (fuse) {
       launch(3);
-      HIP_CHECK(hipEventRecord(ev_packed_, stream));
     } else {
       launch(1);
       HIP_CHECK(hipEventRecord(ev_packed_, stream));
       launch(0);
+      HIP_CHECK(hipStreamWaitEvent(comm_st_, ev_packed_, 0));
     }
-    HIP_CHECK(hipStreamWaitEvent(comm_st_, ev_packed_, 0));
     tr_->group_start();
     for (int f = 0; f < nf; ++f) {
       const HaloField& F = fields[f];
       for (int p = 0; p < nranks_; ++p) {
         int ns = send_peer_count_[F.kind][p], nr = recv_peer_count_[F.kind][p];
-        if (ns) tr_->send(sendbuf_ + foff[f] + (size_t)send_peer_start_[F.kind][p] * F.nk, (size_t)ns * F.nk, p, comm_st_);
-        if (nr) tr_->recv(recvbuf_ + foff[f] + (size_t)recv_peer_start_[F.kind][p] * F.nk, (size_t)nr * F.nk, p, comm_st_);
+        if (ns) tr_->send(sendbuf_ + foff[f] + (size_t)send_peer_start_[F.kind][p] * F.nk, (size_t)ns * F.nk, p, mst);
+        if (nr) tr_->recv(recvbuf_ + foff[f] + (size_t)recv_peer_start_[F.kind][p] * F.nk, (size_t)nr * F.nk, p, mst);
       }
     }
-    tr_->group_end(comm_st_);
-    HIP_CHECK(hipEventRecord(ev_recvd_, comm_st_));
-    HIP_CHECK(hipStreamWaitEvent(stream, ev_recvd_, 0));
+    tr_->group_end(mst);
+    if (!fuse) {
+      HIP_CHECK(hipEventRecord(ev_recvd_, comm_st_));
+      HIP_CHECK(hipStreamWaitEvent(stream, ev_recvd_, 0));
+    }
     launch(2);
     return;
   }
