@@ -59,7 +59,9 @@ __host__ __device__ inline int span_s(int e) { return e >> 19; }
 __host__ __device__ inline bool span_ex(int e) { return ((e >> 18) & 1) != 0; }
 __host__ __device__ inline int span_a0(int e) { return (e >> 6) & 4095; }
 __host__ __device__ inline int span_nout(int e) { return (e & 63) + 1; }
-// levels per wave of a span: class 0 one (> 26 outputs), 1 two (<= 26), 2 four (<= 10)
+// levels per wave of a span: class 0 one (> 26 outputs), 1 two (<= 26), 2 four (<= 10).
+// (Capping the tile-edge spans at two / one levels per wave measured 34.0-34.2 / 35.5 ms per
+// step against 33.1-33.2: the four-level waves stay)
 inline int span_class(int nout) { return nout <= MW / 4 - 6 ? 2 : (nout <= MW / 2 - 6 ? 1 : 0); }
 // DXL (the thermo march's tile-edge strips): the dxa of the <= 8 tile-edge columns a strip
 // can hold (I = -2 .. 1, N-2 .. N+1) for the segment's rows live in LDS, one region per wave,
