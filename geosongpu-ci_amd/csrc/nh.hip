@@ -1040,6 +1040,9 @@ void edge_profile(const Ctx& c, int npz, const double* dp0, const double* crx, c
   else if (variant != 1 && npz >= 3 && npz <= 80)
     GT_LAUNCH(edge_prof_reg_k<80>, g2(d, Lf, 4 * d.nsub), dim3(BX, BY), 0, c.st, d, npz, dp0, crx, xfx, cry, yfx,
               crx_e, xfx_e, cry_e, yfx_e);
+  else if (variant != 1 && npz >= 3 && npz <= 144)
+    GT_LAUNCH(edge_prof_reg_k<144>, g2(d, Lf, 4 * d.nsub), dim3(BX, BY), 0, c.st, d, npz, dp0, crx, xfx, cry, yfx,
+              crx_e, xfx_e, cry_e, yfx_e);
   else
     GT_LAUNCH(edge_prof_k, g2(d, Lf, d.nsub), dim3(BX, BY), 0, c.st, d, npz, dp0, crx, xfx, cry, yfx, crx_e,
               xfx_e, cry_e, yfx_e);

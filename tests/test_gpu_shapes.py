@@ -5,8 +5,8 @@
   strip seams and multi-segment marches all run; single fields, pairs, MF on and off,
   hord 5 and 6, against oracle/tp_core.py fv_tp_2d (bar 1e-12 relative, the SURVEY §8c
   adopted tolerance) and pairs bit for bit against single launches.
-* update_dz_d at L72 (register-column edge profile edge_prof_reg_k<80>) and L137 (the
-  blocked edge_prof_k) against oracle/nh_core.py (edge_profile, then the zh transport),
+* update_dz_d at L72 and L137 (register-column edge profiles edge_prof_reg_k<80> / <144>, and
+  the blocked edge_prof_k) against oracle/nh_core.py (edge_profile, then the zh transport),
   and the register form bit for bit against the blocked form on the same inputs.
 """
 import importlib
@@ -133,9 +133,9 @@ def test_fv_tp_2d_c180_bands(pkg, require_gpu):
 
 @pytest.mark.parametrize("npz", [72, 137])
 def test_update_dz_d_levels(pkg, require_gpu, npz):
-    """update_dz_d at the benchmark level counts: L72 runs the register-column edge profile
-    (edge_prof_reg_k<80>), L137 the blocked edge_prof_k; both against the oracle, and the
-    register form against the blocked form bit for bit."""
+    """update_dz_d at the benchmark level counts: the register-column edge profile
+    (edge_prof_reg_k<80> at L72, edge_prof_reg_k<144> at L137 -- its column in 256 VGPRs + 98
+    AGPRs) against the oracle, and against the blocked edge_prof_k bit for bit."""
     state = importlib.import_module(pkg.__name__ + ".state")
     d = pkg.Domain(npx=25, npz=npz, nq=1)
     try:
