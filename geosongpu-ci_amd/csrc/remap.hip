@@ -599,7 +599,7 @@ enum { JK_PT = 0, JK_DZ = 1, JK_W = 2, JK_UV = 3, JK_Q = 4 };
 // the column forms to rounding (tests/test_gpu_remap.py), not bit for bit.  No scratch planes;
 // each job's source column and output field move once, the source edges once per job.
 constexpr int RB_WAVES = 4;
-constexpr int RB_NT = 4;  // tracers per wave of remap_blkq_k
+constexpr int RB_NT = 4;  // tracers per wave of remap_blkq_k at nq <= 4 (more above: the launcher)
 typedef unsigned int RbU2 __attribute__((ext_vector_type(2)));
 template <int M, int NB, bool PART, int JK>
 __global__ void __launch_bounds__(64 * RB_WAVES) remap_blk_k(RemapArgs a) {
@@ -1336,7 +1336,23 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
       if (variant == 3) {
         GT_LAUNCH((remap_blk_k<M, NB, PART, JK_Q>), dim3(gx, nq, d.nsub), tb, 0, c.st, a);
       } else {
-        GT_LAUNCH((remap_blkq_k<M, NB, PART, RB_NT>), dim3(gx, cdiv(nq, RB_NT), d.nsub), tb, 0, c.st, a);
+        // tracers per wave: the pressure part is formed once per wave and shared, so more
+        // tracers per wave cost less per tracer -- C360 L137 x 54: 76.1 / 69.8 / 66.8 / 65.6 ms
+        // per step for 4 / 8 / 16 / 32 (`profiles/r05n_*`).  Default 16 above 8 tracers, 8
+        // above 4; GTFV3_REMAP_NT (4, 8, 16, 32) overrides
+        static const int nt_env = [] {
+          const char* e = std::getenv("GTFV3_REMAP_NT");
+          return e ? std::atoi(e) : 0;
+        }();
+        const int nt = nt_env > 0 ? nt_env : (nq > 8 ? 16 : (nq > 4 ? 8 : RB_NT));
+        if (nt >= 32 && nq > 16)
+          GT_LAUNCH((remap_blkq_k<M, NB, PART, 32>), dim3(gx, cdiv(nq, 32), d.nsub), tb, 0, c.st, a);
+        else if (nt >= 16 && nq > 8)
+          GT_LAUNCH((remap_blkq_k<M, NB, PART, 16>), dim3(gx, cdiv(nq, 16), d.nsub), tb, 0, c.st, a);
+        else if (nt >= 8 && nq > RB_NT)
+          GT_LAUNCH((remap_blkq_k<M, NB, PART, 8>), dim3(gx, cdiv(nq, 8), d.nsub), tb, 0, c.st, a);
+        else
+          GT_LAUNCH((remap_blkq_k<M, NB, PART, RB_NT>), dim3(gx, cdiv(nq, RB_NT), d.nsub), tb, 0, c.st, a);
       }
       gt_bytes(nq * L * 2 * e.C + L1 * e.C);
     }
