@@ -146,14 +146,27 @@ __global__ void max_k(long n, const double* __restrict__ x, double* __restrict__
   for (; t < n; t += stride) y[t] = fmax(y[t], x[t]);
 }
 
-// the halo ring [-NG, n+NG) x [-NG, n+NG) minus the compute domain, src -> dst, per plane
-__global__ void __launch_bounds__(256) copy_ring_k(Dims d, const double* __restrict__ src, double* __restrict__ dst) {
-  Launch2D L{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
+// the halo ring [-NG, n+NG) x [-NG, n+NG) minus the compute domain, src -> dst, per plane: one
+// lane per ring point (the NG rows above, the NG rows below, then the 2 NG side points of each
+// compute row), planes strided over grid y -- a launch over whole planes would schedule ~30x
+// the lanes for the 3 % of each plane that the ring is
+__global__ void __launch_bounds__(256) copy_ring_k(Dims d, long nplanes, const double* __restrict__ src,
+                                                   double* __restrict__ dst) {
+  const int W = d.nx + 2 * NG;
+  const int t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= 2 * NG * W + 2 * NG * d.ny) return;
   int i, j;
-  if (!thread_point(L, i, j)) return;
-  if (i >= 0 && i < d.nx && j >= 0 && j < d.ny) return;
-  const long o = (long)blockIdx.z * d.plane + pidx(d, i, j);
-  dst[o] = src[o];
+  if (t < 2 * NG * W) {
+    const int r = t / W;
+    i = t - r * W - NG;
+    j = r < NG ? r - NG : d.ny + r - NG;
+  } else {
+    const int s = t - 2 * NG * W, c = s % (2 * NG);
+    j = s / (2 * NG);
+    i = c < NG ? c - NG : d.nx + c - NG;
+  }
+  const long o = pidx(d, i, j);
+  for (long p = blockIdx.y; p < nplanes; p += gridDim.y) dst[p * d.plane + o] = src[p * d.plane + o];
 }
 
 // global tracer diagnostics (FV3 fv_diagnostics prt_mass / g_sum): one block per (sub-domain,
@@ -301,8 +314,10 @@ void held_suarez(const Ctx& c, int npz, double dt, const double* pe, double* pt,
 
 void copy_halo_ring(const Ctx& c, int nplanes, const double* src, double* dst) {
   const Dims& d = c.d;
-  Launch2D L{-NG, -NG, d.nx + 2 * NG, d.ny + 2 * NG};
-  GT_LAUNCH(copy_ring_k, g2(d, L, nplanes), dim3(BX, BY), 0, c.st, d, src, dst);
+  if (nplanes <= 0) return;
+  const int ring = 2 * NG * (d.nx + 2 * NG) + 2 * NG * d.ny;
+  const dim3 grid((unsigned)cdiv(ring, 256), (unsigned)std::min(nplanes, 32768));
+  GT_LAUNCH(copy_ring_k, grid, dim3(256), 0, c.st, d, (long)nplanes, src, dst);
   HIP_LAUNCH_CHECK();
   gt_bytes(2.0 * nplanes * ((d.nx + 2.0 * NG) * (d.ny + 2.0 * NG) - (double)d.nx * d.ny));
 }
