@@ -257,8 +257,17 @@ def cpu_baseline(pkg, npx, npz, nq, dt, moist=False, procs=8):
         ctx = mp.get_context("spawn")  # fresh interpreters: nothing of this process's GPU state
         with ctx.Manager() as man:
             bar = man.Barrier(procs)
-            with ctx.Pool(procs) as pool:
+            # close + join, not the context manager: Pool.__exit__ calls terminate(), which
+            # SIGTERMs the replicas, and under rocprofv3 each then logs an abort trace
+            pool = ctx.Pool(procs)
+            try:
                 els = pool.map(_cpu_replica, [(st, ak, bk, grid, nl, moist, cd_info, bar)] * procs)
+                pool.close()
+            except BaseException:
+                pool.terminate()
+                raise
+            finally:
+                pool.join()
     finally:
         for k, v in env.items():
             if v is None:

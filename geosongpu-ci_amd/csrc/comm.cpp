@@ -20,9 +20,14 @@ namespace {
 class NcclTransport : public Transport {
  public:
   NcclTransport(int nranks, int rank, const void* id_bytes) {
-    if (!id_bytes) throw std::runtime_error("multi-rank run needs an ncclUniqueId");
     ncclUniqueId id;
-    std::memcpy(&id, id_bytes, sizeof(id));
+    if (id_bytes) {
+      std::memcpy(&id, id_bytes, sizeof(id));
+    } else {
+      // a one-rank communicator makes its own id (Namelist::rccl_self); several ranks share one
+      if (nranks != 1) throw std::runtime_error("multi-rank run needs an ncclUniqueId");
+      if (ncclGetUniqueId(&id) != ncclSuccess) throw std::runtime_error("ncclGetUniqueId failed");
+    }
     if (ncclCommInitRank(&comm_, nranks, id, rank) != ncclSuccess) throw std::runtime_error("ncclCommInitRank failed");
   }
   ~NcclTransport() override {

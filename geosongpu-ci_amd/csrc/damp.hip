@@ -315,6 +315,17 @@ __global__ void __launch_bounds__(256) dl_wdamp_k(Dims d, const SubInfo* __restr
   AT(hw, 0, 0) = ke_dt - x * (AT(w, 0, 0) + 0.5 * x);
 }
 
+// update_dz_d's damping of the heights (FV3 nh_utils update_dz_d: del6_vt_flux of zh with
+// (nord_v, damp_vt), zh += (fx2 - fx2(i+1) + fy2 - fy2(j+1)) rarea) on compute cells
+__global__ void __launch_bounds__(256) dl_divadd_k(Dims d, const SubInfo* __restrict__ subs,
+                                                   const double* __restrict__ M, int npz, int k0, int nkw,
+                                                   const double* __restrict__ fx2, const double* __restrict__ fy2,
+                                                   double* __restrict__ q) {
+  Launch2D L{0, 0, d.nx, d.ny};
+  WSETUP()
+  AT(q, 0, 0) = AT(q, 0, 0) + (AT(fx2, 0, 0) - AT(fx2, 1, 0) + AT(fy2, 0, 0) - AT(fy2, 0, 1)) * MA(MT(M_RAREA), 0, 0);
+}
+
 __global__ void __launch_bounds__(256) dl_wadd_k(Dims d, const SubInfo* __restrict__ subs, int npz, int k0, int nkw,
                                                  const double* __restrict__ dw, double* __restrict__ w) {
   Launch2D L{0, 0, d.nx, d.ny};
@@ -537,9 +548,11 @@ std::vector<LevelDamp> column_damping(const Namelist& nl, double da_min, double 
         x.dvt = 0.5 * d2;
       }
     };
+    // FV3 dyn_core: k == 1, k == max(2, n_sponge - 1), k == max(3, n_sponge) (1-based)
+    const int k2 = std::max(1, nl.n_sponge - 2), k3 = std::max(2, nl.n_sponge - 1);
     sponge(p[0], std::max(std::max(0.01, nl.d2_bg), nl.d2_bg_k1), true);
-    if (npz > 1 && nl.d2_bg_k2 > 0.01) sponge(p[1], std::max(nl.d2_bg, nl.d2_bg_k2), true);
-    if (npz > 2 && nl.d2_bg_k2 > 0.05) sponge(p[2], std::max(nl.d2_bg, 0.2 * nl.d2_bg_k2), false);
+    if (npz > k2 && nl.d2_bg_k2 > 0.01) sponge(p[k2], std::max(nl.d2_bg, nl.d2_bg_k2), true);
+    if (npz > k3 && nl.d2_bg_k2 > 0.05) sponge(p[k3], std::max(nl.d2_bg, 0.2 * nl.d2_bg_k2), false);
   }
   std::vector<LevelDamp> out(npz);
   for (int k = 0; k < npz; ++k) {
@@ -621,6 +634,20 @@ void w_damping0_fused(const Ctx& c, int npz, int k0, int nk, const LevelDamp* lv
   // w read, w_new read and written (hw written) per level; seven metric planes
   const Ext e = ext(d);
   gt_bytes(nk * (hw ? 4.0 : 3.0) * e.C + 7.0 * e.C);
+}
+
+void deln_div_add(const Ctx& c, int npz, int k0, int nk, const double* fx2, const double* fy2, double* q) {
+  const Dims& d = c.d;
+  Launch2D L{0, 0, d.nx, d.ny};
+  GT_LAUNCH(dl_divadd_k, g2(L, d.nsub * nk), dim3(BX, BY), 0, c.st, d, c.subs, c.met, npz, k0, nk, fx2, fy2, q);
+  HIP_LAUNCH_CHECK();
+}
+
+std::vector<LevelDamp> height_damping(const std::vector<LevelDamp>& col) {
+  // FV3 update_dz_d: damp(km+1) = damp(km), ndif(km+1) = ndif(km)
+  std::vector<LevelDamp> out(col);
+  if (!out.empty()) out.push_back(out.back());
+  return out;
 }
 
 void w_damping_add(const Ctx& c, int npz, int k0, int nk, const double* dw, double* w) {

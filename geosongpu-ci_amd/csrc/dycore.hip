@@ -47,6 +47,7 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
 
   int max_nk = std::max(nl.npz + 1, nl.npz * std::max(nl.nq, 1));
   if (nl.host_only) {
+    halo.set_self_messages(nl.rccl_self);  // (the tables only: no communicator)
     halo.build(*cs, dc, d, max_nk, 8, false);
     return;
   }
@@ -97,7 +98,13 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
   debug_canary("metrics", dmet, hm.m.data(), sizeof(double) * hm.m.size());
   debug_canary("corner_w", dcornerw, hm.corner_w.data(), sizeof(double) * hm.corner_w.size());
 
-  if (nranks > 1) {
+  if (nl.rccl_self) {
+    // one rank talking to itself over RCCL (Namelist::rccl_self): a size-1 communicator
+    if (nranks != 1 || nl.loopback) throw std::runtime_error("rccl_self needs one rank and no loopback group");
+    comm = make_nccl_transport(1, 0, nullptr);
+    halo.set_transport(comm.get());
+    halo.set_self_messages(true);
+  } else if (nranks > 1) {
     comm = nl.loopback ? make_loopback_transport(nl.loopback, nranks, rank) : make_nccl_transport(nranks, rank, nccl_id);
     halo.set_transport(comm.get());
   }
@@ -115,7 +122,7 @@ Dycore::~Dycore() {
     if (debug_sync_launch()) {
       double* base = kv.second.p - kGuardElems;
       debug_canary_drop(base);
-      debug_canary_drop(kv.second.p + field_elems(kv.second.nk));
+      debug_canary_drop(guard_hi(kv.second.p, kv.second.nk));
       (void)hipFree(base);
     } else {
       (void)hipFree(kv.second.p);
@@ -128,6 +135,7 @@ Dycore::~Dycore() {
   if (ev_cmax) (void)hipEventDestroy(ev_cmax);
   if (dsubs) (void)hipFree(dsubs);
   if (dlevel) (void)hipFree(dlevel);
+  if (dlevel_zh) (void)hipFree(dlevel_zh);
   if (dmet) (void)hipFree(dmet);
   if (dcornerw) (void)hipFree(dcornerw);
   if (darea4) (void)hipFree(darea4);
@@ -152,24 +160,27 @@ Field& Dycore::field(const std::string& name, int nk) {
   f.nk = nk;
   ++field_gen;
   size_t bytes = sizeof(double) * (size_t)field_elems(nk);
+  const size_t pad = sizeof(double) * (size_t)kFieldTailPlanes * d.plane;
   if (debug_sync_launch()) {
-    // debug mode: guard zones either side of the field, checked after every launch
+    // debug mode: guard zones either side of the field, checked after every launch; the
+    // high guard sits after the tail pad the level-block loads may read into (not in it)
     const size_t gb = sizeof(double) * kGuardElems;
     double* base = nullptr;
-    HIP_CHECK(hipMalloc(&base, bytes + 2 * gb));
-    HIP_CHECK(hipMemset(base, 0xA5, bytes + 2 * gb));
+    HIP_CHECK(hipMalloc(&base, bytes + pad + 2 * gb));
+    HIP_CHECK(hipMemset(base, 0xA5, bytes + pad + 2 * gb));
     f.p = base + kGuardElems;
-    HIP_CHECK(hipMemset(f.p, 0, bytes));
+    HIP_CHECK(hipMemset(f.p, 0, bytes + pad));
     const std::vector<unsigned char> pat(gb, 0xA5);
     debug_canary(("guard-lo " + name).c_str(), base, pat.data(), gb);
-    debug_canary(("guard-hi " + name).c_str(), f.p + field_elems(nk), pat.data(), gb);
+    debug_canary(("guard-hi " + name).c_str(), guard_hi(f.p, nk), pat.data(), gb);
     return fields[name] = f;
   }
-  const size_t pad = sizeof(double) * (size_t)kFieldTailPlanes * d.plane;
   HIP_CHECK(hipMalloc(&f.p, bytes + pad));
   HIP_CHECK(hipMemsetAsync(f.p, 0, bytes + pad, st));
   return fields[name] = f;
 }
+
+double* Dycore::guard_hi(double* p, int nk) const { return p + field_elems(nk) + (long)kFieldTailPlanes * d.plane; }
 
 Field* Dycore::find(const std::string& name) {
   auto it = fields.find(name);
@@ -395,22 +406,25 @@ const double* Dycore::vertical_dev() {
   return v.p;
 }
 
-const LevelDamp* Dycore::level_table(const std::vector<LevelDamp>& t) {
+const LevelDamp* Dycore::level_table(const std::vector<LevelDamp>& t, int slot) {
+  std::vector<LevelDamp>& h = slot ? hlevel_zh : hlevel;
+  LevelDamp*& dv = slot ? dlevel_zh : dlevel;
+  size_t& cap = slot ? dlevel_zh_cap : dlevel_cap;
   const size_t bytes = sizeof(LevelDamp) * t.size();
-  if (dlevel && t.size() == hlevel.size() && std::memcmp(t.data(), hlevel.data(), bytes) == 0) return dlevel;
-  if (t.size() > dlevel_cap) {
+  if (dv && t.size() == h.size() && std::memcmp(t.data(), h.data(), bytes) == 0) return dv;
+  if (t.size() > cap) {
     // nothing queued may still read the old table
-    if (dlevel) {
+    if (dv) {
       HIP_CHECK(hipDeviceSynchronize());
-      HIP_CHECK(hipFree(dlevel));
+      HIP_CHECK(hipFree(dv));
     }
-    HIP_CHECK(hipMalloc(&dlevel, bytes));
-    dlevel_cap = t.size();
+    HIP_CHECK(hipMalloc(&dv, bytes));
+    cap = t.size();
   }
-  hlevel = t;
-  HIP_CHECK(hipMemcpyAsync(dlevel, hlevel.data(), bytes, hipMemcpyHostToDevice, st));
+  h = t;
+  HIP_CHECK(hipMemcpyAsync(dv, h.data(), bytes, hipMemcpyHostToDevice, st));
   HIP_CHECK(hipStreamSynchronize(st));
-  return dlevel;
+  return dv;
 }
 
 // One fv_dynamics call (FV3 fv_dynamics.F90 / dyn_core.F90 sequence, non-hydrostatic,
@@ -623,6 +637,12 @@ void Dycore::step() {
   // update_dz_d writes the new heights into a second set of planes (the march reads the
   // old heights' neighbours), which then become "zh" (pointer swap, as the thermo fields)
   za.zh_out = S("_zh_alt", k1);
+  if (vdamp) {
+    // damp_vt on the heights too (FV3 dyn_core: "for delp, delz, and vorticity")
+    za.lv = level_table(height_damping(col), 1);
+    za.hlv = hlevel_zh.data();
+    za.d2 = S("_ud_d2", k1); za.fx2 = S("_ud_fx2", k1); za.fy2 = S("_ud_fy2", k1);
+  }
 
   Riem3Args ra{};
   ra.npz = npz;

@@ -110,12 +110,15 @@ class Dycore {
   const double* vertical_dev();                  // ak | bk | dp_ref on device
   // a column of d_sw parameters on the device (uploaded when it differs from the last one;
   // the pointer stays valid until the next upload of a longer column)
-  const LevelDamp* level_table(const std::vector<LevelDamp>& t);
-  std::vector<LevelDamp> hlevel;
+  // (slot 0: d_sw's column, npz levels; slot 1: update_dz_d's, npz+1 interface levels)
+  const LevelDamp* level_table(const std::vector<LevelDamp>& t, int slot = 0);
+  std::vector<LevelDamp> hlevel, hlevel_zh;
   LevelDamp* dlevel = nullptr;
-  size_t dlevel_cap = 0;
+  LevelDamp* dlevel_zh = nullptr;
+  size_t dlevel_cap = 0, dlevel_zh_cap = 0;
   Ctx ctx() const;
   long field_elems(int nk) const { return (long)d.nsub * nk * d.plane; }
+  double* guard_hi(double* p, int nk) const;  // GTFV3_SYNC_LAUNCH=1: a field's high guard zone
 
   // host <-> device copies of a whole named field in the padded device layout
   void upload(const std::string& name, const double* host, int nk);

@@ -67,6 +67,10 @@ struct Namelist {
   double ptop = 1.0;
   bool host_only = false;            // grid + tables only (CPU tests)
   int loopback = 0;                  // >0: in-process multi-rank group id (single-GPU tests)
+  // one rank only: every same-rank halo point goes through the message path -- pack, RCCL
+  // ncclSend / ncclRecv to itself on a size-1 communicator, unpack -- and the tracer Courant
+  // maximum through ncclAllReduce, so the NcclTransport runs on a one-GPU box
+  bool rccl_self = false;
 };
 
 // One sub-domain (tile piece) owned by this rank.

@@ -62,6 +62,12 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
   d_ = d;
   rank_ = dc.rank;
   nranks_ = dc.nranks;
+  if (self_msgs_ && nranks_ != 1) throw std::runtime_error("halo: self messages need a one-rank layout");
+  remote_ = nranks_ > 1 || self_msgs_;
+  // a same-rank source point: gathered locally, or (self messages) packed, sent to this
+  // rank and unpacked -- the send and receive entries are pushed at the same point in the
+  // same walk, so their orders match as a peer's do
+  const bool local_gather = !self_msgs_;
   const int nper = dc.nsub_per_rank();
   const int nx = d.nx, ny = d.ny;
 
@@ -170,8 +176,12 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
                 continue;
               }
               int doff = (int)pidx(d, i, j);
-              if (s.rank == rank_) h_local_[kind].push_back({ls, doff, s.lsub, s.off, c | (s.comp << 1), s.sign});
-              else recv[s.rank].push_back({ls, doff, c, 0, 0, 0});
+              if (s.rank == rank_ && local_gather)
+                h_local_[kind].push_back({ls, doff, s.lsub, s.off, c | (s.comp << 1), s.sign});
+              else {
+                if (s.rank == rank_) send[rank_].push_back({s.lsub, s.off, s.comp, s.sign, 0, 0});
+                recv[s.rank].push_back({ls, doff, c, 0, 0, 0});
+              }
             }
             if (kind == H_CSYNC) continue;
           }
@@ -188,9 +198,12 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
               Src s = csc_redirect(kind, resolve(g, kind, c, i, j));
               int doff = (int)pidx(d, i, j);
               if (s.zero) h_local_[kind].push_back({ls, doff, -1, 0, c, 0});
-              else if (s.rank == rank_)
+              else if (s.rank == rank_ && local_gather)
                 h_local_[kind].push_back({ls, doff, s.lsub, s.off, c | (s.comp << 1), s.sign});
-              else recv[s.rank].push_back({ls, doff, c, 0, 0, 0});
+              else {
+                if (s.rank == rank_) send[rank_].push_back({s.lsub, s.off, s.comp, s.sign, 0, 0});
+                recv[s.rank].push_back({ls, doff, c, 0, 0, 0});
+              }
             }
         }
       }
@@ -240,7 +253,7 @@ void HaloExchanger::build(const CubedSphere& cs, const Decomp& dc, const Dims& d
     HIP_CHECK(hipMemset(sendbuf_, 0, sizeof(double) * buf_elems_));
     HIP_CHECK(hipMemset(recvbuf_, 0, sizeof(double) * buf_elems_));
   }
-  if (nranks_ > 1) {
+  if (remote_) {
     HIP_CHECK(hipStreamCreateWithFlags(&comm_st_, hipStreamNonBlocking));
     HIP_CHECK(hipEventCreateWithFlags(&ev_packed_, hipEventDisableTiming));
     HIP_CHECK(hipEventCreateWithFlags(&ev_recvd_, hipEventDisableTiming));
@@ -395,7 +408,7 @@ void batched_copy(const CopyMsg* msgs, int nmsg, hipStream_t st) {
 }
 
 void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream) {
-  const bool remote = nranks_ > 1;
+  const bool remote = remote_;
   std::vector<size_t> foff(nf);
   if (remote) {
     size_t off = 0;

@@ -43,6 +43,8 @@ class HaloExchanger {
   ~HaloExchanger();
   void build(const CubedSphere& cs, const Decomp& dc, const Dims& d, int max_nk, int max_fields, bool device = true);
   void set_transport(Transport* t) { tr_ = t; }
+  // before build(): one rank, its same-rank halo points as messages to itself (Namelist::rccl_self)
+  void set_self_messages(bool on) { self_msgs_ = on; }
   // fill halos of all listed fields (enqueued on `stream`)
   void exchange(const HaloField* fields, int nf, hipStream_t stream);
   // host copies of tables for tests
@@ -51,11 +53,13 @@ class HaloExchanger {
   std::vector<int> remote_table(int kind, int dir) const;
   int nranks() const { return nranks_; }
   // an exchange enqueues without host waits (one rank, or a capturable transport)
-  bool capturable() const { return nranks_ == 1 || !tr_ || tr_->capturable(); }
+  bool capturable() const { return !remote_ || !tr_ || tr_->capturable(); }
 
  private:
   Dims d_{};
   int rank_ = 0, nranks_ = 1;
+  bool self_msgs_ = false;
+  bool remote_ = false;  // the exchange runs the message path (several ranks, or self messages)
   Transport* tr_ = nullptr;
   std::vector<HaloEntry> h_local_[H_NKIND];
   std::vector<PackEntry> h_send_[H_NKIND], h_recv_[H_NKIND];

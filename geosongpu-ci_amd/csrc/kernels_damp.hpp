@@ -61,6 +61,12 @@ void deln_add(const Ctx& c, int npz, int k0, int nk, const LevelDamp* lv, const 
 void w_damping(const Ctx& c, int npz, int k0, int nk, double ke_dt, const double* fx2, const double* fy2,
                const double* w, double* dw, double* hw);
 void w_damping_add(const Ctx& c, int npz, int k0, int nk, const double* dw, double* w);
+// q += (fx2 - fx2(i+1) + fy2 - fy2(j+1)) rarea on compute cells of levels [k0, k0+nk)
+// (update_dz_d's height damping)
+void deln_div_add(const Ctx& c, int npz, int k0, int nk, const double* fx2, const double* fy2, double* q);
+// update_dz_d's per-interface column (npz+1 levels): the d_sw column with the bottom level's
+// (nord_v, damp_vt) repeated for the surface interface (FV3: damp(km+1) = damp(km))
+std::vector<LevelDamp> height_damping(const std::vector<LevelDamp>& col);
 // nord_w = 0 levels after the fused thermo march, one pass: dw from the old w, w_new += dw,
 // hw (nullable) its heat -- bit-identical to deln_fluxes + w_damping + w_damping_add
 void w_damping0_fused(const Ctx& c, int npz, int k0, int nk, const LevelDamp* lv, double ke_dt, const double* w,

@@ -4,6 +4,8 @@
 
 namespace gtfv3 {
 
+struct LevelDamp;  // kernels_damp.hpp
+
 // per-column work planes (each npz+1 levels, [sub][k][plane])
 struct NhScratch {
   double* s[14];
@@ -25,6 +27,12 @@ struct UdzdArgs {
   double *crx_e, *cry_e, *xfx_e, *yfx_e;
   const double* zh;
   double* zh_out;  // the updated heights (out of place: the march reads zh's neighbours)
+  // damp_vt of the heights (FV3 update_dz_d's del6_vt_flux of zh): the npz+1-level column of
+  // kernels_damp.hpp height_damping, device and host copies; null: no level damps.  d2, fx2,
+  // fy2: npz+1-level scratch planes
+  const LevelDamp* lv = nullptr;
+  const LevelDamp* hlv = nullptr;
+  double *d2 = nullptr, *fx2 = nullptr, *fy2 = nullptr;
 };
 void update_dz_d(const Ctx& c, const UdzdArgs& a);
 // update_dz_d's edge_profile of (crx, xfx) on x-face and (cry, yfx) on y-face columns.

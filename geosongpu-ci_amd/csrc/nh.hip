@@ -9,6 +9,7 @@
 #include <climits>
 
 #include "fastmath.hpp"
+#include "kernels_damp.hpp"
 #include "kernels_nh.hpp"
 #include "stencil_common.hpp"
 
@@ -1064,6 +1065,14 @@ void update_dz_d(const Ctx& c, const UdzdArgs& a) {
   t.zh_out = a.zh_out;
   fv_tp_2d(c, t);
   (void)d;
+  if (!a.hlv) return;
+  // the heights' del-n damping from the old heights (their halo filled), added to the new ones
+  // before riem_solver3's dz_min clamp (FV3 update_dz_d: one expression, transport + damping)
+  level_runs(a.hlv, k1, [](const LevelDamp& l) { return l.vt4 > 0.0 ? l.nord_v : -1; },
+             [&](int k0, int nk, int nord) {
+               deln_fluxes(c, k1, k0, nk, nord, a.lv, DL_VT4, a.zh, a.d2, a.fx2, a.fy2);
+               deln_div_add(c, k1, k0, nk, a.fx2, a.fy2, a.zh_out);
+             });
 }
 
 void pk3_pe_halo(const Ctx& c, int npz, double ptop, bool do_pe, const double* delp, double* pk3, double* pe) {

@@ -189,6 +189,11 @@ def fv_dynamics(st, ak, bk, g, nl):
                                    do_vort_damp=bool(nl.get("do_vort_damp", 0)), nord_v=nl.get("nord_v"),
                                    d_con=d_con, **sp)
     groups = level_groups(cols)
+    # update_dz_d's height damping: (nord_v, (damp_vt da_min_c)^(nord_v+1)) per interface, the
+    # bottom layer's repeated for the surface (FV3 damp(km+1) = damp(km))
+    zdamp = [(c["nord_v"], (c["damp_vt"] * g.da_min_c) ** (c["nord_v"] + 1) if c["damp_vt"] > 1e-5 else 0.0)
+             for c in cols]
+    zdamp = zdamp + zdamp[-1:] if any(z[1] > 0.0 for z in zdamp) else None
     d4_bg, ke_bg = float(nl.get("d4_bg", 0.0)), float(nl.get("ke_bg", 0.0))
     if nord > 0:
         st["divgd"] = np.zeros(shp)
@@ -239,7 +244,7 @@ def fv_dynamics(st, ak, bk, g, nl):
             m, sub, P = g.ms[s], g.subs[s], g.P[s]
             r = ds[s]
             zh, ws = nh_core.update_dz_d(st["zh"][s], r["crx"], r["cry"], r["xfx"], r["yfx"], zs[s], sub, m, nx, ny,
-                                         dp0, dt, nl["hord_tm"], nl["dz_min"])
+                                         dp0, dt, nl["hord_tm"], nl["dz_min"], zdamp)
             o = nh_core.riem_solver3(dt, st["delp"][s], st["pt"][s], st["w"][s], zh, zs[s], ws, ptop, nl["p_fac"],
                                      comp[s], last)
             st["w"][s] = o["w"]

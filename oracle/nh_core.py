@@ -237,11 +237,21 @@ def update_dz_d_transport(zh, crx, cry, xfx, yfx, sub, m, nx, ny, dp0, hord):
     return np.where(comp, new, zh)
 
 
-def update_dz_d(zh, crx, cry, xfx, yfx, zs, sub, m, nx, ny, dp0, dt, hord, dz_min):
+def update_dz_d(zh, crx, cry, xfx, yfx, zs, sub, m, nx, ny, dp0, dt, hord, dz_min, damp=None):
+    """FV3 nh_utils update_dz_d: the heights transported (update_dz_d_transport), plus, on the
+    interfaces whose damp_vt > 1e-5, del6_vt_flux's diffusive fluxes of the old heights with
+    coefficient (damp_vt da_min_c)^(nord_v+1) (`damp`: per interface level (nord_v, coefficient
+    or 0); FV3 damp(km+1) = damp(km)), zh += div(fx2, fy2) rarea; then the dz_min clamp and ws"""
     km = crx.shape[0]
     P = Plane(sub, nx, ny, zh.shape[-2], zh.shape[-1])
     comp = P.reg(0, nx - 1, 0, ny - 1)
     out = update_dz_d_transport(zh, crx, cry, xfx, yfx, sub, m, nx, ny, dp0, hord)
+    if damp is not None:
+        from .sw_core import deln_flux
+        for k, (nord_v, coef) in enumerate(damp):
+            if coef > 0.0:
+                fx2, fy2 = deln_flux(nord_v, coef, zh[k], sub, m, nx, ny)
+                out[k] = np.where(comp, out[k] + (fx2 - sh(fx2, 1, 0) + fy2 - sh(fy2, 0, 1)) * m["rarea"], out[k])
     ws = np.where(comp, (zs - out[km]) * (1.0 / dt), 0.0)
     for k in range(km - 1, -1, -1):
         out[k] = np.where(comp, np.maximum(out[k], out[k + 1] + dz_min), out[k])

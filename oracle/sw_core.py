@@ -327,8 +327,9 @@ def column_namelist(npz, nord=0, d2_bg=0.0, vtdm4=0.0, do_vort_damp=False, nord_
     nord_v / damp_vt.  Sponge layers (npz > 1, n_sponge >= 0), no special damping of pt:
       level 0:  nord 0, d2_divg = max(0.01, d2_bg, d2_bg_k1), w del-2 with damp_w = d2_divg,
                 with do_vort_damp vorticity / delp del-2 with damp_vt = d2_divg / 2, d_con 0;
-      level 1 (d2_bg_k2 > 0.01): the same with d2_divg = max(d2_bg, d2_bg_k2);
-      level 2 (d2_bg_k2 > 0.05): nord 0, d2_divg = max(d2_bg, 0.2 d2_bg_k2), w del-2, d_con 0.
+      level max(1, n_sponge-2) (d2_bg_k2 > 0.01): the same with d2_divg = max(d2_bg, d2_bg_k2);
+      level max(2, n_sponge-1) (d2_bg_k2 > 0.05): nord 0, d2_divg = max(d2_bg, 0.2 d2_bg_k2),
+      w del-2, d_con 0 (levels 1 and 2 for n_sponge <= 3).
     npz = 1 or n_sponge < 0: d2_divg = d2_bg on every level."""
     nv = min(2, nord) if nord_v is None else int(nord_v)
     dvt = float(vtdm4) if do_vort_damp else 0.0
@@ -344,11 +345,13 @@ def column_namelist(npz, nord=0, d2_bg=0.0, vtdm4=0.0, do_vort_damp=False, nord_
         c.update(nord=0, d2_divg=d2, nord_w=0, damp_w=d2, d_con=0.0)
         if vort and do_vort_damp:
             c.update(nord_v=0, damp_vt=0.5 * d2)
+    # dyn_core's levels (1-based) k == 1, k == max(2, n_sponge - 1), k == max(3, n_sponge)
+    k2, k3 = max(1, n_sponge - 2), max(2, n_sponge - 1)
     sponge(cols[0], max(0.01, d2_bg, d2_bg_k1), True)
-    if npz > 1 and d2_bg_k2 > 0.01:
-        sponge(cols[1], max(d2_bg, d2_bg_k2), True)
-    if npz > 2 and d2_bg_k2 > 0.05:
-        sponge(cols[2], max(d2_bg, 0.2 * d2_bg_k2), False)
+    if npz > k2 and d2_bg_k2 > 0.01:
+        sponge(cols[k2], max(d2_bg, d2_bg_k2), True)
+    if npz > k3 and d2_bg_k2 > 0.05:
+        sponge(cols[k3], max(d2_bg, 0.2 * d2_bg_k2), False)
     return cols
 
 

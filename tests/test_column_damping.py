@@ -25,6 +25,10 @@ CASES = {
     "nord3_del2": dict(nord=3, d4_bg=0.12, d2_bg=0.005, vtdm4=0.02, do_vort_damp=1, nord_v=1),
     "strong_sponge": dict(d2_bg_k1=0.25, d2_bg_k2=0.12, ke_bg=3.0, do_vort_damp=1, vtdm4=0.0),
     "convert_ke": dict(convert_ke=1, d2_bg_k1=0.0),
+    # deeper sponge: dyn_core's second / third overrides at levels max(2, n_sponge-1) and
+    # max(3, n_sponge) (1-based), here 4 and 5
+    "n_sponge5": dict(n_sponge=5),
+    "n_sponge5_vort": dict(n_sponge=5, do_vort_damp=1, vtdm4=0.03),
 }
 
 
@@ -78,6 +82,43 @@ def test_held_suarez_sponge_levels(pkg):
     assert [c["w4"] for c in col[:4]] == [0.2 * dac, 0.1 * dac, 0.2 * 0.1 * dac, 0.0]
     assert all(c["vt4"] == 0.0 and c["dp4"] == 0.0 and c["pt4"] == 0.0 for c in col)
     assert n_con == 2
+
+
+def test_deep_sponge_override_levels(pkg):
+    """n_sponge = 5: the overrides land on levels 0, 3 and 4 (0-based), levels 1-2 ordinary"""
+    d = pkg.Domain(npx=13, npz=10, nq=1, host_only=1, n_sponge=5)
+    try:
+        col, _ = d.level_damping()
+    finally:
+        d.close()
+    assert [c["d2_divg"] for c in col[:6]] == [0.2, 0.0, 0.0, 0.1, 0.2 * 0.1, 0.0]
+
+
+def test_height_damping_column(pkg):
+    """update_dz_d's damping of the heights (ADVICE r05): with do_vort_damp the oracle's
+    update_dz_d adds del6_vt_flux of the old heights, an effect far above the step's parity bar"""
+    import numpy as np
+
+    from oracle import nh_core
+    from conftest import metrics_of
+    d = pkg.Domain(npx=13, npz=4, nq=1, host_only=1)
+    try:
+        m = metrics_of(d)[0]
+        sub, nx, ny = d.subs[0], d.nx, d.ny
+        sh = d.shape(5)[1:]
+        r = np.random.default_rng(5)
+        zh = 1e4 - 2e3 * np.arange(5)[:, None, None] + 50.0 * r.standard_normal(sh)
+        z4 = np.zeros(d.shape(4)[1:])
+        dp0 = np.full(4, 2000.0)
+        args = (zh, z4, z4, z4, z4, zh[4], sub, m, nx, ny, dp0, 75.0, 6, 2.0)
+        plain, _ = nh_core.update_dz_d(*args)
+        damp = [(0, 0.0), (0, 0.02 * 1e8), (1, 0.0), (1, 0.0), (1, 0.0)]
+        damped, _ = nh_core.update_dz_d(*args, damp=damp)
+    finally:
+        d.close()
+    c = (slice(None), slice(3, 3 + ny), slice(3, 3 + nx))
+    diff = np.abs(damped - plain)[c]
+    assert diff[1].max() > 1e-3 and diff[0].max() == 0.0 and diff[2:].max() == 0.0
 
 
 def test_config_kord_and_sponge_keys(pkg, capfd):

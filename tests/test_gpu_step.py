@@ -267,3 +267,45 @@ def test_stream_forms_bitwise(pkg, require_gpu, monkeypatch, mode):
     for key, got in out.items():
         for k in ref:
             assert np.array_equal(ref[k], got[k]), f"{k}: {key} differs from the default three-stream step"
+
+
+def test_hip_step_dry_mass_with_corner_anomaly(pkg, require_gpu):
+    """Global dry mass of the full HIP step with a sharp delp anomaly
+    (+30 %, e-folding 1.5 cells) centred on the (0, 0) cube corner of every tile, so the
+    sub-steps' mass fluxes through the corner-adjacent tile edges -- the ones each tile forms
+    from its own copy_corners fill -- carry a strong gradient.  Measured on the oracle (numpy,
+    C12 L10): 4.8e-12 / 6.0e-13 per step with the anomaly against 1.4e-11 / 1.6e-12 for the
+    smooth JW06 state, i.e. the corner fluxes do not dominate the step's mass budget; the bar
+    is the smooth state's documented drift (3e-11 per step, tests/test_oracle_props.py), and
+    the HIP step must also match the oracle's change to 1e-12 of the mass."""
+    from oracle import fv_dynamics as fvd
+    state = importlib.import_module(pkg.__name__ + ".state")
+    npz = 10
+    d = pkg.Domain(npx=13, npz=npz, nq=2)
+    ak, bk, ks = state.hybrid_levels(npz)
+    st = state.jablonowski_williamson(d, ak, bk)
+    n = d.N
+    jj, ii = np.meshgrid(np.arange(-NG, d.nj - NG), np.arange(-NG, d.pitch - NG), indexing="ij")
+    st["delp"] = st["delp"] * (1.0 + 0.3 * np.exp(-((ii + 0.5) ** 2 + (jj + 0.5) ** 2) / 1.5 ** 2))[None, None]
+    d.set_vertical(ak, bk, ks)
+    for k, v in st.items():
+        d.upload(k, v)
+    area = d.metric("area")[:, None, NG:NG + n, NG:NG + n]
+
+    def mass(dp):
+        return float((dp[..., NG:NG + n, NG:NG + n] * area).sum())
+
+    m0 = mass(st["delp"])
+    d.step(1)
+    m1 = mass(d.download("delp"))
+    ms = metrics_of(d)
+    sc = oracle_scalars(d)
+    g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
+    d.close()
+    nl = dict(n_split=6, dt_atmos=900.0, hord_mt=6, hord_vt=6, hord_tm=6, hord_dp=6, hord_tr=6, dddmp=0.2,
+              d2_bg=0.0, p_fac=0.05, dz_min=2.0, fill=1, nq=2)
+    ref = fvd.fv_dynamics(st, ak, bk, g, nl)
+    mr = mass(ref["delp"])
+    print(f"corner anomaly: HIP mass change {(m1 - m0) / m0:.2e}, oracle {(mr - m0) / m0:.2e} per step")
+    assert abs(m1 - m0) / m0 < 3e-11, (m1 - m0) / m0
+    assert abs(m1 - mr) / m0 < 1e-12, (m1 - mr) / m0

@@ -5,7 +5,9 @@ the CPU (~75 s; too slow to repeat inside a GPU test).  The fixture keeps, per s
 the value at a fixed random sample of compute-domain points and the mean over the compute
 domain of every (sub-domain, level) plane:
 
-    python tools/make_c48_golden.py  ->  tests/golden/c48_l72_step.npz
+    python tools/make_c48_golden.py              ->  tests/golden/c48_l72_step.npz
+    python tools/make_c48_golden.py --no-sponge  ->  tests/golden/c48_l72_step_nosponge.npz
+                                                     (n_sponge = -1: the round-4 namelist)
 
 tests/test_gpu_configs.py runs the HIP step on the same state and compares."""
 import importlib
@@ -32,6 +34,8 @@ NL = dict(n_split=6, dt_atmos=DT, hord_mt=6, hord_vt=6, hord_tm=6, hord_dp=6, ho
 
 
 def main():
+    nosponge = "--no-sponge" in sys.argv
+    nl = dict(NL, n_sponge=-1) if nosponge else NL
     pkg = gtfv3_pkg.load()
     state = importlib.import_module(pkg.__name__ + ".state")
     d = pkg.Domain(npx=NPX, npz=NPZ, nq=NQ, host_only=1)
@@ -41,7 +45,7 @@ def main():
     sc = oracle_scalars(d)
     g = fvd.Grid(d.N, 1, 1, ms, sc["corner_w"], sc["da_min_c"], d.nj, d.pitch)
     t0 = time.time()
-    ref = fvd.fv_dynamics(st, ak, bk, g, NL)
+    ref = fvd.fv_dynamics(st, ak, bk, g, nl)
     print(f"oracle step {time.time() - t0:.1f} s")
     n = d.N
     r = np.random.default_rng(4872)
@@ -52,7 +56,8 @@ def main():
         out[f"{k}_idx"] = idx
         out[f"{k}_val"] = a[tuple(idx.T)]
         out[f"{k}_mean"] = a.mean(axis=(2, 3))
-    np.savez_compressed(os.path.join(ROOT, "tests", "golden", "c48_l72_step.npz"), **out)
+    np.savez_compressed(os.path.join(ROOT, "tests", "golden",
+                                     "c48_l72_step_nosponge.npz" if nosponge else "c48_l72_step.npz"), **out)
 
 
 if __name__ == "__main__":
