@@ -201,16 +201,9 @@ class NullTransport : public Transport {
       }
     }
     // the group's copies in one launch, as RCCL moves a grouped set of point-to-point
-    // messages in one kernel (GTFV3_NULL_COPIES=1: one hipMemcpyAsync per message)
-    static const bool each = [] {
-      const char* e = std::getenv("GTFV3_NULL_COPIES");
-      return e && e[0] == '1';
-    }();
-    if (each) {
-      for (auto& m : msgs) HIP_CHECK(hipMemcpyAsync(m.dst, m.src, sizeof(double) * m.n, hipMemcpyDeviceToDevice, st));
-    } else if (!msgs.empty()) {
-      batched_copy(msgs.data(), (int)msgs.size(), st);
-    }
+    // messages in one kernel (one hipMemcpyAsync per message: 6.99 against 5.85 ms at the
+    // 8-rank share)
+    if (!msgs.empty()) batched_copy(msgs.data(), (int)msgs.size(), st);
     sends_.clear();
     recvs_.clear();
   }

@@ -51,31 +51,18 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
     halo.build(*cs, dc, d, max_nk, 8, false);
     return;
   }
-  {
-    // GTFV3_STREAM_PRIO="a,b,c" (h: the greatest priority, anything else the default): the
-    // dispatch priority of the step's three streams (tuning; default all equal)
-    const char* e = std::getenv("GTFV3_STREAM_PRIO");
-    if (e && *e) {
-      int least = 0, greatest = 0;
-      HIP_CHECK(hipDeviceGetStreamPriorityRange(&least, &greatest));
-      const std::string pr = e;
-      auto prio = [&](int n) { return (int)pr.size() > 2 * n && pr[2 * n] == 'h' ? greatest : least; };
-      HIP_CHECK(hipStreamCreateWithPriority(&st, hipStreamNonBlocking, prio(0)));
-      HIP_CHECK(hipStreamCreateWithPriority(&st_b, hipStreamNonBlocking, prio(1)));
-      HIP_CHECK(hipStreamCreateWithPriority(&st_c, hipStreamNonBlocking, prio(2)));
-    } else {
-      HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
-      HIP_CHECK(hipStreamCreateWithFlags(&st_b, hipStreamNonBlocking));
-      HIP_CHECK(hipStreamCreateWithFlags(&st_c, hipStreamNonBlocking));
-    }
-  }
+  // the step's three streams, default priority (dispatch priorities measured no gain at C180
+  // and starved the side streams at the 8-rank share: 7.0 -> 12.1-12.7 ms)
+  HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
+  HIP_CHECK(hipStreamCreateWithFlags(&st_b, hipStreamNonBlocking));
+  HIP_CHECK(hipStreamCreateWithFlags(&st_c, hipStreamNonBlocking));
   for (hipEvent_t* e : {&ev_fork, &ev_b, &ev_c, &ev_s, &ev_v, &ev_ut})
     HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   {
     const char* e = std::getenv("GTFV3_STREAMS");
     fork_substep = e ? e[0] == '1' : true;
-    const char* w = std::getenv("GTFV3_EARLY_WINDS");
-    early_winds = w && *w ? std::atoi(w) : 1;
+    const char* w = std::getenv("GTFV3_EARLY_WINDS");  // 0: the wind stage after the Courant numbers
+    early_winds = w && *w && w[0] == '0' ? 0 : 1;
   }
   HIP_CHECK(hipMalloc(&dsubs, sizeof(SubInfo) * d.nsub));
   HIP_CHECK(hipMemcpy(dsubs, hsubs.data(), sizeof(SubInfo) * d.nsub, hipMemcpyHostToDevice));
@@ -236,6 +223,18 @@ void Dycore::download(const std::string& name, double* host) {
 }
 
 void Dycore::halo_update(const std::vector<std::pair<std::string, char>>& items) {
+  const std::vector<HaloField> hf = halo_fields(items);
+  halo.exchange(hf.data(), (int)hf.size(), st);
+}
+
+void Dycore::halo_begin(const std::vector<std::pair<std::string, char>>& items) {
+  const std::vector<HaloField> hf = halo_fields(items);
+  halo.exchange_begin(hf.data(), (int)hf.size(), st);
+}
+
+void Dycore::halo_end() { halo.exchange_end(st); }
+
+std::vector<HaloField> Dycore::halo_fields(const std::vector<std::pair<std::string, char>>& items) {
   std::vector<HaloField> hf;
   for (size_t n = 0; n < items.size(); ++n) {
     const auto& it = items[n];
@@ -262,7 +261,7 @@ void Dycore::halo_update(const std::vector<std::pair<std::string, char>>& items)
     }
     hf.push_back(h);
   }
-  halo.exchange(hf.data(), (int)hf.size(), st);
+  return hf;
 }
 
 void Dycore::allreduce_max(double* dev, int n) {
@@ -498,6 +497,17 @@ void Dycore::moist_physics(double dt) {
   radcouple(c, r);
 }
 
+// GTFV3_HALO_SPLIT (read per step): the interior / boundary split of the uc / vc and u / v
+// exchanges.  Unset: on where the messages cross GPUs (RCCL with several ranks), off for the
+// null / loopback transports and the one-rank RCCL self messages, whose messages are device
+// copies that take less than the split's two cross-queue hand-offs (the 8-rank share on the
+// null transport: 5.91 ms whole exchanges, 6.37 ms split with four-rectangle frames);
+// "1" on, "0" off wherever the exchanges carry messages.
+static int halo_split_mode() {
+  const char* e = std::getenv("GTFV3_HALO_SPLIT");
+  return e && *e ? (e[0] == '0' ? 0 : 1) : -1;
+}
+
 // GTFV3_GRAPH=1: the acoustic sub-steps replayed as one captured HIP graph (read per step).
 // Off by default: measured on one MI355X, the graph saves the launch gaps of the small
 // per-rank shares (rank 0 of the 8-rank layout alone: 6.91 -> 6.66 ms per step) but loses
@@ -711,11 +721,26 @@ void Dycore::step() {
   // regions) holds the same value whichever set is current -- the in-place update's semantics
   copy_halo_ring(c, d.nsub * k1, zh, za.zh_out);
   bool in_graph = false;  // the loop is being captured: no event records inside
+  // Interior / boundary split of the exchanges with messages (several ranks, or RCCL self
+  // messages; GTFV3_HALO_SPLIT=0: off): the uc / vc and the u / v exchanges begin (pack, same-rank
+  // gather, messages on the exchange's communication stream), the stencil that consumes them
+  // runs on the points that read no halo value -- ds_utvt1 after uc / vc, cs_tmp after u / v --
+  // while the messages fly, then the exchange ends (unpack) and the boundary frame follows.
+  const int split_mode = halo_split_mode();
+  const bool split = halo.remote() && split_fits(d) && kloop_levels() > 0 &&
+                     (split_mode == 1 || (split_mode < 0 && dc.nranks > 1 && !nl.loopback));
   auto acoustic = [&]() {
   const bool early = fork_substep && early_winds != 0;
+  bool uv_open = false;  // the previous sub-step's u, v exchange has begun and not ended
   for (int it = 0; it < nl.n_split; ++it) {
     const bool last = it == nl.n_split - 1;
-    if (early && early_winds == 1) {
+    if (uv_open) {
+      c_sw_transport(c, ca, 1);  // cs_tmp's interior beside the messages
+      halo_end();
+      uv_open = false;
+    }
+    const int csw_part = split && it > 0 ? 2 : 0;
+    if (early) {
       // d_sw's cell vorticity needs only this sub-step's starting u, v (final here: the last
       // sub-step's exchange, or the step's first): formed on stream c beside c_sw, so the
       // wind stage after the fork is the kinetic energy and the vorticity march alone
@@ -726,7 +751,7 @@ void Dycore::step() {
       d_sw_vort(cc, da);
       HIP_CHECK(hipEventRecord(ev_v, st_c));
     }
-    c_sw_transport(c, ca);
+    c_sw_transport(c, ca, csw_part);
     // nord > 0: c_sw's divergence_corner from the D-grid winds and d2a2c's ua, va
     if (nl.nord > 0) divergence_corner(c, npz, u.p, v.p, ua, va, const_cast<double*>(da.divg));
     // c_sw's wind stage (vorticity, uc / vc) beside update_dz_c + riem_solver_c: they share
@@ -736,10 +761,6 @@ void Dycore::step() {
       HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
       Ctx cb = c;
       cb.st = st_b;
-      // (early winds, form 2: d_sw's cell vorticity here, ahead of c_sw's wind stage on the
-      // same stream -- u, v are this sub-step's starting winds until the d_sw march; measured
-      // 32.98-33.10 against form 1's 32.69-32.95 ms per step on one box: not the default)
-      if (early && early_winds == 2) d_sw_vort(cb, da);
       c_sw_winds(cb, ca);
       HIP_CHECK(hipEventRecord(ev_b, st_b));
     } else {
@@ -754,15 +775,24 @@ void Dycore::step() {
     // the cube corners -- the corner circulation of c_sw -- and so do their mass fluxes:
     // a dry-mass drift of 3e-7 per step, 1.5e-11 with the sync); the sync and the C halo
     // as one exchange (H_CSC, bit-identical to 'S' then 'C')
-    if (nl.nord > 0) halo_update({{"uc", 'X'}, {"vc", 'X'}, {"divgd", 'b'}});
-    else halo_update({{"uc", 'X'}, {"vc", 'X'}});
+    {
+      std::vector<std::pair<std::string, char>> cx = {{"uc", 'X'}, {"vc", 'X'}};
+      if (nl.nord > 0) cx.push_back({"divgd", 'b'});
+      if (split) {
+        halo_begin(cx);
+        d_sw_courant(c, da, nullptr, 1);  // ds_utvt1's interior beside the messages
+        halo_end();
+      } else {
+        halo_update(cx);
+      }
+    }
     if (last && !in_graph) record_mark(SM_CWINDS, st);
     // fork: after the Courant numbers, the wind stage of d_sw (stream b) and update_dz_d
     // (stream c) run beside the mass / thermodynamic transport (and the wind stage on beside
     // riem_solver3 and the exchange of delp, pt, zh, ppe, w).  Default on (GTFV3_STREAMS=0: one
     // stream): with the thermo march at one or two waves per SIMD the side streams fill
     // the chip -- C180 on one GPU 43.8 -> 42.4 ms per step.
-    d_sw_courant(c, da, early ? ev_ut : nullptr);
+    d_sw_courant(c, da, early ? ev_ut : nullptr, split ? 2 : 0);
     if (!fork_substep) {
       d_sw_thermo(c, da);
       if (tfused) thermo_swap();
@@ -781,7 +811,7 @@ void Dycore::step() {
         // ds_courant, and the vorticity march waits for those and the vorticity
         HIP_CHECK(hipStreamWaitEvent(st_b, ev_ut, 0));
         const hipEvent_t before_march[2] = {ev_fork, ev_v};
-        d_sw_winds(cb, da, true, before_march, early_winds == 1 ? 2 : 1);
+        d_sw_winds(cb, da, true, before_march, 2);
       } else {
         HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
         d_sw_winds(cb, da);
@@ -808,7 +838,14 @@ void Dycore::step() {
     if (fork_substep) HIP_CHECK(hipStreamWaitEvent(st, ev_b, 0));
     if (d_sw_post_needed(da)) d_sw_post(c, da);  // the new delp and u, v: after both d_sw stages
     nh_p_grad(c, pa);
-    if (!last) halo_update({{"u", 'd'}, {"v", 'd'}});
+    if (!last) {
+      if (split) {
+        halo_begin({{"u", 'd'}, {"v", 'd'}});
+        uv_open = true;
+      } else {
+        halo_update({{"u", 'd'}, {"v", 'd'}});
+      }
+    }
   }
   };
   // The n_split acoustic sub-steps (~40 launches each, on three streams, with their halo
@@ -828,7 +865,7 @@ void Dycore::step() {
                                (double)nl.hord_tm, (double)nl.hord_dp, (double)early_winds,
                                // launch-shape switches read at every launch (tests flip them in-process)
                                (double)kloop_levels(),
-                               (double)riem_variant(), (double)remap_variant()};
+                               (double)riem_variant(), (double)remap_variant(), (double)halo_split_mode()};
     for (const Field* f : {&u, &v, &w, &delz, &pt, &delp, &phis})
       key.push_back((double)reinterpret_cast<uintptr_t>(f->p));
     for (const double* p : {vert, dp_ref}) key.push_back((double)reinterpret_cast<uintptr_t>(p));

@@ -49,8 +49,9 @@ class Dycore {
   hipStream_t st_b = nullptr, st_c = nullptr;
   hipEvent_t ev_fork = nullptr, ev_b = nullptr, ev_c = nullptr;
   // early d_sw winds (GTFV3_EARLY_WINDS: 0 off, 1 (default) the cell vorticity on stream c
-  // from the sub-step's start, 2 on stream b ahead of c_sw's wind stage): the sub-step's start
-  // (u, v final), the vorticity formed on stream c, ut / vt written
+  // from the sub-step's start; the form on stream b ahead of c_sw's wind stage measured slower
+  // and was removed in round 6): the sub-step's start (u, v final), the vorticity formed on
+  // stream c, ut / vt written
   hipEvent_t ev_s = nullptr, ev_v = nullptr, ev_ut = nullptr;
   int early_winds = 1;
   bool fork_substep = true;  // GTFV3_STREAMS=0: one stream
@@ -132,6 +133,10 @@ class Dycore {
   // halo update of named fields; kinds: 'c' cell, 'b' corner, 'd' D-grid pair, 'C' C-grid pair, 'a' A-grid pair,
   // 'S' C-grid pair tile-edge synchronisation (east / north edge values from the neighbour)
   void halo_update(const std::vector<std::pair<std::string, char>>& items);
+  // the two halves of an exchange (HaloExchanger::exchange_begin / exchange_end), on st
+  void halo_begin(const std::vector<std::pair<std::string, char>>& items);
+  void halo_end();
+  std::vector<HaloField> halo_fields(const std::vector<std::pair<std::string, char>>& items);
   // max-reduce across ranks (in place, device, n doubles)
   void allreduce_max(double* dev, int n);
 

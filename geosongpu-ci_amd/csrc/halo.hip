@@ -407,108 +407,145 @@ void batched_copy(const CopyMsg* msgs, int nmsg, hipStream_t st) {
   }
 }
 
-void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream) {
-  const bool remote = remote_;
-  std::vector<size_t> foff(nf);
-  if (remote) {
-    size_t off = 0;
-    for (int f = 0; f < nf; ++f) {
-      foff[f] = off;
-      off += (size_t)std::max(n_send_[fields[f].kind], n_recv_[fields[f].kind]) * fields[f].nk;
-    }
-    if (off > buf_elems_) throw std::runtime_error("halo: exchange buffer too small");
-    if (!tr_) throw std::runtime_error("halo: multi-rank exchange without a transport");
+std::vector<size_t> HaloExchanger::buffer_offsets(const HaloField* fields, int nf) const {
+  std::vector<size_t> foff(nf, 0);
+  if (!remote_) return foff;
+  size_t off = 0;
+  for (int f = 0; f < nf; ++f) {
+    foff[f] = off;
+    off += (size_t)std::max(n_send_[fields[f].kind], n_recv_[fields[f].kind]) * fields[f].nk;
   }
-  // one launch per stage for (up to HB) fields; stage 0 local gather, 1 pack, 2 unpack,
-  // 3 pack + local gather together
-  auto batch = [&](int stage, int f0, HaloBatch& b, int& maxn, int& maxk) {
+  if (off > buf_elems_) throw std::runtime_error("halo: exchange buffer too small");
+  if (!tr_) throw std::runtime_error("halo: multi-rank exchange without a transport");
+  return foff;
+}
+
+// one launch per stage for (up to HB) fields; stage 0 local gather, 1 pack, 2 unpack,
+// 3 pack + local gather together
+void HaloExchanger::launch_stage(int stage, const HaloField* fields, int nf, const std::vector<size_t>& foff,
+                                 hipStream_t stream) {
+  auto batch = [&](int stg, int f0, HaloBatch& b, int& maxn, int& maxk) {
     b = HaloBatch{};
     int nb = 0;
     for (int f = f0; f < nf && f < f0 + HB; ++f) {
       const HaloField& F = fields[f];
-      const int n = stage == 0 ? n_local_[F.kind] : (stage == 1 ? n_send_[F.kind] : n_recv_[F.kind]);
+      const int n = stg == 0 ? n_local_[F.kind] : (stg == 1 ? n_send_[F.kind] : n_recv_[F.kind]);
       if (!n) continue;
-      b.tab[nb] = stage == 0 ? (const void*)d_local_[F.kind]
-                             : (stage == 1 ? (const void*)d_send_[F.kind] : (const void*)d_recv_[F.kind]);
+      b.tab[nb] = stg == 0 ? (const void*)d_local_[F.kind]
+                           : (stg == 1 ? (const void*)d_send_[F.kind] : (const void*)d_recv_[F.kind]);
       b.n[nb] = n;
       b.nk[nb] = F.nk;
       b.p0[nb] = F.p[0];
       b.p1[nb] = F.p[1] ? F.p[1] : F.p[0];
-      b.boff[nb] = stage ? (long)foff[f] : 0;
+      b.boff[nb] = stg ? (long)foff[f] : 0;
       maxn = std::max(maxn, n);
       maxk = std::max(maxk, F.nk);
       ++nb;
     }
     return nb;
   };
-  auto launch = [&](int stage) {
-    for (int f0 = 0; f0 < nf; f0 += HB) {
-      HaloBatch b{}, bl{};
-      int maxn = 0, maxk = 0;
-      const int nb = batch(stage == 3 ? 1 : stage, f0, b, maxn, maxk);
-      const int nl = stage == 3 ? batch(0, f0, bl, maxn, maxk) : 0;
-      if (!nb && !nl) continue;
-      if ((long)cdiv(maxn, 256) * cdiv(maxk, 8) * (nb + nl) >= 2048) {  // >= 8 workgroups per CU at HK = 8
-        const dim3 g(cdiv(maxn, 256), cdiv(maxk, 8), nb + nl);
-        if (stage == 0) GT_LAUNCH_N("halo_local_kernel", halo_local_kernel<8>, g, dim3(256), 0, stream, b, d_.plane);
-        else if (stage == 1) GT_LAUNCH_N("halo_pack_kernel", halo_pack_kernel<8>, g, dim3(256), 0, stream, b, d_.plane, sendbuf_);
-        else if (stage == 2) GT_LAUNCH_N("halo_unpack_kernel", halo_unpack_kernel<8>, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
-        else GT_LAUNCH_N("halo_pack_local_kernel", halo_pack_local_kernel<8>, g, dim3(256), 0, stream, b, nb, bl, d_.plane, sendbuf_);
-      } else {
-        const dim3 g(cdiv(maxn, 256), maxk, nb + nl);
-        if (stage == 0) GT_LAUNCH_N("halo_local_kernel", halo_local_kernel<1>, g, dim3(256), 0, stream, b, d_.plane);
-        else if (stage == 1) GT_LAUNCH_N("halo_pack_kernel", halo_pack_kernel<1>, g, dim3(256), 0, stream, b, d_.plane, sendbuf_);
-        else if (stage == 2) GT_LAUNCH_N("halo_unpack_kernel", halo_unpack_kernel<1>, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
-        else GT_LAUNCH_N("halo_pack_local_kernel", halo_pack_local_kernel<1>, g, dim3(256), 0, stream, b, nb, bl, d_.plane, sendbuf_);
-      }
-      HIP_LAUNCH_CHECK();
-      // every halo point of every level: one value read, one written
-      double pts = 0.0;
-      for (int q = 0; q < nb; ++q) pts += (double)b.n[q] * b.nk[q];
-      for (int q = 0; q < nl; ++q) pts += (double)bl.n[q] * bl.nk[q];
-      ktimer_bytes(16.0 * pts);
-    }
-  };
-  if (remote) {
-    // Default (GTFV3_HALO_FUSE=1): the pack and the same-rank gather in one launch, the
-    // messages and the unpack after it, all on the exchange's own stream -- with nothing left
-    // to overlap the messages with, a separate communication stream only added two cross-queue
-    // hand-offs per exchange (pack -> messages -> unpack: ~13 us each in an 8-rank trace, 0.5 ms
-    // per step).  GTFV3_HALO_FUSE=0: the round-4 form -- the pack, then the messages on the
-    // communication stream while the gather runs on the compute stream, then the unpack.
-    // Either way the next exchange's pack follows this unpack in stream order, so the pack
-    // buffers are never rewritten while a send may still read them.
-    static const bool fuse = [] {
-      const char* e = std::getenv("GTFV3_HALO_FUSE");
-      return !(e && e[0] == '0');
-    }();
-    hipStream_t mst = fuse ? stream : comm_st_;
-    if (fuse) {
-      launch(3);
+  for (int f0 = 0; f0 < nf; f0 += HB) {
+    HaloBatch b{}, bl{};
+    int maxn = 0, maxk = 0;
+    const int nb = batch(stage == 3 ? 1 : stage, f0, b, maxn, maxk);
+    const int nl = stage == 3 ? batch(0, f0, bl, maxn, maxk) : 0;
+    if (!nb && !nl) continue;
+    if ((long)cdiv(maxn, 256) * cdiv(maxk, 8) * (nb + nl) >= 2048) {  // >= 8 workgroups per CU at HK = 8
+      const dim3 g(cdiv(maxn, 256), cdiv(maxk, 8), nb + nl);
+      if (stage == 0) GT_LAUNCH_N("halo_local_kernel", halo_local_kernel<8>, g, dim3(256), 0, stream, b, d_.plane);
+      else if (stage == 1) GT_LAUNCH_N("halo_pack_kernel", halo_pack_kernel<8>, g, dim3(256), 0, stream, b, d_.plane, sendbuf_);
+      else if (stage == 2) GT_LAUNCH_N("halo_unpack_kernel", halo_unpack_kernel<8>, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
+      else GT_LAUNCH_N("halo_pack_local_kernel", halo_pack_local_kernel<8>, g, dim3(256), 0, stream, b, nb, bl, d_.plane, sendbuf_);
     } else {
-      launch(1);
-      HIP_CHECK(hipEventRecord(ev_packed_, stream));
-      launch(0);
-      HIP_CHECK(hipStreamWaitEvent(comm_st_, ev_packed_, 0));
+      const dim3 g(cdiv(maxn, 256), maxk, nb + nl);
+      if (stage == 0) GT_LAUNCH_N("halo_local_kernel", halo_local_kernel<1>, g, dim3(256), 0, stream, b, d_.plane);
+      else if (stage == 1) GT_LAUNCH_N("halo_pack_kernel", halo_pack_kernel<1>, g, dim3(256), 0, stream, b, d_.plane, sendbuf_);
+      else if (stage == 2) GT_LAUNCH_N("halo_unpack_kernel", halo_unpack_kernel<1>, g, dim3(256), 0, stream, b, d_.plane, recvbuf_);
+      else GT_LAUNCH_N("halo_pack_local_kernel", halo_pack_local_kernel<1>, g, dim3(256), 0, stream, b, nb, bl, d_.plane, sendbuf_);
     }
-    tr_->group_start();
-    for (int f = 0; f < nf; ++f) {
-      const HaloField& F = fields[f];
-      for (int p = 0; p < nranks_; ++p) {
-        int ns = send_peer_count_[F.kind][p], nr = recv_peer_count_[F.kind][p];
-        if (ns) tr_->send(sendbuf_ + foff[f] + (size_t)send_peer_start_[F.kind][p] * F.nk, (size_t)ns * F.nk, p, mst);
-        if (nr) tr_->recv(recvbuf_ + foff[f] + (size_t)recv_peer_start_[F.kind][p] * F.nk, (size_t)nr * F.nk, p, mst);
-      }
+    HIP_LAUNCH_CHECK();
+    // every halo point of every level: one value read, one written
+    double pts = 0.0;
+    for (int q = 0; q < nb; ++q) pts += (double)b.n[q] * b.nk[q];
+    for (int q = 0; q < nl; ++q) pts += (double)bl.n[q] * bl.nk[q];
+    ktimer_bytes(16.0 * pts);
+  }
+}
+
+// the messages of an exchange, one NCCL group, on stream mst
+void HaloExchanger::post_messages(const HaloField* fields, int nf, const std::vector<size_t>& foff, hipStream_t mst) {
+  tr_->group_start();
+  for (int f = 0; f < nf; ++f) {
+    const HaloField& F = fields[f];
+    for (int p = 0; p < nranks_; ++p) {
+      int ns = send_peer_count_[F.kind][p], nr = recv_peer_count_[F.kind][p];
+      if (ns) tr_->send(sendbuf_ + foff[f] + (size_t)send_peer_start_[F.kind][p] * F.nk, (size_t)ns * F.nk, p, mst);
+      if (nr) tr_->recv(recvbuf_ + foff[f] + (size_t)recv_peer_start_[F.kind][p] * F.nk, (size_t)nr * F.nk, p, mst);
     }
-    tr_->group_end(mst);
-    if (!fuse) {
-      HIP_CHECK(hipEventRecord(ev_recvd_, comm_st_));
-      HIP_CHECK(hipStreamWaitEvent(stream, ev_recvd_, 0));
-    }
-    launch(2);
+  }
+  tr_->group_end(mst);
+}
+
+void HaloExchanger::exchange(const HaloField* fields, int nf, hipStream_t stream) {
+  if (pending_open_) throw std::runtime_error("halo: an exchange is still open (exchange_end missing)");
+  if (!remote_) {
+    launch_stage(0, fields, nf, {}, stream);
     return;
   }
-  launch(0);
+  const std::vector<size_t> foff = buffer_offsets(fields, nf);
+  // Default (GTFV3_HALO_FUSE=1): the pack and the same-rank gather in one launch, the
+  // messages and the unpack after it, all on the exchange's own stream -- with nothing left
+  // to overlap the messages with, a separate communication stream only added two cross-queue
+  // hand-offs per exchange (pack -> messages -> unpack: ~13 us each in an 8-rank trace, 0.5 ms
+  // per step).  GTFV3_HALO_FUSE=0: the round-4 form -- the pack, then the messages on the
+  // communication stream while the gather runs on the compute stream, then the unpack.
+  // Either way the next exchange's pack follows this unpack in stream order, so the pack
+  // buffers are never rewritten while a send may still read them.
+  static const bool fuse = [] {
+    const char* e = std::getenv("GTFV3_HALO_FUSE");
+    return !(e && e[0] == '0');
+  }();
+  hipStream_t mst = fuse ? stream : comm_st_;
+  if (fuse) {
+    launch_stage(3, fields, nf, foff, stream);
+  } else {
+    launch_stage(1, fields, nf, foff, stream);
+    HIP_CHECK(hipEventRecord(ev_packed_, stream));
+    launch_stage(0, fields, nf, foff, stream);
+    HIP_CHECK(hipStreamWaitEvent(comm_st_, ev_packed_, 0));
+  }
+  post_messages(fields, nf, foff, mst);
+  if (!fuse) {
+    HIP_CHECK(hipEventRecord(ev_recvd_, comm_st_));
+    HIP_CHECK(hipStreamWaitEvent(stream, ev_recvd_, 0));
+  }
+  launch_stage(2, fields, nf, foff, stream);
+}
+
+void HaloExchanger::exchange_begin(const HaloField* fields, int nf, hipStream_t stream) {
+  if (pending_open_) throw std::runtime_error("halo: an exchange is still open (exchange_end missing)");
+  if (!remote_) {
+    launch_stage(0, fields, nf, {}, stream);
+    return;
+  }
+  pending_.assign(fields, fields + nf);
+  pending_off_ = buffer_offsets(fields, nf);
+  pending_open_ = true;
+  // the pack and the same-rank gather on the caller's stream, the messages on the
+  // communication stream once the pack is done; the unpack waits for them in exchange_end
+  launch_stage(3, fields, nf, pending_off_, stream);
+  HIP_CHECK(hipEventRecord(ev_packed_, stream));
+  HIP_CHECK(hipStreamWaitEvent(comm_st_, ev_packed_, 0));
+  post_messages(fields, nf, pending_off_, comm_st_);
+  HIP_CHECK(hipEventRecord(ev_recvd_, comm_st_));
+}
+
+void HaloExchanger::exchange_end(hipStream_t stream) {
+  if (!pending_open_) return;
+  HIP_CHECK(hipStreamWaitEvent(stream, ev_recvd_, 0));
+  launch_stage(2, pending_.data(), (int)pending_.size(), pending_off_, stream);
+  pending_open_ = false;
+  pending_.clear();
 }
 
 }  // namespace gtfv3

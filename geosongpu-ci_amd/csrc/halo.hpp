@@ -47,6 +47,15 @@ class HaloExchanger {
   void set_self_messages(bool on) { self_msgs_ = on; }
   // fill halos of all listed fields (enqueued on `stream`)
   void exchange(const HaloField* fields, int nf, hipStream_t stream);
+  // the same exchange in two halves, for the interior / boundary split: begin enqueues the
+  // pack and same-rank gather on `stream` and the messages on the exchange's communication
+  // stream; whatever the caller enqueues on `stream` before end() runs beside the messages (it
+  // must read no halo point and write no point the pack reads); end() makes `stream` wait for
+  // the messages and unpacks.  One exchange at a time.  Without messages (one rank, no self
+  // messages) begin is the whole exchange and end does nothing.
+  void exchange_begin(const HaloField* fields, int nf, hipStream_t stream);
+  void exchange_end(hipStream_t stream);
+  bool remote() const { return remote_; }
   // host copies of tables for tests
   const std::vector<HaloEntry>& local_table(int kind) const { return h_local_[kind]; }
   // remote tables (dir 0: send/pack, 1: recv/unpack) as (sub, off, comp, sign, pos_in_peer_segment, peer)
@@ -78,6 +87,14 @@ class HaloExchanger {
   // gather (and whatever precedes the unpack) overlaps them
   hipStream_t comm_st_ = nullptr;
   hipEvent_t ev_packed_ = nullptr, ev_recvd_ = nullptr;
+  // one stage of an exchange (0 same-rank gather, 1 pack, 2 unpack, 3 pack + gather) for the
+  // fields and their pack-buffer offsets
+  void launch_stage(int stage, const HaloField* fields, int nf, const std::vector<size_t>& foff, hipStream_t stream);
+  std::vector<size_t> buffer_offsets(const HaloField* fields, int nf) const;
+  void post_messages(const HaloField* fields, int nf, const std::vector<size_t>& foff, hipStream_t mst);
+  std::vector<HaloField> pending_;  // an exchange begun and not yet ended
+  std::vector<size_t> pending_off_;
+  bool pending_open_ = false;
 };
 
 }  // namespace gtfv3

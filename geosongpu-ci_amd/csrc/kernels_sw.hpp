@@ -15,7 +15,12 @@ struct CswArgs {
   double *utmp, *vtmp, *ke, *vort;  // scratch
 };
 void c_sw(const Ctx& c, const CswArgs& a);            // the two stages in order
-void c_sw_transport(const Ctx& c, const CswArgs& a);  // d2a2c_vect, delpc / ptc / wc, ke
+// d2a2c_vect, delpc / ptc / wc, ke.  part (the interior / boundary split of the u, v exchange,
+// Dycore::step): 0 everything; 1 cs_tmp on the points that read no halo value only (while the
+// exchange's messages fly); 2 the rest -- cs_tmp's boundary frame and the stages after it
+void c_sw_transport(const Ctx& c, const CswArgs& a, int part = 0);
+// the split needs sub-domains of at least 6 x 6 cells
+bool split_fits(const Dims& d);
 void c_sw_winds(const Ctx& c, const CswArgs& a);      // vorticity, uc / vc update
 int kloop_levels();                                          // GTFV3_KLOOP (stencil_common.hpp)
 
@@ -51,7 +56,9 @@ struct DswArgs {
 void d_sw(const Ctx& c, const DswArgs& a);  // the three stages in order
 // ut, vt, Courant numbers and area fluxes; utvt_done (optional) is recorded once ut / vt are
 // written (d_sw's kinetic energy needs those, not the Courant numbers)
-void d_sw_courant(const Ctx& c, const DswArgs& a, hipEvent_t utvt_done = nullptr);
+// part as c_sw_transport's, for the uc, vc exchange: 1 ds_utvt1 on the points that read no
+// halo value, 2 its boundary frame and the stages after it
+void d_sw_courant(const Ctx& c, const DswArgs& a, hipEvent_t utvt_done = nullptr, int part = 0);
 void d_sw_thermo(const Ctx& c, const DswArgs& a);   // delp / w / pt transport, flux accumulation
 // kinetic energy, vorticity transport, u, v.  vort_done: the cell vorticity was formed already
 // (d_sw_vort, from the same u, v); the stream waits for the nwait events of march_wait before

@@ -555,6 +555,86 @@ __global__ void __launch_bounds__(256) a2b_edge_k(Dims d, const SubInfo* __restr
   if (set) AT(qout, 0, 0) = val;
 }
 
+// The same values as a2b_edge_k, one workgroup per 256 points of one tile-edge line of one
+// plane: the line's x- (or y-) interpolants at its points and two beyond either end are formed
+// once into LDS (each an edge-form PPM value: four q loads, two dxa loads, one division) and
+// every point's colv / rowv reads its four from there -- a2b_edge_k formed all four per point
+// (78 us per launch of nh_p_grad's four fields at C180, a quarter of a2b_march_k's time).
+// blockIdx.y: 0 the west line I = 0, 1 east I = N, 2 south J = 0, 3 north J = N (lines the
+// sub-domain does not have, and the y-line points an x line holds, write nothing).
+constexpr int AE_T = 256;
+__global__ void __launch_bounds__(AE_T) a2b_edge2_k(Dims d, const SubInfo* __restrict__ subs,
+                                                    const double* __restrict__ M, A2bF F, const double* __restrict__ cw) {
+  // the field of this plane by a uniform compare chain (a2b_edge_k's: a reference to the
+  // kernel argument, as a2b_select takes it, put the table in scratch memory here)
+  const int zg = blockIdx.z;
+  const int f = (zg >= F.zb[1]) + (zg >= F.zb[2]) + (zg >= F.zb[3]);
+  A2bSel fs;
+  fs.nk = f == 0 ? F.nk[0] : (f == 1 ? F.nk[1] : (f == 2 ? F.nk[2] : F.nk[3]));
+  fs.z = zg - (f == 0 ? F.zb[0] : (f == 1 ? F.zb[1] : (f == 2 ? F.zb[2] : F.zb[3])));
+  fs.q = f == 0 ? F.q[0] : (f == 1 ? F.q[1] : (f == 2 ? F.q[2] : F.q[3]));
+  fs.qo = f == 0 ? F.qo[0] : (f == 1 ? F.qo[1] : (f == 2 ? F.qo[2] : F.qo[3]));
+  fs.sc = f == 0 ? F.sc[0] : (f == 1 ? F.sc[1] : (f == 2 ? F.sc[2] : F.sc[3]));
+  const int s = fs.z / fs.nk;
+  const SubInfo sub = subs[s];
+  const int N = sub.N, io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+  const int line = blockIdx.y;
+  const bool xl = line < 2;
+  if (line == 0 && io != 0) return;
+  if (line == 1 && io + nx != N) return;
+  if (line == 2 && jo != 0) return;
+  if (line == 3 && jo + ny != N) return;
+  const int len = xl ? ny + 1 : nx + 1;
+  const int p0 = blockIdx.x * AE_T;
+  if (p0 >= len) return;
+  const long zo = (long)fs.z * d.plane;
+  const A2bEdge E{A2bPoint{d, sub, fs.q + zo, met(M, d, M_DXA, s), met(M, d, M_DYA, s), fs.sc}, fs.q + zo,
+                  cw + (long)s * 12, N, io, jo};
+  // this line's fixed local index; the interpolant along it (j on an x line, i on a y line)
+  // at positions p0 - 2 .. p0 + AE_T + 1 into LDS
+  const int fix = line == 0 ? 0 : (line == 1 ? nx : (line == 2 ? 0 : ny));
+  __shared__ double sq[AE_T + 4];
+  const int t = threadIdx.x;
+  {
+    const int pa = p0 - 2 + t, pb = p0 - 2 + AE_T + (t & 3);
+    sq[t] = xl ? E.P.qx(fix, pa) : E.P.qy(pa, fix);
+    const double vb = xl ? E.P.qx(fix, pb) : E.P.qy(pb, fix);
+    if (t < 4) sq[AE_T + t] = vb;
+  }
+  __syncthreads();
+  const int p = p0 + t;
+  if (p >= len) return;
+  // S(pp) = sq[pp - p0 + 2]; colv / rowv at position pp from LDS (pp - 2 .. pp + 1 lie in this
+  // block's range for every pp a point of the block reads: its own, or 2 / N-2 for the
+  // positions next to the ends)
+  const int b = 2 - p0;
+  const int i = xl ? fix : p, j = xl ? p : fix;
+  const int I = i + io, J = j + jo;
+  double val;
+  bool set = true;
+  if ((I == 0 || I == N) && (J == 0 || J == N)) {
+    if (!xl && ((I == 0 && io == 0) || (I == N && io + nx == N))) return;  // the x line's point
+    val = E.edge_or_corner(I, J);
+  } else {
+    if (!xl && ((I == 0 && io == 0) || (I == N && io + nx == N))) return;  // the x line's point
+    // the position along the line and its offset in the tile (J on an x line, I on a y line)
+    const int P_ = xl ? J : I, off = xl ? jo : io, lim = xl ? ny : nx;
+    const int q2 = 2 - off + b, qn = N - 2 - off + b, qp = p + b;
+    if (P_ == 1 && off == 0) {
+      const double lv = AA2 * (sq[q2 - 2] + sq[q2 + 1]) + AA1 * (sq[q2 - 1] + sq[q2]);
+      val = AC1 * (sq[b] + sq[1 + b]) + AC2 * ((xl ? E.edge_or_corner(I, 0) : E.edge_or_corner(0, J)) + lv);
+    } else if (P_ == N - 1 && off + lim == N) {
+      const double lv = AA2 * (sq[qn - 2] + sq[qn + 1]) + AA1 * (sq[qn - 1] + sq[qn]);
+      val = AC1 * (sq[qn] + sq[qn + 1]) + AC2 * (lv + (xl ? E.edge_or_corner(I, N) : E.edge_or_corner(N, J)));
+    } else if (P_ >= max(2, off) && P_ <= min(N - 2, off + lim)) {
+      val = AA2 * (sq[qp - 2] + sq[qp + 1]) + AA1 * (sq[qp - 1] + sq[qp]);
+    } else {
+      set = false;
+    }
+  }
+  if (set) fs.qo[zo + pidx(d, i, j)] = val;
+}
+
 // ---- a2b_ord4 interior, column-marching form (default) ----
 // One wavefront owns 64 columns c = a-2 .. a+61 of one (sub-domain, level) and marches up
 // a segment of corner rows; corners a .. a+60 are its outputs.  Per cell row r it loads
@@ -1111,8 +1191,17 @@ void a2b_ord4_multi(const Ctx& c, int nf, const int* nk, const double* const* q,
   F.zb[A2B_MAXF] = INT_MAX;
   if (nz >= 65536) throw std::runtime_error("a2b_ord4: too many planes for one launch");
   // corner / tile-edge values first: the interior points next to the tile edges use them
-  GT_LAUNCH(a2b_edge_k, dim3(cdiv(edge_line_count(0, d.nx, 0, d.ny), 256), 1, (unsigned)nz), dim3(256), 0, c.st, d,
-            c.subs, c.met, F, c.cornerw);
+  // (GTFV3_A2B_EDGE=0: the one-point-per-lane form, read per call)
+  const char* ee = std::getenv("GTFV3_A2B_EDGE");
+  // (the position next to a line's far end reads two positions back: not across a block start)
+  auto end_ok = [](int len) { return len - 2 < AE_T || (len - 2) % AE_T >= 2; };
+  if ((ee && ee[0] == '0') || !end_ok(d.nx + 1) || !end_ok(d.ny + 1)) {
+    GT_LAUNCH(a2b_edge_k, dim3(cdiv(edge_line_count(0, d.nx, 0, d.ny), 256), 1, (unsigned)nz), dim3(256), 0, c.st,
+              d, c.subs, c.met, F, c.cornerw);
+  } else {
+    GT_LAUNCH_N("a2b_edge_k", a2b_edge2_k, dim3(cdiv(std::max(d.nx, d.ny) + 1, AE_T), 4, (unsigned)nz), dim3(AE_T), 0,
+                c.st, d, c.subs, c.met, F, c.cornerw);
+  }
   HIP_LAUNCH_CHECK();
   // interior corners: column-marching kernel (balanced segments of at most 46 corner
   // rows: C180 has 181 corner rows -> 4 x 46, not 4 x 45 + 1)

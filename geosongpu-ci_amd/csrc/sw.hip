@@ -225,12 +225,15 @@ __global__ void __launch_bounds__(256) cs_transport_ke_ld(
 // ua, va.  The four u rows and four v columns of the 4th-order forms (the outer two at offset
 // 0 where the point takes no 4th-order value) and the two metric terms in one group; the
 // 4th-order / tile-edge / BIG choice made afterwards
-__global__ void __launch_bounds__(256) cs_tmp_ld(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
-                                                 int npz, const double* __restrict__ u, const double* __restrict__ v,
+// (L: the whole plane or its interior, H: a hole of L left to another launch -- the interior /
+// boundary split of the u, v exchange, Dycore::step)
+__global__ void __launch_bounds__(256) cs_tmp_ld(Dims d, Launch2D L, Launch2D H, const SubInfo* __restrict__ subs,
+                                                 const double* __restrict__ M, int npz,
+                                                 const double* __restrict__ u, const double* __restrict__ v,
                                                  double* __restrict__ utmp, double* __restrict__ vtmp,
                                                  double* __restrict__ ua, double* __restrict__ va) {
-  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   KSETUP(npz)
+  if (i >= H.i0 && i < H.i0 + H.ni && j >= H.j0 && j < H.j0 + H.nj) return;
   const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
   const long p = d.pitch;
   const bool inr = i <= nx + NG - 1 && j <= ny + NG - 1;
@@ -477,13 +480,15 @@ __global__ void __launch_bounds__(256) ds_courant(Dims d, const SubInfo* __restr
 // the point are loaded once for its block of levels (which of them a point needs is fixed by
 // its position), then the same expressions per level as above.  (The same form of
 // ds_courant and ds_ke measured slower: 1.56 -> 1.68 and 2.65 -> 3.37 ms per step)
-__global__ void __launch_bounds__(256) ds_utvt1_kl(Dims d, const SubInfo* __restrict__ subs,
+// (L: the whole plane or its interior, H: a hole of L left to another launch -- the interior /
+// boundary split of the uc, vc exchange)
+__global__ void __launch_bounds__(256) ds_utvt1_kl(Dims d, Launch2D L, Launch2D H, const SubInfo* __restrict__ subs,
                                                    const double* __restrict__ M, int npz, int nkb, int klb,
                                                    double dt, const double* __restrict__ uc,
                                                    const double* __restrict__ vc, double* __restrict__ ut,
                                                    double* __restrict__ vt) {
-  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   KLSETUP(npz)
+  if (i >= H.i0 && i < H.i0 + H.ni && j >= H.j0 && j < H.j0 + H.nj) return;
   const SubInfo sub = subs[s];
   const int N = sub.N, I = i + sub.ioff, J = j + sub.joff, nx = d.nx, ny = d.ny;
   const long pt = d.pitch;
@@ -722,22 +727,39 @@ inline dim3 g2(const Dims& d, const Launch2D& L, int nz) {
 }  // namespace
 
 void c_sw(const Ctx& c, const CswArgs& a) {
-  c_sw_transport(c, a);
+  c_sw_transport(c, a, 0);
   c_sw_winds(c, a);
 }
 
 // c_sw first stage: d2a2c_vect (uc, vc, ua, va, ut, vt), the half-step transport (delpc,
 // ptc, wc) and the kinetic energy
-void c_sw_transport(const Ctx& c, const CswArgs& a) {
+// the boundary frame runs as one whole-plane launch with the interior as its hole (four
+// rectangle launches cost more in launch latency at the small per-rank shares)
+static const Launch2D kNoHole{0, 0, 0, 0};
+
+bool split_fits(const Dims& d) { return d.nx >= 6 && d.ny >= 6; }
+
+void c_sw_transport(const Ctx& c, const CswArgs& a, int part) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
-  GT_LAUNCH_N("cs_tmp", cs_tmp_ld, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.u, a.v,
-              a.utmp, a.vtmp, a.ua, a.va);
-  HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   const double L = a.npz;
-  gt_bytes(L * (e.Y + e.X + 4 * e.C) + 2 * e.C);
+  // cs_tmp reads u on rows j-1 .. j+2 and v on columns i-1 .. i+2 of the point: on
+  // [1, nx-2] x [1, ny-2] only owned values, none an exchange writes
+  const Launch2D inner{1, 1, d.nx - 2, d.ny - 2};
+  auto tmp = [&](const Launch2D& r, const Launch2D& h) {
+    GT_LAUNCH_N("cs_tmp", cs_tmp_ld, g2(d, r, nz), dim3(BX, BY), 0, c.st, d, r, h, c.subs, c.met, a.npz, a.u, a.v,
+                a.utmp, a.vtmp, a.ua, a.va);
+    HIP_LAUNCH_CHECK();
+  };
+  if (part == 1) {
+    tmp(inner, kNoHole);
+    gt_bytes(L * (e.Y + e.X + 4 * e.C) + 2 * e.C);
+    return;
+  }
+  tmp(full, part == 2 ? inner : kNoHole);
+  if (part == 0) gt_bytes(L * (e.Y + e.X + 4 * e.C) + 2 * e.C);
   GT_LAUNCH(cs_corner_fix, dim3(nz), dim3(64), 0, c.st, d, c.subs, a.npz, a.utmp, a.vtmp, a.ua, a.va);
   HIP_LAUNCH_CHECK();
   GT_LAUNCH(cs_cgrid, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
@@ -785,21 +807,36 @@ bool d_sw_thermo_fused(const DswArgs& a) {
   return on && !deln && a.delp_o && a.w_o && a.pt_o && a.hord_dp == a.hord_vt && a.hord_vt == a.hord_tm;
 }
 
-void d_sw_courant(const Ctx& c, const DswArgs& a, hipEvent_t utvt_done) {
+void d_sw_courant(const Ctx& c, const DswArgs& a, hipEvent_t utvt_done, int part) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   Launch2D full{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
   const int klb = kloop_levels(), nkb = klb ? (a.npz + klb - 1) / klb : 0;
-  if (klb) {
-    GT_LAUNCH_N("ds_utvt1_kl", ds_utvt1_kl, kloop_grid(full, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs,
-                c.met, a.npz, nkb, klb, a.dt, a.uc, a.vc, a.ut, a.vt);
-  } else
-    GT_LAUNCH(ds_utvt1, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.uc, a.vc,
-                       a.ut, a.vt);
-  HIP_LAUNCH_CHECK();
   const Ext e = ext(d);
   const double L = a.npz;
-  gt_bytes(L * (2 * e.X + 2 * e.Y) + 8 * e.C);
+  // ds_utvt1 reads uc at (i, j), (i+1, j-1), (i+1, j) and vc at (i, j), (i-1, j), (i-1, j+1),
+  // (i, j+1): on [1, nx-1] x [1, ny-1] only owned values, none an exchange writes (the split
+  // form needs the level-loop kernel, which takes its region)
+  const Launch2D inner{1, 1, d.nx - 1, d.ny - 1};
+  auto utvt1 = [&](const Launch2D& r, const Launch2D& h) {
+    GT_LAUNCH_N("ds_utvt1_kl", ds_utvt1_kl, kloop_grid(r, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, r, h, c.subs,
+                c.met, a.npz, nkb, klb, a.dt, a.uc, a.vc, a.ut, a.vt);
+    HIP_LAUNCH_CHECK();
+  };
+  if (part == 1) {
+    if (!klb) throw std::runtime_error("d_sw_courant: the split form needs GTFV3_KLOOP > 0");
+    utvt1(inner, kNoHole);
+    gt_bytes(L * (2 * e.X + 2 * e.Y) + 8 * e.C);
+    return;
+  }
+  if (klb) {
+    utvt1(full, part == 2 ? inner : kNoHole);
+  } else {
+    GT_LAUNCH(ds_utvt1, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.uc, a.vc,
+                       a.ut, a.vt);
+    HIP_LAUNCH_CHECK();
+  }
+  if (part == 0) gt_bytes(L * (2 * e.X + 2 * e.Y) + 8 * e.C);
   GT_LAUNCH(ds_utvt2, dim3(cdiv(edge_line_count(-NG, d.nx + NG, -NG, d.ny + NG), 256), 1, nz), dim3(256), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.ut,
                      a.vt);
   HIP_LAUNCH_CHECK();

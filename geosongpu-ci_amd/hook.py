@@ -15,6 +15,17 @@ on one GPU, one process) every array carries a trailing tile axis of length 6.
 
 The keyword `is` of the reference argument list is spelled `is_` here (Python
 keyword); `is` is also accepted through **kwargs.
+
+The CI's two environment switches (ci/pipeline/gtfv3_config.py:11,19-21) are honoured:
+  * PACE_FLOAT_PRECISION (32 | 64, unset: either): the precision of the state arrays the hook
+    takes -- 32 routes float32 arrays through geos_gtfv3_run_c (the CI's benchmark mode,
+    gtfv3_config.py:27), 64 float64 arrays through geos_gtfv3_run_f64_c; arrays of the other
+    precision raise TypeError.  The stencils compute in fp64 either way: the
+    arithmetic is never below the precision the switch names.
+  * GTFV3_BACKEND: this build has one backend, the HIP kernels for gfx950.  Unset, "hip" or
+    "hip:gfx950" select it; the reference's GPU backends ("dace:gpu", "gt:gpu", "cuda") are
+    mapped to it; a CPU backend ("numpy", "gt:cpu_ifirst", "dace:cpu", ...) or "fortran" (the
+    Fortran dycore: the hook is not called at all) raise ValueError.
 """
 import ctypes
 import os
@@ -54,6 +65,21 @@ def expected_sizes(kw):
     return {k: v * (tiles if k not in ("ak", "bk") else 1) for k, v in n.items()}
 
 
+GPU_BACKENDS = ("hip", "hip:gfx950", "dace:gpu", "gt:gpu", "cuda", "gpu")
+
+
+def check_environment():
+    """(precision in bits or None, backend name) from PACE_FLOAT_PRECISION / GTFV3_BACKEND"""
+    prec = os.environ.get("PACE_FLOAT_PRECISION", "").strip()
+    if prec not in ("", "32", "64"):
+        raise ValueError(f"PACE_FLOAT_PRECISION must be 32 or 64, not {prec!r}")
+    backend = os.environ.get("GTFV3_BACKEND", "hip").strip() or "hip"
+    if backend not in GPU_BACKENDS:
+        raise ValueError(f"GTFV3_BACKEND={backend!r}: this build runs the HIP (gfx950) backend only; "
+                         f"accepted: {', '.join(GPU_BACKENDS)}")
+    return (int(prec) if prec else None), backend
+
+
 def _norm(kwargs):
     if "is_" in kwargs:
         kwargs = dict(kwargs)
@@ -78,6 +104,7 @@ class GEOS_GTFV3:
     """init / run / finalize with the reference hook's argument names and order."""
 
     def init(self, **kwargs):
+        check_environment()
         kw = _norm(kwargs)
         lib().geos_gtfv3_init_c(*_scalar_args(kw, INIT_ARGS))
 
@@ -87,6 +114,9 @@ class GEOS_GTFV3:
         dtype = np.asarray(kw["u"]).dtype
         if dtype not in (np.float32, np.float64):
             raise TypeError("geos_gtfv3.run: state arrays must be float32 or float64")
+        prec, _ = check_environment()
+        if prec is not None and dtype != (np.float32 if prec == 32 else np.float64):
+            raise TypeError(f"geos_gtfv3.run: PACE_FLOAT_PRECISION={prec} but the state arrays are {dtype}")
         ct = ctypes.c_double if dtype == np.float64 else ctypes.c_float
         need = expected_sizes(kw)
         for n in RUN_ARRAYS:

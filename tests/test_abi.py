@@ -114,3 +114,31 @@ def test_config_separators_and_malformed_values(pkg):
         h = lib.gtfv3_create(bad, 0, 1, None)
         assert not h, bad
         assert lib.geos_gtfv3_last_error(buf, 256) > 0 and what in buf.value, buf.value
+
+
+def test_hook_environment_switches(pkg, monkeypatch):
+    """The CI's PACE_FLOAT_PRECISION / GTFV3_BACKEND (ci/pipeline/gtfv3_config.py:11,19-21)
+    are read by the hook: the precision names the state arrays' dtype (32: the fp32 entry
+    point, the CI's benchmark mode), the backend must be a GPU one (this build: HIP gfx950)"""
+    import importlib
+
+    import numpy as np
+    hook = importlib.import_module(pkg.__name__ + ".hook")
+    monkeypatch.delenv("PACE_FLOAT_PRECISION", raising=False)
+    monkeypatch.delenv("GTFV3_BACKEND", raising=False)
+    assert hook.check_environment() == (None, "hip")
+    monkeypatch.setenv("PACE_FLOAT_PRECISION", "32")
+    monkeypatch.setenv("GTFV3_BACKEND", "dace:gpu")
+    assert hook.check_environment() == (32, "dace:gpu")
+    for bad in ("numpy", "gt:cpu_ifirst", "fortran"):
+        monkeypatch.setenv("GTFV3_BACKEND", bad)
+        with pytest.raises(ValueError):
+            hook.check_environment()
+    monkeypatch.setenv("GTFV3_BACKEND", "hip")
+    monkeypatch.setenv("PACE_FLOAT_PRECISION", "16")
+    with pytest.raises(ValueError):
+        hook.check_environment()
+    # a float64 state under PACE_FLOAT_PRECISION=32 is refused before any library call
+    monkeypatch.setenv("PACE_FLOAT_PRECISION", "32")
+    with pytest.raises(TypeError):
+        hook.geos_gtfv3.run(u=np.zeros(4))

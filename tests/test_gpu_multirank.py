@@ -55,6 +55,19 @@ def _run_ranks(pkg, nranks, layout, npx=13, npz=10, nq=2):
 def test_multirank_step_matches_single_rank(pkg, require_gpu, nranks, layout, npx, npz):
     """(6, 1x1, C180 L72): BASELINE.json config 3's layout (one tile per rank, held_suarez.py:149-151)
     at its own size"""
+    _check_multirank(pkg, nranks, layout, npx, npz)
+
+
+@pytest.mark.parametrize("nranks,layout,npx,npz", [(8, (1, 4), 25, 10), (6, (1, 1), 49, 10), (2, (1, 1), 13, 10)])
+def test_multirank_split_exchange_matches_single_rank(pkg, require_gpu, monkeypatch, nranks, layout, npx, npz):
+    """The interior / boundary split of the uc / vc and u / v exchanges forced on
+    (GTFV3_HALO_SPLIT=1; by default it runs only where the messages cross GPUs): every rank's
+    state after a step through the loopback transport equals the single-rank step bit for bit"""
+    monkeypatch.setenv("GTFV3_HALO_SPLIT", "1")
+    _check_multirank(pkg, nranks, layout, npx, npz)
+
+
+def _check_multirank(pkg, nranks, layout, npx, npz):
     state = importlib.import_module(pkg.__name__ + ".state")
     ak, bk, ks = state.hybrid_levels(npz)
     ref = pkg.Domain(npx=npx, npz=npz, nq=2, layout_x=layout[0], layout_y=layout[1])
@@ -136,3 +149,29 @@ def test_multirank_aquaplanet_step_matches_single_rank(pkg, require_gpu):
     finally:
         for d in doms:
             d.close()
+
+
+@pytest.mark.parametrize("proxy,npx,layout", [(8, 181, (1, 4)), (2, 49, (1, 1))])
+def test_halo_split_bitwise_on_rank_proxy(pkg, require_gpu, monkeypatch, proxy, npx, layout):
+    """The interior / boundary split of the uc / vc and u / v exchanges (messages on the
+    exchange's communication stream beside ds_utvt1's / cs_tmp's interior; GTFV3_HALO_SPLIT)
+    against the whole exchanges, on rank 0 of the 8-rank bands (bench.py --rank-proxy 8) and of
+    two ranks, null transport: two steps bit for bit (NaN equal to NaN: the proxy's reflected
+    halos)"""
+    state = importlib.import_module(pkg.__name__ + ".state")
+    npz = 20
+    ak, bk, ks = state.hybrid_levels(npz)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GTFV3_HALO_SPLIT", mode)
+        d = pkg.Domain(0, proxy, None, npx=npx, npz=npz, nq=2, layout_x=layout[0], layout_y=layout[1], loopback=-1,
+                       dt=450.0 * 180.0 / (npx - 1))
+        st = state.jablonowski_williamson(d, ak, bk)
+        d.set_vertical(ak, bk, ks)
+        for k, v in st.items():
+            d.upload(k, v)
+        d.step(2)
+        out[mode] = {k: d.download(k) for k in FIELDS}
+        d.close()
+    for k in FIELDS:
+        assert np.array_equal(out["0"][k], out["1"][k], equal_nan=True), f"{k}: the split exchange differs"

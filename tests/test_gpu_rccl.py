@@ -31,8 +31,13 @@ def _domain(pkg, npx, npz, nq, **kw):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("npx,npz,steps", [(49, 72, 2), (181, 72, 1)])
-def test_rccl_self_step_matches_gather(pkg, require_gpu, npx, npz, steps):
+@pytest.mark.parametrize("npx,npz,steps,split", [(49, 72, 2, "1"), (181, 72, 1, "1"), (49, 72, 2, "0")])
+def test_rccl_self_step_matches_gather(pkg, require_gpu, monkeypatch, npx, npz, steps, split):
+    """split "1" (the default with messages): the uc / vc and u / v exchanges begin, ds_utvt1's
+    and cs_tmp's interiors run beside the RCCL messages on the exchange's communication stream,
+    the exchanges end and the boundary frames follow (Dycore::step); "0": the whole exchange,
+    then the stencil"""
+    monkeypatch.setenv("GTFV3_HALO_SPLIT", split)
     nq = 4
     ref = _domain(pkg, npx, npz, nq)
     t0 = time.perf_counter()

@@ -236,13 +236,12 @@ def test_acoustic_graph_bitwise(pkg, require_gpu, monkeypatch, proxy):
         assert np.array_equal(out["0"][k], out["1"][k], equal_nan=bool(proxy)), f"{k}: graph replay differs"
 
 
-@pytest.mark.parametrize("mode", ["streams1", "late_winds", "vort_on_b"])
+@pytest.mark.parametrize("mode", ["streams1", "late_winds"])
 def test_stream_forms_bitwise(pkg, require_gpu, monkeypatch, mode):
     """The default three-stream step (d_sw's cell vorticity on stream c from the sub-step's
     start, its kinetic energy on stream b from ut / vt on, the vorticity march after the
     Courant numbers: GTFV3_EARLY_WINDS=1) against every kernel on one stream
-    (GTFV3_STREAMS=0), the wind stage forked after the Courant numbers (GTFV3_EARLY_WINDS=0)
-    and the vorticity on stream b ahead of c_sw's wind stage (GTFV3_EARLY_WINDS=2): three C48
+    (GTFV3_STREAMS=0) and the wind stage forked after the Courant numbers (GTFV3_EARLY_WINDS=0): three C48
     L20 steps with the HIP graph off and on, bit for bit on every state field -- a missing
     cross-stream dependency shows up here as a race."""
     state = importlib.import_module(pkg.__name__ + ".state")
@@ -253,7 +252,7 @@ def test_stream_forms_bitwise(pkg, require_gpu, monkeypatch, mode):
         for graph in ("0", "1"):
             monkeypatch.setenv("GTFV3_GRAPH", graph)
             monkeypatch.setenv("GTFV3_STREAMS", "0" if form == "streams1" else "1")
-            monkeypatch.setenv("GTFV3_EARLY_WINDS", {"late_winds": "0", "vort_on_b": "2"}.get(form, "1"))
+            monkeypatch.setenv("GTFV3_EARLY_WINDS", "0" if form == "late_winds" else "1")
             d = pkg.Domain(npx=49, npz=npz, nq=2)
             st = state.jablonowski_williamson(d, ak, bk)
             d.set_vertical(ak, bk, ks)
@@ -309,3 +308,27 @@ def test_hip_step_dry_mass_with_corner_anomaly(pkg, require_gpu):
     print(f"corner anomaly: HIP mass change {(m1 - m0) / m0:.2e}, oracle {(mr - m0) / m0:.2e} per step")
     assert abs(m1 - m0) / m0 < 3e-11, (m1 - m0) / m0
     assert abs(m1 - mr) / m0 < 1e-12, (m1 - mr) / m0
+
+
+@pytest.mark.parametrize("npx,layout,npz", [(13, (1, 1), 10), (25, (2, 2), 10), (181, (1, 4), 10), (361, (1, 1), 6)])
+def test_a2b_edge_forms_bitwise(pkg, require_gpu, monkeypatch, npx, layout, npz):
+    """a2b_ord4's tile-edge lines with the line's interpolants shared through LDS (a2b_edge2_k)
+    against one point per lane (a2b_edge_k, GTFV3_A2B_EDGE=0): two steps bit for bit -- west /
+    east / south / north lines, the cube corners and the J = 1, N-1 forms, sub-domains with
+    and without tile edges (2x2, 1x4 bands), a line longer than one block (C360)"""
+    state = importlib.import_module(pkg.__name__ + ".state")
+    ak, bk, ks = state.hybrid_levels(npz)
+    out = {}
+    for mode in ("0", "1"):
+        monkeypatch.setenv("GTFV3_A2B_EDGE", mode)
+        d = pkg.Domain(npx=npx, npz=npz, nq=2, layout_x=layout[0], layout_y=layout[1], dt=450.0 * 180.0 / (npx - 1))
+        st = state.jablonowski_williamson(d, ak, bk)
+        d.set_vertical(ak, bk, ks)
+        for k, v in st.items():
+            d.upload(k, v)
+        del st
+        d.step(2)
+        out[mode] = {k: d.download(k) for k in ("u", "v", "w", "pt", "delp", "delz", "q", "ps", "pe", "ua", "va")}
+        d.close()
+    for k in out["0"]:
+        assert np.array_equal(out["0"][k], out["1"][k]), f"{k}: the LDS tile-edge lines differ"

@@ -23,7 +23,7 @@ def main():
     npx = int(sys.argv[1]) if len(sys.argv) > 1 else 181
     pkg = gtfv3_pkg.load()
     dt = 450.0 * 180.0 / (npx - 1)
-    r = bench.cpu_baseline(pkg, npx, 72, 4, dt)
+    r = bench.cpu_baseline(pkg, npx, 72, 4, dt, procs=1)  # one replica: one host core
     r["host"] = platform.processor() or platform.machine()
     r["threads_env"] = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "OPENBLAS_NUM_THREADS")}
     print(json.dumps(r))
