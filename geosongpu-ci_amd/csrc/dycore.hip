@@ -674,7 +674,9 @@ void Dycore::step() {
 
   // fused d_sw thermo march: delp / w / pt are updated into a second set of planes, which
   // then become the fields (pointer swap; n_split even ends on the original planes).  The
-  // second set starts as a copy so the halo points no exchange fills match the first.
+  // second set takes the first's halo ring, so the halo points no exchange fills (the
+  // cube-corner regions) match whichever set is current; the march writes every compute
+  // point (a whole-plane copy, 0.15 ms per C180 step, was not needed).
   DswArgs probe{};
   probe.hord_vt = nl.hord_vt; probe.hord_tm = nl.hord_tm; probe.hord_dp = nl.hord_dp;
   probe.delp_o = probe.w_o = probe.pt_o = delp.p;  // (only their presence is tested)
@@ -688,7 +690,7 @@ void Dycore::step() {
     const char* an[3] = {"_delp_alt", "_w_alt", "_pt_alt"};
     for (int f = 0; f < 3; ++f) {
       alt[f] = &field(an[f], npz);
-      copy_levels(c, field_elems(npz), cur3[f]->p, alt[f]->p);
+      copy_halo_ring(c, d.nsub * npz, cur3[f]->p, alt[f]->p);
     }
   }
   auto zh_swap = [&]() {
