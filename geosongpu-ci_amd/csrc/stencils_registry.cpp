@@ -325,6 +325,40 @@ std::map<std::string, Fn>& reg() {
          copy_halo_ring(dy.ctx(), dy.d.nsub * k1, zh.p, zo.p);
          copy_levels(dy.ctx(), dy.field_elems(k1), zo.p, zh.p);
        }},
+      // p_grad_c(delpc, pkc, gz | uc, vc): the C-grid pressure gradient of dyn_core (pkc, gz:
+      // npz+1 interface levels with their first halo ring; uc, vc updated in place).  params: dt2
+      {"p_grad_c",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 5, "p_grad_c");
+         Field& dp = F(dy, f[0]);
+         const int npz = dp.nk;
+         if (F(dy, f[1]).nk != npz + 1 || F(dy, f[2]).nk != npz + 1 || F(dy, f[3]).nk != npz ||
+             F(dy, f[4]).nk != npz)
+           throw std::runtime_error("p_grad_c: field shapes");
+         p_grad_c(dy.ctx(), npz, p.at(0), dp.p, F(dy, f[1]).p, F(dy, f[2]).p, F(dy, f[3]).p, F(dy, f[4]).p);
+       }},
+      // nh_p_grad(pp, pk3, gz, delp | u, v): the D-grid pressure gradient (a2b_ord4 of pp, pk3, gz
+      // and delp to the corners, then u, v += the gradient terms, times rdx / rdy: the winds leave
+      // d_sw as u dx, v dy).  pp, pk3, gz: npz+1 levels with halos; the top interface's pp and
+      // pk3 are the model-top constants 0 and ptop**kappa.  params: dt, ptop
+      {"nh_p_grad",
+       [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>& p) {
+         need(f, 6, "nh_p_grad");
+         Field& dp = F(dy, f[3]);
+         const int npz = dp.nk, k1 = npz + 1;
+         for (int n = 0; n < 3; ++n)
+           if (F(dy, f[n]).nk != k1) throw std::runtime_error("nh_p_grad: pp, pk3, gz need npz+1 levels");
+         if (F(dy, f[4]).nk != npz || F(dy, f[5]).nk != npz) throw std::runtime_error("nh_p_grad: u, v levels");
+         NhPgArgs a{};
+         a.npz = npz;
+         a.dt = p.at(0);
+         a.ptop = p.at(1);
+         a.pp = F(dy, f[0]).p; a.pk3 = F(dy, f[1]).p; a.gz = F(dy, f[2]).p; a.delp = dp.p;
+         a.ppb = dy.field("_pg_pp", k1).p; a.pkb = dy.field("_pg_pk", k1).p; a.gzb = dy.field("_pg_gz", k1).p;
+         a.wk1 = dy.field("_pg_wk", npz).p; a.qx = dy.field("_pg_qx", k1).p; a.qy = dy.field("_pg_qy", k1).p;
+         a.u = F(dy, f[4]).p; a.v = F(dy, f[5]).p;
+         nh_p_grad(dy.ctx(), a);
+       }},
       // a2b_ord4(q | qout): cell means -> cell corners (4th order, cubed-sphere edge forms)
       {"a2b_ord4",
        [](Dycore& dy, const std::vector<std::string>& f, const std::vector<double>&) {

@@ -62,6 +62,8 @@ riem_solver3 = StencilDef("riem_solver3", 12, (2, 4) + tuple(range(5, 12)), ("dt
 edge_profile = StencilDef("edge_profile", 8, (4, 5, 6, 7), ("variant",))
 update_dz_d = StencilDef("update_dz_d", 5, (0,), ("hord",))
 a2b_ord4 = StencilDef("a2b_ord4", 2, (1,))
+p_grad_c = StencilDef("p_grad_c", 5, (3, 4), ("dt2",))
+nh_p_grad = StencilDef("nh_p_grad", 6, (4, 5), ("dt", "ptop"))
 held_suarez = StencilDef("held_suarez", 4, (1, 2, 3), ("dt",))
 moist_qsat = StencilDef("moist_qsat", 5, (2, 3, 4))
 fillq2zero = StencilDef("fillq2zero", 3, (0, 2))
