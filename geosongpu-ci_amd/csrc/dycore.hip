@@ -56,7 +56,8 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
   HIP_CHECK(hipStreamCreateWithFlags(&st, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&st_b, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&st_c, hipStreamNonBlocking));
-  for (hipEvent_t* e : {&ev_fork, &ev_b, &ev_c, &ev_s, &ev_v, &ev_ut})
+  HIP_CHECK(hipStreamCreateWithFlags(&st_d, hipStreamNonBlocking));
+  for (hipEvent_t* e : {&ev_fork, &ev_b, &ev_c, &ev_s, &ev_v, &ev_ut, &ev_df, &ev_dj})
     HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   {
     const char* e = std::getenv("GTFV3_STREAMS");
@@ -126,13 +127,14 @@ Dycore::~Dycore() {
   if (dmet) (void)hipFree(dmet);
   if (dcornerw) (void)hipFree(dcornerw);
   if (darea4) (void)hipFree(darea4);
-  for (hipEvent_t e : {ev_fork, ev_b, ev_c, ev_s, ev_v, ev_ut})
+  for (hipEvent_t e : {ev_fork, ev_b, ev_c, ev_s, ev_v, ev_ut, ev_df, ev_dj})
     if (e) (void)hipEventDestroy(e);
   for (auto& set : ev_ph)
     for (hipEvent_t e : set)
       if (e) (void)hipEventDestroy(e);
   if (st_b) (void)hipStreamDestroy(st_b);
   if (st_c) (void)hipStreamDestroy(st_c);
+  if (st_d) (void)hipStreamDestroy(st_d);
   if (st) (void)hipStreamDestroy(st);
 }
 
@@ -518,6 +520,13 @@ static bool graph_enabled() {
   return e && e[0] == '1';
 }
 
+// GTFV3_EDGE_SIDE (default 1): the thermo march's tile-edge kernel on its own stream beside the
+// interior kernel; 0: in series
+static bool edge_side() {
+  const char* e = std::getenv("GTFV3_EDGE_SIDE");
+  return !(e && e[0] == '0');
+}
+
 void Dycore::step() {
   if (nl.host_only) throw std::runtime_error("host-only dycore cannot step");
   if (nl.k_split != 1) throw std::runtime_error("step: only k_split = 1 is supported");
@@ -729,6 +738,13 @@ void Dycore::step() {
   // runs on the points that read no halo value -- ds_utvt1 after uc / vc, cs_tmp after u / v --
   // while the messages fly, then the exchange ends (unpack) and the boundary frame follows.
   const int split_mode = halo_split_mode();
+  // the thermo march's tile-edge kernel on stream d beside its interior kernel (tp.hip march2)
+  Ctx ct = c;
+  if (fork_substep && edge_side()) {
+    ct.side = st_d;
+    ct.side_fork = ev_df;
+    ct.side_join = ev_dj;
+  }
   const bool split = halo.remote() && split_fits(d) && kloop_levels() > 0 &&
                      (split_mode == 1 || (split_mode < 0 && dc.nranks > 1 && !nl.loopback));
   auto acoustic = [&]() {
@@ -796,7 +812,7 @@ void Dycore::step() {
     // the chip -- C180 on one GPU 43.8 -> 42.4 ms per step.
     d_sw_courant(c, da, early ? ev_ut : nullptr, split ? 2 : 0);
     if (!fork_substep) {
-      d_sw_thermo(c, da);
+      d_sw_thermo(ct, da);
       if (tfused) thermo_swap();
       d_sw_winds(c, da);
       update_dz_d(c, za);
@@ -821,7 +837,7 @@ void Dycore::step() {
       update_dz_d(cc, za);
       zh_swap();
     }
-    d_sw_thermo(c, da);
+    d_sw_thermo(ct, da);
     if (tfused) thermo_swap();
     HIP_CHECK(hipEventRecord(ev_b, st_b));
     HIP_CHECK(hipEventRecord(ev_c, st_c));
@@ -867,7 +883,8 @@ void Dycore::step() {
                                (double)nl.hord_tm, (double)nl.hord_dp, (double)early_winds,
                                // launch-shape switches read at every launch (tests flip them in-process)
                                (double)kloop_levels(),
-                               (double)riem_variant(), (double)remap_variant(), (double)halo_split_mode()};
+                               (double)riem_variant(), (double)remap_variant(), (double)halo_split_mode(),
+                               (double)edge_side()};
     for (const Field* f : {&u, &v, &w, &delz, &pt, &delp, &phis})
       key.push_back((double)reinterpret_cast<uintptr_t>(f->p));
     for (const double* p : {vert, dp_ref}) key.push_back((double)reinterpret_cast<uintptr_t>(p));

@@ -48,6 +48,10 @@ class Dycore {
   // its thermodynamic transport (fork after the Courant numbers, join before riem_solver3)
   hipStream_t st_b = nullptr, st_c = nullptr;
   hipEvent_t ev_fork = nullptr, ev_b = nullptr, ev_c = nullptr;
+  // the thermo march's tile-edge kernel beside its interior kernel (Ctx::side; GTFV3_EDGE_SIDE=0:
+  // in series on the main stream)
+  hipStream_t st_d = nullptr;
+  hipEvent_t ev_df = nullptr, ev_dj = nullptr;
   // early d_sw winds (GTFV3_EARLY_WINDS: 0 off, 1 (default) the cell vorticity on stream c
   // from the sub-step's start; the form on stream b ahead of c_sw's wind stage measured slower
   // and was removed in round 6): the sub-step's start (u, v final), the vorticity formed on

@@ -32,6 +32,10 @@ struct Ctx {
   const double* area4;     // device [nsub][4][plane]: the cell area four times (tp_march lane groups)
   double da_min, da_min_c;
   hipStream_t st;
+  // optional side stream of a stage whose launches split into independent parts (the thermo
+  // march's tile-edge kernel beside its interior one): fork / join events; null: one stream
+  hipStream_t side = nullptr;
+  hipEvent_t side_fork = nullptr, side_join = nullptr;
 };
 
 // fv_tp_2d: nt fields q[s][t][k] advected with fluxes [s][k]; fx/fy [s][t][k]

@@ -907,21 +907,33 @@ void march2(const Ctx& c, const TpM& m0, double bytes, const char* name_ex, cons
   const double fex = plan_spans(c, pex, pin);
   // (shorter segments for the tile-edge launch, 15 or 23 rows against the interior's 45,
   // measured 32.12 / 32.02 against 32.00 ms per step: not kept)
-  auto go = [&](const std::vector<int>& pr, bool ex) {
+  auto go = [&](const std::vector<int>& pr, bool ex, hipStream_t st) {
     TpM m = m0;
     const long waves = set_spans(m, pr);
     const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
-    if (ex) GT_LAUNCH_N(name_ex, (tp_march<ORD, A2_EX, MF, NF, TM, OCC_EX, 1>), g, b, 0, c.st, m);
-    else GT_LAUNCH_N(name_in, (tp_march<ORD, A2_IN, MF, NF, TM, OCC_IN, 2>), g, b, 0, c.st, m);
+    if (ex) GT_LAUNCH_N(name_ex, (tp_march<ORD, A2_EX, MF, NF, TM, OCC_EX, 1>), g, b, 0, st, m);
+    else GT_LAUNCH_N(name_in, (tp_march<ORD, A2_IN, MF, NF, TM, OCC_IN, 2>), g, b, 0, st, m);
     HIP_LAUNCH_CHECK();
   };
+  // The tile-edge kernel's few waves (one per SIMD at most, ~1000 at C180) each march a whole
+  // segment: alone, the chip idles behind them for its length.  With a side stream (Ctx::side)
+  // it runs there, beside the interior kernel (disjoint outputs and accumulator points).
+  const bool side = c.side && !pex.empty() && !pin.empty();
+  if (side) {
+    HIP_CHECK(hipEventRecord(c.side_fork, c.st));
+    HIP_CHECK(hipStreamWaitEvent(c.side, c.side_fork, 0));
+  }
   if (!pex.empty()) {
-    go(pex, true);
+    go(pex, true, side ? c.side : c.st);
     ktimer_bytes(bytes * fex);
   }
   if (!pin.empty()) {
-    go(pin, false);
+    go(pin, false, c.st);
     ktimer_bytes(bytes * (1.0 - fex));
+  }
+  if (side) {
+    HIP_CHECK(hipEventRecord(c.side_join, c.side));
+    HIP_CHECK(hipStreamWaitEvent(c.st, c.side_join, 0));
   }
 }
 

@@ -134,7 +134,9 @@ def test_williamson1_cosine_bell(pkg, require_gpu, alpha):
     # test_williamson1_corner_mass_matches_oracle)
     mass_bar = 1e-9 if alpha == 0.0 else 1e-3
     assert r48["finite"] and r48["mass"] <= mass_bar, r48
-    assert r24["finite"], r24
+    # C24 (3.75 deg): measured l2 0.12 at both angles -- the resolution Putman & Lin (2007) show
+    # the bell still clipped and spread at (l2 of order 1e-1)
+    assert r24["finite"] and r24["l2"] <= 0.2, r24
     assert r48["l2"] <= 0.05 and r48["linf"] <= 0.05, r48
     assert r24["l2"] / r48["l2"] >= 2.5, (r24["l2"], r48["l2"])
 
