@@ -1338,13 +1338,13 @@ void lagrangian_to_eulerian(const Ctx& c, int npz, int nq, double ptop, bool fil
       } else {
         // tracers per wave: the pressure part is formed once per wave and shared, so more
         // tracers per wave cost less per tracer -- C360 L137 x 54: 76.1 / 69.8 / 66.8 / 65.6 ms
-        // per step for 4 / 8 / 16 / 32 (`profiles/r05n_*`).  Default 16 above 8 tracers, 8
-        // above 4; GTFV3_REMAP_NT (4, 8, 16, 32) overrides
+        // per step for 4 / 8 / 16 / 32 (`profiles/r05n_*`).  Default 32 above 16 tracers, 16
+        // above 8, 8 above 4; GTFV3_REMAP_NT (4, 8, 16, 32) overrides
         static const int nt_env = [] {
           const char* e = std::getenv("GTFV3_REMAP_NT");
           return e ? std::atoi(e) : 0;
         }();
-        const int nt = nt_env > 0 ? nt_env : (nq > 8 ? 16 : (nq > 4 ? 8 : RB_NT));
+        const int nt = nt_env > 0 ? nt_env : (nq > 16 ? 32 : (nq > 8 ? 16 : (nq > 4 ? 8 : RB_NT)));
         if (nt >= 32 && nq > 16)
           GT_LAUNCH((remap_blkq_k<M, NB, PART, 32>), dim3(gx, cdiv(nq, 32), d.nsub), tb, 0, c.st, a);
         else if (nt >= 16 && nq > 8)
