@@ -476,6 +476,13 @@ void bridge_init(void* comm, int npx, int npy, int npz, int ntiles, int is, int 
   const char* const px[] = {"GTFV3_BRIDGE_PROXY", nullptr};
   const bool proxy = nranks > 1 && env_int(px, 0) == 1;
   if (proxy) nl.loopback = -1;
+  // GTFV3_TRANSPORT=ipc: several ranks per GPU (the reference's PER_DEVICE_PROCESS, 12 GEOS
+  // ranks on each GPU): the same-node IPC transport (ipc.cpp) instead of RCCL, which takes one
+  // rank per device; the ncclUniqueId bytes shared below are then the job's key
+  if (const char* tr = std::getenv("GTFV3_TRANSPORT")) {
+    if (std::strcmp(tr, "ipc") == 0) nl.ipc = true;
+    else if (std::strcmp(tr, "rccl") != 0) throw std::runtime_error("GTFV3_TRANSPORT must be rccl or ipc");
+  }
   std::vector<unsigned char> id(128, 0);
   if (nranks > 1 && !proxy) {
     if (rank == 0) {

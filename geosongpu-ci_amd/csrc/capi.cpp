@@ -104,6 +104,7 @@ Namelist parse_config(const char* cfg, const Namelist& base) {
     else if (k == "host_only") nl.host_only = ix != 0;
     else if (k == "loopback") nl.loopback = ix;
     else if (k == "rccl_self") nl.rccl_self = ix != 0;
+    else if (k == "ipc") nl.ipc = ix != 0;
     else if (k == "do_vort_damp") nl.do_vort_damp = ix != 0;
     else if (k == "n_sponge") nl.n_sponge = ix;
     else if (k == "d2_bg_k1") nl.d2_bg_k1 = x;

@@ -36,6 +36,9 @@ struct CopyMsg {
 void batched_copy(const CopyMsg* msgs, int nmsg, hipStream_t st);
 
 std::unique_ptr<Transport> make_nccl_transport(int nranks, int rank, const void* nccl_id);
+// several ranks (processes) on one node's GPUs (ipc.cpp): HIP IPC handles of the send buffers
+// and a shared-memory control block named by the 128-byte key every rank was given
+std::unique_ptr<Transport> make_ipc_transport(int nranks, int rank, const void* key);
 // group < 0: the null transport (one rank alone, each receive answered by its own send to
 // that peer: measurement only)
 std::unique_ptr<Transport> make_loopback_transport(int group, int nranks, int rank);

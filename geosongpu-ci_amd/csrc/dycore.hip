@@ -93,7 +93,9 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
     halo.set_transport(comm.get());
     halo.set_self_messages(true);
   } else if (nranks > 1) {
-    comm = nl.loopback ? make_loopback_transport(nl.loopback, nranks, rank) : make_nccl_transport(nranks, rank, nccl_id);
+    comm = nl.loopback ? make_loopback_transport(nl.loopback, nranks, rank)
+           : nl.ipc    ? make_ipc_transport(nranks, rank, nccl_id)
+                       : make_nccl_transport(nranks, rank, nccl_id);
     halo.set_transport(comm.get());
   }
   halo.build(*cs, dc, d, max_nk, 8);

@@ -71,6 +71,9 @@ struct Namelist {
   // ncclSend / ncclRecv to itself on a size-1 communicator, unpack -- and the tracer Courant
   // maximum through ncclAllReduce, so the NcclTransport runs on a one-GPU box
   bool rccl_self = false;
+  // several ranks per GPU (the reference's PER_DEVICE_PROCESS): the same-node IPC transport
+  // (ipc.cpp) instead of RCCL, which takes one rank per device
+  bool ipc = false;
 };
 
 // One sub-domain (tile piece) owned by this rank.
