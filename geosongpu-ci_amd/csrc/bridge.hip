@@ -480,7 +480,12 @@ void bridge_init(void* comm, int npx, int npy, int npz, int ntiles, int is, int 
   // ranks on each GPU): the same-node IPC transport (ipc.cpp) instead of RCCL, which takes one
   // rank per device; the ncclUniqueId bytes shared below are then the job's key
   if (const char* tr = std::getenv("GTFV3_TRANSPORT")) {
-    if (std::strcmp(tr, "ipc") == 0) nl.ipc = true;
+    if (std::strcmp(tr, "ipc") == 0) {
+      nl.ipc = true;
+      // one hardware queue per rank process unless the job says otherwise (read by the HIP
+      // runtime at its first call: effective when nothing in the process has touched HIP yet)
+      setenv("GPU_MAX_HW_QUEUES", "1", 0);
+    }
     else if (std::strcmp(tr, "rccl") != 0) throw std::runtime_error("GTFV3_TRANSPORT must be rccl or ipc");
   }
   std::vector<unsigned char> id(128, 0);

@@ -61,7 +61,9 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
     HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   {
     const char* e = std::getenv("GTFV3_STREAMS");
-    fork_substep = e ? e[0] == '1' : true;
+    // several rank processes sharing a GPU (the IPC transport): one stream each by default --
+    // every process's queues compete for the GPU's hardware queues
+    fork_substep = e ? e[0] == '1' : !nl.ipc;
     const char* w = std::getenv("GTFV3_EARLY_WINDS");  // 0: the wind stage after the Courant numbers
     early_winds = w && *w && w[0] == '0' ? 0 : 1;
   }

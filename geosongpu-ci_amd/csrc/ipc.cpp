@@ -17,6 +17,7 @@
 #include <atomic>
 #include <chrono>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <stdexcept>
@@ -117,6 +118,9 @@ class IpcTransport : public Transport {
   }
 
   ~IpcTransport() override {
+    if (std::getenv("GTFV3_IPC_TRACE"))
+      std::fprintf(stderr, "ipc rank %d: %ld exchanges; host ms: pack wait %.1f, posted barrier %.1f, copies %.1f, "
+                   "copy wait %.1f, done barrier %.1f\n", me_, nex_, t_[0], t_[1], t_[2], t_[3], t_[4]);
     for (auto& kv : opened_) (void)hipIpcCloseMemHandle(kv.second);
     if (sh_) munmap(sh_, sizeof(IpcShared));
   }
@@ -129,7 +133,16 @@ class IpcTransport : public Transport {
   void recv(double* buf, size_t n, int peer, hipStream_t) override { recvs_.push_back(make(peer, buf, n)); }
 
   void group_end(hipStream_t st) override {
+    using clk = std::chrono::steady_clock;
+    auto lap = [&](int i, clk::time_point& t) {
+      const clk::time_point n = clk::now();
+      t_[i] += std::chrono::duration<double, std::milli>(n - t).count();
+      t = n;
+    };
+    clk::time_point t = clk::now();
+    ++nex_;
     HIP_CHECK(hipStreamSynchronize(st));  // this rank's packed messages are in its send buffer
+    lap(0, t);
     IpcRank& mine = sh_->rank[me_];
     for (int p = 0; p < n_; ++p) mine.npost[p] = 0;
     for (const Pending& s : sends_) {
@@ -141,6 +154,7 @@ class IpcTransport : public Transport {
       mine.post[s.peer][np++] = IpcPost{b, 0, off, (uint64_t)s.n};
     }
     barrier();  // every rank's posts (and exported handles) are visible
+    lap(1, t);
     std::vector<int> taken(n_, 0);
     for (const Pending& r : recvs_) {
       const IpcRank& src = sh_->rank[r.peer];
@@ -153,8 +167,11 @@ class IpcTransport : public Transport {
       const char* base = (const char*)peer_base(r.peer, m.base);
       if (r.n) HIP_CHECK(hipMemcpyAsync(r.p, base + m.off, 8 * r.n, hipMemcpyDeviceToDevice, st));
     }
+    lap(2, t);
     HIP_CHECK(hipStreamSynchronize(st));
+    lap(3, t);
     barrier();  // every receiver has copied: the senders may pack again
+    lap(4, t);
   }
 
   void allreduce_max(double* dev, int n, hipStream_t st) override {
@@ -232,6 +249,8 @@ class IpcTransport : public Transport {
   }
 
   int n_, me_;
+  long nex_ = 0;
+  double t_[5] = {0, 0, 0, 0, 0};
   std::string name_;
   IpcShared* sh_ = nullptr;
   std::vector<const char*> bases_;
