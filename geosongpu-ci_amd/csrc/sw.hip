@@ -164,7 +164,7 @@ __global__ void __launch_bounds__(256) cs_transport_ke_ld(
     const double* __restrict__ u, const double* __restrict__ v, const double* __restrict__ uc,
     const double* __restrict__ vc, const double* __restrict__ ua, const double* __restrict__ va,
     const double* __restrict__ ut, const double* __restrict__ vt, double* __restrict__ delpc,
-    double* __restrict__ ptc, double* __restrict__ wc, double* __restrict__ ke) {
+    double* __restrict__ ptc, double* __restrict__ wc, double* __restrict__ ke, double* __restrict__ vort) {
   Launch2D L{-1, -1, d.nx + 2, d.ny + 2};
   KSETUP(npz)
   const long p = d.pitch;
@@ -219,6 +219,20 @@ __global__ void __launch_bounds__(256) cs_transport_ke_ld(
   }
   const double dt4 = 0.5 * dt2;
   AT(ke, 0, 0) = dt4 * (uav * kk + vav * vv);
+  // c_sw's absolute vorticity at the cell corners [0, nx] x [0, ny] (cs_vort's expressions and
+  // order): uc, vc here are final, and the point's own uc0 / vc0 are already loaded
+  if (i >= 0 && j >= 0) {
+    const double* dxc = MT(M_DXC);
+    const double* dyc = MT(M_DYC);
+    const double fxs = AT(uc, 0, -1) * MA(dxc, 0, -1);
+    const double fx0 = uc0 * MA(dxc, 0, 0);
+    const double fyw = AT(vc, -1, 0) * MA(dyc, -1, 0);
+    const double fy0 = vc0 * MA(dyc, 0, 0);
+    double cv = fxs - fx0 - fyw + fy0;
+    if ((I == 0 && J == 0) || (I == 0 && J == N)) cv = cv + fyw;
+    if ((I == N && J == 0) || (I == N && J == N)) cv = cv - fy0;
+    AT(vort, 0, 0) = MA(MT(M_FC), 0, 0) + MA(MT(M_RAREA_C), 0, 0) * cv;
+  }
 }
 
 // d2a2c_vect part 1: utmp, vtmp (4th order interior / 2nd order near tile edges) and generic
@@ -271,24 +285,6 @@ __global__ void __launch_bounds__(256) cs_tmp_ld(Dims d, Launch2D L, Launch2D H,
   }
   AT(ua, 0, 0) = a;
   AT(va, 0, 0) = b;
-}
-
-// c_sw: absolute vorticity at cell corners from the C-grid circulation
-__global__ void __launch_bounds__(256) cs_vort(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
-                                               int npz, const double* __restrict__ uc, const double* __restrict__ vc,
-                                               double* __restrict__ vort) {
-  Launch2D L{0, 0, d.nx + 1, d.ny + 1};
-  KSETUP(npz)
-  const double* dxc = MT(M_DXC);
-  const double* dyc = MT(M_DYC);
-  double fxs = AT(uc, 0, -1) * MA(dxc, 0, -1);
-  double fx0 = AT(uc, 0, 0) * MA(dxc, 0, 0);
-  double fyw = AT(vc, -1, 0) * MA(dyc, -1, 0);
-  double fy0 = AT(vc, 0, 0) * MA(dyc, 0, 0);
-  double vt = fxs - fx0 - fyw + fy0;
-  if ((I == 0 && J == 0) || (I == 0 && J == N)) vt = vt + fyw;
-  if ((I == N && J == 0) || (I == N && J == N)) vt = vt - fy0;
-  AT(vort, 0, 0) = MA(MT(M_FC), 0, 0) + MA(MT(M_RAREA_C), 0, 0) * vt;
 }
 
 // c_sw: time-centred C-grid winds (vorticity flux + KE gradient).  Both upwind vorticity
@@ -732,7 +728,7 @@ void c_sw(const Ctx& c, const CswArgs& a) {
 }
 
 // c_sw first stage: d2a2c_vect (uc, vc, ua, va, ut, vt), the half-step transport (delpc,
-// ptc, wc) and the kinetic energy
+// ptc, wc), the kinetic energy and the corner vorticity
 // the boundary frame runs as one whole-plane launch with the interior as its hole (four
 // rectangle launches cost more in launch latency at the small per-rank shares)
 static const Launch2D kNoHole{0, 0, 0, 0};
@@ -767,23 +763,25 @@ void c_sw_transport(const Ctx& c, const CswArgs& a, int part) {
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (3 * e.X + 3 * e.Y + 4 * e.C) + 12 * e.C);
   Launch2D Lt{-1, -1, d.nx + 2, d.ny + 2};
+  // the corner vorticity of the wind stage formed here too (the separate cs_vort launch
+  // re-read uc, vc: 32.17-32.47 -> 31.98-32.23 ms per step)
+  double* vort = a.vort;
   GT_LAUNCH_N("cs_transport_ke", cs_transport_ke_ld, g2(d, Lt, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
-              a.npz, a.dt2, a.delp, a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke);
+              a.npz, a.dt2, a.delp, a.pt, a.w, a.u, a.v, a.uc, a.vc, a.ua, a.va, a.ut, a.vt, a.delpc, a.ptc, a.wc, a.ke,
+              vort);
   HIP_LAUNCH_CHECK();
-  gt_bytes(L * (9 * e.C + 3 * e.X + 3 * e.Y) + 9 * e.C);
+  gt_bytes(L * (9 * e.C + 3 * e.X + 3 * e.Y + e.K) + 13 * e.C);
 }
 
-// c_sw second stage: vorticity and the time-centred C-grid winds (touches uc, vc, vort and
-// reads ke: independent of update_dz_c / riem_solver_c, which may run beside it)
+// c_sw second stage: the time-centred C-grid winds from the corner vorticity and ke of the
+// first stage (touches uc, vc: independent of update_dz_c / riem_solver_c, which may run
+// beside it)
 void c_sw_winds(const Ctx& c, const CswArgs& a) {
   const Dims& d = c.d;
   const int nz = d.nsub * a.npz;
   const Ext e = ext(d);
   const double L = a.npz;
   Launch2D Lc{0, 0, d.nx + 1, d.ny + 1};
-  GT_LAUNCH(cs_vort, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.vort);
-  HIP_LAUNCH_CHECK();
-  gt_bytes(L * (e.X + e.Y + e.K) + 4 * e.C);
   GT_LAUNCH_N("cs_update", cs_update_ld, g2(d, Lc, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2,
               a.u, a.v, a.vort, a.ke, a.uc, a.vc);
   HIP_LAUNCH_CHECK();
