@@ -619,6 +619,11 @@ void Dycore::step() {
   da.ut = S("_ds_ut", npz); da.vt = S("_ds_vt", npz);
   da.fx = S("_ds_fx", npz); da.fy = S("_ds_fy", npz); da.gwx = S("_ds_gwx", npz); da.gwy = S("_ds_gwy", npz);
   da.gtx = S("_ds_gtx", npz); da.gty = S("_ds_gty", npz); da.ke = S("_ds_ke", npz); da.vort = S("_ds_vort", npz);
+  // d_sw's cell vorticity formed by c_sw's cs_tmp, which reads the same starting u, v (a
+  // ds_vort launch and its reads of u, v less per sub-step: 31.48-31.53 -> 31.33-31.43 ms in
+  // one box's A/B)
+  ca.dvort = da.vort;
+  const bool vort_early = true;
   // d_sw's damping (damp.hip): the column of per-level parameters of FV3 dyn_core (the sponge
   // layers' divergence and w damping at the top in the Held-Suarez namelist)
   const std::vector<LevelDamp> col = column_damping(nl, c.da_min, c.da_min_c);
@@ -762,7 +767,7 @@ void Dycore::step() {
       uv_open = false;
     }
     const int csw_part = split && it > 0 ? 2 : 0;
-    if (early) {
+    if (early && !vort_early) {
       // d_sw's cell vorticity needs only this sub-step's starting u, v (final here: the last
       // sub-step's exchange, or the step's first): formed on stream c beside c_sw, so the
       // wind stage after the fork is the kinetic energy and the vorticity march alone
@@ -818,7 +823,7 @@ void Dycore::step() {
     if (!fork_substep) {
       d_sw_thermo(ct, da);
       if (tfused) thermo_swap();
-      d_sw_winds(c, da);
+      d_sw_winds(c, da, vort_early);
       update_dz_d(c, za);
       zh_swap();
     } else {
@@ -833,10 +838,10 @@ void Dycore::step() {
         // ds_courant, and the vorticity march waits for those and the vorticity
         HIP_CHECK(hipStreamWaitEvent(st_b, ev_ut, 0));
         const hipEvent_t before_march[2] = {ev_fork, ev_v};
-        d_sw_winds(cb, da, true, before_march, 2);
+        d_sw_winds(cb, da, true, before_march, vort_early ? 1 : 2);
       } else {
         HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
-        d_sw_winds(cb, da);
+        d_sw_winds(cb, da, vort_early);
       }
       update_dz_d(cc, za);
       zh_swap();

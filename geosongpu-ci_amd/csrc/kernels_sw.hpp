@@ -13,6 +13,9 @@ struct CswArgs {
   double *uc, *vc, *ua, *va, *ut, *vt;  // outputs (ut, vt: dt2 * area fluxes)
   double *delpc, *ptc, *wc;
   double *utmp, *vtmp, *ke, *vort;  // scratch
+  // optional: d_sw's cell vorticity + Coriolis of this sub-step's starting u, v (ds_vort's
+  // expressions), formed by d2a2c's first kernel, which reads those u, v already
+  double* dvort = nullptr;
 };
 void c_sw(const Ctx& c, const CswArgs& a);            // the two stages in order
 // d2a2c_vect, delpc / ptc / wc, ke.  part (the interior / boundary split of the u, v exchange,

@@ -245,7 +245,8 @@ __global__ void __launch_bounds__(256) cs_tmp_ld(Dims d, Launch2D L, Launch2D H,
                                                  const double* __restrict__ M, int npz,
                                                  const double* __restrict__ u, const double* __restrict__ v,
                                                  double* __restrict__ utmp, double* __restrict__ vtmp,
-                                                 double* __restrict__ ua, double* __restrict__ va) {
+                                                 double* __restrict__ ua, double* __restrict__ va,
+                                                 double* __restrict__ dvort) {
   KSETUP(npz)
   if (i >= H.i0 && i < H.i0 + H.ni && j >= H.j0 && j < H.j0 + H.nj) return;
   const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
@@ -285,6 +286,16 @@ __global__ void __launch_bounds__(256) cs_tmp_ld(Dims d, Launch2D L, Launch2D H,
   }
   AT(ua, 0, 0) = a;
   AT(va, 0, 0) = b;
+  // d_sw's cell vorticity + Coriolis on [-NG, nx+NG-1] x [-NG, ny+NG-1] (ds_vort's expressions
+  // and order) from the u(j+1), v(i+1) loaded above
+  if (dvort && inr) {
+    const double* dx = MT(M_DX);
+    const double* dy = MT(M_DY);
+    const double udx0 = u0 * MA(dx, 0, 0), udx1 = u1 * MA(dx, 0, 1);
+    const double vdy0 = v0 * MA(dy, 0, 0), vdy1 = v1 * MA(dy, 1, 0);
+    const double wk = MA(MT(M_RAREA), 0, 0) * (udx0 - udx1 + vdy1 - vdy0);
+    AT(dvort, 0, 0) = wk + MA(MT(M_F0), 0, 0);
+  }
 }
 
 // c_sw: time-centred C-grid winds (vorticity flux + KE gradient).  Both upwind vorticity
@@ -746,16 +757,18 @@ void c_sw_transport(const Ctx& c, const CswArgs& a, int part) {
   const Launch2D inner{1, 1, d.nx - 2, d.ny - 2};
   auto tmp = [&](const Launch2D& r, const Launch2D& h) {
     GT_LAUNCH_N("cs_tmp", cs_tmp_ld, g2(d, r, nz), dim3(BX, BY), 0, c.st, d, r, h, c.subs, c.met, a.npz, a.u, a.v,
-                a.utmp, a.vtmp, a.ua, a.va);
+                a.utmp, a.vtmp, a.ua, a.va, a.dvort);
     HIP_LAUNCH_CHECK();
   };
+  // (d_sw's cell vorticity when asked: one more plane written, dx dy rarea f0 read)
+  const double tb = L * (e.Y + e.X + 4 * e.C) + 2 * e.C + (a.dvort ? L * e.C + 4 * e.C : 0.0);
   if (part == 1) {
     tmp(inner, kNoHole);
-    gt_bytes(L * (e.Y + e.X + 4 * e.C) + 2 * e.C);
+    gt_bytes(tb);
     return;
   }
   tmp(full, part == 2 ? inner : kNoHole);
-  if (part == 0) gt_bytes(L * (e.Y + e.X + 4 * e.C) + 2 * e.C);
+  if (part == 0) gt_bytes(tb);
   GT_LAUNCH(cs_corner_fix, dim3(nz), dim3(64), 0, c.st, d, c.subs, a.npz, a.utmp, a.vtmp, a.ua, a.va);
   HIP_LAUNCH_CHECK();
   GT_LAUNCH(cs_cgrid, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
