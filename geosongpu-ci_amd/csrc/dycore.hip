@@ -57,7 +57,7 @@ Dycore::Dycore(const Namelist& nl_, int rank, int nranks, const void* nccl_id) :
   HIP_CHECK(hipStreamCreateWithFlags(&st_b, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&st_c, hipStreamNonBlocking));
   HIP_CHECK(hipStreamCreateWithFlags(&st_d, hipStreamNonBlocking));
-  for (hipEvent_t* e : {&ev_fork, &ev_b, &ev_c, &ev_s, &ev_v, &ev_ut, &ev_df, &ev_dj})
+  for (hipEvent_t* e : {&ev_fork, &ev_b, &ev_c, &ev_ut, &ev_df, &ev_dj})
     HIP_CHECK(hipEventCreateWithFlags(e, hipEventDisableTiming));
   {
     const char* e = std::getenv("GTFV3_STREAMS");
@@ -131,7 +131,7 @@ Dycore::~Dycore() {
   if (dmet) (void)hipFree(dmet);
   if (dcornerw) (void)hipFree(dcornerw);
   if (darea4) (void)hipFree(darea4);
-  for (hipEvent_t e : {ev_fork, ev_b, ev_c, ev_s, ev_v, ev_ut, ev_df, ev_dj})
+  for (hipEvent_t e : {ev_fork, ev_b, ev_c, ev_ut, ev_df, ev_dj})
     if (e) (void)hipEventDestroy(e);
   for (auto& set : ev_ph)
     for (hipEvent_t e : set)
@@ -623,7 +623,6 @@ void Dycore::step() {
   // ds_vort launch and its reads of u, v less per sub-step: 31.48-31.53 -> 31.33-31.43 ms in
   // one box's A/B)
   ca.dvort = da.vort;
-  const bool vort_early = true;
   // d_sw's damping (damp.hip): the column of per-level parameters of FV3 dyn_core (the sponge
   // layers' divergence and w damping at the top in the Held-Suarez namelist)
   const std::vector<LevelDamp> col = column_damping(nl, c.da_min, c.da_min_c);
@@ -767,17 +766,6 @@ void Dycore::step() {
       uv_open = false;
     }
     const int csw_part = split && it > 0 ? 2 : 0;
-    if (early && !vort_early) {
-      // d_sw's cell vorticity needs only this sub-step's starting u, v (final here: the last
-      // sub-step's exchange, or the step's first): formed on stream c beside c_sw, so the
-      // wind stage after the fork is the kinetic energy and the vorticity march alone
-      HIP_CHECK(hipEventRecord(ev_s, st));
-      HIP_CHECK(hipStreamWaitEvent(st_c, ev_s, 0));
-      Ctx cc = c;
-      cc.st = st_c;
-      d_sw_vort(cc, da);
-      HIP_CHECK(hipEventRecord(ev_v, st_c));
-    }
     c_sw_transport(c, ca, csw_part);
     // nord > 0: c_sw's divergence_corner from the D-grid winds and d2a2c's ua, va
     if (nl.nord > 0) divergence_corner(c, npz, u.p, v.p, ua, va, const_cast<double*>(da.divg));
@@ -823,7 +811,7 @@ void Dycore::step() {
     if (!fork_substep) {
       d_sw_thermo(ct, da);
       if (tfused) thermo_swap();
-      d_sw_winds(c, da, vort_early);
+      d_sw_winds(c, da, true);
       update_dz_d(c, za);
       zh_swap();
     } else {
@@ -837,11 +825,10 @@ void Dycore::step() {
         // the kinetic energy needs ut / vt, not the Courant numbers: it starts beside
         // ds_courant, and the vorticity march waits for those and the vorticity
         HIP_CHECK(hipStreamWaitEvent(st_b, ev_ut, 0));
-        const hipEvent_t before_march[2] = {ev_fork, ev_v};
-        d_sw_winds(cb, da, true, before_march, vort_early ? 1 : 2);
+        d_sw_winds(cb, da, true, &ev_fork, 1);
       } else {
         HIP_CHECK(hipStreamWaitEvent(st_b, ev_fork, 0));
-        d_sw_winds(cb, da, vort_early);
+        d_sw_winds(cb, da, true);
       }
       update_dz_d(cc, za);
       zh_swap();

@@ -52,11 +52,10 @@ class Dycore {
   // in series on the main stream)
   hipStream_t st_d = nullptr;
   hipEvent_t ev_df = nullptr, ev_dj = nullptr;
-  // early d_sw winds (GTFV3_EARLY_WINDS: 0 off, 1 (default) the cell vorticity on stream c
-  // from the sub-step's start; the form on stream b ahead of c_sw's wind stage measured slower
-  // and was removed in round 6): the sub-step's start (u, v final), the vorticity formed on
-  // stream c, ut / vt written
-  hipEvent_t ev_s = nullptr, ev_v = nullptr, ev_ut = nullptr;
+  // early d_sw winds (GTFV3_EARLY_WINDS: 0 off, 1 (default) the kinetic energy on stream b as
+  // soon as ut / vt exist, beside ds_courant; the cell vorticity is formed by c_sw's cs_tmp):
+  // ut / vt written
+  hipEvent_t ev_ut = nullptr;
   int early_winds = 1;
   bool fork_substep = true;  // GTFV3_STREAMS=0: one stream
   std::unique_ptr<Transport> comm;  // null for one rank
