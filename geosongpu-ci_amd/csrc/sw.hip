@@ -37,6 +37,21 @@ __device__ __forceinline__ double ei4(double u0, double u1, double u2, double u3
   return 0.5 * (((t1 + d1) * u1 - d1 * u0) / t1 + ((t2 + d2) * u2 - d2 * u3) / t2);
 }
 
+// d_sw's advective Courant number and area flux of one face (ds_courant's expressions and order):
+// x faces from ut with rdxa(i-1) / rdxa(i), dy and sin_sg3(i-1) / sin_sg1(i) by the upwind side;
+// y faces from vt with rdya(j-1) / rdya(j), dx and sin_sg4(j-1) / sin_sg2(j)
+__device__ __forceinline__ void courant_face(double dt, double w, double r_up, double r_dn, double len, double s_up,
+                                             double s_dn, double& c, double& f) {
+  const double xf = dt * w;
+  if (xf > 0.0) {
+    c = xf * r_up;
+    f = len * xf * s_up;
+  } else {
+    c = xf * r_dn;
+    f = len * xf * s_dn;
+  }
+}
+
 // ---------------- c_sw ----------------
 
 // d2a2c_vect cube-corner fixes of utmp/vtmp/ua/va (reads generic values at non-corner points only)
@@ -368,9 +383,14 @@ struct CornerMap {
 };
 
 // ut, vt edge-adjacent cross terms and the cube-corner 2x2 solves (in place; sources never targets)
+// (crx non-null: the Courant numbers of the lane's point re-formed from the final ut / vt, and
+// the flux capacitor's sums on the lines ds_utvt1_kl leaves to this kernel -- see there)
 __global__ void __launch_bounds__(256) ds_utvt2(Dims d, const SubInfo* __restrict__ subs, const double* __restrict__ M,
                                                 int npz, const double* __restrict__ uc, const double* __restrict__ vc,
-                                                double* __restrict__ ut, double* __restrict__ vt) {
+                                                double* __restrict__ ut, double* __restrict__ vt, double dt,
+                                                double* __restrict__ crx, double* __restrict__ cry,
+                                                double* __restrict__ xfx, double* __restrict__ yfx,
+                                                double* __restrict__ cx, double* __restrict__ cy) {
   // all targets lie on the tile-edge lines: one lane per line point
   const int z = blockIdx.z, s = z / npz;
   const SubInfo sub = subs[s];
@@ -438,6 +458,26 @@ __global__ void __launch_bounds__(256) ds_utvt2(Dims d, const SubInfo* __restric
   // targets and sources are disjoint point sets, so no barrier is needed
   if (has_ut) AT(ut, 0, 0) = nut;
   if (has_vt) AT(vt, 0, 0) = nvt;
+  if (crx) {
+    const long pt = d.pitch;
+    // x faces on the y-lines (ut's targets), y faces on the x-lines (vt's): one lane per point
+    if ((J == -1 || J == 0 || J == N - 1 || J == N) && i >= 0 && i <= nx && j <= ny + NG - 1) {
+      double c = 0.0, f = 0.0;
+      courant_face(dt, has_ut ? nut : AT(ut, 0, 0), met(M, d, M_RDXA, s)[o - 1], met(M, d, M_RDXA, s)[o],
+                   met(M, d, M_DY, s)[o], met(M, d, M_SIN3, s)[o - 1], met(M, d, M_SIN1, s)[o], c, f);
+      AT(crx, 0, 0) = c;
+      AT(xfx, 0, 0) = f;
+      if (cx) AT(cx, 0, 0) += c;
+    }
+    if ((I == -1 || I == 0 || I == N - 1 || I == N) && j >= 0 && j <= ny && i <= nx + NG - 1) {
+      double c = 0.0, f = 0.0;
+      courant_face(dt, has_vt ? nvt : AT(vt, 0, 0), met(M, d, M_RDYA, s)[o - pt], met(M, d, M_RDYA, s)[o],
+                   met(M, d, M_DX, s)[o], met(M, d, M_SIN4, s)[o - pt], met(M, d, M_SIN2, s)[o], c, f);
+      AT(cry, 0, 0) = c;
+      AT(yfx, 0, 0) = f;
+      if (cy) AT(cy, 0, 0) += c;
+    }
+  }
 }
 
 // advective Courant numbers and area fluxes (saved per level for update_dz_d) + ra_x, ra_y
@@ -489,16 +529,36 @@ __global__ void __launch_bounds__(256) ds_courant(Dims d, const SubInfo* __restr
 // ds_courant and ds_ke measured slower: 1.56 -> 1.68 and 2.65 -> 3.37 ms per step)
 // (L: the whole plane or its interior, H: a hole of L left to another launch -- the interior /
 // boundary split of the uc, vc exchange)
+// With crx non-null the Courant numbers and area fluxes of ds_courant are formed here too from
+// the ut / vt just computed (ds_utvt2 re-forms them on the tile-edge lines where it corrects ut /
+// vt), and with cx / cy non-null the flux capacitor's Courant sums take them -- except on the
+// lines ds_utvt2 owns (x faces on J = -1, 0, N-1, N; y faces on I = -1, 0, N-1, N), which it sums.
 __global__ void __launch_bounds__(256) ds_utvt1_kl(Dims d, Launch2D L, Launch2D H, const SubInfo* __restrict__ subs,
                                                    const double* __restrict__ M, int npz, int nkb, int klb,
                                                    double dt, const double* __restrict__ uc,
                                                    const double* __restrict__ vc, double* __restrict__ ut,
-                                                   double* __restrict__ vt) {
+                                                   double* __restrict__ vt, double* __restrict__ crx,
+                                                   double* __restrict__ cry, double* __restrict__ xfx,
+                                                   double* __restrict__ yfx, double* __restrict__ cx,
+                                                   double* __restrict__ cy) {
   KLSETUP(npz)
   if (i >= H.i0 && i < H.i0 + H.ni && j >= H.j0 && j < H.j0 + H.nj) return;
   const SubInfo sub = subs[s];
   const int N = sub.N, I = i + sub.ioff, J = j + sub.joff, nx = d.nx, ny = d.ny;
   const long pt = d.pitch;
+  // ds_courant's regions and metric terms of the point (once for its block of levels)
+  const bool xr = crx && i >= 0 && i <= nx && j <= ny + NG - 1, yr = crx && j >= 0 && j <= ny && i <= nx + NG - 1;
+  double rxm = 0.0, rx0 = 0.0, dyp = 0.0, s3m = 0.0, s10 = 0.0, rym = 0.0, ry0 = 0.0, dxp = 0.0, s4m = 0.0, s20 = 0.0;
+  if (xr) {
+    rxm = met(M, d, M_RDXA, s)[o - 1]; rx0 = met(M, d, M_RDXA, s)[o]; dyp = met(M, d, M_DY, s)[o];
+    s3m = met(M, d, M_SIN3, s)[o - 1]; s10 = met(M, d, M_SIN1, s)[o];
+  }
+  if (yr) {
+    rym = met(M, d, M_RDYA, s)[o - pt]; ry0 = met(M, d, M_RDYA, s)[o]; dxp = met(M, d, M_DX, s)[o];
+    s4m = met(M, d, M_SIN4, s)[o - pt]; s20 = met(M, d, M_SIN2, s)[o];
+  }
+  const bool xsum = xr && cx && !(J == -1 || J == 0 || J == N - 1 || J == N);
+  const bool ysum = yr && cy && !(I == -1 || I == 0 || I == N - 1 || I == N);
   // x: 0 none, 1 tile-edge division, 2 generic; y likewise
   int mx = 0, my = 0;
   double ax = 0.0, bx = 0.0, ay = 0.0, by = 0.0;
@@ -532,6 +592,17 @@ __global__ void __launch_bounds__(256) ds_utvt1_kl(Dims d, Launch2D L, Launch2D 
     else if (my == 2) b = (v0 - 0.25 * ay * (us + use + u0 + ue)) * by;
     ut[lk] = a;
     vt[lk] = b;
+    if (crx) {
+      double ca = 0.0, fa = 0.0, cb = 0.0, fb = 0.0;
+      if (xr) courant_face(dt, a, rxm, rx0, dyp, s3m, s10, ca, fa);
+      if (yr) courant_face(dt, b, rym, ry0, dxp, s4m, s20, cb, fb);
+      crx[lk] = ca;
+      xfx[lk] = fa;
+      cry[lk] = cb;
+      yfx[lk] = fb;
+      if (xsum) cx[lk] += ca;
+      if (ysum) cy[lk] += cb;
+    }
   }
 }
 
@@ -829,15 +900,24 @@ void d_sw_courant(const Ctx& c, const DswArgs& a, hipEvent_t utvt_done, int part
   // (i, j+1): on [1, nx-1] x [1, ny-1] only owned values, none an exchange writes (the split
   // form needs the level-loop kernel, which takes its region)
   const Launch2D inner{1, 1, d.nx - 1, d.ny - 1};
+  // the Courant numbers (and with the fused thermo march, the flux capacitor's Courant sums)
+  // inside the level-loop ds_utvt1 and ds_utvt2: ds_courant's launch and its re-read of ut / vt
+  // only with GTFV3_KLOOP=0
+  const bool acc = d_sw_thermo_fused(a);
+  // (A/B in one box: 32.34 -> 31.59-31.63 ms per step)
+  const bool fold = klb > 0;
+  double* const ccx = fold && acc ? a.cx : nullptr;
+  double* const ccy = fold && acc ? a.cy : nullptr;
+  const double cb = fold ? L * ((acc ? 4 : 2) * e.X + (acc ? 4 : 2) * e.Y) + 8 * e.C : 0.0;
   auto utvt1 = [&](const Launch2D& r, const Launch2D& h) {
     GT_LAUNCH_N("ds_utvt1_kl", ds_utvt1_kl, kloop_grid(r, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, r, h, c.subs,
-                c.met, a.npz, nkb, klb, a.dt, a.uc, a.vc, a.ut, a.vt);
+                c.met, a.npz, nkb, klb, a.dt, a.uc, a.vc, a.ut, a.vt, a.crx, a.cry, a.xfx, a.yfx, ccx, ccy);
     HIP_LAUNCH_CHECK();
   };
   if (part == 1) {
     if (!klb) throw std::runtime_error("d_sw_courant: the split form needs GTFV3_KLOOP > 0");
     utvt1(inner, kNoHole);
-    gt_bytes(L * (2 * e.X + 2 * e.Y) + 8 * e.C);
+    gt_bytes(L * (2 * e.X + 2 * e.Y) + 8 * e.C + cb);
     return;
   }
   if (klb) {
@@ -847,12 +927,13 @@ void d_sw_courant(const Ctx& c, const DswArgs& a, hipEvent_t utvt_done, int part
                        a.ut, a.vt);
     HIP_LAUNCH_CHECK();
   }
-  if (part == 0) gt_bytes(L * (2 * e.X + 2 * e.Y) + 8 * e.C);
-  GT_LAUNCH(ds_utvt2, dim3(cdiv(edge_line_count(-NG, d.nx + NG, -NG, d.ny + NG), 256), 1, nz), dim3(256), 0, c.st, d, c.subs, c.met, a.npz, a.uc, a.vc, a.ut,
-                     a.vt);
+  if (part == 0) gt_bytes(L * (2 * e.X + 2 * e.Y) + 8 * e.C + cb);
+  GT_LAUNCH(ds_utvt2, dim3(cdiv(edge_line_count(-NG, d.nx + NG, -NG, d.ny + NG), 256), 1, nz), dim3(256), 0, c.st,
+            d, c.subs, c.met, a.npz, a.uc, a.vc, a.ut, a.vt, a.dt, fold ? a.crx : nullptr, a.cry, a.xfx, a.yfx,
+            ccx, ccy);
   HIP_LAUNCH_CHECK();
   if (utvt_done) HIP_CHECK(hipEventRecord(utvt_done, c.st));
-  const bool acc = d_sw_thermo_fused(a);
+  if (fold) return;
   GT_LAUNCH(ds_courant, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt, a.ut, a.vt,
                      a.crx, a.cry, a.xfx, a.yfx, acc ? a.cx : nullptr, acc ? a.cy : nullptr);
   HIP_LAUNCH_CHECK();

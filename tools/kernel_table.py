@@ -58,8 +58,8 @@ for name, v in rows[:n_rows]:
     pk = list(find(pmc, dn))
     pg = (sum(pmc[k]["traffic_bytes"] * pmc[k]["launches"] for k in pk) / sum(pmc[k]["launches"] for k in pk) / 1e9
           if pk else None)
-    bpl = v.get("bytes_per_launch", 0.0)
-    tbs = v.get("gbs", 0.0) / 1e3
+    bpl = v.get("bytes_per_launch") or 0.0
+    tbs = (v.get("gbs") or 0.0) / 1e3
     print(f"| `{name.strip('()')}` | {lps:.0f} | {v['ms_per_step']:.2f} | {us:.0f} | {bpl / 1e9:.2f} | {tbs:.2f} | "
           f"{tbs / 8.0:.2f} | {'–' if pg is None else f'{pg:.2f}'} |" if us is not None else
           f"| `{name.strip('()')}` | {lps:.0f} | {v['ms_per_step']:.2f} | – | {bpl / 1e9:.2f} | {tbs:.2f} | {tbs / 8.0:.2f} | "
