@@ -461,20 +461,30 @@ __global__ void __launch_bounds__(256) ds_utvt2(Dims d, const SubInfo* __restric
   if (crx) {
     const long pt = d.pitch;
     // x faces on the y-lines (ut's targets), y faces on the x-lines (vt's): one lane per point
+    // (re-formed where this kernel changed ut / vt; elsewhere ds_utvt1_kl's values stand and
+    // only the sum is taken)
     if ((J == -1 || J == 0 || J == N - 1 || J == N) && i >= 0 && i <= nx && j <= ny + NG - 1) {
-      double c = 0.0, f = 0.0;
-      courant_face(dt, has_ut ? nut : AT(ut, 0, 0), met(M, d, M_RDXA, s)[o - 1], met(M, d, M_RDXA, s)[o],
-                   met(M, d, M_DY, s)[o], met(M, d, M_SIN3, s)[o - 1], met(M, d, M_SIN1, s)[o], c, f);
-      AT(crx, 0, 0) = c;
-      AT(xfx, 0, 0) = f;
+      double c, f;
+      if (has_ut) {
+        courant_face(dt, nut, met(M, d, M_RDXA, s)[o - 1], met(M, d, M_RDXA, s)[o], met(M, d, M_DY, s)[o],
+                     met(M, d, M_SIN3, s)[o - 1], met(M, d, M_SIN1, s)[o], c, f);
+        AT(crx, 0, 0) = c;
+        AT(xfx, 0, 0) = f;
+      } else {
+        c = AT(crx, 0, 0);
+      }
       if (cx) AT(cx, 0, 0) += c;
     }
     if ((I == -1 || I == 0 || I == N - 1 || I == N) && j >= 0 && j <= ny && i <= nx + NG - 1) {
-      double c = 0.0, f = 0.0;
-      courant_face(dt, has_vt ? nvt : AT(vt, 0, 0), met(M, d, M_RDYA, s)[o - pt], met(M, d, M_RDYA, s)[o],
-                   met(M, d, M_DX, s)[o], met(M, d, M_SIN4, s)[o - pt], met(M, d, M_SIN2, s)[o], c, f);
-      AT(cry, 0, 0) = c;
-      AT(yfx, 0, 0) = f;
+      double c, f;
+      if (has_vt) {
+        courant_face(dt, nvt, met(M, d, M_RDYA, s)[o - pt], met(M, d, M_RDYA, s)[o], met(M, d, M_DX, s)[o],
+                     met(M, d, M_SIN4, s)[o - pt], met(M, d, M_SIN2, s)[o], c, f);
+        AT(cry, 0, 0) = c;
+        AT(yfx, 0, 0) = f;
+      } else {
+        c = AT(cry, 0, 0);
+      }
       if (cy) AT(cy, 0, 0) += c;
     }
   }
