@@ -54,56 +54,98 @@ __device__ __forceinline__ void courant_face(double dt, double w, double r_up, d
 
 // ---------------- c_sw ----------------
 
-// d2a2c_vect cube-corner fixes of utmp/vtmp/ua/va (reads generic values at non-corner points only)
-__global__ void cs_corner_fix(Dims d, const SubInfo* __restrict__ subs, int npz, double* __restrict__ utmp,
-                              double* __restrict__ vtmp, double* __restrict__ ua, double* __restrict__ va) {
-  const int z = blockIdx.x, s = z / npz;
-  const SubInfo sub = subs[s];
+// d2a2c_vect part 1's interpolation form at tile-global (I, J): second order within three
+// cells of a tile edge (on the sub-domain's data range), fourth order elsewhere
+__device__ __forceinline__ bool cs_two(const Dims& d, const SubInfo& sub, int I, int J) {
   const int N = sub.N, io = sub.ioff, jo = sub.joff;
-  const long zo = (long)z * d.plane;
-  auto P = [&](double* a, int I, int J) -> double& { return a[zo + pidx(d, I - io, J - jo)]; };
-  auto own = [&](int I, int J) { return I >= io && I <= io + d.nx && J >= jo && J <= jo + d.ny; };
-  const int t = threadIdx.x;
-  // gather everything first (threads act on disjoint targets; sources are never targets)
-  double val = 0.0;
-  double* tgt = nullptr;
-  if (own(0, 0)) {
-    if (t < 3) { int Ig = -3 + t; val = -P(vtmp, -1, -Ig - 1); tgt = &P(utmp, Ig, -1); }
-    else if (t < 6) { int Jg = -3 + (t - 3); val = -P(utmp, -Jg - 1, -1); tgt = &P(vtmp, -1, Jg); }
-    else if (t == 6) { val = -P(va, -1, 1); tgt = &P(ua, -2, -1); }
-    else if (t == 7) { val = -P(va, -1, 0); tgt = &P(ua, -1, -1); }
-    else if (t == 8) { val = -P(ua, 1, -1); tgt = &P(va, -1, -2); }
-    else if (t == 9) { val = -P(ua, 0, -1); tgt = &P(va, -1, -1); }
+  const int jsd = jo - NG, jed = jo + d.ny + NG - 1, isd = io - NG, ied = io + d.nx + NG - 1;
+  const bool mid = J >= max(3, jsd) && J <= min(N - 4, jed);
+  bool two = false;
+  if (J >= jsd && J <= 2) two = true;
+  if (J >= N - 3 && J <= jed) two = true;
+  if (mid && I >= isd && I <= 2) two = true;
+  if (mid && I >= N - 3 && I <= ied) two = true;
+  return two;
+}
+
+// d2a2c_vect part 1 at one point (local i, j of sub-domain s, level plane zo): the 4th-order
+// interpolated ut, vt (2nd order next to the tile edges, BIG outside the range) and the A-grid
+// winds ua, va from them; u0 u1 v0 v1 are u(j), u(j+1), v(i), v(i+1) for the vorticity
+struct CsTmpPt {
+  double ut, vt, a, b, u0, u1, v0, v1;
+  bool inr;
+};
+
+__device__ __forceinline__ CsTmpPt cs_tmp_pt(const Dims& d, const SubInfo& sub, const double* __restrict__ M, int s,
+                                             const double* __restrict__ u, const double* __restrict__ v, long zo,
+                                             int i, int j) {
+  const int N = sub.N, io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
+  const int I = i + io, J = j + jo;
+  const long o = pidx(d, i, j);
+  const long p = d.pitch;
+  CsTmpPt r;
+  r.inr = i <= nx + NG - 1 && j <= ny + NG - 1;
+  const bool rows = r.inr && J >= max(3, jo - 1) && J <= min(N - 4, jo + ny);
+  const bool cols = r.inr && I >= max(3, io - 1) && I <= min(N - 4, io + nx);
+  const double* U = u + zo + o;
+  const double* V = v + zo + o;
+  const long u1o = r.inr ? p : 0, umo = rows ? -p : 0, u2o = rows ? 2 * p : 0;
+  const long v1o = r.inr ? 1 : 0, vmo = cols ? -1 : 0, v2o = cols ? 2 : 0;
+  r.u0 = U[0];
+  r.u1 = U[u1o];
+  r.v0 = V[0];
+  r.v1 = V[v1o];
+  const double um = U[umo], u2 = U[u2o];
+  const double vm = V[vmo], v2 = V[v2o];
+  const double cs = MA(MT(M_COSA_S), 0, 0), r2 = MA(MT(M_RSIN2), 0, 0);
+  double ut = BIG, vt = BIG;
+  if (r.inr) {
+    if (rows) ut = A2 * (um + u2) + A1 * (r.u0 + r.u1);
+    if (cols) vt = A2 * (vm + v2) + A1 * (r.v0 + r.v1);
+    if (cs_two(d, sub, I, J)) {
+      ut = 0.5 * (r.u0 + r.u1);
+      vt = 0.5 * (r.v0 + r.v1);
+    }
   }
-  if (own(N, 0) && t >= 16 && t < 32) {
-    int q = t - 16;
-    if (q < 3) { val = P(vtmp, N, q); tgt = &P(utmp, N + q, -1); }
-    else if (q < 6) { int Jg = -3 + (q - 3); val = P(utmp, N + Jg, -1); tgt = &P(vtmp, N, Jg); }
-    else if (q == 6) { val = P(va, N, 0); tgt = &P(ua, N, -1); }
-    else if (q == 7) { val = P(va, N, 1); tgt = &P(ua, N + 1, -1); }
-    else if (q == 8) { val = P(ua, N - 1, -1); tgt = &P(va, N, -1); }
-    else if (q == 9) { val = P(ua, N - 2, -1); tgt = &P(va, N, -2); }
+  r.ut = ut;
+  r.vt = vt;
+  r.a = 0.0;
+  r.b = 0.0;
+  if (i >= -2 && i <= nx + 1 && j >= -2 && j <= ny + 1) {
+    r.a = (ut - vt * cs) * r2;
+    r.b = (vt - ut * cs) * r2;
   }
-  if (own(N, N) && t >= 32 && t < 48) {
-    int q = t - 32;
-    if (q < 3) { val = -P(vtmp, N, N - 1 - q); tgt = &P(utmp, N + q, N); }
-    else if (q < 6) { int jj = q - 3; val = -P(utmp, N - jj - 1, N); tgt = &P(vtmp, N, N + jj); }
-    else if (q == 6) { val = -P(va, N, N - 1); tgt = &P(ua, N, N); }
-    else if (q == 7) { val = -P(va, N, N - 2); tgt = &P(ua, N + 1, N); }
-    else if (q == 8) { val = -P(ua, N - 1, N); tgt = &P(va, N, N); }
-    else if (q == 9) { val = -P(ua, N - 2, N); tgt = &P(va, N, N + 1); }
+  return r;
+}
+
+// d2a2c_vect's cube-corner fills, as targets: the tile-global source point (SI, SJ) and sign of
+// a target of utmp (f 0), vtmp (1), ua (2) or va (3) at (I, J) of an owned corner, false if
+// (I, J) is not one.  utmp / vtmp take the source's vtmp / utmp, ua / va its va / ua; sources
+// are never targets, so a target point computes its source's own values
+__device__ __forceinline__ bool cs_corner_src(int f, int I, int J, int N, bool own_sw, bool own_se, bool own_ne,
+                                              bool own_nw, int& SI, int& SJ, double& sg) {
+  if (f == 0) {
+    if (own_sw && J == -1 && I >= -3 && I <= -1) { SI = -1; SJ = -I - 1; sg = -1.0; return true; }
+    if (own_se && J == -1 && I >= N && I <= N + 2) { SI = N; SJ = I - N; sg = 1.0; return true; }
+    if (own_ne && J == N && I >= N && I <= N + 2) { SI = N; SJ = 2 * N - 1 - I; sg = -1.0; return true; }
+    if (own_nw && J == N && I >= -3 && I <= -1) { SI = -1; SJ = N + I; sg = 1.0; return true; }
+  } else if (f == 1) {
+    if (own_sw && I == -1 && J >= -3 && J <= -1) { SI = -J - 1; SJ = -1; sg = -1.0; return true; }
+    if (own_se && I == N && J >= -3 && J <= -1) { SI = N + J; SJ = -1; sg = 1.0; return true; }
+    if (own_ne && I == N && J >= N && J <= N + 2) { SI = 2 * N - 1 - J; SJ = N; sg = -1.0; return true; }
+    if (own_nw && I == -1 && J >= N && J <= N + 2) { SI = J - N; SJ = N; sg = 1.0; return true; }
+  } else if (f == 2) {
+    if (own_sw && J == -1 && (I == -2 || I == -1)) { SI = -1; SJ = -1 - I; sg = -1.0; return true; }
+    if (own_se && J == -1 && (I == N || I == N + 1)) { SI = N; SJ = I - N; sg = 1.0; return true; }
+    if (own_ne && J == N && (I == N || I == N + 1)) { SI = N; SJ = 2 * N - 1 - I; sg = -1.0; return true; }
+    if (own_nw && J == N && (I == -2 || I == -1)) { SI = -1; SJ = N + I; sg = 1.0; return true; }
+  } else {
+    if (own_sw && I == -1 && (J == -2 || J == -1)) { SI = -1 - J; SJ = -1; sg = -1.0; return true; }
+    if (own_se && I == N && (J == -1 || J == -2)) { SI = N + J; SJ = -1; sg = 1.0; return true; }
+    if (own_ne && I == N && (J == N || J == N + 1)) { SI = 2 * N - 1 - J; SJ = N; sg = -1.0; return true; }
+    if (own_nw && I == -1 && (J == N || J == N + 1)) { SI = J - N; SJ = N; sg = 1.0; return true; }
   }
-  if (own(0, N) && t >= 48 && t < 64) {
-    int q = t - 48;
-    if (q < 3) { int Ig = -3 + q; val = P(vtmp, -1, N + Ig); tgt = &P(utmp, Ig, N); }
-    else if (q < 6) { int jj = q - 3; val = P(utmp, jj, N); tgt = &P(vtmp, -1, N + jj); }
-    else if (q == 6) { val = P(va, -1, N - 2); tgt = &P(ua, -2, N); }
-    else if (q == 7) { val = P(va, -1, N - 1); tgt = &P(ua, -1, N); }
-    else if (q == 8) { val = P(ua, 0, N); tgt = &P(va, -1, N); }
-    else if (q == 9) { val = P(ua, 1, N); tgt = &P(va, -1, N + 1); }
-  }
-  __syncthreads();
-  if (tgt) *tgt = val;
+  return false;
 }
 
 // d2a2c_vect part 2 (uc, ut | vc, vt) + the dt2*area scaling of ut, vt done by c_sw
@@ -256,6 +298,9 @@ __global__ void __launch_bounds__(256) cs_transport_ke_ld(
 // 4th-order / tile-edge / BIG choice made afterwards
 // (L: the whole plane or its interior, H: a hole of L left to another launch -- the interior /
 // boundary split of the u, v exchange, Dycore::step)
+// d2a2c_vect part 1 (utmp, vtmp, ua, va) on the launch region minus the hole, the cube-corner
+// fills included (formerly the cs_corner_fix launch after this one: a target thread forms its
+// source point's values itself, same expressions, so the result is the same bits)
 __global__ void __launch_bounds__(256) cs_tmp_ld(Dims d, Launch2D L, Launch2D H, const SubInfo* __restrict__ subs,
                                                  const double* __restrict__ M, int npz,
                                                  const double* __restrict__ u, const double* __restrict__ v,
@@ -264,50 +309,34 @@ __global__ void __launch_bounds__(256) cs_tmp_ld(Dims d, Launch2D L, Launch2D H,
                                                  double* __restrict__ dvort) {
   KSETUP(npz)
   if (i >= H.i0 && i < H.i0 + H.ni && j >= H.j0 && j < H.j0 + H.nj) return;
-  const int io = sub.ioff, jo = sub.joff, nx = d.nx, ny = d.ny;
-  const long p = d.pitch;
-  const bool inr = i <= nx + NG - 1 && j <= ny + NG - 1;
-  const bool rows = inr && J >= max(3, jo - 1) && J <= min(N - 4, jo + ny);
-  const bool cols = inr && I >= max(3, io - 1) && I <= min(N - 4, io + nx);
-  const double* U = u + zo + o;
-  const double* V = v + zo + o;
-  const long u1o = inr ? p : 0, umo = rows ? -p : 0, u2o = rows ? 2 * p : 0;
-  const long v1o = inr ? 1 : 0, vmo = cols ? -1 : 0, v2o = cols ? 2 : 0;
-  const double u0 = U[0], u1 = U[u1o], um = U[umo], u2 = U[u2o];
-  const double v0 = V[0], v1 = V[v1o], vm = V[vmo], v2 = V[v2o];
-  const double cs = MA(MT(M_COSA_S), 0, 0), r2 = MA(MT(M_RSIN2), 0, 0);
-  double ut = BIG, vt = BIG;
-  if (inr) {
-    if (rows) ut = A2 * (um + u2) + A1 * (u0 + u1);
-    if (cols) vt = A2 * (vm + v2) + A1 * (v0 + v1);
-    const int jsd = jo - NG, jed = jo + ny + NG - 1, isd = io - NG, ied = io + nx + NG - 1;
-    const bool mid = J >= max(3, jsd) && J <= min(N - 4, jed);
-    bool two = false;
-    if (J >= jsd && J <= 2) two = true;
-    if (J >= N - 3 && J <= jed) two = true;
-    if (mid && I >= isd && I <= 2) two = true;
-    if (mid && I >= N - 3 && I <= ied) two = true;
-    if (two) {
-      ut = 0.5 * (u0 + u1);
-      vt = 0.5 * (v0 + v1);
+  const CsTmpPt t = cs_tmp_pt(d, sub, M, s, u, v, zo, i, j);
+  double out[4] = {t.ut, t.vt, t.a, t.b};
+  // cube-corner halo points (at most 10 per owned corner of a level): rare, so divergent
+  const int io = sub.ioff, jo = sub.joff;
+  // (every target lies west or east of the tile: I < 0 or I >= N)
+  if (I < 0 || I >= N) {
+    auto own = [&](int CI, int CJ) { return CI >= io && CI <= io + d.nx && CJ >= jo && CJ <= jo + d.ny; };
+    const bool osw = own(0, 0), ose = own(N, 0), one = own(N, N), onw = own(0, N);
+    for (int f = 0; f < 4; ++f) {
+      int SI, SJ;
+      double sg;
+      if (!cs_corner_src(f, I, J, N, osw, ose, one, onw, SI, SJ, sg)) continue;
+      const CsTmpPt q = cs_tmp_pt(d, sub, M, s, u, v, zo, SI - io, SJ - jo);
+      const double src = f == 0 ? q.vt : f == 1 ? q.ut : f == 2 ? q.b : q.a;
+      out[f] = sg < 0.0 ? -src : src;
     }
   }
-  AT(utmp, 0, 0) = ut;
-  AT(vtmp, 0, 0) = vt;
-  double a = 0.0, b = 0.0;
-  if (i >= -2 && i <= nx + 1 && j >= -2 && j <= ny + 1) {
-    a = (ut - vt * cs) * r2;
-    b = (vt - ut * cs) * r2;
-  }
-  AT(ua, 0, 0) = a;
-  AT(va, 0, 0) = b;
+  AT(utmp, 0, 0) = out[0];
+  AT(vtmp, 0, 0) = out[1];
+  AT(ua, 0, 0) = out[2];
+  AT(va, 0, 0) = out[3];
   // d_sw's cell vorticity + Coriolis on [-NG, nx+NG-1] x [-NG, ny+NG-1] (ds_vort's expressions
   // and order) from the u(j+1), v(i+1) loaded above
-  if (dvort && inr) {
+  if (dvort && t.inr) {
     const double* dx = MT(M_DX);
     const double* dy = MT(M_DY);
-    const double udx0 = u0 * MA(dx, 0, 0), udx1 = u1 * MA(dx, 0, 1);
-    const double vdy0 = v0 * MA(dy, 0, 0), vdy1 = v1 * MA(dy, 1, 0);
+    const double udx0 = t.u0 * MA(dx, 0, 0), udx1 = t.u1 * MA(dx, 0, 1);
+    const double vdy0 = t.v0 * MA(dy, 0, 0), vdy1 = t.v1 * MA(dy, 1, 0);
     const double wk = MA(MT(M_RAREA), 0, 0) * (udx0 - udx1 + vdy1 - vdy0);
     AT(dvort, 0, 0) = wk + MA(MT(M_F0), 0, 0);
   }
@@ -850,8 +879,6 @@ void c_sw_transport(const Ctx& c, const CswArgs& a, int part) {
   }
   tmp(full, part == 2 ? inner : kNoHole);
   if (part == 0) gt_bytes(tb);
-  GT_LAUNCH(cs_corner_fix, dim3(nz), dim3(64), 0, c.st, d, c.subs, a.npz, a.utmp, a.vtmp, a.ua, a.va);
-  HIP_LAUNCH_CHECK();
   GT_LAUNCH(cs_cgrid, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
                      a.utmp, a.vtmp, a.ua, a.va, a.uc, a.vc, a.ut, a.vt);
   HIP_LAUNCH_CHECK();
