@@ -202,6 +202,108 @@ __global__ void __launch_bounds__(256) cs_cgrid(Dims d, const SubInfo* __restric
   AT(vt, 0, 0) = vtv;
 }
 
+// level-loop form of cs_cgrid (stencil_common.hpp kloop_levels): the point's metric terms --
+// which of them it needs is fixed by its position -- loaded once for its block of levels, so
+// the upwind sin_sg pick is a select instead of a dependent load per level; per level the same
+// expressions as cs_cgrid
+__global__ void __launch_bounds__(256) cs_cgrid_kl(Dims d, const SubInfo* __restrict__ subs,
+                                                   const double* __restrict__ M, int npz, int nkb, int klb,
+                                                   double dt2, const double* __restrict__ u,
+                                                   const double* __restrict__ v, const double* __restrict__ utmp,
+                                                   const double* __restrict__ vtmp, const double* __restrict__ ua,
+                                                   const double* __restrict__ va, double* __restrict__ uc,
+                                                   double* __restrict__ vc, double* __restrict__ ut,
+                                                   double* __restrict__ vt) {
+  Launch2D L{-NG, -NG, d.nx + 2 * NG + 1, d.ny + 2 * NG + 1};
+  KLSETUP(npz)
+  const SubInfo sub = subs[s];
+  const int N = sub.N, I = i + sub.ioff, J = j + sub.joff, nx = d.nx, ny = d.ny;
+  const long pt = d.pitch;
+  // x: y-edges, local i in [-1, nx+1], j in [-1, ny]; y: x-edges, i in [-1, nx], j in [-1, ny+1]
+  const bool xr = i >= -1 && i <= nx + 1 && j >= -1 && j <= ny;
+  const bool yr = i >= -1 && i <= nx && j >= -1 && j <= ny + 1;
+  const bool xl = I == 0 || I == N, yl = J == 0 || J == N;
+  double dxa[4] = {0, 0, 0, 0}, dya[4] = {0, 0, 0, 0};
+  double cau = 0, rsu = 0, dyp = 0, s3m = 0, s10 = 0, cav = 0, rsv = 0, dxp = 0, s4m = 0, s20 = 0;
+  if (xr) {
+    if (xl) {
+      const double* m = met(M, d, M_DXA, s) + o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dxa[q] = m[q - 2];
+    } else {
+      cau = met(M, d, M_COSA_U, s)[o];
+      rsu = met(M, d, M_RSIN_U, s)[o];
+    }
+    dyp = met(M, d, M_DY, s)[o];
+    s3m = met(M, d, M_SIN3, s)[o - 1];
+    s10 = met(M, d, M_SIN1, s)[o];
+  }
+  if (yr) {
+    if (yl) {
+      const double* m = met(M, d, M_DYA, s) + o;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) dya[q] = m[(q - 2) * pt];
+    } else {
+      cav = met(M, d, M_COSA_V, s)[o];
+      rsv = met(M, d, M_RSIN_V, s)[o];
+    }
+    dxp = met(M, d, M_DX, s)[o];
+    s4m = met(M, d, M_SIN4, s)[o - pt];
+    s20 = met(M, d, M_SIN2, s)[o];
+  }
+  // the x stencil's four inputs along i (ua on the tile-edge lines, utmp elsewhere), the y
+  // stencil's along j
+  const double* XS = (xl ? ua : utmp) + o;
+  const double* YS = (yl ? va : vtmp) + o;
+  for (int k = k0; k < k1; ++k) {
+    const long zo = ((long)s * npz + k) * P;
+    double ucv = 0.0, utv = 0.0, vcv = 0.0, vtv = 0.0;
+    double xs[4] = {0, 0, 0, 0}, ys[4] = {0, 0, 0, 0};
+    double v0 = 0.0, u0 = 0.0;
+    if (xr) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) xs[q] = XS[zo + q - 2];
+      v0 = v[zo + o];
+    }
+    if (yr) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ys[q] = YS[zo + (q - 2) * pt];
+      u0 = u[zo + o];
+    }
+    if (xr) {
+      if (xl) {
+        const double e = ei4(xs[0], xs[1], xs[2], xs[3], dxa[0], dxa[1], dxa[2], dxa[3]);
+        ucv = e * (e > 0.0 ? s3m : s10);
+        utv = e;
+      } else {
+        if (I == -1 || I == N - 1) ucv = C1 * xs[0] + C2 * xs[1] + C3 * xs[2];
+        else if (I == 1) ucv = C1 * xs[3] + C2 * xs[2] + C3 * xs[1];
+        else if (I == N + 1) ucv = C3 * xs[1] + C2 * xs[2] + C1 * xs[3];
+        else ucv = A2 * (xs[0] + xs[3]) + A1 * (xs[1] + xs[2]);
+        utv = (ucv - v0 * cau) * rsu;
+      }
+      utv = utv > 0.0 ? dt2 * utv * dyp * s3m : dt2 * utv * dyp * s10;
+    }
+    if (yr) {
+      if (yl) {
+        const double e = ei4(ys[0], ys[1], ys[2], ys[3], dya[0], dya[1], dya[2], dya[3]);
+        vcv = e * (e > 0.0 ? s4m : s20);
+        vtv = e;
+      } else {
+        if (J == -1 || J == N - 1) vcv = C1 * ys[0] + C2 * ys[1] + C3 * ys[2];
+        else if (J == 1 || J == N + 1) vcv = C1 * ys[3] + C2 * ys[2] + C3 * ys[1];
+        else vcv = A2 * (ys[0] + ys[3]) + A1 * (ys[1] + ys[2]);
+        vtv = (vcv - u0 * cav) * rsv;
+      }
+      vtv = vtv > 0.0 ? dt2 * vtv * dxp * s4m : dt2 * vtv * dxp * s20;
+    }
+    uc[zo + o] = ucv;
+    ut[zo + o] = utv;
+    vc[zo + o] = vcv;
+    vt[zo + o] = vtv;
+  }
+}
+
 // ---- loads-first forms: every input a point needs is loaded before any arithmetic --
 // addresses of the points outside the kernel's ranges clamped to an interior point, tile-edge
 // inputs loaded only by the waves holding tile-edge lines, both upwind candidates of a
@@ -293,14 +395,12 @@ __global__ void __launch_bounds__(256) cs_transport_ke_ld(
 }
 
 // d2a2c_vect part 1: utmp, vtmp (4th order interior / 2nd order near tile edges) and generic
-// ua, va.  The four u rows and four v columns of the 4th-order forms (the outer two at offset
-// 0 where the point takes no 4th-order value) and the two metric terms in one group; the
-// 4th-order / tile-edge / BIG choice made afterwards
+// ua, va (cs_tmp_pt: the four u rows and four v columns of the 4th-order forms and the two
+// metric terms in one group, the 4th-order / tile-edge / BIG choice made afterwards), the
+// cube-corner fills included (formerly a cs_corner_fix launch after this one: a target thread
+// forms its source point's values itself, same expressions, so the same bits)
 // (L: the whole plane or its interior, H: a hole of L left to another launch -- the interior /
 // boundary split of the u, v exchange, Dycore::step)
-// d2a2c_vect part 1 (utmp, vtmp, ua, va) on the launch region minus the hole, the cube-corner
-// fills included (formerly the cs_corner_fix launch after this one: a target thread forms its
-// source point's values itself, same expressions, so the result is the same bits)
 __global__ void __launch_bounds__(256) cs_tmp_ld(Dims d, Launch2D L, Launch2D H, const SubInfo* __restrict__ subs,
                                                  const double* __restrict__ M, int npz,
                                                  const double* __restrict__ u, const double* __restrict__ v,
@@ -879,8 +979,15 @@ void c_sw_transport(const Ctx& c, const CswArgs& a, int part) {
   }
   tmp(full, part == 2 ? inner : kNoHole);
   if (part == 0) gt_bytes(tb);
-  GT_LAUNCH(cs_cgrid, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
-                     a.utmp, a.vtmp, a.ua, a.va, a.uc, a.vc, a.ut, a.vt);
+  // (the level-loop form: 32.0-32.15 -> 31.54-31.57 ms per step as an A/B pair)
+  if (const int klb = kloop_levels()) {
+    const int nkb = (a.npz + klb - 1) / klb;
+    GT_LAUNCH_N("cs_cgrid", cs_cgrid_kl, kloop_grid(full, d.nsub, nkb), dim3(BX, BY), 0, c.st, d, c.subs, c.met,
+                a.npz, nkb, klb, a.dt2, a.u, a.v, a.utmp, a.vtmp, a.ua, a.va, a.uc, a.vc, a.ut, a.vt);
+  } else {
+    GT_LAUNCH(cs_cgrid, g2(d, full, nz), dim3(BX, BY), 0, c.st, d, c.subs, c.met, a.npz, a.dt2, a.u, a.v,
+                       a.utmp, a.vtmp, a.ua, a.va, a.uc, a.vc, a.ut, a.vt);
+  }
   HIP_LAUNCH_CHECK();
   gt_bytes(L * (3 * e.X + 3 * e.Y + 4 * e.C) + 12 * e.C);
   Launch2D Lt{-1, -1, d.nx + 2, d.ny + 2};
