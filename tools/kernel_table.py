@@ -25,6 +25,7 @@ DEV = {
     "cs_transport_ke": "cs_transport_ke_ld",
     "cs_update": "cs_update_ld",
     "cs_tmp": "cs_tmp_ld",
+    "cs_cgrid": "cs_cgrid_kl",
     "a2b_edge_k": "a2b_edge2_k",
     "halo_local_kernel": "halo_local_kernel<",
 }
