@@ -907,13 +907,18 @@ void march2(const Ctx& c, const TpM& m0, double bytes, const char* name_ex, cons
   const double fex = plan_spans(c, pex, pin);
   // (shorter segments for the tile-edge launch, 15 or 23 rows against the interior's 45,
   // measured 32.12 / 32.02 against 32.00 ms per step: not kept)
+  // a launch carries at most MAXSPAN spans in its arguments; more (many sub-domains in one
+  // process: C720 at 1x4 is 24 x 15) go as consecutive launches of disjoint spans
   auto go = [&](const std::vector<int>& pr, bool ex, hipStream_t st) {
-    TpM m = m0;
-    const long waves = set_spans(m, pr);
-    const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
-    if (ex) GT_LAUNCH_N(name_ex, (tp_march<ORD, A2_EX, MF, NF, TM, OCC_EX, 1>), g, b, 0, st, m);
-    else GT_LAUNCH_N(name_in, (tp_march<ORD, A2_IN, MF, NF, TM, OCC_IN, 2>), g, b, 0, st, m);
-    HIP_LAUNCH_CHECK();
+    for (size_t b0 = 0; b0 < pr.size(); b0 += MAXSPAN) {
+      const std::vector<int> part(pr.begin() + b0, pr.begin() + std::min(pr.size(), b0 + MAXSPAN));
+      TpM m = m0;
+      const long waves = set_spans(m, part);
+      const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
+      if (ex) GT_LAUNCH_N(name_ex, (tp_march<ORD, A2_EX, MF, NF, TM, OCC_EX, 1>), g, b, 0, st, m);
+      else GT_LAUNCH_N(name_in, (tp_march<ORD, A2_IN, MF, NF, TM, OCC_IN, 2>), g, b, 0, st, m);
+      HIP_LAUNCH_CHECK();
+    }
   };
   // The tile-edge kernel's few waves (one per SIMD at most, ~1000 at C180) each march a whole
   // segment: alone, the chip idles behind them for its length.  With a side stream (Ctx::side)
@@ -1177,49 +1182,58 @@ void fv_tp_2d(const Ctx& c, const TpArgs& a) {
     // MF: separate mass fluxes (w, pt and the tracers) or xfx / yfx themselves
     // (the paired last strip of the split thermo march measured 7 us slower per launch here,
     // 242 -> 249 us at C180, in either wave order: single-kernel marches keep one level per wave)
-    const long waves = set_spans(m, spans);
-    const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
+    // a launch carries at most MAXSPAN spans in its arguments; more (many sub-domains in one
+    // process: C720 at 1x4 is 24 x 15) go as consecutive launches of disjoint spans, the
+    // algorithmic bytes registered with the last
+    const size_t nchunk = (spans.size() + MAXSPAN - 1) / MAXSPAN;
+    for (size_t ci = 0; ci < nchunk; ++ci) {
+      const std::vector<int> part(spans.begin() + ci * MAXSPAN,
+                                  spans.begin() + std::min(spans.size(), (ci + 1) * MAXSPAN));
+      const double share = ci + 1 == nchunk ? 1.0 : 0.0;
+      const long waves = set_spans(m, part);
+      const dim3 g(cdiv(waves, MWAVES)), b(MW * MWAVES);
 #define TP_GO(O, M_, F_)                                                                           \
   do {                                                                                             \
     GT_LAUNCH_N("tp_march<" #O ", " #M_ ", " #F_ ">", (tp_march<O, true, M_, F_>), g, b, 0, c.st, m); \
     HIP_LAUNCH_CHECK();                                                                            \
-    gt_bytes(bytes / 8.0);                                                                         \
+    gt_bytes(share * bytes / 8.0);                                                                 \
   } while (0)
-    if (uv) {
-      // q read; crx cry xfx yfx read; ke, u, v read, u, v written; dx, dy once
-      const double ub = 8.0 * a.nk * ((e.C + 2 * (e.X + e.Y)) + e.K + 2 * (e.X + e.Y)) + 16.0 * e.C;
-      if (a.ord == 5) GT_LAUNCH_N("tp_march_uv<5>", (tp_march<5, true, false, 1, 3>), g, b, 0, c.st, m);
-      else GT_LAUNCH_N("tp_march_uv<6>", (tp_march<6, true, false, 1, 3>), g, b, 0, c.st, m);
-      HIP_LAUNCH_CHECK();
-      gt_bytes(ub / 8.0);
-      return;
-    }
-    if (zup) {
-      // zh read and written; crx cry xfx yfx read (the 2-D area plane not counted)
-      const double zb = 8.0 * a.nk * (2 * e.C + 2 * (e.X + e.Y));
-      if (a.ord == 5) GT_LAUNCH_N("tp_march_zh<5>", (tp_march<5, true, false, 1, 4>), g, b, 0, c.st, m);
-      else GT_LAUNCH_N("tp_march_zh<6>", (tp_march<6, true, false, 1, 4>), g, b, 0, c.st, m);
-      HIP_LAUNCH_CHECK();
-      gt_bytes(zb / 8.0);
-      return;
-    }
-    if (tupd) {
+      if (uv) {
+        // q read; crx cry xfx yfx read; ke, u, v read, u, v written; dx, dy once
+        const double ub = 8.0 * a.nk * ((e.C + 2 * (e.X + e.Y)) + e.K + 2 * (e.X + e.Y)) + 16.0 * e.C;
+        if (a.ord == 5) GT_LAUNCH_N("tp_march_uv<5>", (tp_march<5, true, false, 1, 3>), g, b, 0, c.st, m);
+        else GT_LAUNCH_N("tp_march_uv<6>", (tp_march<6, true, false, 1, 3>), g, b, 0, c.st, m);
+        HIP_LAUNCH_CHECK();
+        gt_bytes(share * ub / 8.0);
+        continue;
+      }
+      if (zup) {
+        // zh read and written; crx cry xfx yfx read (the 2-D area plane not counted)
+        const double zb = 8.0 * a.nk * (2 * e.C + 2 * (e.X + e.Y));
+        if (a.ord == 5) GT_LAUNCH_N("tp_march_zh<5>", (tp_march<5, true, false, 1, 4>), g, b, 0, c.st, m);
+        else GT_LAUNCH_N("tp_march_zh<6>", (tp_march<6, true, false, 1, 4>), g, b, 0, c.st, m);
+        HIP_LAUNCH_CHECK();
+        gt_bytes(share * zb / 8.0);
+        continue;
+      }
+      if (tupd) {
 #define TQ_GO(O, F_)                                                                                  \
   do {                                                                                                \
     GT_LAUNCH_N("tp_march_tracer<" #O ", " #F_ ">", (tp_march<O, true, true, F_, 2>), g, b, 0, c.st, m); \
     HIP_LAUNCH_CHECK();                                                                               \
-    gt_bytes(bytes / 8.0);                                                                            \
+    gt_bytes(share * bytes / 8.0);                                                                    \
   } while (0)
-      if (NFw == 3) { if (a.ord == 5) TQ_GO(5, 3); else TQ_GO(6, 3); }
-      else if (NFw == 2) { if (a.ord == 5) TQ_GO(5, 2); else TQ_GO(6, 2); }
-      else { if (a.ord == 5) TQ_GO(5, 1); else TQ_GO(6, 1); }
+        if (NFw == 3) { if (a.ord == 5) TQ_GO(5, 3); else TQ_GO(6, 3); }
+        else if (NFw == 2) { if (a.ord == 5) TQ_GO(5, 2); else TQ_GO(6, 2); }
+        else { if (a.ord == 5) TQ_GO(5, 1); else TQ_GO(6, 1); }
 #undef TQ_GO
-    } else if (a.mfx) {
-      if (NFw == 2) { if (a.ord == 5) TP_GO(5, true, 2); else TP_GO(6, true, 2); }
-      else { if (a.ord == 5) TP_GO(5, true, 1); else TP_GO(6, true, 1); }
-    } else {
-      if (NFw == 2) { if (a.ord == 5) TP_GO(5, false, 2); else TP_GO(6, false, 2); }
-      else { if (a.ord == 5) TP_GO(5, false, 1); else TP_GO(6, false, 1); }
+      } else if (a.mfx) {
+        if (NFw == 2) { if (a.ord == 5) TP_GO(5, true, 2); else TP_GO(6, true, 2); }
+        else { if (a.ord == 5) TP_GO(5, true, 1); else TP_GO(6, true, 1); }
+      } else {
+        if (NFw == 2) { if (a.ord == 5) TP_GO(5, false, 2); else TP_GO(6, false, 2); }
+        else { if (a.ord == 5) TP_GO(5, false, 1); else TP_GO(6, false, 1); }
+      }
     }
 #undef TP_GO
   }

@@ -19,12 +19,12 @@ FIELDS = ("u", "v", "w", "delz", "pt", "delp", "q", "ps", "pe", "ua", "va", "omg
 _gid = itertools.count(101)
 
 
-def _run_ranks(pkg, nranks, layout, npx=13, npz=10, nq=2):
+def _run_ranks(pkg, nranks, layout, npx=13, npz=10, nq=2, **kw):
     state = importlib.import_module(pkg.__name__ + ".state")
     ak, bk, ks = state.hybrid_levels(npz)
     gid = next(_gid)
     doms = [pkg.Domain(r, nranks, None, npx=npx, npz=npz, nq=nq, layout_x=layout[0], layout_y=layout[1],
-                       loopback=gid) for r in range(nranks)]
+                       loopback=gid, **kw) for r in range(nranks)]
     for d in doms:
         st = state.jablonowski_williamson(d, ak, bk)
         d.set_vertical(ak, bk, ks)
@@ -67,24 +67,35 @@ def test_multirank_split_exchange_matches_single_rank(pkg, require_gpu, monkeypa
     _check_multirank(pkg, nranks, layout, npx, npz)
 
 
-def _check_multirank(pkg, nranks, layout, npx, npz):
+def _check_multirank(pkg, nranks, layout, npx, npz, **kw):
     state = importlib.import_module(pkg.__name__ + ".state")
     ak, bk, ks = state.hybrid_levels(npz)
-    ref = pkg.Domain(npx=npx, npz=npz, nq=2, layout_x=layout[0], layout_y=layout[1])
+    ref = pkg.Domain(npx=npx, npz=npz, nq=2, layout_x=layout[0], layout_y=layout[1], **kw)
     st = state.jablonowski_williamson(ref, ak, bk)
     ref.set_vertical(ak, bk, ks)
     for k, v in st.items():
         ref.upload(k, v)
     ref.step(1)
     want = {k: ref.download(k) for k in FIELDS}
-    doms, got = _run_ranks(pkg, nranks, layout, npx=npx, npz=npz)
-    nper = doms[0].nsub
     nx, ny = ref.nx, ref.ny
+    ref.close()
+    doms, got = _run_ranks(pkg, nranks, layout, npx=npx, npz=npz, **kw)
+    nper = doms[0].nsub
     for r, d in enumerate(doms):
         for k in FIELDS:
             a = got[r][k][..., NG:NG + ny, NG:NG + nx]
             b = want[k][r * nper:(r + 1) * nper, ..., NG:NG + ny, NG:NG + nx]
             assert np.array_equal(a, b), f"rank {r} field {k} differs from the single-rank step"
+
+
+def test_multirank_c720_config5_layout(pkg, require_gpu, monkeypatch):
+    """BASELINE.json config 5's decomposition (C720 on 8 GPUs: 1x4 bands, three 720 x 180
+    sub-domains per rank) through the loopback transport with the interior / boundary split on,
+    as the RCCL ranks run it: every rank's state after a full step equals the single-rank step
+    bit for bit.  Reduced levels and tracers (L8, nq 2: config 5's L137 x 54 state is 0.2 TB);
+    dt scaled to the resolution (450 s x 180 / 720)."""
+    monkeypatch.setenv("GTFV3_HALO_SPLIT", "1")
+    _check_multirank(pkg, 8, (1, 4), 721, 8, dt=112.5)
 
 
 MOIST_FIELDS = FIELDS + ("clls", "clcn", "qlcn", "qicn", "prec_rain", "prec_snow", "prec_graupel", "prec_ice",
